@@ -1,0 +1,259 @@
+// tsdf_device.h -- device-side data layout and float math of the MI355X TSDF engine.
+//
+// Layout in HBM (one engine = one GPU shard):
+//   table    : 2^22 hash entries x 16 B {int16 x, y, z, offset; int32 idx; int32 pad}; the two
+//              entries of a bucket share one 32-B segment (reference VoxelBlock is 12 B AoS,
+//              voxel_mem.cuh:73-93; NUM_BUCKET 2^21 x 2, voxel_hash.cuh:12-25).
+//   lock_tag : 2^21 u32 bucket locks, "locked" == current lock epoch (no per-launch reset pass;
+//              reference resets 8 MiB twice per frame, voxel_tsdf.cu:385,487).
+//   pool     : 2^bits voxel blocks x 6 KiB, block-major {f32 tsdf[512] | f32 prob[512] |
+//              u8x4 rgbw[512]} so one block's state is one contiguous 6 KiB run (reference: three
+//              SoA arrays of 2^27 voxels, voxel_mem.cu:13-27).
+//   occ      : 2^22-bit occupancy bitmap of the table (replaces the full 48 MiB table scans of
+//              check_visibility_kernel / check_valid_kernel with a 512 KiB bitmap sweep).
+//
+// Float math restates utils/cuda/{camera,lie_group}.cuh with Eigen 3.3's evaluation order; the
+// library is compiled with -ffp-contract=off and IEEE division / sqrt so results are bit-identical
+// to the CPU oracle (oracle/tsdf_oracle.c) for everything except expf/logf (probability only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tsdf {
+
+constexpr int kBlockLenBits = 3;
+constexpr int kBlockLen = 8;
+constexpr int kBlockVolume = 512;
+constexpr int kBlockVolumeBits = 9;
+constexpr int kNumBucketBits = 21;
+constexpr uint32_t kNumBucket = 1u << kNumBucketBits;
+constexpr uint32_t kBucketMask = kNumBucket - 1;
+constexpr uint32_t kNumEntry = kNumBucket * 2;
+constexpr uint32_t kEntryMask = kNumEntry - 1;
+constexpr uint32_t kOccWords = kNumEntry / 64;
+constexpr int kBlockBytes = kBlockVolume * 12;  // 6 KiB per voxel block
+constexpr int kProbOffset = kBlockVolume * 4;   // byte offsets inside a block record
+constexpr int kRgbwOffset = kBlockVolume * 8;
+constexpr uint32_t kNewKeyCap = 1u << 17;       // unique new blocks per frame
+constexpr int kResolveThreads = 1024;
+
+struct f3 {
+  float x, y, z;
+};
+struct quatf {
+  float x, y, z, w;
+};
+
+// Per-frame constants, passed by value (host computes K^-1 and world_T_cam exactly like the
+// reference does on the host: CameraParams ctor camera.cuh:65, SE3::Inverse lie_group.cuh:22).
+struct FrameParams {
+  float fx, fy, cx, cy;      // intrinsics
+  float ifx, ify, icx, icy;  // intrinsics_inv
+  quatf cq;                  // cam_T_world
+  f3 ct;
+  quatf wq;                  // world_T_cam
+  f3 wt;
+  float voxel, trunc, max_depth;
+  int W, H;
+  int maxs;                  // DDA samples reserved per pixel in the candidate order space
+  int shard_index, shard_count;
+};
+
+// one visible block: snapshot of its hash entry (gather_visible_blocks_kernel copies entries)
+struct alignas(16) VisRec {
+  int16_t x, y, z, pad;
+  int32_t idx;
+  int32_t entry;
+};
+
+struct DevCounters {
+  int32_t free_count;     // VoxelMemPool::num_free_blocks_
+  uint32_t lock_epoch;    // current lock epoch
+  uint32_t claim_gen;     // resolver claim generation
+  int32_t nk_count;       // unique new keys inserted by the DDA this frame
+  int32_t n_sorted;       // ordered new keys (compaction output)
+  int32_t n_fresh;        // blocks acquired this frame
+  int32_t n_vis;          // visible blocks this frame
+  int32_t n_cand;         // carve candidates this frame (compaction output)
+  uint32_t status;        // TSDF_STATUS_* bits
+  int32_t last_alloc;
+  int32_t last_deleted;
+  int32_t last_new_keys;
+  unsigned long long last_updated;
+  unsigned long long total_visible;
+  unsigned long long total_updated;
+  unsigned long long total_alloc;
+  unsigned long long total_deleted;
+  unsigned long long frames;
+};
+
+// ------------------------------------------------------------------------------------------
+// float math (bit-exact restatement; see header comment)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ f3 cross3(f3 a, f3 b) {  // Eigen MatrixBase::cross
+  f3 r;
+  r.x = a.y * b.z - a.z * b.y;
+  r.y = a.z * b.x - a.x * b.z;
+  r.z = a.x * b.y - a.y * b.x;
+  return r;
+}
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
+__device__ __forceinline__ f3 qrot(quatf q, f3 v) {  // QuaternionBase::_transformVector
+  const f3 qv = {q.x, q.y, q.z};
+  f3 uv = cross3(qv, v);
+  uv.x += uv.x;
+  uv.y += uv.y;
+  uv.z += uv.z;
+  const f3 c = cross3(qv, uv);
+  f3 r;
+  r.x = (v.x + q.w * uv.x) + c.x;
+  r.y = (v.y + q.w * uv.y) + c.y;
+  r.z = (v.z + q.w * uv.z) + c.z;
+  return r;
+}
+__device__ __forceinline__ f3 se3_apply(quatf q, f3 t, f3 v) {  // SE3::Apply, lie_group.cuh:30
+  f3 r = qrot(q, v);
+  r.x = r.x + t.x;
+  r.y = r.y + t.y;
+  r.z = r.z + t.z;
+  return r;
+}
+__device__ __forceinline__ int32_t f2i(float f) {  // cvt.rzi.s32.f32 semantics
+  if (f != f) return 0;
+  if (f >= 2147483648.0f) return 2147483647;
+  if (f <= -2147483648.0f) return (-2147483647 - 1);
+  return (int32_t)f;
+}
+__device__ __forceinline__ int16_t f2s(float f) {
+  if (f != f) return 0;
+  if (f >= 32767.0f) return 32767;
+  if (f <= -32768.0f) return -32768;
+  return (int16_t)f;
+}
+__device__ __forceinline__ uint8_t f2u8(float f) {
+  if (!(f > 0.0f)) return 0;
+  if (f >= 255.0f) return 255;
+  return (uint8_t)f;
+}
+
+// voxel_hash.cu:31-35
+__device__ __host__ __forceinline__ uint32_t hash_block(int16_t x, int16_t y, int16_t z) {
+  return (((uint32_t)(int32_t)x * 73856093u) ^ ((uint32_t)(int32_t)y * 19349669u) ^
+          ((uint32_t)(int32_t)z * 83492791u)) & kBucketMask;
+}
+// shard owner of a block: a 4^3-block brick (16 cm at 5 mm) hashed to a GPU
+__device__ __host__ __forceinline__ uint32_t brick_owner(int16_t x, int16_t y, int16_t z,
+                                                        uint32_t shards) {
+  uint32_t h = ((uint32_t)(int32_t)(x >> 2) * 0x9E3779B1u) ^
+               ((uint32_t)(int32_t)(y >> 2) * 0x85EBCA77u) ^
+               ((uint32_t)(int32_t)(z >> 2) * 0xC2B2AE3Du);
+  h ^= h >> 16;
+  h *= 0x7FEB352Du;
+  h ^= h >> 15;
+  return shards <= 1 ? 0u : h % shards;
+}
+
+__device__ __forceinline__ uint64_t pack_key(int16_t x, int16_t y, int16_t z) {
+  return (uint64_t)(uint16_t)x | ((uint64_t)(uint16_t)y << 16) | ((uint64_t)(uint16_t)z << 32) |
+         (1ull << 48);
+}
+__device__ __forceinline__ void unpack_key(uint64_t k, int16_t& x, int16_t& y, int16_t& z) {
+  x = (int16_t)(k & 0xFFFF);
+  y = (int16_t)((k >> 16) & 0xFFFF);
+  z = (int16_t)((k >> 32) & 0xFFFF);
+}
+
+// hash entry as loaded from the table (int4 = 16 B)
+struct Ent {
+  int16_t x, y, z, off;
+  int32_t idx;
+};
+__device__ __forceinline__ Ent load_ent(const int4* table, uint32_t e) {
+  const int4 v = table[e];
+  Ent r;
+  r.x = (int16_t)(v.x & 0xFFFF);
+  r.y = (int16_t)((uint32_t)v.x >> 16);
+  r.z = (int16_t)(v.y & 0xFFFF);
+  r.off = (int16_t)((uint32_t)v.y >> 16);
+  r.idx = v.z;
+  return r;
+}
+__device__ __forceinline__ void store_ent(int4* table, uint32_t e, int16_t x, int16_t y, int16_t z,
+                                          int16_t off, int32_t idx) {
+  int4 v;
+  v.x = (int32_t)((uint32_t)(uint16_t)x | ((uint32_t)(uint16_t)y << 16));
+  v.y = (int32_t)((uint32_t)(uint16_t)z | ((uint32_t)(uint16_t)off << 16));
+  v.z = idx;
+  v.w = 0;
+  table[e] = v;
+}
+__device__ __forceinline__ void store_off(int4* table, uint32_t e, int16_t off) {
+  // the offset is the high half of the second dword
+  uint16_t* p = reinterpret_cast<uint16_t*>(&table[e]) + 3;
+  *p = (uint16_t)off;
+}
+__device__ __forceinline__ void store_off_idx(int4* table, uint32_t e, int16_t off, int32_t idx) {
+  uint16_t* p = reinterpret_cast<uint16_t*>(&table[e]) + 3;
+  *p = (uint16_t)off;
+  reinterpret_cast<int32_t*>(&table[e])[2] = idx;
+}
+
+// VoxelHashTable::RetrieveMutable lookup (voxel_hash.cuh:124-161): entry index or -1
+__device__ __forceinline__ int32_t find_entry(const int4* __restrict__ table, int16_t x, int16_t y,
+                                              int16_t z) {
+  const uint32_t e0 = hash_block(x, y, z) << 1;
+  const Ent a = load_ent(table, e0);
+  if (a.x == x && a.y == y && a.z == z && a.idx >= 0) return (int32_t)e0;
+  Ent b = load_ent(table, e0 + 1);
+  if (b.x == x && b.y == y && b.z == z && b.idx >= 0) return (int32_t)(e0 + 1);
+  uint32_t last = e0 + 1;
+  while (b.off) {
+    last = (uint32_t)(last + (int32_t)b.off) & kEntryMask;
+    b = load_ent(table, last);
+    if (b.x == x && b.y == y && b.z == z && b.idx >= 0) return (int32_t)last;
+  }
+  return -1;
+}
+
+// camera.cuh:47-51 and voxel_tsdf.cu:48-57 is_voxel_visible
+__device__ __forceinline__ bool voxel_visible(const FrameParams& P, int16_t gx, int16_t gy,
+                                              int16_t gz) {
+  const f3 pw = {(float)gx * P.voxel, (float)gy * P.voxel, (float)gz * P.voxel};
+  const f3 pc = se3_apply(P.cq, P.ct, pw);
+  const float hx = P.fx * pc.x + P.cx * pc.z;
+  const float hy = P.fy * pc.y + P.cy * pc.z;
+  const float hz = pc.z;
+  const float u = hx / hz, v = hy / hz;
+  return u >= 0 && u <= (float)(P.W - 1) && v >= 0 && v <= (float)(P.H - 1) && hz >= 0;
+}
+// voxel_tsdf.cu:59-80 is_block_visible<Full>
+template <bool Full>
+__device__ __forceinline__ bool block_visible(const FrameParams& P, int16_t bx, int16_t by,
+                                              int16_t bz) {
+  const int16_t x = (int16_t)(bx << kBlockLenBits), y = (int16_t)(by << kBlockLenBits),
+                z = (int16_t)(bz << kBlockLenBits);
+  bool vis = Full;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const bool v = voxel_visible(P, (int16_t)(x + ((i >> 0) & 1) * (kBlockLen - 1)),
+                                 (int16_t)(y + ((i >> 1) & 1) * (kBlockLen - 1)),
+                                 (int16_t)(z + ((i >> 2) & 1) * (kBlockLen - 1)));
+    if (Full)
+      vis = vis && v;
+    else
+      vis = vis || v;
+  }
+  return vis;
+}
+
+// pixel -> normalised camera ray K^-1 [x, y, 1] (camera.cuh:47-51 with intrinsics_inv)
+__device__ __forceinline__ f3 pixel_ray(const FrameParams& P, int x, int y) {
+  f3 pc;
+  pc.x = P.ifx * (float)x + P.icx * 1.0f;
+  pc.y = P.ify * (float)y + P.icy * 1.0f;
+  pc.z = 1.0f;
+  return pc;
+}
+
+}  // namespace tsdf

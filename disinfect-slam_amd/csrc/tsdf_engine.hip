@@ -1,0 +1,777 @@
+// tsdf_engine.hip -- host side of the MI355X TSDF engine: buffers, launch sequence and the C ABI
+// declared in include/disinfect_tsdf.h. No HIP type crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "disinfect_tsdf.h"
+#include "tsdf_kernels.h"
+
+using namespace tsdf;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+void set_error(const char* what, hipError_t e) {
+  char buf[512];
+  std::snprintf(buf, sizeof(buf), "%s: %s", what, hipGetErrorString(e));
+  g_last_error = buf;
+}
+void set_error(const char* what) { g_last_error = what; }
+
+#define HIP_OK(expr)                  \
+  do {                                \
+    hipError_t _e = (expr);           \
+    if (_e != hipSuccess) {           \
+      set_error(#expr, _e);           \
+      return TSDF_ERR_HIP;            \
+    }                                 \
+  } while (0)
+
+#define LAUNCH_OK(what)                        \
+  do {                                         \
+    hipError_t _e = hipGetLastError();         \
+    if (_e != hipSuccess) {                    \
+      set_error(what, _e);                     \
+      return TSDF_ERR_HIP;                     \
+    }                                          \
+  } while (0)
+
+// ---- host float math: same expressions (and -ffp-contract=off) as tsdf_device.h / the oracle ----
+f3 h_cross(f3 a, f3 b) {
+  f3 r;
+  r.x = a.y * b.z - a.z * b.y;
+  r.y = a.z * b.x - a.x * b.z;
+  r.z = a.x * b.y - a.y * b.x;
+  return r;
+}
+f3 h_qrot(quatf q, f3 v) {
+  const f3 qv = {q.x, q.y, q.z};
+  f3 uv = h_cross(qv, v);
+  uv.x += uv.x;
+  uv.y += uv.y;
+  uv.z += uv.z;
+  const f3 c = h_cross(qv, uv);
+  f3 r;
+  r.x = (v.x + q.w * uv.x) + c.x;
+  r.y = (v.y + q.w * uv.y) + c.y;
+  r.z = (v.z + q.w * uv.z) + c.z;
+  return r;
+}
+int16_t h_f2s(float f) {
+  if (f != f) return 0;
+  if (f >= 32767.0f) return 32767;
+  if (f <= -32768.0f) return -32768;
+  return (int16_t)f;
+}
+
+template <typename T>
+hipError_t dmalloc(T** p, size_t count) {
+  return hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(count, 1) * sizeof(T));
+}
+
+}  // namespace
+
+struct tsdf_engine {
+  tsdf_config cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  EngineDev D{};
+  int maxs = 3;
+  int64_t obits_bits = 0;
+  int obits_words = 0;
+  int wgcnt_cap = 0;
+  int64_t max_pixels = 0;
+  // host-frame staging
+  uint8_t* s_rgb = nullptr;
+  float* s_depth = nullptr;
+  float* s_ht = nullptr;
+  float* s_lt = nullptr;
+  // raycast / query / test scratch
+  uchar4* rc_rgba = nullptr;
+  uchar4* rc_norm = nullptr;
+  VisRec* q_sel = nullptr;
+  int32_t* q_count = nullptr;
+  float4* q_out = nullptr;
+  int64_t q_out_cap = 0;
+  int16_t* t_keys = nullptr;
+  VisRec* t_recs = nullptr;
+  int32_t* t_count = nullptr;
+  int32_t* t_i32 = nullptr;
+  uint32_t* t_u32 = nullptr;
+  float* t_f0 = nullptr;
+  float* t_f1 = nullptr;
+  short4* t_s4 = nullptr;
+  int t_cap = 0;
+  DevCounters* h_ctr = nullptr;  // pinned readback
+  // profiling
+  bool profiling = false;
+  std::vector<std::array<hipEvent_t, 5>> events;
+  size_t ev_used = 0;
+  unsigned long long prof_vis0 = 0, prof_upd0 = 0;
+};
+
+namespace {
+
+void free_all(tsdf_engine* e) {
+  EngineDev& D = e->D;
+  void* ptrs[] = {D.table,  D.lock_tag, D.claim,   D.heap,    D.pool,   D.occ,       D.ctr,
+                  D.nk_key, D.nk_order, D.nk_list, D.obits,   D.order_slot, D.sorted, D.fresh,
+                  D.visbits, D.wgcnt,   D.vis,     D.candbits, D.cand,   D.pix,       e->s_rgb,
+                  e->s_depth, e->s_ht,  e->s_lt,   e->rc_rgba, e->rc_norm, e->q_sel,  e->q_count,
+                  e->q_out, e->t_keys,  e->t_recs, e->t_count, e->t_i32, e->t_u32,    e->t_f0,
+                  e->t_f1,  e->t_s4};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (e->h_ctr) (void)hipHostFree(e->h_ctr);
+  for (auto& ev : e->events)
+    for (hipEvent_t x : ev) (void)hipEventDestroy(x);
+  if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+}
+
+FrameParams make_params(const tsdf_engine* e, const tsdf_intrinsics* K, int W, int H,
+                        const tsdf_pose* p, float max_depth) {
+  FrameParams P{};
+  P.fx = K->fx;
+  P.fy = K->fy;
+  P.cx = K->cx;
+  P.cy = K->cy;
+  P.ifx = 1.0f / K->fx;  // CameraIntrinsics::Inverse (camera.cuh:34-39)
+  P.ify = 1.0f / K->fy;
+  P.icx = -K->cx * P.ifx;
+  P.icy = -K->cy * P.ify;
+  P.cq = {p->qx, p->qy, p->qz, p->qw};
+  P.ct = {p->tx, p->ty, p->tz};
+  // SE3::Inverse on the host (lie_group.cuh:22-24); squaredNorm as a Packet4f reduction
+  const float n2 = (p->qx * p->qx + p->qz * p->qz) + (p->qy * p->qy + p->qw * p->qw);
+  if (n2 > 0.0f)
+    P.wq = {-p->qx / n2, -p->qy / n2, -p->qz / n2, p->qw / n2};
+  else
+    P.wq = {0.f, 0.f, 0.f, 0.f};
+  const f3 nt = {-p->tx, -p->ty, -p->tz};
+  P.wt = h_qrot(P.wq, nt);
+  P.voxel = e->cfg.voxel_size;
+  P.trunc = e->cfg.truncation;
+  P.max_depth = max_depth;
+  P.W = W;
+  P.H = H;
+  P.maxs = e->maxs;
+  P.shard_index = e->cfg.shard_index;
+  P.shard_count = e->cfg.shard_count;
+  return P;
+}
+
+int ensure_test_cap(tsdf_engine* e, int n) {
+  if (n <= e->t_cap) return TSDF_OK;
+  void* ptrs[] = {e->t_keys, e->t_recs, e->t_i32, e->t_u32, e->t_f0, e->t_f1, e->t_s4};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  const int cap = std::max(n, 1024);
+  HIP_OK(dmalloc(&e->t_keys, (size_t)cap * 3));
+  HIP_OK(dmalloc(&e->t_recs, (size_t)cap));
+  HIP_OK(dmalloc(&e->t_i32, (size_t)cap));
+  HIP_OK(dmalloc(&e->t_u32, (size_t)cap));
+  HIP_OK(dmalloc(&e->t_f0, (size_t)cap));
+  HIP_OK(dmalloc(&e->t_f1, (size_t)cap));
+  HIP_OK(dmalloc(&e->t_s4, (size_t)cap));
+  e->t_cap = cap;
+  return TSDF_OK;
+}
+
+// ordered compaction of `nwords` 64-bit words into `out`, count to `out_count` (device)
+int launch_compact(tsdf_engine* e, unsigned long long* bits, int nwords, int32_t* out,
+                   int32_t* out_count) {
+  const int nwg = (nwords + 255) / 256;
+  if (nwg > e->wgcnt_cap) {
+    set_error("compaction grid exceeds wgcnt capacity");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  hipLaunchKernelGGL(k_compact_count, dim3(nwg), dim3(256), 0, e->stream, bits, nwords,
+                     e->D.wgcnt);
+  hipLaunchKernelGGL(k_compact_emit, dim3(nwg), dim3(256), 0, e->stream, bits, nwords,
+                     e->D.wgcnt, nwg, out, out_count);
+  LAUNCH_OK("compaction");
+  return TSDF_OK;
+}
+
+// order bits -> resolver -> fresh block init (shared by integrate and the hash_allocate test op)
+int launch_allocate_tail(tsdf_engine* e, int64_t order_bits, int count_stats) {
+  hipLaunchKernelGGL(k_order_mark, dim3(256), dim3(256), 0, e->stream, e->D);
+  const int nwords = (int)((order_bits + 63) / 64);
+  int rc = launch_compact(e, e->D.obits, nwords, e->D.sorted, &e->D.ctr->n_sorted);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_resolve_alloc, dim3(1), dim3(kResolveThreads), 0, e->stream, e->D,
+                     count_stats);
+  hipLaunchKernelGGL(k_fresh_init, dim3(512), dim3(256), 0, e->stream, e->D);
+  LAUNCH_OK("allocate");
+  return TSDF_OK;
+}
+
+int read_counters(tsdf_engine* e) {
+  HIP_OK(hipMemcpyAsync(e->h_ctr, e->D.ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return TSDF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void tsdf_config_default(tsdf_config* c) {
+  if (!c) return;
+  c->voxel_size = 0.005f;
+  c->truncation = 0.03f;
+  c->max_width = 1920;
+  c->max_height = 1080;
+  c->num_block_bits = 18;
+  c->shard_index = 0;
+  c->shard_count = 1;
+  c->stream = nullptr;
+}
+
+const char* tsdf_error_string(int code) {
+  switch (code) {
+    case TSDF_OK: return "ok";
+    case TSDF_ERR_INVALID_ARG: return "invalid argument";
+    case TSDF_ERR_OUT_OF_MEMORY: return "out of device memory";
+    case TSDF_ERR_HIP: return "HIP runtime error";
+    case TSDF_ERR_CAPACITY: return "output buffer too small";
+    case TSDF_ERR_NO_DEVICE: return "no HIP device";
+    default: return "unknown error";
+  }
+}
+const char* tsdf_last_error(void) { return g_last_error.c_str(); }
+
+uint32_t tsdf_hash_block(int16_t x, int16_t y, int16_t z) { return hash_block(x, y, z); }
+int32_t tsdf_block_owner(int16_t x, int16_t y, int16_t z, int32_t n) {
+  return (int32_t)brick_owner(x, y, z, (uint32_t)(n < 1 ? 1 : n));
+}
+int32_t tsdf_num_entries(void) { return (int32_t)kNumEntry; }
+int32_t tsdf_num_blocks(const tsdf_engine* e) { return e ? e->D.nblocks : 0; }
+
+int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
+  if (!out) return TSDF_ERR_INVALID_ARG;
+  *out = nullptr;
+  tsdf_config cfg;
+  if (cfg_in)
+    cfg = *cfg_in;
+  else
+    tsdf_config_default(&cfg);
+  if (!(cfg.voxel_size > 0) || !(cfg.truncation > 0) || cfg.max_width <= 0 ||
+      cfg.max_height <= 0 || cfg.num_block_bits < 1 || cfg.num_block_bits > 22 ||
+      cfg.shard_count < 1 || cfg.shard_index < 0 || cfg.shard_index >= cfg.shard_count) {
+    set_error("tsdf_create: invalid config");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) {
+    set_error("tsdf_create: no such HIP device");
+    return TSDF_ERR_NO_DEVICE;
+  }
+  HIP_OK(hipSetDevice(device));
+  tsdf_engine* e = new tsdf_engine();
+  e->cfg = cfg;
+  e->device = device;
+  // DDA samples per pixel: step_grid = ceil(max|2 trunc dir / voxel| / 8) + 1 (voxel_tsdf.cu:136)
+  e->maxs = (int)std::ceil(2.0 * cfg.truncation / cfg.voxel_size * 1.0001 / kBlockLen) + 1;
+  e->max_pixels = (int64_t)cfg.max_width * cfg.max_height;
+  e->obits_bits = e->max_pixels * e->maxs;
+  if (e->obits_bits >= (1ll << 31)) {
+    delete e;
+    set_error("tsdf_create: image too large for the candidate order space");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  e->obits_words = (int)((e->obits_bits + 63) / 64);
+  e->wgcnt_cap = std::max<int>((e->obits_words + 255) / 256, (int)(kOccWords / 256)) + 8;
+  const int nb = 1 << cfg.num_block_bits;
+  EngineDev& D = e->D;
+  D.nblocks = nb;
+  auto fail = [&](int code) {
+    free_all(e);
+    delete e;
+    return code;
+  };
+#define ALLOC(ptr, n)                                 \
+  do {                                                \
+    hipError_t _e = dmalloc(&(ptr), (size_t)(n));     \
+    if (_e != hipSuccess) {                           \
+      set_error("tsdf_create: hipMalloc " #ptr, _e);  \
+      return fail(TSDF_ERR_OUT_OF_MEMORY);            \
+    }                                                 \
+  } while (0)
+  ALLOC(D.table, kNumEntry);
+  ALLOC(D.lock_tag, kNumBucket);
+  ALLOC(D.claim, kNumBucket);
+  ALLOC(D.heap, nb);
+  ALLOC(D.pool, (size_t)nb * kBlockBytes);
+  ALLOC(D.occ, kOccWords);
+  ALLOC(D.ctr, 1);
+  ALLOC(D.nk_key, kNewKeyCap);
+  ALLOC(D.nk_order, kNewKeyCap);
+  ALLOC(D.nk_list, kNewKeyCap);
+  ALLOC(D.obits, e->obits_words);
+  ALLOC(D.order_slot, e->obits_bits);
+  ALLOC(D.sorted, kNewKeyCap);
+  ALLOC(D.fresh, kNewKeyCap);
+  ALLOC(D.visbits, kOccWords);
+  ALLOC(D.wgcnt, e->wgcnt_cap);
+  ALLOC(D.vis, nb);
+  ALLOC(D.candbits, (nb + 63) / 64);
+  ALLOC(D.cand, nb);
+  ALLOC(D.pix, e->max_pixels);
+  ALLOC(e->s_rgb, e->max_pixels * 3);
+  ALLOC(e->s_depth, e->max_pixels);
+  ALLOC(e->s_ht, e->max_pixels);
+  ALLOC(e->s_lt, e->max_pixels);
+  ALLOC(e->rc_rgba, e->max_pixels);
+  ALLOC(e->rc_norm, e->max_pixels);
+  ALLOC(e->q_sel, nb);
+  ALLOC(e->q_count, 1);
+  ALLOC(e->t_count, 1);
+#undef ALLOC
+  if (hipHostMalloc(reinterpret_cast<void**>(&e->h_ctr), sizeof(DevCounters)) != hipSuccess)
+    return fail(TSDF_ERR_OUT_OF_MEMORY);
+  if (cfg.stream) {
+    e->stream = reinterpret_cast<hipStream_t>(cfg.stream);
+  } else {
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+      return fail(TSDF_ERR_HIP);
+    e->own_stream = true;
+  }
+  hipStream_t s = e->stream;
+  bool ok = true;
+  ok &= hipMemsetAsync(D.lock_tag, 0, sizeof(uint32_t) * kNumBucket, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.claim, 0, sizeof(unsigned long long) * kNumBucket, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.pool, 0, (size_t)nb * kBlockBytes, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.occ, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.nk_key, 0, sizeof(unsigned long long) * kNewKeyCap, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.nk_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.obits, 0, sizeof(unsigned long long) * e->obits_words, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.candbits, 0, sizeof(unsigned long long) * ((nb + 63) / 64), s) == hipSuccess;
+  ok &= hipMemsetAsync(D.visbits, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
+  DevCounters c0{};
+  c0.free_count = nb;
+  ok &= hipMemcpyAsync(D.ctr, &c0, sizeof(c0), hipMemcpyHostToDevice, s) == hipSuccess;
+  hipLaunchKernelGGL(k_init_table, dim3(kNumEntry / 256), dim3(256), 0, s, D.table);
+  hipLaunchKernelGGL(k_init_heap, dim3((nb + 255) / 256), dim3(256), 0, s, D.heap, nb);
+  ok &= hipGetLastError() == hipSuccess;
+  ok &= hipStreamSynchronize(s) == hipSuccess;
+  if (!ok) {
+    set_error("tsdf_create: initialisation failed");
+    return fail(TSDF_ERR_HIP);
+  }
+  *out = e;
+  return TSDF_OK;
+}
+
+int tsdf_destroy(tsdf_engine* e) {
+  if (!e) return TSDF_ERR_INVALID_ARG;
+  (void)hipSetDevice(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  free_all(e);
+  delete e;
+  return TSDF_OK;
+}
+
+int tsdf_synchronize(tsdf_engine* e) {
+  if (!e) return TSDF_ERR_INVALID_ARG;
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return TSDF_OK;
+}
+
+int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
+                   const tsdf_pose* pose, float max_depth) {
+  if (!e || !f || !K || !pose || !f->depth || !f->rgb || f->width <= 0 || f->height <= 0 ||
+      (int64_t)f->width * f->height > e->max_pixels || f->width > e->cfg.max_width ||
+      f->height > e->cfg.max_height || (f->ht == nullptr) != (f->lt == nullptr)) {
+    set_error("tsdf_integrate: invalid argument");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  const int W = f->width, H = f->height;
+  const size_t np = (size_t)W * H;
+  hipStream_t s = e->stream;
+  const float* depth = f->depth;
+  const uint8_t* rgb = f->rgb;
+  const float* ht = f->ht;
+  const float* lt = f->lt;
+  if (f->mem_kind == TSDF_MEM_HOST) {  // voxel_tsdf.cu:358-365 (pageable H2D)
+    HIP_OK(hipMemcpyAsync(e->s_rgb, rgb, np * 3, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(e->s_depth, depth, np * 4, hipMemcpyHostToDevice, s));
+    rgb = e->s_rgb;
+    depth = e->s_depth;
+    if (ht) {
+      HIP_OK(hipMemcpyAsync(e->s_ht, ht, np * 4, hipMemcpyHostToDevice, s));
+      HIP_OK(hipMemcpyAsync(e->s_lt, lt, np * 4, hipMemcpyHostToDevice, s));
+      ht = e->s_ht;
+      lt = e->s_lt;
+    }
+  } else if (f->mem_kind != TSDF_MEM_DEVICE) {
+    set_error("tsdf_integrate: bad mem_kind");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  const FrameParams P = make_params(e, K, W, H, pose, max_depth);
+  std::array<hipEvent_t, 5>* ev = nullptr;
+  if (e->profiling) {
+    if (e->ev_used == e->events.size()) {
+      std::array<hipEvent_t, 5> a{};
+      for (auto& x : a) HIP_OK(hipEventCreate(&x));
+      e->events.push_back(a);
+    }
+    ev = &e->events[e->ev_used++];
+    HIP_OK(hipEventRecord((*ev)[0], s));
+  }
+  // ---- allocate (voxel_tsdf.cu:377-386) ----
+  hipLaunchKernelGGL(k_ingest_dda, dim3((W + 15) / 16, (H + 15) / 16), dim3(256), 0, s, e->D, P,
+                     depth, rgb, ht, lt);
+  LAUNCH_OK("k_ingest_dda");
+  int rc = launch_allocate_tail(e, (int64_t)np * e->maxs, 1);
+  if (rc) return rc;
+  if (ev) HIP_OK(hipEventRecord((*ev)[1], s));
+  // ---- visibility (voxel_tsdf.cu:388-397) ----
+  hipLaunchKernelGGL(k_vis_count, dim3(kOccWords / 256), dim3(256), 0, s, e->D, P);
+  hipLaunchKernelGGL(k_vis_emit, dim3(kOccWords / 256), dim3(256), 0, s, e->D, e->D.vis,
+                     &e->D.ctr->n_vis);
+  LAUNCH_OK("visibility");
+  if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
+  // ---- update (voxel_tsdf.cu:474-481) ----
+  hipLaunchKernelGGL(k_integrate, dim3(1024), dim3(256), 0, s, e->D, P);
+  LAUNCH_OK("k_integrate");
+  if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
+  // ---- space carving (voxel_tsdf.cu:483-488) ----
+  rc = launch_compact(e, e->D.candbits, (e->D.nblocks + 63) / 64, e->D.cand, &e->D.ctr->n_cand);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kResolveThreads), 0, s, e->D, e->D.cand,
+                     &e->D.ctr->n_cand, e->D.vis, kResolveThreads, 1);
+  LAUNCH_OK("k_resolve_delete");
+  if (ev) HIP_OK(hipEventRecord((*ev)[4], s));
+  return TSDF_OK;
+}
+
+int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const tsdf_pose* pose,
+                 float max_depth, uint8_t* rgba, uint8_t* normal, int mem_kind) {
+  if (!e || !K || !pose || W <= 0 || H <= 0 || (int64_t)W * H > e->max_pixels ||
+      (mem_kind != TSDF_MEM_HOST && mem_kind != TSDF_MEM_DEVICE)) {
+    set_error("tsdf_raycast: invalid argument");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  const FrameParams P = make_params(e, K, W, H, pose, max_depth);
+  uchar4* o1 = mem_kind == TSDF_MEM_DEVICE ? reinterpret_cast<uchar4*>(rgba) : (rgba ? e->rc_rgba : nullptr);
+  uchar4* o2 = mem_kind == TSDF_MEM_DEVICE ? reinterpret_cast<uchar4*>(normal) : (normal ? e->rc_norm : nullptr);
+  hipLaunchKernelGGL(k_raycast, dim3((W + 15) / 16, (H + 15) / 16), dim3(256), 0, e->stream, e->D,
+                     P, e->cfg.truncation / 2, o1, o2);
+  LAUNCH_OK("k_raycast");
+  if (mem_kind == TSDF_MEM_HOST) {
+    const size_t bytes = (size_t)W * H * 4;
+    if (rgba) HIP_OK(hipMemcpyAsync(rgba, e->rc_rgba, bytes, hipMemcpyDeviceToHost, e->stream));
+    if (normal) HIP_OK(hipMemcpyAsync(normal, e->rc_norm, bytes, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+  }
+  return TSDF_OK;
+}
+
+int tsdf_query(tsdf_engine* e, const float* bounds, tsdf_voxel* out, int64_t capacity,
+               int64_t* count) {
+  if (!e || !count) return TSDF_ERR_INVALID_ARG;
+  HIP_OK(hipSetDevice(e->device));
+  short4 lo = make_short4(0, 0, 0, 0), hi = make_short4(0, 0, 0, 0);
+  if (bounds) {  // BoundingCube::Scale<short>(1. / voxel_size_) (voxel_tsdf.cuh:21-26, :429)
+    const float scale = (float)(1. / (double)e->cfg.voxel_size);
+    lo = make_short4(h_f2s(bounds[0] * scale), h_f2s(bounds[2] * scale), h_f2s(bounds[4] * scale), 0);
+    hi = make_short4(h_f2s(bounds[1] * scale), h_f2s(bounds[3] * scale), h_f2s(bounds[5] * scale), 0);
+  }
+  hipStream_t s = e->stream;
+  hipLaunchKernelGGL(k_query_count, dim3(kOccWords / 256), dim3(256), 0, s, e->D, bounds ? 1 : 0,
+                     lo, hi);
+  hipLaunchKernelGGL(k_vis_emit, dim3(kOccWords / 256), dim3(256), 0, s, e->D, e->q_sel,
+                     e->q_count);
+  LAUNCH_OK("query select");
+  int32_t nsel = 0;
+  HIP_OK(hipMemcpyAsync(&nsel, e->q_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  const int64_t nvox = (int64_t)nsel * kBlockVolume;
+  *count = nvox;
+  if (!out) return TSDF_OK;
+  if (capacity < nvox) {
+    set_error("tsdf_query: capacity too small");
+    return TSDF_ERR_CAPACITY;
+  }
+  if (nsel == 0) return TSDF_OK;
+  if (e->q_out_cap < nvox) {
+    if (e->q_out) (void)hipFree(e->q_out);
+    e->q_out = nullptr;
+    HIP_OK(dmalloc(&e->q_out, (size_t)nvox));
+    e->q_out_cap = nvox;
+  }
+  hipLaunchKernelGGL(k_query_download, dim3(nsel), dim3(kBlockVolume), 0, s, e->D, e->q_sel,
+                     e->cfg.voxel_size, e->q_out);
+  LAUNCH_OK("k_query_download");
+  HIP_OK(hipMemcpyAsync(out, e->q_out, (size_t)nvox * sizeof(float4), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return TSDF_OK;
+}
+
+int tsdf_get_stats(tsdf_engine* e, tsdf_stats* o, int clear_status) {
+  if (!e || !o) return TSDF_ERR_INVALID_ARG;
+  HIP_OK(hipSetDevice(e->device));
+  int rc = read_counters(e);
+  if (rc) return rc;
+  const DevCounters& c = *e->h_ctr;
+  std::memset(o, 0, sizeof(*o));
+  o->frames = (int64_t)c.frames;
+  o->free_blocks = c.free_count;
+  o->active_blocks = e->D.nblocks - c.free_count;
+  o->last_num_visible = c.n_vis;
+  o->last_num_alloc = c.last_alloc;
+  o->last_num_deleted = c.last_deleted;
+  o->last_num_new_keys = c.last_new_keys;
+  o->last_num_updated = (int64_t)c.last_updated;
+  o->total_visible = (int64_t)c.total_visible;
+  o->total_updated = (int64_t)c.total_updated;
+  o->total_alloc = (int64_t)c.total_alloc;
+  o->total_deleted = (int64_t)c.total_deleted;
+  o->status = c.status;
+  if (clear_status && c.status) {
+    HIP_OK(hipMemsetAsync(&e->D.ctr->status, 0, sizeof(uint32_t), e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+  }
+  return TSDF_OK;
+}
+
+int tsdf_profile_begin(tsdf_engine* e) {
+  if (!e) return TSDF_ERR_INVALID_ARG;
+  int rc = read_counters(e);
+  if (rc) return rc;
+  e->prof_vis0 = e->h_ctr->total_visible;
+  e->prof_upd0 = e->h_ctr->total_updated;
+  e->ev_used = 0;
+  e->profiling = true;
+  return TSDF_OK;
+}
+
+int tsdf_profile_end(tsdf_engine* e, tsdf_profile* o) {
+  if (!e || !o) return TSDF_ERR_INVALID_ARG;
+  e->profiling = false;
+  int rc = read_counters(e);
+  if (rc) return rc;
+  std::memset(o, 0, sizeof(*o));
+  o->frames = (int64_t)e->ev_used;
+  for (size_t i = 0; i < e->ev_used; ++i) {
+    float ms[4];
+    for (int k = 0; k < 4; ++k)
+      HIP_OK(hipEventElapsedTime(&ms[k], e->events[i][k], e->events[i][k + 1]));
+    o->ms_allocate += ms[0];
+    o->ms_visible += ms[1];
+    o->ms_integrate += ms[2];
+    o->ms_carve += ms[3];
+  }
+  o->sum_visible = (int64_t)(e->h_ctr->total_visible - e->prof_vis0);
+  o->sum_updated = (int64_t)(e->h_ctr->total_updated - e->prof_upd0);
+  return TSDF_OK;
+}
+
+int tsdf_debug_dump(tsdf_engine* e, int16_t* pos_off, int32_t* idx, int32_t* heap,
+                    int32_t* free_count, float* tsdf_out, float* prob, uint8_t* rgbw) {
+  if (!e) return TSDF_ERR_INVALID_ARG;
+  HIP_OK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  if (pos_off || idx) {
+    short4* dpos = nullptr;
+    int32_t* didx = nullptr;
+    HIP_OK(dmalloc(&dpos, kNumEntry));
+    HIP_OK(dmalloc(&didx, kNumEntry));
+    hipLaunchKernelGGL(k_dump_table, dim3(kNumEntry / 256), dim3(256), 0, s, e->D, dpos, didx);
+    hipError_t err = hipGetLastError();
+    if (err == hipSuccess && pos_off)
+      err = hipMemcpyAsync(pos_off, dpos, sizeof(short4) * kNumEntry, hipMemcpyDeviceToHost, s);
+    if (err == hipSuccess && idx)
+      err = hipMemcpyAsync(idx, didx, sizeof(int32_t) * kNumEntry, hipMemcpyDeviceToHost, s);
+    if (err == hipSuccess) err = hipStreamSynchronize(s);
+    (void)hipFree(dpos);
+    (void)hipFree(didx);
+    if (err != hipSuccess) {
+      set_error("tsdf_debug_dump table", err);
+      return TSDF_ERR_HIP;
+    }
+  }
+  if (heap)
+    HIP_OK(hipMemcpyAsync(heap, e->D.heap, sizeof(int32_t) * e->D.nblocks, hipMemcpyDeviceToHost, s));
+  if (free_count) {
+    int rc = read_counters(e);
+    if (rc) return rc;
+    *free_count = e->h_ctr->free_count;
+  }
+  if (tsdf_out || prob || rgbw) {
+    const size_t nv = (size_t)e->D.nblocks * kBlockVolume;
+    float* dt = nullptr;
+    float* dp = nullptr;
+    uint32_t* dc = nullptr;
+    HIP_OK(dmalloc(&dt, nv));
+    HIP_OK(dmalloc(&dp, nv));
+    HIP_OK(dmalloc(&dc, nv));
+    hipLaunchKernelGGL(k_dump_pool, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s, e->D, dt,
+                       dp, dc);
+    hipError_t err = hipGetLastError();
+    if (err == hipSuccess && tsdf_out) err = hipMemcpyAsync(tsdf_out, dt, nv * 4, hipMemcpyDeviceToHost, s);
+    if (err == hipSuccess && prob) err = hipMemcpyAsync(prob, dp, nv * 4, hipMemcpyDeviceToHost, s);
+    if (err == hipSuccess && rgbw) err = hipMemcpyAsync(rgbw, dc, nv * 4, hipMemcpyDeviceToHost, s);
+    if (err == hipSuccess) err = hipStreamSynchronize(s);
+    (void)hipFree(dt);
+    (void)hipFree(dp);
+    (void)hipFree(dc);
+    if (err != hipSuccess) {
+      set_error("tsdf_debug_dump pool", err);
+      return TSDF_ERR_HIP;
+    }
+  }
+  HIP_OK(hipStreamSynchronize(s));
+  return TSDF_OK;
+}
+
+int tsdf_hash_allocate(tsdf_engine* e, const int16_t* keys, int n) {
+  if (!e || n < 0 || (n > 0 && !keys) || n > (int)kNewKeyCap || (int64_t)n > e->obits_bits)
+    return TSDF_ERR_INVALID_ARG;
+  if (n == 0) return TSDF_OK;
+  HIP_OK(hipSetDevice(e->device));
+  int rc = ensure_test_cap(e, n);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(e->t_keys, keys, sizeof(int16_t) * 3 * n, hipMemcpyHostToDevice, e->stream));
+  hipLaunchKernelGGL(k_keys_to_newset, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->D,
+                     e->t_keys, n);
+  LAUNCH_OK("k_keys_to_newset");
+  rc = launch_allocate_tail(e, n, 0);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return TSDF_OK;
+}
+
+int tsdf_hash_delete(tsdf_engine* e, const int16_t* keys, int n) {
+  if (!e || n < 0 || (n > 0 && !keys)) return TSDF_ERR_INVALID_ARG;
+  if (n == 0) return TSDF_OK;
+  HIP_OK(hipSetDevice(e->device));
+  int rc = ensure_test_cap(e, n);
+  if (rc) return rc;
+  std::vector<VisRec> recs(n);
+  for (int i = 0; i < n; ++i) {
+    recs[i].x = keys[3 * i];
+    recs[i].y = keys[3 * i + 1];
+    recs[i].z = keys[3 * i + 2];
+    recs[i].pad = 0;
+    recs[i].idx = -1;
+    recs[i].entry = -1;
+  }
+  HIP_OK(hipMemcpyAsync(e->t_recs, recs.data(), sizeof(VisRec) * n, hipMemcpyHostToDevice, e->stream));
+  HIP_OK(hipMemcpyAsync(e->t_count, &n, sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
+  hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kResolveThreads), 0, e->stream, e->D,
+                     (const int32_t*)nullptr, e->t_count, e->t_recs, 1, 0);
+  LAUNCH_OK("k_resolve_delete");
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return TSDF_OK;
+}
+
+int tsdf_hash_retrieve(tsdf_engine* e, const int16_t* pts, int n, uint8_t* rgbw, float* tsdf_out,
+                       float* prob, int16_t* bpo, int32_t* bidx) {
+  if (!e || n < 0 || (n > 0 && !pts)) return TSDF_ERR_INVALID_ARG;
+  if (n == 0) return TSDF_OK;
+  HIP_OK(hipSetDevice(e->device));
+  int rc = ensure_test_cap(e, n);
+  if (rc) return rc;
+  hipStream_t s = e->stream;
+  HIP_OK(hipMemcpyAsync(e->t_keys, pts, sizeof(int16_t) * 3 * n, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_hash_retrieve, dim3((n + 255) / 256), dim3(256), 0, s, e->D, e->t_keys, n,
+                     e->t_u32, e->t_f0, e->t_f1, e->t_s4, e->t_i32);
+  LAUNCH_OK("k_hash_retrieve");
+  if (rgbw) HIP_OK(hipMemcpyAsync(rgbw, e->t_u32, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
+  if (tsdf_out) HIP_OK(hipMemcpyAsync(tsdf_out, e->t_f0, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
+  if (prob) HIP_OK(hipMemcpyAsync(prob, e->t_f1, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
+  if (bpo) HIP_OK(hipMemcpyAsync(bpo, e->t_s4, 8 * (size_t)n, hipMemcpyDeviceToHost, s));
+  if (bidx) HIP_OK(hipMemcpyAsync(bidx, e->t_i32, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return TSDF_OK;
+}
+
+int tsdf_hash_assign(tsdf_engine* e, const int16_t* pts, int n, const uint8_t* rgbw, int* missing) {
+  if (!e || n < 0 || (n > 0 && (!pts || !rgbw))) return TSDF_ERR_INVALID_ARG;
+  if (missing) *missing = 0;
+  if (n == 0) return TSDF_OK;
+  HIP_OK(hipSetDevice(e->device));
+  int rc = ensure_test_cap(e, n);
+  if (rc) return rc;
+  hipStream_t s = e->stream;
+  HIP_OK(hipMemcpyAsync(e->t_keys, pts, sizeof(int16_t) * 3 * n, hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync(e->t_u32, rgbw, 4 * (size_t)n, hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemsetAsync(e->t_count, 0, sizeof(int32_t), s));
+  hipLaunchKernelGGL(k_hash_assign, dim3((n + 255) / 256), dim3(256), 0, s, e->D, e->t_keys, n,
+                     e->t_u32, e->t_count);
+  LAUNCH_OK("k_hash_assign");
+  int m = 0;
+  HIP_OK(hipMemcpyAsync(&m, e->t_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  if (missing) *missing = m;
+  return TSDF_OK;
+}
+
+int tsdf_num_active_blocks(tsdf_engine* e, int32_t* out) {
+  if (!e || !out) return TSDF_ERR_INVALID_ARG;
+  int rc = read_counters(e);
+  if (rc) return rc;
+  *out = e->D.nblocks - e->h_ctr->free_count;
+  return TSDF_OK;
+}
+
+int tsdf_pool_acquire(tsdf_engine* e, int n, int32_t* idx_out) {
+  if (!e || n < 0 || (n > 0 && !idx_out)) return TSDF_ERR_INVALID_ARG;
+  if (n == 0) return TSDF_OK;
+  int rc = ensure_test_cap(e, n);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_pool_acquire, dim3(1), dim3(64), 0, e->stream, e->D, n, e->t_i32);
+  LAUNCH_OK("k_pool_acquire");
+  HIP_OK(hipMemcpyAsync(idx_out, e->t_i32, 4 * (size_t)n, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return TSDF_OK;
+}
+
+int tsdf_pool_release(tsdf_engine* e, const int32_t* idx, int n) {
+  if (!e || n < 0 || (n > 0 && !idx)) return TSDF_ERR_INVALID_ARG;
+  if (n == 0) return TSDF_OK;
+  int rc = ensure_test_cap(e, n);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(e->t_i32, idx, 4 * (size_t)n, hipMemcpyHostToDevice, e->stream));
+  hipLaunchKernelGGL(k_pool_release, dim3(1), dim3(64), 0, e->stream, e->D, e->t_i32, n);
+  LAUNCH_OK("k_pool_release");
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return TSDF_OK;
+}
+
+int tsdf_pool_set_weight(tsdf_engine* e, int32_t block, uint8_t w) {
+  if (!e || block < 0 || block >= e->D.nblocks) return TSDF_ERR_INVALID_ARG;
+  hipLaunchKernelGGL(k_pool_weight, dim3(1), dim3(kBlockVolume), 0, e->stream, e->D, block, 1, w,
+                     (uint8_t*)nullptr);
+  LAUNCH_OK("k_pool_weight");
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return TSDF_OK;
+}
+
+int tsdf_pool_get_weights(tsdf_engine* e, int32_t block, uint8_t* out) {
+  if (!e || !out || block < 0 || block >= e->D.nblocks) return TSDF_ERR_INVALID_ARG;
+  int rc = ensure_test_cap(e, kBlockVolume);
+  if (rc) return rc;
+  uint8_t* d = reinterpret_cast<uint8_t*>(e->t_u32);
+  hipLaunchKernelGGL(k_pool_weight, dim3(1), dim3(kBlockVolume), 0, e->stream, e->D, block, 0,
+                     (uint8_t)0, d);
+  LAUNCH_OK("k_pool_weight");
+  HIP_OK(hipMemcpyAsync(out, d, kBlockVolume, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return TSDF_OK;
+}
+
+}  // extern "C"

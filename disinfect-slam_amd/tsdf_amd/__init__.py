@@ -1,0 +1,369 @@
+"""tsdf_amd -- Python host mirror of the reference TSDF interface over the MI355X C ABI.
+
+Reference interface mirrored (yuzhou42/disinfect-slam):
+  * TSDFGrid            utils/tsdf/voxel_tsdf.cuh:32-124  (Integrate / RayCast / GatherValid /
+                        GatherVoxels) -- here `TSDFGrid`, same argument meaning and order;
+  * CameraIntrinsics    utils/cuda/camera.cuh:12-51, CameraParams :53-68
+  * SE3                 utils/cuda/lie_group.cuh:6-45
+  * BoundingCube        utils/tsdf/voxel_tsdf.cuh:12-27
+  * VoxelSpatialTSDF    utils/tsdf/voxel_types.cuh:48-57 (numpy structured dtype VOXEL_DTYPE)
+The C++17 facade (TSDFSystem / TSDFGrid / DISINFSystem TSDF methods) lives in ../host/.
+Frames may be numpy arrays (host, copied by the engine) or torch CUDA tensors (device, no copy).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+
+import numpy as np
+
+from . import _lib
+from ._lib import (STATUS_DDA_OVERFLOW, STATUS_NEWKEY_OVERFLOW, STATUS_POOL_EXHAUSTED,
+                   TSDF_MEM_DEVICE, TSDF_MEM_HOST, TSDFError)
+
+NUM_ENTRY = 1 << 22
+NUM_BUCKET = 1 << 21
+BLOCK_LEN = 8
+BLOCK_VOLUME = 512
+VOXEL_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("tsdf", "<f4")])
+
+__all__ = [
+    "CameraIntrinsics", "CameraParams", "SE3", "BoundingCube", "TSDFGrid", "Engine",
+    "VOXEL_DTYPE", "TSDFError", "hash_block", "block_owner", "load_library",
+]
+
+
+def load_library():
+    return _lib.load()
+
+
+def hash_block(x: int, y: int, z: int) -> int:
+    """voxel_hash.cu:31-35 Hash."""
+    return int(_lib.load().tsdf_hash_block(x, y, z))
+
+
+def block_owner(x: int, y: int, z: int, shard_count: int) -> int:
+    return int(_lib.load().tsdf_block_owner(x, y, z, shard_count))
+
+
+@dataclasses.dataclass(frozen=True)
+class CameraIntrinsics:
+    """camera.cuh:12-51 CameraIntrinsics<float>."""
+    fx: float
+    fy: float
+    cx: float
+    cy: float
+
+    def Inverse(self) -> "CameraIntrinsics":
+        f32 = np.float32
+        fx_inv = f32(1) / f32(self.fx)
+        fy_inv = f32(1) / f32(self.fy)
+        return CameraIntrinsics(float(fx_inv), float(fy_inv), float(-f32(self.cx) * fx_inv),
+                                float(-f32(self.cy) * fy_inv))
+
+    def _c(self) -> _lib.Intrinsics:
+        return _lib.Intrinsics(self.fx, self.fy, self.cx, self.cy)
+
+
+@dataclasses.dataclass(frozen=True)
+class CameraParams:
+    """camera.cuh:53-68 CameraParams(intrinsics, img_h, img_w)."""
+    intrinsics: CameraIntrinsics
+    img_h: int
+    img_w: int
+
+
+def _qmul_sse(a, b):
+    """Eigen quat_product<SSE, float> (host Eigen, Geometry/arch/Geometry_SSE.h)."""
+    f32 = np.float32
+    a0, a1, a2, a3 = (f32(v) for v in a)
+    b0, b1, b2, b3 = (f32(v) for v in b)
+    x = (a0 * b3 - a2 * b1) + (a1 * b2 + a3 * b0)
+    y = (a1 * b3 - a0 * b2) + (a2 * b0 + a3 * b1)
+    z = (a2 * b3 - a1 * b0) + (a0 * b1 + a3 * b2)
+    w = (a3 * b3 - a0 * b0) - (a2 * b2 + a1 * b1)
+    return np.array([x, y, z, w], np.float32)
+
+
+def _qrot(q, v):
+    """Eigen QuaternionBase::_transformVector."""
+    f32 = np.float32
+    qx, qy, qz, qw = (f32(c) for c in q)
+    vx, vy, vz = (f32(c) for c in v)
+    ux = qy * vz - qz * vy
+    uy = qz * vx - qx * vz
+    uz = qx * vy - qy * vx
+    ux, uy, uz = ux + ux, uy + uy, uz + uz
+    cx = qy * uz - qz * uy
+    cy = qz * ux - qx * uz
+    cz = qx * uy - qy * ux
+    return np.array([(vx + qw * ux) + cx, (vy + qw * uy) + cy, (vz + qw * uz) + cz], np.float32)
+
+
+class SE3:
+    """lie_group.cuh:6-45 SE3<float>: rotation quaternion (x, y, z, w) + translation."""
+
+    def __init__(self, q_xyzw=(0.0, 0.0, 0.0, 1.0), t=(0.0, 0.0, 0.0)):
+        self.q = np.asarray(q_xyzw, dtype=np.float32).reshape(4).copy()
+        self.t = np.asarray(t, dtype=np.float32).reshape(3).copy()
+
+    @staticmethod
+    def Identity() -> "SE3":
+        return SE3()
+
+    def GetR(self):
+        return self.q.copy()
+
+    def GetT(self):
+        return self.t.copy()
+
+    def Inverse(self) -> "SE3":
+        f32 = np.float32
+        x, y, z, w = (f32(c) for c in self.q)
+        n2 = (x * x + z * z) + (y * y + w * w)
+        qi = np.array([-x / n2, -y / n2, -z / n2, w / n2], np.float32) if n2 > 0 else np.zeros(4, np.float32)
+        return SE3(qi, _qrot(qi, -self.t))
+
+    def Apply(self, v):
+        return (_qrot(self.q, v) + self.t).astype(np.float32)
+
+    def __mul__(self, other: "SE3") -> "SE3":
+        return SE3(_qmul_sse(self.q, other.q), _qrot(self.q, other.t) + self.t)
+
+    def _c(self) -> _lib.Pose:
+        return _lib.Pose(*[float(v) for v in self.q], *[float(v) for v in self.t])
+
+
+@dataclasses.dataclass(frozen=True)
+class BoundingCube:
+    """voxel_tsdf.cuh:12-27 BoundingCube<float>."""
+    xmin: float
+    xmax: float
+    ymin: float
+    ymax: float
+    zmin: float
+    zmax: float
+
+    def as_array(self):
+        return np.array([self.xmin, self.xmax, self.ymin, self.ymax, self.zmin, self.zmax], np.float32)
+
+
+def _is_torch_cuda(x) -> bool:
+    return hasattr(x, "data_ptr") and hasattr(x, "is_cuda") and bool(x.is_cuda)
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if _is_torch_cuda(x):
+        return C.c_void_p(x.data_ptr())
+    return x.ctypes.data_as(C.c_void_p)
+
+
+def _np(a, dtype):
+    return None if a is None else np.ascontiguousarray(a, dtype=dtype)
+
+
+class Engine:
+    """One MI355X TSDF volume (one GPU shard). Thin owner of a tsdf_engine* handle."""
+
+    def __init__(self, voxel_size=0.005, truncation=0.03, max_width=1920, max_height=1080,
+                 num_block_bits=18, device=0, shard_index=0, shard_count=1, stream=None):
+        L = _lib.load()
+        cfg = _lib.Config()
+        L.tsdf_config_default(C.byref(cfg))
+        cfg.voxel_size = voxel_size
+        cfg.truncation = truncation
+        cfg.max_width = max_width
+        cfg.max_height = max_height
+        cfg.num_block_bits = num_block_bits
+        cfg.shard_index = shard_index
+        cfg.shard_count = shard_count
+        cfg.stream = stream
+        h = C.c_void_p()
+        _lib.check(L.tsdf_create(C.byref(cfg), device, C.byref(h)), "tsdf_create")
+        self._h = h
+        self.voxel_size = voxel_size
+        self.truncation = truncation
+        self.num_blocks = int(L.tsdf_num_blocks(h))
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().tsdf_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- hot path ----
+    def integrate(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float):
+        dev = _is_torch_cuda(depth)
+        if dev:
+            H, W = int(depth.shape[0]), int(depth.shape[1])
+            for a in (rgb, depth, ht, lt):
+                if a is not None and not a.is_contiguous():
+                    raise ValueError("device frames must be contiguous")
+        else:
+            rgb = _np(rgb, np.uint8)
+            depth = _np(depth, np.float32)
+            ht = _np(ht, np.float32)
+            lt = _np(lt, np.float32)
+            H, W = depth.shape
+        if tuple(rgb.shape[:2]) != (H, W):
+            raise ValueError("rgb / depth size mismatch (voxel_tsdf.cu:352-353)")
+        fr = _lib.Frame(W, H, _ptr(rgb), _ptr(depth), _ptr(ht), _ptr(lt),
+                        TSDF_MEM_DEVICE if dev else TSDF_MEM_HOST)
+        Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        _lib.check(_lib.load().tsdf_integrate(self._h, C.byref(fr), C.byref(Kc),
+                                              C.byref(cam_T_world._c()), max_depth),
+                   "tsdf_integrate")
+
+    def synchronize(self):
+        _lib.check(_lib.load().tsdf_synchronize(self._h), "tsdf_synchronize")
+
+    # ---- extraction ----
+    def raycast(self, K, width, height, cam_T_world: SE3, max_depth: float, rgba=None, normal=None):
+        Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        if rgba is not None and _is_torch_cuda(rgba):
+            _lib.check(_lib.load().tsdf_raycast(self._h, C.byref(Kc), width, height,
+                                                C.byref(cam_T_world._c()), max_depth, _ptr(rgba),
+                                                _ptr(normal), TSDF_MEM_DEVICE), "tsdf_raycast")
+            return rgba, normal
+        rgba = np.zeros((height, width, 4), np.uint8)
+        normal = np.zeros((height, width, 4), np.uint8)
+        _lib.check(_lib.load().tsdf_raycast(self._h, C.byref(Kc), width, height,
+                                            C.byref(cam_T_world._c()), max_depth, _ptr(rgba),
+                                            _ptr(normal), TSDF_MEM_HOST), "tsdf_raycast")
+        return rgba, normal
+
+    def query(self, bounds=None) -> np.ndarray:
+        L = _lib.load()
+        b = None if bounds is None else np.ascontiguousarray(
+            bounds.as_array() if isinstance(bounds, BoundingCube) else bounds, dtype=np.float32)
+        n = C.c_int64()
+        _lib.check(L.tsdf_query(self._h, _ptr(b), None, 0, C.byref(n)), "tsdf_query")
+        out = np.zeros(n.value, VOXEL_DTYPE)
+        if n.value:
+            _lib.check(L.tsdf_query(self._h, _ptr(b), out.ctypes.data_as(C.c_void_p), n.value,
+                                    C.byref(n)), "tsdf_query")
+        return out
+
+    def stats(self, clear_status=False) -> dict:
+        s = _lib.Stats()
+        _lib.check(_lib.load().tsdf_get_stats(self._h, C.byref(s), int(clear_status)), "tsdf_get_stats")
+        return {k: getattr(s, k) for k, _ in _lib.Stats._fields_}
+
+    def profile_begin(self):
+        _lib.check(_lib.load().tsdf_profile_begin(self._h), "tsdf_profile_begin")
+
+    def profile_end(self) -> dict:
+        p = _lib.Profile()
+        _lib.check(_lib.load().tsdf_profile_end(self._h, C.byref(p)), "tsdf_profile_end")
+        return {k: getattr(p, k) for k, _ in _lib.Profile._fields_}
+
+    def dump(self, pool: bool = True) -> dict:
+        pos = np.zeros((NUM_ENTRY, 4), np.int16)
+        idx = np.zeros(NUM_ENTRY, np.int32)
+        heap = np.zeros(self.num_blocks, np.int32)
+        free = np.zeros(1, np.int32)
+        out = dict(entry_pos=pos, entry_idx=idx, heap=heap)
+        tsdf = prob = rgbw = None
+        if pool:
+            nv = self.num_blocks * BLOCK_VOLUME
+            tsdf = np.zeros(nv, np.float32)
+            prob = np.zeros(nv, np.float32)
+            rgbw = np.zeros((nv, 4), np.uint8)
+            out.update(tsdf=tsdf, prob=prob, rgbw=rgbw)
+        _lib.check(_lib.load().tsdf_debug_dump(self._h, _ptr(pos), _ptr(idx), _ptr(heap), _ptr(free),
+                                               _ptr(tsdf), _ptr(prob), _ptr(rgbw)), "tsdf_debug_dump")
+        out["free"] = int(free[0])
+        return out
+
+    # ---- VoxelHashTable / VoxelMemPool level ----
+    def hash_allocate(self, keys):
+        k = np.ascontiguousarray(keys, dtype=np.int16).reshape(-1, 3)
+        _lib.check(_lib.load().tsdf_hash_allocate(self._h, _ptr(k), k.shape[0]), "tsdf_hash_allocate")
+
+    def hash_delete(self, keys):
+        k = np.ascontiguousarray(keys, dtype=np.int16).reshape(-1, 3)
+        _lib.check(_lib.load().tsdf_hash_delete(self._h, _ptr(k), k.shape[0]), "tsdf_hash_delete")
+
+    def hash_retrieve(self, points) -> dict:
+        p = np.ascontiguousarray(points, dtype=np.int16).reshape(-1, 3)
+        n = p.shape[0]
+        rgbw = np.zeros((n, 4), np.uint8)
+        tsdf = np.zeros(n, np.float32)
+        prob = np.zeros(n, np.float32)
+        bpo = np.zeros((n, 4), np.int16)
+        bidx = np.zeros(n, np.int32)
+        _lib.check(_lib.load().tsdf_hash_retrieve(self._h, _ptr(p), n, _ptr(rgbw), _ptr(tsdf),
+                                                  _ptr(prob), _ptr(bpo), _ptr(bidx)), "tsdf_hash_retrieve")
+        return dict(rgbw=rgbw, tsdf=tsdf, prob=prob, block_pos_off=bpo, block_idx=bidx)
+
+    def hash_assign(self, points, rgbw) -> int:
+        p = np.ascontiguousarray(points, dtype=np.int16).reshape(-1, 3)
+        v = np.ascontiguousarray(rgbw, dtype=np.uint8).reshape(-1, 4)
+        missing = C.c_int()
+        _lib.check(_lib.load().tsdf_hash_assign(self._h, _ptr(p), p.shape[0], _ptr(v),
+                                                C.byref(missing)), "tsdf_hash_assign")
+        return missing.value
+
+    def num_active_blocks(self) -> int:
+        n = C.c_int32()
+        _lib.check(_lib.load().tsdf_num_active_blocks(self._h, C.byref(n)), "tsdf_num_active_blocks")
+        return n.value
+
+    def pool_acquire(self, n: int) -> np.ndarray:
+        out = np.zeros(n, np.int32)
+        _lib.check(_lib.load().tsdf_pool_acquire(self._h, n, _ptr(out)), "tsdf_pool_acquire")
+        return out
+
+    def pool_release(self, idx):
+        i = np.ascontiguousarray(idx, dtype=np.int32)
+        _lib.check(_lib.load().tsdf_pool_release(self._h, _ptr(i), i.shape[0]), "tsdf_pool_release")
+
+    def pool_set_weight(self, block: int, w: int):
+        _lib.check(_lib.load().tsdf_pool_set_weight(self._h, int(block), int(w)), "tsdf_pool_set_weight")
+
+    def pool_get_weights(self, block: int) -> np.ndarray:
+        out = np.zeros(BLOCK_VOLUME, np.uint8)
+        _lib.check(_lib.load().tsdf_pool_get_weights(self._h, int(block), _ptr(out)), "tsdf_pool_get_weights")
+        return out
+
+
+class TSDFGrid:
+    """voxel_tsdf.cuh:32-124 TSDFGrid(voxel_size, truncation) on the MI355X engine."""
+
+    def __init__(self, voxel_size: float, truncation: float, **engine_kw):
+        self.engine = Engine(voxel_size=voxel_size, truncation=truncation, **engine_kw)
+
+    def Integrate(self, img_rgb, img_depth, img_ht, img_lt, max_depth: float,
+                  intrinsics: CameraIntrinsics, cam_T_world: SE3):
+        """voxel_tsdf.cu:347-375. img_ht / img_lt are required here as in the reference."""
+        self.engine.integrate(img_rgb, img_depth, img_ht, img_lt, intrinsics, cam_T_world, max_depth)
+
+    def RayCast(self, max_depth: float, virtual_cam: CameraParams, cam_T_world: SE3):
+        """voxel_tsdf.cu:490-506; returns (rgba, normal) HxWx4 uint8 images."""
+        return self.engine.raycast(virtual_cam.intrinsics, virtual_cam.img_w, virtual_cam.img_h,
+                                   cam_T_world, max_depth)
+
+    def GatherValid(self) -> np.ndarray:
+        """voxel_tsdf.cu:399-425."""
+        return self.engine.query(None)
+
+    def GatherVoxels(self, volumn: BoundingCube) -> np.ndarray:
+        """voxel_tsdf.cu:427-454."""
+        return self.engine.query(volumn)
+
+    def close(self):
+        self.engine.close()

@@ -1,0 +1,199 @@
+"""Synthetic RGB-D + high/low-touch frame source (SURVEY.md 8d / BASELINE.md 4).
+
+The reference benchmarks nothing and ships no recorded frames, so every measurement and parity
+run in this repo integrates a deterministic analytic scene:
+
+* scene: a closed 6 x 5 x 3 m room containing 3 axis-aligned boxes and 2 spheres;
+* trajectory: a smooth orbit, 1 cm of arc and 0.5 deg of yaw per frame (seed 0x5EED);
+* depth: analytic ray cast, + N(0, 1 mm) noise (seeded), quantised to uint16 / 5000 (TUM factor,
+  configs/TUM_RGBD_rgbd_1.yaml:44) and back to float32 metres, 2 % holes, readings beyond 3.9 m
+  dropped so that depth != max_depth (the reference's 0/0 case, voxel_tsdf.cu:182-191);
+* ht: a smooth per-surface field in [0.02, 0.98]; lt = 1 - ht (no log(0), voxel_tsdf.cu:196-202);
+* rgb: a deterministic per-surface checker pattern (uint8, RGB order as TSDFGrid expects).
+
+Frames are produced on the host with numpy (float64 geometry, one float32 rounding at the end), so
+the HIP engine and the CPU oracle integrate byte-identical inputs.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+import numpy as np
+
+SEED = 0x5EED
+
+# configs/TUM_RGBD_rgbd_1.yaml:11-14 (640x480)
+TUM_FR1 = (517.306408, 516.469215, 318.643040, 255.313989)
+# 2 x configs/zed_native_l515.yaml:27-30 (L515 full resolution 1280x720)
+L515_FULL = (913.7234, 913.54254, 644.2084, 375.5897)
+DEPTH_FACTOR = 5000.0
+MAX_RANGE = 3.9
+
+ROOM_MIN = np.array([0.0, 0.0, 0.0])
+ROOM_MAX = np.array([6.0, 5.0, 3.0])
+BOXES = [  # (min, max, surface id)
+    (np.array([0.6, 0.5, 0.0]), np.array([1.6, 1.3, 0.75]), 7),   # table
+    (np.array([4.3, 3.6, 0.0]), np.array([5.4, 4.6, 1.1]), 8),    # cabinet
+    (np.array([2.6, 4.2, 0.0]), np.array([3.4, 4.8, 1.8]), 9),    # shelf
+]
+SPHERES = [  # (centre, radius, surface id)
+    (np.array([4.6, 1.2, 0.9]), 0.45, 10),
+    (np.array([1.4, 3.7, 1.2]), 0.35, 11),
+]
+NUM_SURFACES = 12
+
+
+@dataclasses.dataclass
+class Camera:
+    width: int
+    height: int
+    fx: float
+    fy: float
+    cx: float
+    cy: float
+
+    @property
+    def K(self) -> np.ndarray:
+        return np.array([self.fx, self.fy, self.cx, self.cy], dtype=np.float32)
+
+
+def camera(width: int = 640, height: int = 480, intrinsics=TUM_FR1) -> Camera:
+    """Pinhole camera; intrinsics scaled with the image size relative to their native size."""
+    native_w = 640 if intrinsics is TUM_FR1 else 1280
+    s = width / native_w
+    fx, fy, cx, cy = intrinsics
+    return Camera(width, height, fx * s, fy * s, (cx + 0.5) * s - 0.5, (cy + 0.5) * s - 0.5)
+
+
+def _rot_to_quat_xyzw(R: np.ndarray) -> np.ndarray:
+    """Rotation matrix -> unit quaternion (x, y, z, w), float64 (Shoemake)."""
+    t = np.trace(R)
+    if t > 0:
+        s = math.sqrt(t + 1.0) * 2
+        w = 0.25 * s
+        x = (R[2, 1] - R[1, 2]) / s
+        y = (R[0, 2] - R[2, 0]) / s
+        z = (R[1, 0] - R[0, 1]) / s
+    else:
+        i = int(np.argmax(np.diag(R)))
+        j, k = (i + 1) % 3, (i + 2) % 3
+        s = math.sqrt(R[i, i] - R[j, j] - R[k, k] + 1.0) * 2
+        q = [0.0, 0.0, 0.0]
+        q[i] = 0.25 * s
+        w = (R[k, j] - R[j, k]) / s
+        q[j] = (R[j, i] + R[i, j]) / s
+        q[k] = (R[k, i] + R[i, k]) / s
+        x, y, z = q
+    q = np.array([x, y, z, w])
+    return q / np.linalg.norm(q)
+
+
+def pose(frame: int, orbit_centre=(3.0, 2.5, 1.45), pitch_deg: float = -12.0):
+    """world_T_cam of frame `frame`: camera on a circle of radius 1 cm / 0.5 deg, looking outward.
+
+    Returns (R_wc float64 3x3, p_wc float64 3) and (q_cw xyzw float32, t_cw float32), the latter
+    being the cam_T_world the engine API takes (voxel_tsdf.cuh:58-60).
+    """
+    dtheta = math.radians(0.5)
+    radius = 0.01 / dtheta
+    theta = frame * dtheta
+    c = np.asarray(orbit_centre, dtype=np.float64)
+    p = c + radius * np.array([math.cos(theta), math.sin(theta), 0.0])
+    p[2] += 0.05 * math.sin(frame * 0.02)
+    yaw = theta + math.radians(35.0)
+    fwd = np.array([math.cos(yaw), math.sin(yaw), 0.0])
+    pitch = math.radians(pitch_deg + 4.0 * math.sin(frame * 0.013))
+    fwd = math.cos(pitch) * fwd + math.sin(pitch) * np.array([0.0, 0.0, 1.0])
+    up = np.array([0.0, 0.0, 1.0])
+    right = np.cross(fwd, up)
+    right /= np.linalg.norm(right)
+    down = np.cross(fwd, right)
+    R_wc = np.stack([right, down, fwd], axis=1)  # columns: camera x (right), y (down), z (fwd)
+    R_cw = R_wc.T
+    t_cw = -R_cw @ p
+    q = _rot_to_quat_xyzw(R_cw).astype(np.float32)
+    return (R_wc, p), (q, t_cw.astype(np.float32))
+
+
+def _ray_scene(o: np.ndarray, d: np.ndarray):
+    """Nearest hit of rays o + s d (d: N x 3, unnormalised) with the scene. Returns (s, id, point)."""
+    n = d.shape[0]
+    inv = np.where(np.abs(d) > 1e-12, 1.0 / np.where(d == 0, 1.0, d), 1e12)
+    # room interior: exit distance
+    t_hi = np.maximum((ROOM_MIN - o) * inv, (ROOM_MAX - o) * inv)
+    s_room = np.min(t_hi, axis=1)
+    axis = np.argmin(t_hi, axis=1)
+    positive = d[np.arange(n), axis] > 0
+    sid = axis * 2 + positive.astype(np.int64)  # walls 0..5 (x-,x+,y-,y+,z- floor, z+ ceiling)
+    best = s_room.copy()
+    for bmin, bmax, ident in BOXES:
+        t0 = (bmin - o) * inv
+        t1 = (bmax - o) * inv
+        tn = np.max(np.minimum(t0, t1), axis=1)
+        tf = np.min(np.maximum(t0, t1), axis=1)
+        hit = (tn <= tf) & (tn > 1e-6) & (tn < best)
+        best = np.where(hit, tn, best)
+        sid = np.where(hit, ident, sid)
+    for cen, rad, ident in SPHERES:
+        oc = o - cen
+        a = np.einsum("ij,ij->i", d, d)
+        b = 2.0 * (d @ oc)
+        cc = oc @ oc - rad * rad
+        disc = b * b - 4 * a * cc
+        ok = disc >= 0
+        sq = np.sqrt(np.where(ok, disc, 0.0))
+        s0 = (-b - sq) / (2 * a)
+        hit = ok & (s0 > 1e-6) & (s0 < best)
+        best = np.where(hit, s0, best)
+        sid = np.where(hit, ident, sid)
+    pts = o + best[:, None] * d
+    return best, sid, pts
+
+
+_PALETTE = np.array(
+    [[200, 190, 170], [190, 180, 160], [170, 180, 200], [160, 170, 190], [120, 100, 80],
+     [230, 230, 230], [0, 0, 0], [150, 60, 40], [60, 120, 160], [90, 140, 70], [200, 60, 60],
+     [230, 190, 40]], dtype=np.float64)
+_TOUCH_BASE = np.array([0.05, 0.06, 0.04, 0.08, 0.15, 0.02, 0.0, 0.85, 0.6, 0.35, 0.9, 0.7])
+
+
+def render(cam: Camera, frame: int, noise: bool = True, holes: float = 0.02):
+    """Render frame `frame`: returns dict(rgb HxWx3 u8, depth HxW f32, ht, lt HxW f32, q, t)."""
+    (R_wc, p), (q, t) = pose(frame)
+    H, W = cam.height, cam.width
+    u, v = np.meshgrid(np.arange(W, dtype=np.float64), np.arange(H, dtype=np.float64))
+    dc = np.stack([(u - cam.cx) / cam.fx, (v - cam.cy) / cam.fy, np.ones_like(u)], axis=-1)
+    dw = dc.reshape(-1, 3) @ R_wc.T
+    o = np.broadcast_to(p, dw.shape)
+    s, sid, pts = _ray_scene(p, dw)  # s = depth along camera z because dc.z == 1
+    rng = np.random.Generator(np.random.PCG64(SEED + frame))
+    depth = s.copy()
+    if noise:
+        depth = depth + rng.normal(0.0, 0.001, size=depth.shape)
+    depth = np.round(depth * DEPTH_FACTOR).clip(0, 65535).astype(np.uint16)
+    depth = (depth.astype(np.float32) / np.float32(DEPTH_FACTOR)).astype(np.float32)
+    depth[depth > MAX_RANGE] = 0.0
+    if holes > 0:
+        depth[rng.random(depth.shape) < holes] = 0.0
+    # per-surface smooth touch field and checker colour
+    wave = np.sin(3.1 * pts[:, 0] + 1.7 * pts[:, 1]) * np.cos(2.3 * pts[:, 2] + 0.4 * pts[:, 0])
+    ht = np.clip(_TOUCH_BASE[sid] + 0.08 * wave, 0.02, 0.98).astype(np.float32)
+    lt = (np.float32(1.0) - ht).astype(np.float32)
+    chk = ((np.floor(pts[:, 0] / 0.2) + np.floor(pts[:, 1] / 0.2) + np.floor(pts[:, 2] / 0.2)) % 2)
+    shade = 0.75 + 0.25 * chk
+    rgb = np.clip(_PALETTE[sid] * shade[:, None] + 10 * wave[:, None], 0, 255).astype(np.uint8)
+    del o
+    return dict(
+        rgb=np.ascontiguousarray(rgb.reshape(H, W, 3)),
+        depth=np.ascontiguousarray(depth.reshape(H, W)),
+        ht=np.ascontiguousarray(ht.reshape(H, W)),
+        lt=np.ascontiguousarray(lt.reshape(H, W)),
+        q=q,
+        t=t,
+    )
+
+
+def frames(cam: Camera, start: int, count: int, **kw):
+    for f in range(start, start + count):
+        yield render(cam, f, **kw)

@@ -1,0 +1,172 @@
+/*
+ * disinfect_tsdf.h -- C ABI of the MI355X (gfx950) TSDF semantic-fusion engine.
+ *
+ * Drop-in boundary for the TSDF hot path of yuzhou42/disinfect-slam. The reference exposes this
+ * path as C++ classes (no FFI): TSDFGrid (utils/tsdf/voxel_tsdf.cuh:32-124), VoxelHashTable
+ * (utils/tsdf/voxel_hash.cuh:47-183), VoxelMemPool (utils/tsdf/voxel_mem.cuh:95-174) and the
+ * threaded TSDFSystem facade (modules/tsdf_module.h:35-107). Each entry point below names the
+ * reference interface it replaces. Plain pointers and sizes only: no HIP, torch or OpenCV types.
+ * The C++17 facade in disinfect-slam_amd/host/ rebuilds TSDFGrid / TSDFSystem on top of it.
+ *
+ * All calls return TSDF_OK (0) or a TSDF_ERR_* code; nothing throws across this boundary
+ * (the reference returns void and only printf's CUDA errors in Debug, utils/cuda/errors.cuh:9-29).
+ * An engine handle is not thread safe (TSDFGrid is not re-entrant either); TSDFSystem serialises.
+ */
+#ifndef DISINFECT_TSDF_H
+#define DISINFECT_TSDF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSDF_OK 0
+#define TSDF_ERR_INVALID_ARG 1
+#define TSDF_ERR_OUT_OF_MEMORY 2
+#define TSDF_ERR_HIP 3
+#define TSDF_ERR_CAPACITY 4 /* caller buffer too small (two-call pattern) */
+#define TSDF_ERR_NO_DEVICE 5
+
+#define TSDF_MEM_HOST 0   /* pointer is host memory: engine copies it (pageable is fine) */
+#define TSDF_MEM_DEVICE 1 /* pointer is device memory on the engine's GPU */
+
+/* status bits (tsdf_stats.status): sticky, cleared by tsdf_get_stats(..., clear=1) */
+#define TSDF_STATUS_POOL_EXHAUSTED 1u  /* an allocation found no free block (voxel_mem.cu:39) */
+#define TSDF_STATUS_NEWKEY_OVERFLOW 2u /* more new blocks in one frame than the key set holds */
+#define TSDF_STATUS_DDA_OVERFLOW 4u    /* a DDA ray took more samples than sized for */
+#define TSDF_STATUS_RESOLVE_ABORT 8u   /* allocation resolver made no progress (internal error) */
+
+typedef struct tsdf_engine tsdf_engine;
+
+typedef struct tsdf_config {
+  float voxel_size;   /* [m] TSDFGrid(voxel_size, truncation), voxel_tsdf.cuh:40 */
+  float truncation;   /* [m] */
+  int max_width;      /* largest integrate / raycast image; reference MAX_IMG_* = 1920x1080 */
+  int max_height;     /*   (voxel_tsdf.cu:10-12) */
+  int num_block_bits; /* voxel-block pool = 2^bits blocks; reference NUM_BLOCK_BITS 18 */
+  int shard_index;    /* spatial sharding: this engine owns blocks b with owner(b) == index */
+  int shard_count;    /*   owner(b) = hash(b >> 2) mod count; 1 = unsharded */
+  void* stream;       /* optional hipStream_t to run on; NULL = engine-owned stream */
+} tsdf_config;
+
+/* Fill reference defaults: 5 mm / 3 cm, 1920x1080, 2^18 blocks, unsharded. */
+void tsdf_config_default(tsdf_config* cfg);
+
+typedef struct tsdf_intrinsics { /* CameraIntrinsics<float> (utils/cuda/camera.cuh:12-51) */
+  float fx, fy, cx, cy;
+} tsdf_intrinsics;
+
+typedef struct tsdf_pose { /* SE3<float> cam_T_world (utils/cuda/lie_group.cuh:6-45) */
+  float qx, qy, qz, qw;    /* Eigen::Quaternionf coefficients (x, y, z, w) */
+  float tx, ty, tz;
+} tsdf_pose;
+
+typedef struct tsdf_frame { /* the four cv::Mat inputs of TSDFGrid::Integrate (voxel_tsdf.cuh:58) */
+  int width, height;
+  const uint8_t* rgb;  /* height x width x 3, RGB order (CV_8UC3) */
+  const float* depth;  /* height x width metres (CV_32FC1); 0 = invalid */
+  const float* ht;     /* height x width high-touch probability; NULL -> all ones */
+  const float* lt;     /* height x width low-touch probability;  NULL -> all ones */
+  int mem_kind;        /* TSDF_MEM_HOST or TSDF_MEM_DEVICE (all four pointers alike) */
+} tsdf_frame;
+
+typedef struct tsdf_voxel { /* VoxelSpatialTSDF (utils/tsdf/voxel_types.cuh:48-57), 16 B */
+  float x, y, z, tsdf;
+} tsdf_voxel;
+
+typedef struct tsdf_stats {
+  int64_t frames;            /* integrate calls so far */
+  int32_t active_blocks;     /* VoxelHashTable::NumActiveBlock (voxel_hash.cu:207) */
+  int32_t free_blocks;       /* VoxelMemPool::NumFreeBlocks (voxel_mem.cu:63-67) */
+  int32_t last_num_visible;  /* N_vis of the last integrate */
+  int32_t last_num_alloc;    /* blocks allocated by the last integrate */
+  int32_t last_num_deleted;  /* blocks removed by space carving in the last integrate */
+  int32_t last_num_new_keys; /* unique missing visible keys the last DDA produced */
+  int64_t last_num_updated;  /* voxels updated by the last integrate */
+  int64_t total_visible;     /* sum of N_vis over all integrate calls */
+  int64_t total_updated;     /* sum of updated voxels over all integrate calls */
+  int64_t total_alloc;
+  int64_t total_deleted;
+  uint32_t status;           /* TSDF_STATUS_* bits */
+  uint32_t reserved;
+} tsdf_stats;
+
+typedef struct tsdf_profile { /* device time of the integrate phases between begin/end */
+  int64_t frames;
+  double ms_allocate;  /* DDA + new-key ordering + allocation resolve + block init */
+  double ms_visible;   /* visibility compaction */
+  double ms_integrate; /* the fused TSDF/RGB/weight/semantic update kernel (+ carve minimum) */
+  double ms_carve;     /* space-carving compaction + delete resolve */
+  int64_t sum_visible; /* sum of N_vis over the profiled frames */
+  int64_t sum_updated; /* sum of updated voxels over the profiled frames */
+} tsdf_profile;
+
+/* ---- engine lifetime: TSDFGrid::TSDFGrid / ~TSDFGrid (voxel_tsdf.cu:309-345) ---- */
+int tsdf_create(const tsdf_config* cfg, int device, tsdf_engine** out);
+int tsdf_destroy(tsdf_engine* e);
+
+/* TSDFGrid::Integrate (voxel_tsdf.cu:347-375): allocate -> visibility -> update -> carve.
+ * Asynchronous on the engine stream when the frame is TSDF_MEM_DEVICE (inputs must stay valid
+ * until the next engine call or tsdf_synchronize); host frames are copied before returning. */
+int tsdf_integrate(tsdf_engine* e, const tsdf_frame* frame, const tsdf_intrinsics* K,
+                   const tsdf_pose* cam_T_world, float max_depth);
+
+/* TSDFGrid::RayCast (voxel_tsdf.cu:490-506; ray_cast_kernel :232-307). rgba / normal are
+ * height x width x 4 u8 (either may be NULL), host or device memory per mem_kind. */
+int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int width, int height,
+                 const tsdf_pose* cam_T_world, float max_depth, uint8_t* rgba, uint8_t* normal,
+                 int mem_kind);
+
+/* TSDFGrid::GatherVoxels (bounds = {xmin, xmax, ymin, ymax, zmin, zmax}, voxel_tsdf.cu:427-454)
+ * or GatherValid (bounds == NULL, :399-425). Two-call pattern: *count receives the number of
+ * voxels (blocks x 512, entry order then OffsetToIndex); out (host) is filled when non-NULL and
+ * capacity >= *count, else TSDF_ERR_CAPACITY. */
+int tsdf_query(tsdf_engine* e, const float* bounds, tsdf_voxel* out, int64_t capacity,
+               int64_t* count);
+
+int tsdf_get_stats(tsdf_engine* e, tsdf_stats* out, int clear_status);
+int tsdf_synchronize(tsdf_engine* e);
+int tsdf_profile_begin(tsdf_engine* e);
+int tsdf_profile_end(tsdf_engine* e, tsdf_profile* out);
+
+/* Test-only full state dump (Query exposes only tsdf): the 2^22-entry hash table as
+ * (x, y, z, offset) int16 quadruples + pool idx int32, the free-block heap, the free counter and
+ * the SoA voxel pools (tsdf f32, prob f32, rgbw u8x4 per voxel, pool-index major). Host buffers;
+ * any NULL pointer is skipped. */
+int tsdf_debug_dump(tsdf_engine* e, int16_t* entry_pos_off, int32_t* entry_idx, int32_t* heap,
+                    int32_t* free_count, float* tsdf, float* prob, uint8_t* rgbw);
+int32_t tsdf_num_entries(void);
+int32_t tsdf_num_blocks(const tsdf_engine* e);
+
+/* ---- VoxelHashTable / VoxelMemPool level (voxel_hash.cu, voxel_mem.cu), host arrays ---- */
+/* One launch of VoxelHashTable::Allocate over keys (xyz int16 triples) + ResetLocks. Keys are
+ * linearised in list order. */
+int tsdf_hash_allocate(tsdf_engine* e, const int16_t* keys, int n);
+/* One launch of VoxelHashTable::Delete over keys in list order + ResetLocks. */
+int tsdf_hash_delete(tsdf_engine* e, const int16_t* keys, int n);
+/* VoxelHashTable::Retrieve (voxel_hash.cuh:104-161) of voxel points: rgbw, tsdf, prob (defaults
+ * 0 / 1 / 0 when missing) and the block meta (x, y, z, offset; idx -1 if missing). */
+int tsdf_hash_retrieve(tsdf_engine* e, const int16_t* points, int n, uint8_t* rgbw, float* tsdf,
+                       float* prob, int16_t* block_pos_off, int32_t* block_idx);
+/* RetrieveMutable + store of rgbw (voxel_hash_test.cu:47-54); *missing = points not found. */
+int tsdf_hash_assign(tsdf_engine* e, const int16_t* points, int n, const uint8_t* rgbw,
+                     int* missing);
+int tsdf_num_active_blocks(tsdf_engine* e, int32_t* out);
+/* VoxelMemPool::AquireBlock / ReleaseBlock, n sequential calls (voxel_mem.cu:37-61). */
+int tsdf_pool_acquire(tsdf_engine* e, int n, int32_t* idx_out);
+int tsdf_pool_release(tsdf_engine* e, const int32_t* idx, int n);
+int tsdf_pool_set_weight(tsdf_engine* e, int32_t block, uint8_t weight);
+int tsdf_pool_get_weights(tsdf_engine* e, int32_t block, uint8_t* out512);
+
+/* Hash of a block coordinate (voxel_hash.cu:31-35) and the shard owner of a block. */
+uint32_t tsdf_hash_block(int16_t x, int16_t y, int16_t z);
+int32_t tsdf_block_owner(int16_t x, int16_t y, int16_t z, int32_t shard_count);
+
+const char* tsdf_error_string(int code);
+const char* tsdf_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DISINFECT_TSDF_H */

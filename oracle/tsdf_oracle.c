@@ -1,0 +1,740 @@
+/*
+ * tsdf_oracle.c -- CPU restatement of yuzhou42/disinfect-slam's CUDA TSDF engine.
+ *
+ * TEST INFRASTRUCTURE ONLY (parity checker + bench cpu_baseline). See tsdf_oracle.h for the
+ * pinning status. Every function cites the reference file:line it restates. Eigen 3.3 expression
+ * evaluation orders are reproduced explicitly:
+ *   - fixed-size 3-vector sum / dot / squaredNorm: a0 + (a1 + a2)  (redux_novec_unroller split)
+ *   - q * v  : uv = 2 (q.vec x v); v + w uv + q.vec x uv           (QuaternionBase::_transformVector)
+ *   - host q.inverse(): n2 = (x^2 + z^2) + (y^2 + w^2)               (SSE/NEON predux of a Vector4f)
+ * Compile with -ffp-contract=off so no multiply-add is fused.
+ */
+#include "tsdf_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---- constants: voxel_mem.cuh:10-20, voxel_hash.cuh:12-25 ---- */
+#define BLOCK_LEN_BITS 3
+#define BLOCK_LEN 8
+#define BLOCK_AREA 64
+#define BLOCK_VOLUME 512
+#define BLOCK_VOLUME_BITS 9
+#define NUM_BUCKET_BITS 21
+#define NUM_BUCKET (1 << NUM_BUCKET_BITS)
+#define BUCKET_MASK (NUM_BUCKET - 1)
+#define NUM_ENTRY_PER_BUCKET 2
+#define NUM_ENTRY (1 << (NUM_BUCKET_BITS + 1))
+#define ENTRY_MASK (NUM_ENTRY - 1)
+#define ENTRY_PER_BUCKET_MASK 1
+
+typedef struct { float x, y, z; } v3;
+typedef struct { float x, y, z, w; } quat;
+typedef struct { quat q; v3 t; } se3;
+typedef struct { float fx, fy, cx, cy; } intr;
+typedef struct { int16_t x, y, z; } s3;
+
+/* voxel_mem.cuh:73-93 VoxelBlock */
+typedef struct { s3 pos; int16_t offset; int32_t idx; } entry;
+
+struct ora_grid {
+  float voxel, trunc;
+  int nb_bits, nblocks;
+  entry* table;
+  uint8_t* locks;
+  int32_t* heap;
+  int32_t free_count;
+  float* tsdf;     /* voxels_tsdf_  */
+  float* prob;     /* voxels_segm_  */
+  uint8_t* rgbw;   /* voxels_rgbw_ (r,g,b,weight) */
+  float* range;    /* img_depth_to_range_ */
+  int range_cap;
+  int32_t* vis;    /* visible_blocks_ entry indices (entry order) */
+  ora_stats st;
+};
+
+/* ---------------- float math (utils/cuda/camera.cuh, lie_group.cuh, Eigen 3.3) ------------- */
+static v3 v3_cross(v3 a, v3 b) { /* Eigen MatrixBase::cross (OrthoMethods.h) */
+  v3 r;
+  r.x = a.y * b.z - a.z * b.y;
+  r.y = a.z * b.x - a.x * b.z;
+  r.z = a.x * b.y - a.y * b.x;
+  return r;
+}
+static float v3_dot(v3 a, v3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
+static float v3_norm(v3 a) { return sqrtf(v3_dot(a, a)); }
+
+/* Eigen QuaternionBase::_transformVector (used by lie_group.cuh:30 R_ * vec3) */
+static v3 qrot(quat q, v3 v) {
+  v3 qv = {q.x, q.y, q.z};
+  v3 uv = v3_cross(qv, v);
+  uv.x += uv.x; uv.y += uv.y; uv.z += uv.z;
+  v3 c = v3_cross(qv, uv);
+  v3 r;
+  r.x = (v.x + q.w * uv.x) + c.x;
+  r.y = (v.y + q.w * uv.y) + c.y;
+  r.z = (v.z + q.w * uv.z) + c.z;
+  return r;
+}
+/* lie_group.cuh:30-32 SE3::Apply = R * v + t */
+static v3 se3_apply(const se3* T, v3 v) {
+  v3 r = qrot(T->q, v);
+  r.x = r.x + T->t.x; r.y = r.y + T->t.y; r.z = r.z + T->t.z;
+  return r;
+}
+/* lie_group.cuh:22-24 SE3::Inverse = (R^-1, R^-1 * (-t)), evaluated on the host (voxel_tsdf.cu:382,497).
+ * Eigen QuaternionBase::inverse(): conj(q).coeffs() / squaredNorm(); host squaredNorm of the 4
+ * coefficients is a Packet4f reduction: (x*x + z*z) + (y*y + w*w). */
+static se3 se3_inverse(const se3* T) {
+  const quat q = T->q;
+  const float n2 = (q.x * q.x + q.z * q.z) + (q.y * q.y + q.w * q.w);
+  se3 r;
+  if (n2 > 0.0f) {
+    r.q.x = -q.x / n2; r.q.y = -q.y / n2; r.q.z = -q.z / n2; r.q.w = q.w / n2;
+  } else {
+    r.q.x = r.q.y = r.q.z = r.q.w = 0.0f;
+  }
+  v3 nt = {-T->t.x, -T->t.y, -T->t.z};
+  r.t = qrot(r.q, nt);
+  return r;
+}
+/* camera.cuh:34-39 CameraIntrinsics::Inverse */
+static intr intr_inverse(intr k) {
+  intr r;
+  r.fx = 1.0f / k.fx;
+  r.fy = 1.0f / k.fy;
+  r.cx = -k.cx * r.fx;
+  r.cy = -k.cy * r.fy;
+  return r;
+}
+/* camera.cuh:47-51 CameraIntrinsics::operator* */
+static v3 intr_mul(intr k, v3 v) {
+  v3 r;
+  r.x = k.fx * v.x + k.cx * v.z;
+  r.y = k.fy * v.y + k.cy * v.z;
+  r.z = v.z;
+  return r;
+}
+
+/* float -> integer conversions with GPU (cvt.rzi / v_cvt_i32_f32) semantics: truncate toward
+ * zero, saturate, NaN -> 0. Makes the oracle deterministic where C leaves it undefined. */
+static int32_t f2i(float f) {
+  if (f != f) return 0;
+  if (f >= 2147483648.0f) return INT32_MAX;
+  if (f <= -2147483648.0f) return INT32_MIN;
+  return (int32_t)f;
+}
+static int16_t f2s(float f) {
+  if (f != f) return 0;
+  if (f >= 32767.0f) return 32767;
+  if (f <= -32768.0f) return -32768;
+  return (int16_t)f;
+}
+static uint8_t f2u8(float f) {
+  if (!(f > 0.0f)) return 0; /* NaN and negatives */
+  if (f >= 255.0f) return 255;
+  return (uint8_t)f;
+}
+
+/* ---------------- hash table (voxel_hash.cu) ---------------- */
+uint32_t ora_hash(int16_t x, int16_t y, int16_t z) { /* voxel_hash.cu:31-35 */
+  return (((uint32_t)(int32_t)x * 73856093u) ^ ((uint32_t)(int32_t)y * 19349669u) ^
+          ((uint32_t)(int32_t)z * 83492791u)) & BUCKET_MASK;
+}
+static int s3_eq(s3 a, s3 b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
+static s3 point_to_block(s3 p) { /* voxel_mem.cuh:29-32 (arithmetic shift) */
+  s3 r = {(int16_t)(p.x >> BLOCK_LEN_BITS), (int16_t)(p.y >> BLOCK_LEN_BITS),
+          (int16_t)(p.z >> BLOCK_LEN_BITS)};
+  return r;
+}
+static s3 block_to_point(s3 b) { /* voxel_mem.cuh:41-44 */
+  s3 r = {(int16_t)(b.x << BLOCK_LEN_BITS), (int16_t)(b.y << BLOCK_LEN_BITS),
+          (int16_t)(b.z << BLOCK_LEN_BITS)};
+  return r;
+}
+static int offset_to_index(int ox, int oy, int oz) { return ox + oy * BLOCK_LEN + oz * BLOCK_AREA; }
+
+/* voxel_mem.cu:37-52 AquireBlock (weight 0, tsdf -1, prob 0.5; rgb left as is) */
+static int32_t pool_acquire(ora_grid* g) {
+  const int32_t i = g->free_count;
+  if (i < 1) return -1; /* reference: assert(idx >= 1), undefined in release; defined here as a
+                           refused acquisition that leaves the counter alone */
+  g->free_count = i - 1;
+  const int32_t idx = g->heap[i - 1];
+  const int64_t base = (int64_t)idx << BLOCK_VOLUME_BITS;
+  for (int v = 0; v < BLOCK_VOLUME; ++v) {
+    g->rgbw[(base + v) * 4 + 3] = 0;
+    g->tsdf[base + v] = -1.0f;
+    g->prob[base + v] = 0.5f;
+  }
+  return idx;
+}
+/* voxel_mem.cu:54-59 ReleaseBlock (no clearing) */
+static void pool_release(ora_grid* g, int32_t idx) {
+  const int32_t i = g->free_count;
+  g->free_count = i + 1;
+  g->heap[i] = idx;
+}
+
+/* voxel_hash.cu:58-120 VoxelHashTable::Allocate, executed as one step of a sequential launch. */
+static int hash_allocate(ora_grid* g, s3 key) {
+  const uint32_t bucket = ora_hash(key.x, key.y, key.z);
+  const uint32_t e0 = bucket << 1;
+  for (int i = 0; i < NUM_ENTRY_PER_BUCKET; ++i) { /* existence :62-68 */
+    const entry* b = &g->table[e0 + i];
+    if (s3_eq(b->pos, key) && b->idx >= 0) return 0;
+  }
+  uint32_t last = e0 + NUM_ENTRY_PER_BUCKET - 1; /* traverse list :70-77 */
+  while (g->table[last].offset) {
+    last = (uint32_t)(last + (int32_t)g->table[last].offset) & ENTRY_MASK;
+    const entry* b = &g->table[last];
+    if (s3_eq(b->pos, key) && b->idx >= 0) return 0;
+  }
+  for (int i = 0; i < NUM_ENTRY_PER_BUCKET; ++i) { /* current bucket :79-91 */
+    entry* b = &g->table[e0 + i];
+    if (b->idx < 0) {
+      if (g->locks[bucket] == 0) {
+        g->locks[bucket] = 1;
+        if (g->free_count < 1) return -2; /* pool exhausted: insert dropped, lock stays taken */
+        b->pos = key;
+        b->offset = 0;
+        b->idx = pool_acquire(g);
+        return 1;
+      }
+      return -1;
+    }
+  }
+  last = e0 + NUM_ENTRY_PER_BUCKET - 1; /* traverse list again :93-97 */
+  while (g->table[last].offset)
+    last = (uint32_t)(last + (int32_t)g->table[last].offset) & ENTRY_MASK;
+  const uint32_t bucket_last = last >> 1;
+  uint32_t next = last;
+  for (int probes = 0; probes < NUM_ENTRY; ++probes) { /* append :99-119 */
+    next = (next + 1) & ENTRY_MASK;
+    if ((next & ENTRY_PER_BUCKET_MASK) != ENTRY_PER_BUCKET_MASK && g->table[next].idx < 0) {
+      const uint32_t bucket_next = next >> 1;
+      int ok = 0;
+      if (g->locks[bucket_last] == 0) {          /* atomicExch(last) == FREE */
+        g->locks[bucket_last] = 1;
+        if (g->locks[bucket_next] == 0) {        /* && atomicExch(next) == FREE */
+          g->locks[bucket_next] = 1;
+          ok = 1;
+        }
+      }
+      if (ok && g->free_count < 1) return -2; /* pool exhausted (see pool_acquire) */
+      if (ok) {
+        entry* bl = &g->table[last];
+        entry* bn = &g->table[next];
+        const uint32_t wrap = next > last ? 0u : (uint32_t)NUM_ENTRY;
+        bl->offset = (int16_t)(next + wrap - last);
+        bn->pos = key;
+        bn->offset = 0;
+        bn->idx = pool_acquire(g);
+        return 1;
+      }
+      return -1;
+    }
+  }
+  return -1;
+}
+
+/* voxel_hash.cu:122-171 VoxelHashTable::Delete, one step of a sequential launch. */
+static int hash_delete(ora_grid* g, s3 key) {
+  const uint32_t bucket = ora_hash(key.x, key.y, key.z);
+  const uint32_t e0 = bucket << 1;
+  { /* slot 0, lock free :126-135 */
+    entry* b = &g->table[e0];
+    if (s3_eq(b->pos, key) && b->idx >= 0) {
+      pool_release(g, b->idx);
+      b->offset = 0;
+      b->idx = -1;
+      return 1;
+    }
+  }
+  uint32_t last = e0 + NUM_ENTRY_PER_BUCKET - 1;
+  entry* head = &g->table[last];
+  if (s3_eq(head->pos, key) && head->idx >= 0) { /* list head :137-152 */
+    if (g->locks[bucket] == 0) {
+      g->locks[bucket] = 1;
+      const uint32_t nidx = (uint32_t)(last + (int32_t)head->offset) & ENTRY_MASK;
+      entry* nx = &g->table[nidx];
+      pool_release(g, head->idx);
+      head->pos = nx->pos;
+      head->offset = nx->offset ? (int16_t)(head->offset + nx->offset) : 0;
+      head->idx = nx->idx;
+      nx->offset = 0;
+      nx->idx = -1;
+      return 1;
+    }
+    return -1;
+  }
+  while (g->table[last].offset) { /* generic list :154-170 */
+    entry* bl = &g->table[last];
+    const uint32_t cur = (uint32_t)(last + (int32_t)bl->offset) & ENTRY_MASK;
+    entry* bc = &g->table[cur];
+    if (s3_eq(bc->pos, key) && bc->idx >= 0) {
+      if (g->locks[bucket] == 0) {
+        g->locks[bucket] = 1;
+        bl->offset = bc->offset ? (int16_t)(bl->offset + bc->offset) : 0;
+        pool_release(g, bc->idx);
+        bc->offset = 0;
+        bc->idx = -1;
+        return 1;
+      }
+      return -1;
+    }
+    last = cur;
+  }
+  return 0;
+}
+
+/* voxel_hash.cuh:124-161 RetrieveMutable -> entry index or -1 (the 1-entry cache never changes
+ * results because the table is read-only during retrieval). */
+static int64_t hash_find(const ora_grid* g, s3 block) {
+  const uint32_t bucket = ora_hash(block.x, block.y, block.z);
+  const uint32_t e0 = bucket << 1;
+  for (int i = 0; i < NUM_ENTRY_PER_BUCKET; ++i) {
+    const entry* b = &g->table[e0 + i];
+    if (s3_eq(b->pos, block) && b->idx >= 0) return e0 + i;
+  }
+  uint32_t last = e0 + NUM_ENTRY_PER_BUCKET - 1;
+  while (g->table[last].offset) {
+    last = (uint32_t)(last + (int32_t)g->table[last].offset) & ENTRY_MASK;
+    const entry* b = &g->table[last];
+    if (s3_eq(b->pos, block) && b->idx >= 0) return last;
+  }
+  return -1;
+}
+static int64_t voxel_addr(const ora_grid* g, s3 point, int64_t* entry_out) {
+  const s3 block = point_to_block(point);
+  const int64_t e = hash_find(g, block);
+  if (entry_out) *entry_out = e;
+  if (e < 0) return -1;
+  const int off = offset_to_index(point.x & 7, point.y & 7, point.z & 7);
+  return ((int64_t)g->table[e].idx << BLOCK_VOLUME_BITS) + off;
+}
+/* Retrieve<VoxelTSDF> with default VoxelTSDF() = 1 (voxel_types.cu:9) */
+static float retrieve_tsdf(const ora_grid* g, s3 p) {
+  const int64_t a = voxel_addr(g, p, NULL);
+  return a < 0 ? 1.0f : g->tsdf[a];
+}
+
+/* ---------------- visibility (voxel_tsdf.cu:48-80) ---------------- */
+typedef struct {
+  intr K, Kinv;
+  int W, H;
+  se3 cTw, wTc;
+  float voxel, trunc, max_depth;
+} frame_params;
+
+static int voxel_visible(const frame_params* P, s3 pg) {
+  v3 pw = {(float)pg.x * P->voxel, (float)pg.y * P->voxel, (float)pg.z * P->voxel};
+  v3 pc = se3_apply(&P->cTw, pw);
+  v3 ph = intr_mul(P->K, pc);
+  const float u = ph.x / ph.z, v = ph.y / ph.z; /* hnormalized */
+  return u >= 0 && u <= (float)(P->W - 1) && v >= 0 && v <= (float)(P->H - 1) && ph.z >= 0;
+}
+static int block_visible(const frame_params* P, s3 block, int full) {
+  const s3 pg = block_to_point(block);
+  int vis = full;
+  for (int i = 0; i < 8; ++i) {
+    s3 c = {(int16_t)(pg.x + ((i >> 0) & 1) * (BLOCK_LEN - 1)),
+            (int16_t)(pg.y + ((i >> 1) & 1) * (BLOCK_LEN - 1)),
+            (int16_t)(pg.z + ((i >> 2) & 1) * (BLOCK_LEN - 1))};
+    const int v = voxel_visible(P, c);
+    if (full) vis &= v; else vis |= v;
+  }
+  return vis;
+}
+
+/* ---------------- public API ---------------- */
+ora_grid* ora_create(float voxel_size, float truncation, int num_block_bits) {
+  if (num_block_bits < 1 || num_block_bits > 24) return NULL;
+  ora_grid* g = (ora_grid*)calloc(1, sizeof(ora_grid));
+  g->voxel = voxel_size;
+  g->trunc = truncation;
+  g->nb_bits = num_block_bits;
+  g->nblocks = 1 << num_block_bits;
+  g->table = (entry*)calloc(NUM_ENTRY, sizeof(entry)); /* zero position/offset (Appendix A.3b) */
+  for (int i = 0; i < NUM_ENTRY; ++i) g->table[i].idx = -1; /* voxel_hash.cu:26-29 */
+  g->locks = (uint8_t*)calloc(NUM_BUCKET, 1);
+  g->heap = (int32_t*)malloc(sizeof(int32_t) * g->nblocks);
+  for (int i = 0; i < g->nblocks; ++i) g->heap[i] = i; /* voxel_mem.cu:6-11 */
+  g->free_count = g->nblocks;
+  const size_t nv = (size_t)g->nblocks * BLOCK_VOLUME;
+  g->tsdf = (float*)calloc(nv, sizeof(float));
+  g->prob = (float*)calloc(nv, sizeof(float));
+  g->rgbw = (uint8_t*)calloc(nv, 4);
+  g->vis = (int32_t*)malloc(sizeof(int32_t) * NUM_ENTRY);
+  if (!g->table || !g->locks || !g->heap || !g->tsdf || !g->prob || !g->rgbw || !g->vis) {
+    ora_destroy(g);
+    return NULL;
+  }
+  return g;
+}
+
+void ora_destroy(ora_grid* g) {
+  if (!g) return;
+  free(g->table); free(g->locks); free(g->heap); free(g->tsdf); free(g->prob); free(g->rgbw);
+  free(g->range); free(g->vis);
+  free(g);
+}
+
+static void make_params(const ora_grid* g, frame_params* P, const float K[4], int W, int H,
+                        const float q[4], const float t[3], float max_depth) {
+  P->K.fx = K[0]; P->K.fy = K[1]; P->K.cx = K[2]; P->K.cy = K[3];
+  P->Kinv = intr_inverse(P->K); /* camera.cuh:65 CameraParams ctor */
+  P->W = W; P->H = H;
+  P->cTw.q.x = q[0]; P->cTw.q.y = q[1]; P->cTw.q.z = q[2]; P->cTw.q.w = q[3];
+  P->cTw.t.x = t[0]; P->cTw.t.y = t[1]; P->cTw.t.z = t[2];
+  P->wTc = se3_inverse(&P->cTw);
+  P->voxel = g->voxel; P->trunc = g->trunc; P->max_depth = max_depth;
+}
+
+/* voxel_tsdf.cu:104-147 block_allocate_kernel (one pixel); allocations sequential. */
+static void allocate_pixel(ora_grid* g, const frame_params* P, const float* depth, int x, int y) {
+  const int idx = y * P->W + x;
+  const float d = depth[idx];
+  v3 ph = {(float)x, (float)y, 1.0f};
+  v3 pc = intr_mul(P->Kinv, ph);
+  g->range[idx] = v3_norm(pc);
+  if (d == 0 || d > P->max_depth) return;
+  v3 pcd = {pc.x * d, pc.y * d, pc.z * d};
+  v3 pw = se3_apply(&P->wTc, pcd);
+  const float r = g->range[idx];
+  v3 dc = {pc.x / r, pc.y / r, pc.z / r};
+  v3 dw = qrot(P->wTc.q, dc);
+  v3 sw = {pw.x - dw.x * P->trunc, pw.y - dw.y * P->trunc, pw.z - dw.z * P->trunc};
+  v3 dg = {dw.x / P->voxel, dw.y / P->voxel, dw.z / P->voxel};
+  v3 sg = {sw.x / P->voxel, sw.y / P->voxel, sw.z / P->voxel};
+  const float two_trunc = 2 * P->trunc;
+  v3 rg = {two_trunc * dg.x, two_trunc * dg.y, two_trunc * dg.z};
+  const int step_grid = f2i(ceilf(fmaxf(fmaxf(fabsf(rg.x), fabsf(rg.y)), fabsf(rg.z)) / BLOCK_LEN));
+  const float div = fmaxf((float)step_grid, 1);
+  v3 st = {rg.x / div, rg.y / div, rg.z / div};
+  v3 pos = sg;
+  for (int i = 0; i <= step_grid; ++i) {
+    s3 p = {f2s(roundf(pos.x)), f2s(roundf(pos.y)), f2s(roundf(pos.z))};
+    s3 b = point_to_block(p);
+    if (block_visible(P, b, 1)) {
+      const int r2 = hash_allocate(g, b);
+      if (r2 != 0) g->st.last_num_candidates++;
+      if (r2 > 0) g->st.last_num_alloc++;
+    }
+    pos.x += st.x; pos.y += st.y; pos.z += st.z;
+  }
+}
+
+int ora_integrate(ora_grid* g, const uint8_t* rgb, const float* depth, const float* ht,
+                  const float* lt, int W, int H, const float K[4], const float q[4],
+                  const float t[3], float max_depth) {
+  if (W <= 0 || H <= 0) return -1;
+  if (g->range_cap < W * H) {
+    free(g->range);
+    g->range = (float*)malloc(sizeof(float) * (size_t)W * H);
+    g->range_cap = W * H;
+  }
+  frame_params P;
+  make_params(g, &P, K, W, H, q, t, max_depth);
+  g->st.last_num_alloc = 0;
+  g->st.last_num_candidates = 0;
+  g->st.last_num_deleted = 0;
+  g->st.last_num_updated = 0;
+
+  /* ---- Allocate (voxel_tsdf.cu:377-386): sequential raster order, then ResetLocks ---- */
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x) allocate_pixel(g, &P, depth, x, y);
+  memset(g->locks, 0, NUM_BUCKET);
+
+  /* ---- GatherVisible (voxel_tsdf.cu:388-397, 82-102, 456-472): full-table scan ---- */
+  int nvis = 0;
+  for (int e = 0; e < NUM_ENTRY; ++e) {
+    const entry* b = &g->table[e];
+    if (b->idx < 0) continue;
+    if (block_visible(&P, b->pos, 0)) g->vis[nvis++] = e;
+  }
+  g->st.last_num_visible = nvis;
+
+  /* ---- UpdateTSDF (voxel_tsdf.cu:149-205) ---- */
+  s3* snap_pos = (s3*)malloc(sizeof(s3) * (nvis ? nvis : 1));
+  int32_t* snap_idx = (int32_t*)malloc(sizeof(int32_t) * (nvis ? nvis : 1));
+  for (int i = 0; i < nvis; ++i) { /* gather_visible_blocks_kernel copies the entries */
+    snap_pos[i] = g->table[g->vis[i]].pos;
+    snap_idx[i] = g->table[g->vis[i]].idx;
+  }
+  const float neg_trunc = -P.trunc;
+  int64_t nupd = 0;
+  for (int i = 0; i < nvis; ++i) {
+    const s3 bp = block_to_point(snap_pos[i]);
+    const int64_t base = (int64_t)snap_idx[i] << BLOCK_VOLUME_BITS;
+    for (int rz = 0; rz < BLOCK_LEN; ++rz)
+      for (int ry = 0; ry < BLOCK_LEN; ++ry)
+        for (int rx = 0; rx < BLOCK_LEN; ++rx) {
+          const s3 pa = {(int16_t)(bp.x + rx), (int16_t)(bp.y + ry), (int16_t)(bp.z + rz)};
+          v3 pw = {(float)pa.x * P.voxel, (float)pa.y * P.voxel, (float)pa.z * P.voxel};
+          v3 pc = se3_apply(&P.cTw, pw);
+          v3 ph = intr_mul(P.K, pc);
+          const int u = f2i(roundf(ph.x / ph.z));
+          const int v = f2i(roundf(ph.y / ph.z));
+          if (!(u >= 0 && u < W && v >= 0 && v < H)) continue;
+          const int img = v * W + u;
+          const float d = depth[img];
+          if (d == 0 || d > max_depth) continue;
+          const float sdf = g->range[img] * (d - ph.z);
+          if (!(sdf > neg_trunc)) continue;
+          const float tsdf_new = fminf(1, sdf / P.trunc);
+          const int64_t a = base + offset_to_index(rx, ry, rz);
+          uint8_t* rgbw = &g->rgbw[a * 4];
+          const float w_new = (1 - d / max_depth) * 4;
+          const float w_old = (float)rgbw[3];
+          const float wc = w_old + w_new;
+          const float r0 = ((float)rgbw[0] * w_old + (float)rgb[img * 3 + 0] * w_new) / wc;
+          const float r1 = ((float)rgbw[1] * w_old + (float)rgb[img * 3 + 1] * w_new) / wc;
+          const float r2 = ((float)rgbw[2] * w_old + (float)rgb[img * 3 + 2] * w_new) / wc;
+          g->tsdf[a] = (g->tsdf[a] * w_old + tsdf_new * w_new) / wc;
+          rgbw[3] = f2u8(fminf(roundf(wc), 40));
+          rgbw[0] = f2u8(roundf(r0));
+          rgbw[1] = f2u8(roundf(r1));
+          rgbw[2] = f2u8(roundf(r2));
+          const float p = g->prob[a];
+          const float h = ht ? ht[img] : 1.0f;
+          const float l = lt ? lt[img] : 1.0f;
+          const float pos = expf((w_old * logf(p) + w_new * logf(h)) / wc);
+          const float neg = expf((w_old * logf(1 - p) + w_new * logf(l)) / wc);
+          g->prob[a] = pos / (pos + neg);
+          ++nupd;
+        }
+  }
+  g->st.last_num_updated = nupd;
+
+  /* ---- SpaceCarving (voxel_tsdf.cu:207-230, 483-488): deletes in entry order ---- */
+  for (int i = 0; i < nvis; ++i) {
+    const int64_t base = (int64_t)snap_idx[i] << BLOCK_VOLUME_BITS;
+    float mn = fabsf(g->tsdf[base]);
+    for (int v = 1; v < BLOCK_VOLUME; ++v) mn = fminf(mn, fabsf(g->tsdf[base + v]));
+    if (mn >= 0.9f) {
+      if (hash_delete(g, snap_pos[i]) > 0) g->st.last_num_deleted++;
+    }
+  }
+  memset(g->locks, 0, NUM_BUCKET);
+  free(snap_pos);
+  free(snap_idx);
+  g->st.frames++;
+  return 0;
+}
+
+/* voxel_tsdf.cu:232-307 ray_cast_kernel */
+void ora_raycast(const ora_grid* g, const float K[4], int W, int H, const float q[4],
+                 const float t[3], float max_depth, uint8_t* rgba, uint8_t* normal) {
+  frame_params P;
+  make_params(g, &P, K, W, H, q, t, max_depth);
+  const float step_size = g->trunc / 2; /* voxel_tsdf.cu:497 truncation_ / 2 */
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x) {
+      const int idx = y * W + x;
+      uint8_t* o1 = &rgba[idx * 4];
+      uint8_t* o2 = &normal[idx * 4];
+      v3 ph = {(float)x, (float)y, 1.0f};
+      v3 pc = intr_mul(P.Kinv, ph);
+      const float n = v3_dot(pc, pc); /* Eigen normalized() */
+      v3 dc = pc;
+      if (n > 0) { const float s = sqrtf(n); dc.x = pc.x / s; dc.y = pc.y / s; dc.z = pc.z / s; }
+      v3 dw = qrot(P.wTc.q, dc);
+      v3 sg = {dw.x * step_size / P.voxel, dw.y * step_size / P.voxel, dw.z * step_size / P.voxel};
+      const int max_step = f2i(ceilf(max_depth / step_size));
+      v3 pos = {P.wTc.t.x / P.voxel, P.wTc.t.y / P.voxel, P.wTc.t.z / P.voxel};
+      s3 rp = {f2s(roundf(pos.x)), f2s(roundf(pos.y)), f2s(roundf(pos.z))};
+      float prev = retrieve_tsdf(g, rp);
+      pos.x += sg.x; pos.y += sg.y; pos.z += sg.z;
+      int hit = 0;
+      for (int i = 1; i < max_step; ++i) {
+        rp.x = f2s(roundf(pos.x)); rp.y = f2s(roundf(pos.y)); rp.z = f2s(roundf(pos.z));
+        const float cur = retrieve_tsdf(g, rp);
+        if (prev > 0 && cur <= 0 && (double)(prev - cur) <= 1.5) {
+          v3 p1 = {pos.x - sg.x, pos.y - sg.y, pos.z - sg.z};
+          v3 p2 = pos;
+          v3 mid = {(p1.x + p2.x) / 2, (p1.y + p2.y) / 2, (p1.z + p2.z) / 2};
+          for (;;) {
+            v3 dd = {p1.x - p2.x, p1.y - p2.y, p1.z - p2.z};
+            if (!((double)v3_dot(dd, dd) > .1)) break;
+            s3 mp = {f2s(roundf(mid.x)), f2s(roundf(mid.y)), f2s(roundf(mid.z))};
+            if (retrieve_tsdf(g, mp) < 0) p2 = mid; else p1 = mid;
+            mid.x = (p1.x + p2.x) / 2; mid.y = (p1.y + p2.y) / 2; mid.z = (p1.z + p2.z) / 2;
+          }
+          const s3 fg = {f2s(roundf(mid.x)), f2s(roundf(mid.y)), f2s(roundf(mid.z))};
+          const int64_t a = voxel_addr(g, fg, NULL);
+          uint8_t c0 = 0, c1 = 0, c2 = 0;
+          float prob = 0.0f; /* VoxelSEGM() default 0, VoxelRGBW() default 0 */
+          if (a >= 0) {
+            c0 = g->rgbw[a * 4 + 0]; c1 = g->rgbw[a * 4 + 1]; c2 = g->rgbw[a * 4 + 2];
+            prob = g->prob[a];
+          }
+          const s3 xp = {(int16_t)(fg.x + 1), fg.y, fg.z}, xn = {(int16_t)(fg.x - 1), fg.y, fg.z};
+          const s3 yp = {fg.x, (int16_t)(fg.y + 1), fg.z}, yn = {fg.x, (int16_t)(fg.y - 1), fg.z};
+          const s3 zp = {fg.x, fg.y, (int16_t)(fg.z + 1)}, zn = {fg.x, fg.y, (int16_t)(fg.z - 1)};
+          v3 nr = {retrieve_tsdf(g, xp) - retrieve_tsdf(g, xn), retrieve_tsdf(g, yp) - retrieve_tsdf(g, yn),
+                   retrieve_tsdf(g, zp) - retrieve_tsdf(g, zn)};
+          v3 nd = {-dw.x, -dw.y, -dw.z};
+          const float diff = fmaxf(v3_dot(nr, nd) / v3_norm(nr), 0);
+          const float alpha = (float)((double)fmaxf((float)((double)prob - 0.5), 0) / .5);
+          const float oma = 1 - alpha;
+          o1[0] = f2u8(alpha * 255 + oma * (float)c0);
+          o1[1] = f2u8(oma * (float)c1);
+          o1[2] = f2u8(oma * (float)c2);
+          o1[3] = 255;
+          const float sh = oma * diff * 255;
+          o2[0] = f2u8(alpha * 255 + sh);
+          o2[1] = f2u8(sh);
+          o2[2] = f2u8(sh);
+          o2[3] = 255;
+          hit = 1;
+          break;
+        }
+        prev = cur;
+        pos.x += sg.x; pos.y += sg.y; pos.z += sg.z;
+      }
+      if (!hit) {
+        memset(o1, 0, 4);
+        memset(o2, 0, 4);
+      }
+    }
+}
+
+/* voxel_tsdf.cu:14-25 check_bound_kernel, :27-32 check_valid_kernel, :34-46 download_tsdf_kernel,
+ * :399-454 GatherValid / GatherVoxels; bounds scaled by voxel_tsdf.cuh:21-26 BoundingCube::Scale */
+int64_t ora_query(const ora_grid* g, const float* bounds, float* out, int64_t capacity) {
+  int16_t bb[6] = {0, 0, 0, 0, 0, 0};
+  if (bounds) {
+    const float scale = (float)(1. / (double)g->voxel);
+    for (int i = 0; i < 6; ++i) bb[i] = f2s(bounds[i] * scale);
+  }
+  int64_t nblk = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    int64_t k = 0;
+    for (int e = 0; e < NUM_ENTRY; ++e) {
+      const entry* b = &g->table[e];
+      if (b->idx < 0) continue;
+      const s3 vg = block_to_point(b->pos);
+      if (bounds) {
+        const int inside = vg.x >= bb[0] && vg.y >= bb[2] && vg.z >= bb[4] &&
+                           vg.x + BLOCK_LEN - 1 <= bb[1] && vg.y + BLOCK_LEN - 1 <= bb[3] &&
+                           vg.z + BLOCK_LEN - 1 <= bb[5];
+        if (!inside) continue;
+      }
+      if (pass == 1) {
+        const int64_t base = (int64_t)b->idx << BLOCK_VOLUME_BITS;
+        for (int rz = 0; rz < BLOCK_LEN; ++rz)
+          for (int ry = 0; ry < BLOCK_LEN; ++ry)
+            for (int rx = 0; rx < BLOCK_LEN; ++rx) {
+              const int o = offset_to_index(rx, ry, rz);
+              float* w = &out[(k * BLOCK_VOLUME + o) * 4];
+              const s3 pg = {(int16_t)(vg.x + rx), (int16_t)(vg.y + ry), (int16_t)(vg.z + rz)};
+              w[0] = (float)pg.x * g->voxel;
+              w[1] = (float)pg.y * g->voxel;
+              w[2] = (float)pg.z * g->voxel;
+              w[3] = g->tsdf[base + o];
+            }
+      }
+      ++k;
+    }
+    nblk = k;
+    if (!out || capacity < nblk * BLOCK_VOLUME) break;
+  }
+  return nblk * BLOCK_VOLUME;
+}
+
+void ora_get_stats(const ora_grid* g, ora_stats* s) {
+  *s = g->st;
+  s->active_blocks = g->nblocks - g->free_count;
+}
+
+int32_t ora_num_entries(void) { return NUM_ENTRY; }
+int32_t ora_num_blocks(const ora_grid* g) { return g->nblocks; }
+
+void ora_dump(const ora_grid* g, int16_t* pos_off, int32_t* idx, int32_t* heap, int32_t* free_count,
+              float* tsdf, float* prob, uint8_t* rgbw) {
+  if (pos_off || idx)
+    for (int e = 0; e < NUM_ENTRY; ++e) {
+      if (pos_off) {
+        pos_off[e * 4 + 0] = g->table[e].pos.x;
+        pos_off[e * 4 + 1] = g->table[e].pos.y;
+        pos_off[e * 4 + 2] = g->table[e].pos.z;
+        pos_off[e * 4 + 3] = g->table[e].offset;
+      }
+      if (idx) idx[e] = g->table[e].idx;
+    }
+  if (heap) memcpy(heap, g->heap, sizeof(int32_t) * g->nblocks);
+  if (free_count) *free_count = g->free_count;
+  const size_t nv = (size_t)g->nblocks * BLOCK_VOLUME;
+  if (tsdf) memcpy(tsdf, g->tsdf, nv * sizeof(float));
+  if (prob) memcpy(prob, g->prob, nv * sizeof(float));
+  if (rgbw) memcpy(rgbw, g->rgbw, nv * 4);
+}
+
+void ora_hash_allocate(ora_grid* g, const int16_t* keys, int n) {
+  for (int i = 0; i < n; ++i) {
+    s3 k = {keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]};
+    hash_allocate(g, k);
+  }
+  memset(g->locks, 0, NUM_BUCKET); /* VoxelHashTable::ResetLocks */
+}
+
+void ora_hash_delete(ora_grid* g, const int16_t* keys, int n) {
+  for (int i = 0; i < n; ++i) {
+    s3 k = {keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]};
+    hash_delete(g, k);
+  }
+  memset(g->locks, 0, NUM_BUCKET);
+}
+
+void ora_hash_retrieve(const ora_grid* g, const int16_t* points, int n, uint8_t* rgbw, float* tsdf,
+                       float* prob, int16_t* bpo, int32_t* bidx) {
+  for (int i = 0; i < n; ++i) {
+    s3 p = {points[3 * i], points[3 * i + 1], points[3 * i + 2]};
+    int64_t e;
+    const int64_t a = voxel_addr(g, p, &e);
+    if (rgbw) {
+      for (int c = 0; c < 4; ++c) rgbw[i * 4 + c] = a < 0 ? 0 : g->rgbw[a * 4 + c];
+    }
+    if (tsdf) tsdf[i] = a < 0 ? 1.0f : g->tsdf[a];
+    if (prob) prob[i] = a < 0 ? 0.0f : g->prob[a];
+    const s3 blk = point_to_block(p);
+    if (bpo) {
+      /* cache semantics (voxel_hash.cuh:157-159): miss -> {pos, offset -1, idx -1} */
+      bpo[i * 4 + 0] = e < 0 ? blk.x : g->table[e].pos.x;
+      bpo[i * 4 + 1] = e < 0 ? blk.y : g->table[e].pos.y;
+      bpo[i * 4 + 2] = e < 0 ? blk.z : g->table[e].pos.z;
+      bpo[i * 4 + 3] = e < 0 ? -1 : g->table[e].offset;
+    }
+    if (bidx) bidx[i] = e < 0 ? -1 : g->table[e].idx;
+  }
+}
+
+int ora_hash_assign(ora_grid* g, const int16_t* points, int n, const uint8_t* rgbw) {
+  int missing = 0;
+  for (int i = 0; i < n; ++i) {
+    s3 p = {points[3 * i], points[3 * i + 1], points[3 * i + 2]};
+    const int64_t a = voxel_addr(g, p, NULL);
+    if (a < 0) { ++missing; continue; }
+    memcpy(&g->rgbw[a * 4], &rgbw[i * 4], 4);
+  }
+  return missing;
+}
+
+int32_t ora_num_active_blocks(const ora_grid* g) { return g->nblocks - g->free_count; }
+
+void ora_pool_acquire(ora_grid* g, int n, int32_t* out) {
+  for (int i = 0; i < n; ++i) out[i] = pool_acquire(g);
+}
+void ora_pool_release(ora_grid* g, const int32_t* idx, int n) {
+  for (int i = 0; i < n; ++i) pool_release(g, idx[i]);
+}
+void ora_pool_set_weight(ora_grid* g, int32_t b, uint8_t w) {
+  const int64_t base = (int64_t)b << BLOCK_VOLUME_BITS;
+  for (int v = 0; v < BLOCK_VOLUME; ++v) g->rgbw[(base + v) * 4 + 3] = w;
+}
+void ora_pool_get_weights(const ora_grid* g, int32_t b, uint8_t* out) {
+  const int64_t base = (int64_t)b << BLOCK_VOLUME_BITS;
+  for (int v = 0; v < BLOCK_VOLUME; ++v) out[v] = g->rgbw[(base + v) * 4 + 3];
+}
