@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""bench.py -- TSDF integrate frames/s on MI355X (BASELINE.json metric), one JSON line on rank 0.
+
+Workload (N=1): BASELINE.json configs[2] -- synthetic 640x480 depth + per-pixel high/low-touch
+probability maps (the segmentation/inference output shape), fused TSDF + RGB + semantic integrate
+into a 5 mm voxel-hash volume (3 cm truncation, 4 m max depth, TUM fr1 intrinsics). One step =
+one TSDFGrid::Integrate of one frame: DDA block allocation, visibility, fused update, space
+carving. All frames are rendered on the GPU and resident in HBM before timing starts.
+
+N>1 (launched by torch.distributed.run, one rank per GPU): default --mode streams runs one camera
+stream per GPU into that GPU's own volume (a multi-camera rig; no data-path collective), value =
+all frames integrated by all ranks / max rank time, scaling "weak". --mode sharded integrates ONE
+stream with the volume spatially sharded by 4^3-block bricks (each rank allocates and integrates
+only the blocks it owns), value = frames / max rank time, scaling "strong".
+
+roofline: the fused integrate kernel (k_integrate). Algorithmic bytes per launch:
+N_vis * (512 * 12 + 12) voxel state + block metadata read, N_upd * 12 updated voxel state written,
+15 * W * H frame bytes read -- N_vis and N_upd are counted on device. Average launch duration from
+HIP events recorded on the engine stream around every k_integrate launch of the timed region.
+cpu_baseline: the single-threaded CPU oracle (oracle/tsdf_oracle.c, a restatement of the
+reference kernels incl. its full-table visibility scan) on a bounded sample of the same stream.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "disinfect-slam_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=300)
+    p.add_argument("--warmup", type=int, default=30)
+    p.add_argument("--width", type=int, default=640)
+    p.add_argument("--height", type=int, default=480)
+    p.add_argument("--voxel", type=float, default=0.005)
+    p.add_argument("--trunc", type=float, default=0.03)
+    p.add_argument("--max-depth", type=float, default=4.0)
+    p.add_argument("--depth-only", action="store_true", help="config C2: ht = lt = NULL (ones)")
+    p.add_argument("--mode", choices=("streams", "sharded"), default="streams")
+    p.add_argument("--cpu-frames", type=int, default=-1, help="oracle sample size (-1 = auto)")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--block-bits", type=int, default=18)
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and world != 1:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {a.gpus}")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import tsdf_amd
+    from tsdf_amd import synth
+
+    cam = synth.camera(a.width, a.height,
+                       synth.TUM_FR1 if a.width <= 640 else synth.L515_FULL)
+    nframes = a.warmup + a.steps
+    # streams mode: each rank's camera starts a third of an orbit apart (its own stream)
+    offset = rank * 240 if (world > 1 and a.mode == "streams") else 0
+    frames = synth.render_torch(cam, list(range(offset, offset + nframes)), device=dev)
+    torch.cuda.synchronize()
+    shard_index, shard_count = (rank, world) if (a.mode == "sharded" and world > 1) else (0, 1)
+    stream = torch.cuda.current_stream()
+    eng = tsdf_amd.Engine(a.voxel, a.trunc, max_width=a.width, max_height=a.height,
+                          num_block_bits=a.block_bits, device=torch.cuda.current_device(),
+                          shard_index=shard_index, shard_count=shard_count,
+                          stream=stream.cuda_stream)
+    K = cam.K
+    poses = [tsdf_amd.SE3(frames["q"][i], frames["t"][i]) for i in range(nframes)]
+
+    def step(i):
+        ht = None if a.depth_only else frames["ht"][i]
+        lt = None if a.depth_only else frames["lt"][i]
+        eng.integrate(frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i], a.max_depth)
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    eng.profile_begin()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.warmup, nframes):
+        step(i)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    prof = eng.profile_end()
+    st = eng.stats()
+    elapsed = t1 - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        tot = torch.tensor([prof["sum_visible"], prof["sum_updated"]], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot)
+    units = a.steps * (world if a.mode == "streams" else 1)
+    value = units / elapsed
+
+    # ---- roofline of the fused integrate kernel (this rank's launches) ----
+    W, H = a.width, a.height
+    img_bytes = (12 if a.depth_only else 15) * W * H
+    alg_bytes = (prof["sum_visible"] * (512 * 12 + 12) + prof["sum_updated"] * 12) / a.steps + img_bytes
+    t_int = prof["ms_integrate"] / a.steps / 1e3
+    achieved = alg_bytes / t_int / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_integrate_latest.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            if pmc.get("width") == W and pmc.get("height") == H:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        cpu = cpu_baseline(a, cam)
+
+    if rank == 0:
+        workload = ("C2: 640x480 depth-only" if a.depth_only else "C3: 640x480 depth + ht/lt semantic")
+        if (W, H) != (640, 480):
+            workload = f"{W}x{H} depth{'' if a.depth_only else ' + ht/lt semantic'}"
+        out = {
+            "metric": "TSDF integrate frames/s (640x480 depth+label, 5mm voxel)",
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak" if a.mode == "streams" else "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (analytic room scene rendered on GPU, resident in HBM)",
+            "config": {
+                "workload": workload + f", {a.voxel * 1000:g} mm voxel, {a.trunc * 100:g} cm truncation, "
+                            f"{a.max_depth:g} m max depth, TUM fr1 intrinsics, orbit 1 cm + 0.5 deg/frame",
+                "width": W, "height": H, "voxel_m": a.voxel, "truncation_m": a.trunc,
+                "pool_blocks": 1 << a.block_bits,
+                "parallelism": (f"streams{world}" if a.mode == "streams" else f"sharded{world}")
+                if world > 1 else "single",
+            },
+            "roofline": {
+                "kernel": "k_integrate",
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "alg_bytes_per_launch": int(alg_bytes),
+                "us_per_launch": round(t_int * 1e6, 3),
+            },
+            "cpu_baseline": cpu,
+            "phases_ms_per_frame": {
+                "allocate": round(prof["ms_allocate"] / a.steps, 4),
+                "visibility": round(prof["ms_visible"] / a.steps, 4),
+                "integrate": round(prof["ms_integrate"] / a.steps, 4),
+                "carve": round(prof["ms_carve"] / a.steps, 4),
+            },
+            "avg_visible_blocks": round(prof["sum_visible"] / a.steps, 1),
+            "avg_updated_voxels": round(prof["sum_updated"] / a.steps, 1),
+            "active_blocks": st["active_blocks"],
+            "status": st["status"],
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(a, cam):
+    """Single-thread oracle on the first frames of the same stream (empty map), host frames."""
+    import numpy as np
+
+    from tsdf_amd import synth
+    from _oracle import OracleGrid
+
+    ora = OracleGrid(a.voxel, a.trunc, a.block_bits)
+    n = a.cpu_frames
+    budget = 20.0
+    frames_done, spent = 0, 0.0
+    i = 0
+    while True:
+        if n >= 0 and frames_done >= n:
+            break
+        if n < 0 and (spent >= budget or frames_done >= 60):
+            break
+        fr = synth.render(cam, i)
+        ht = None if a.depth_only else fr["ht"]
+        lt = None if a.depth_only else fr["lt"]
+        t0 = time.perf_counter()
+        ora.integrate(fr["rgb"], fr["depth"], ht, lt, a.max_depth, cam.K, fr["q"], fr["t"])
+        spent += time.perf_counter() - t0
+        frames_done += 1
+        i += 1
+    ora.close()
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(frames_done / spent, 4),
+        "unit": "frames/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"first {frames_done} frames of the same {cam.width}x{cam.height} stream from an empty "
+                  f"map, single thread, oracle/tsdf_oracle.c -O2 (host: {model}, nproc={os.cpu_count()})",
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,332 @@
+// tsdf_alloc.hip -- block allocation: frame ingest + DDA, and the in-order allocation resolver.
+//
+// Reference: TSDFGrid::Allocate (utils/tsdf/voxel_tsdf.cu:377-386) launching block_allocate_kernel
+// (:104-147), which calls VoxelHashTable::Allocate (voxel_hash.cu:58-120) from every pixel
+// thread. That insert is racy by design (one structural change per bucket per launch, losers
+// dropped); this engine replays the canonical sequential linearisation:
+// candidates in pixel raster order then DDA step, with the exact bucket-lock semantics.
+#include "tsdf_block.h"
+#include "tsdf_kernels.h"
+
+namespace tsdf {
+
+// ---------------------------------------------------------------------------------------------
+// per-frame new-key set: open addressing on 64-bit packed keys, min candidate order per key
+// ---------------------------------------------------------------------------------------------
+__device__ void nk_insert(const EngineDev& D, uint64_t key, uint32_t order) {
+  uint32_t h = (uint32_t)mix64(key) & (kNewKeyCap - 1);
+  for (int p = 0; p < 256; ++p) {
+    unsigned long long cur = D.nk_key[h];
+    if (cur == 0ull) cur = atomicCAS(&D.nk_key[h], 0ull, (unsigned long long)key);
+    if (cur == 0ull) {
+      const int s = atomicAdd(&D.ctr->nk_count, 1);
+      D.nk_list[s] = (int32_t)h;
+      atomicMin(&D.nk_order[h], order);
+      return;
+    }
+    if (cur == key) {
+      atomicMin(&D.nk_order[h], order);
+      return;
+    }
+    h = (h + 1) & (kNewKeyCap - 1);
+  }
+  atomicOr(&D.ctr->status, 2u);  // TSDF_STATUS_NEWKEY_OVERFLOW
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_ingest_dda: 16x16 pixel tile per workgroup.
+//  1. pack the frame into per-pixel records the integrate kernel gathers:
+//       pixA = {depth, range = |K^-1 [x y 1]|, w_new = (1 - d / max_depth) * 4, rgb}
+//       pixB = {log ht, log lt}
+//     (exactly the values tsdf_integrate_kernel recomputes per voxel, voxel_tsdf.cu:174-201)
+//  2. DDA of [p - trunc dir, p + trunc dir] (voxel_tsdf.cu:116-146); block keys deduplicated in
+//     an LDS hash set with their smallest candidate order (y*W + x)*maxs + i
+//  3. each unique key once: all-8-corners visibility (is_block_visible<true>), shard ownership,
+//     table probe; missing keys go to the global new-key set.
+// ---------------------------------------------------------------------------------------------
+constexpr int kTileSlots = 2048;  // > 256 pixels x maxs (<= 6, checked by tsdf_create)
+
+__global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
+                                                    const float* __restrict__ depth,
+                                                    const uint8_t* __restrict__ rgb,
+                                                    const float* __restrict__ ht,
+                                                    const float* __restrict__ lt) {
+  __shared__ unsigned long long s_key[kTileSlots];
+  __shared__ uint32_t s_ord[kTileSlots];
+  for (int i = threadIdx.x; i < kTileSlots; i += 256) {
+    s_key[i] = 0ull;
+    s_ord[i] = 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+  const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+  if (x < P.W && y < P.H) {
+    const int i = y * P.W + x;
+    const float d = depth[i];
+    const uint32_t c = (uint32_t)rgb[3 * i] | ((uint32_t)rgb[3 * i + 1] << 8) |
+                       ((uint32_t)rgb[3 * i + 2] << 16);
+    const float h = ht ? ht[i] : 1.0f;
+    const float l = lt ? lt[i] : 1.0f;
+    const f3 pc = pixel_ray(P, x, y);
+    const float range = sqrtf(dot3(pc, pc));  // img_depth_to_range (voxel_tsdf.cu:120)
+    const float w_new = (1.0f - d / P.max_depth) * 4.0f;
+    D.pixA[i] = make_float4(d, range, w_new, __uint_as_float(c));
+    D.pixB[i] = make_float2(logf(h), logf(l));
+    if (!(d == 0 || d > P.max_depth)) {
+      const f3 pcd = {pc.x * d, pc.y * d, pc.z * d};
+      const f3 pw = se3_apply(P.wq, P.wt, pcd);
+      const f3 dc = {pc.x / range, pc.y / range, pc.z / range};
+      const f3 dw = qrot(P.wq, dc);
+      const f3 sw = {pw.x - dw.x * P.trunc, pw.y - dw.y * P.trunc, pw.z - dw.z * P.trunc};
+      const f3 dg = {dw.x / P.voxel, dw.y / P.voxel, dw.z / P.voxel};
+      const f3 sg = {sw.x / P.voxel, sw.y / P.voxel, sw.z / P.voxel};
+      const float two_trunc = 2 * P.trunc;
+      const f3 rg = {two_trunc * dg.x, two_trunc * dg.y, two_trunc * dg.z};
+      const int step_grid =
+          f2i(ceilf(fmaxf(fmaxf(fabsf(rg.x), fabsf(rg.y)), fabsf(rg.z)) / kBlockLen));
+      const float div = fmaxf((float)step_grid, 1.0f);
+      const f3 st = {rg.x / div, rg.y / div, rg.z / div};
+      f3 pos = sg;
+      for (int s = 0; s <= step_grid; ++s) {
+        if (s >= P.maxs) {
+          atomicOr(&D.ctr->status, 4u);  // TSDF_STATUS_DDA_OVERFLOW
+          break;
+        }
+        const int16_t kx = (int16_t)(f2s(roundf(pos.x)) >> kBlockLenBits);
+        const int16_t ky = (int16_t)(f2s(roundf(pos.y)) >> kBlockLenBits);
+        const int16_t kz = (int16_t)(f2s(roundf(pos.z)) >> kBlockLenBits);
+        pos.x += st.x;
+        pos.y += st.y;
+        pos.z += st.z;
+        const unsigned long long key = pack_key(kx, ky, kz);
+        const uint32_t order = (uint32_t)i * (uint32_t)P.maxs + (uint32_t)s;
+        uint32_t hs = (uint32_t)mix64(key) & (kTileSlots - 1);
+        for (int p = 0; p < kTileSlots; ++p) {
+          const unsigned long long prev = atomicCAS(&s_key[hs], 0ull, key);
+          if (prev == 0ull || prev == key) {
+            atomicMin(&s_ord[hs], order);
+            break;
+          }
+          hs = (hs + 1) & (kTileSlots - 1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int sl = threadIdx.x; sl < kTileSlots; sl += 256) {
+    const unsigned long long key = s_key[sl];
+    if (!key) continue;
+    int16_t kx, ky, kz;
+    unpack_key(key, kx, ky, kz);
+    if (P.shard_count > 1 &&
+        brick_owner(kx, ky, kz, (uint32_t)P.shard_count) != (uint32_t)P.shard_index)
+      continue;
+    if (!block_visible<true>(P, kx, ky, kz)) continue;
+    if (find_entry(D.table, kx, ky, kz) >= 0) continue;
+    nk_insert(D, key, s_ord[sl]);
+  }
+}
+
+// test path: keys[n] in list order (one VoxelHashTable::Allocate launch, voxel_hash_test.cu)
+__global__ void k_keys_to_newset(EngineDev D, const int16_t* __restrict__ keys, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int16_t x = keys[3 * i], y = keys[3 * i + 1], z = keys[3 * i + 2];
+    if (find_entry(D.table, x, y, z) >= 0) continue;
+    nk_insert(D, pack_key(x, y, z), (uint32_t)i);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_resolve_alloc: one 1024-thread workgroup replays VoxelHashTable::Allocate in candidate order.
+// Every unique missing key K is evaluated against the current table:
+//   SLOT(B, s)   : an empty slot s of its bucket B                  -> takes lock B
+//   APPEND(L, C) : bucket full -> tail T of B's list (bucket L = T/2), first empty slot-0 entry E
+//                  after T (bucket C = E/2)                         -> takes lock L, then lock C
+// A key's outcome depends on earlier keys only through the buckets it locks (every table write
+// happens under those locks), so up to 1024 keys are evaluated speculatively, each claims its
+// buckets in an LDS table (smallest rank wins), and the longest prefix whose keys won all their
+// claims commits in parallel. The first key always wins, so each round commits >= 1 key.
+// Pool blocks are popped in commit order by prefix sum (AquireBlock, voxel_mem.cu:37-52).
+// fresh_mode 1: mark new blocks in fresh_flag (integrate initialises them), 0: list them in
+// D.fresh for k_fresh_init.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, uint32_t range,
+                                                                   int frame_mode) {
+  __shared__ ResolveLds L;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    L.epoch = D.ctr->lock_epoch + 1;
+    D.ctr->lock_epoch = L.epoch;
+    L.sfree = D.ctr->free_count;
+    L.nfresh = 0;
+    L.nalloc = 0;
+  }
+  claims_clear(L);
+  const int n = D.ctr->nk_count;
+  // (order, slot) pairs in a compact scratch array so every batch pass is one coalesced read
+  for (int i = t; i < n; i += kResolveThreads) {
+    const int h = D.nk_list[i];
+    D.pairs[i] = ((unsigned long long)D.nk_order[h] << 32) | (uint32_t)h;
+  }
+  __syncthreads();
+  auto keyf = [&](int i) -> uint32_t { return (uint32_t)(D.pairs[i] >> 32); };
+  const int width = stream_prepare(L, n, range, keyf);
+  const int nbatch = n <= kBatch ? (n > 0 ? 1 : 0) : ((n - 1) >> 10) + 1;
+  int rounds = 0;
+  for (int j = 0; j < nbatch; ++j) {
+    const int m = stream_batch(L, n, width, j, keyf);
+    if (t == 0) L.base = 0;
+    __syncthreads();
+    while (L.base < m) {
+      if (++rounds > n + 8) {  // unreachable: the first key of a round always commits
+        if (t == 0) atomicOr(&D.ctr->status, 8u);
+        j = nbatch;
+        break;
+      }
+      const int base = L.base;
+      const bool have = base + t < m;
+      int kind = 0, slot = 0, h = -1;
+      uint32_t B = 0, Lb = 0, C = 0, T = 0, E = 0;
+      int16_t kx = 0, ky = 0, kz = 0;
+      if (have) {
+        const int li = (int)(L.batch[base + t] & 0xFFFFFFFFu);
+        h = (int)(D.pairs[li] & 0xFFFFFFFFu);
+        unpack_key(D.nk_key[h], kx, ky, kz);
+        B = hash_block(kx, ky, kz);
+        const Ent s0 = load_ent(D.table, 2 * B);
+        const Ent s1 = load_ent(D.table, 2 * B + 1);
+        if (s0.idx < 0) {
+          kind = 1;
+          slot = 0;
+        } else if (s1.idx < 0) {
+          kind = 1;
+          slot = 1;
+        } else {
+          kind = 2;
+          uint32_t last = 2 * B + 1;
+          Ent b = s1;
+          while (b.off) {
+            last = (uint32_t)(last + (int32_t)b.off) & kEntryMask;
+            b = load_ent(D.table, last);
+          }
+          T = last;
+          Lb = T >> 1;
+          uint32_t nx = T;
+          for (uint32_t p = 0; p < kNumEntry; ++p) {
+            nx = (nx + 1) & kEntryMask;
+            if ((nx & 1u) == 0u && load_ent(D.table, nx).idx < 0) break;
+          }
+          E = nx;
+          C = E >> 1;
+        }
+        if (kind == 1) {
+          claim(L, B, (uint32_t)t);
+        } else {
+          claim(L, Lb, (uint32_t)t);
+          claim(L, C, (uint32_t)t);
+        }
+      }
+      if (t == 0) L.first_dirty = kResolveThreads;
+      __syncthreads();
+      if (have) {
+        const bool clean = kind == 1 ? claim_winner(L, B) == (uint32_t)t
+                                     : (claim_winner(L, Lb) == (uint32_t)t &&
+                                        claim_winner(L, C) == (uint32_t)t);
+        if (!clean) atomicMin(&L.first_dirty, t);
+      }
+      __syncthreads();
+      const int first_dirty = L.first_dirty;
+      const bool commit = have && t < first_dirty;
+      bool ok = false;
+      if (commit) {
+        const uint32_t ep = L.epoch;
+        if (kind == 1) {
+          if (D.lock_tag[B] != ep) {
+            D.lock_tag[B] = ep;
+            ok = true;
+          }
+        } else if (D.lock_tag[Lb] != ep) {
+          D.lock_tag[Lb] = ep;
+          if (D.lock_tag[C] != ep) {
+            D.lock_tag[C] = ep;
+            ok = true;
+          }
+        }
+      }
+      int nok;
+      const int rank = block_excl_scan(ok ? 1 : 0, L.scan, &nok);
+      const int free_now = L.sfree;
+      if (ok) {
+        const int hi = free_now - 1 - rank;
+        if (hi < 0) {
+          atomicOr(&D.ctr->status, 1u);  // TSDF_STATUS_POOL_EXHAUSTED: insert dropped
+        } else {
+          const int32_t idx = D.heap[hi];
+          uint32_t e;
+          if (kind == 1) {
+            e = 2 * B + (uint32_t)slot;
+          } else {
+            const uint32_t wrap = E > T ? 0u : kNumEntry;
+            store_off(D.table, T, (int16_t)(E + wrap - T));
+            e = E;
+          }
+          store_ent(D.table, e, kx, ky, kz, 0, idx);
+          atomicOr(&D.occ[e >> 6], 1ull << (e & 63));
+          if (frame_mode)
+            D.fresh_flag[idx] = 1;
+          else
+            D.fresh[L.nfresh + rank] = idx;
+        }
+      }
+      if (commit) {
+        D.nk_key[h] = 0ull;
+        D.nk_order[h] = 0xFFFFFFFFu;
+      }
+      claims_clear(L);
+      __syncthreads();
+      if (t == 0) {
+        const int used = nok < free_now ? nok : (free_now > 0 ? free_now : 0);
+        L.sfree = free_now - used;
+        L.nfresh += used;
+        L.nalloc += used;
+        const int span = m - base < kResolveThreads ? m - base : kResolveThreads;
+        L.base = base + (first_dirty < span ? first_dirty : span);
+      }
+      __syncthreads();
+    }
+  }
+  if (t == 0) {
+    D.ctr->free_count = L.sfree;
+    D.ctr->n_fresh = L.nfresh;
+    D.ctr->nk_count = 0;
+    if (frame_mode) {
+      D.ctr->last_alloc = L.nalloc;
+      D.ctr->last_new_keys = n;
+      D.ctr->total_alloc += (unsigned long long)L.nalloc;
+      D.ctr->last_updated = 0ull;
+      D.ctr->n_vis = 0;
+      D.ctr->n_cand = 0;
+    }
+  }
+}
+
+// AquireBlock's initialisation (voxel_mem.cu:43-51) for the hash-level test path
+__global__ __launch_bounds__(256) void k_fresh_init(EngineDev D) {
+  const int n = D.ctr->n_fresh;
+  const int quads = n * (kBlockVolume / 4);
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += gridDim.x * blockDim.x) {
+    const int b = q >> 7, v = (q & 127) * 4;
+    uint8_t* blk = D.pool + (size_t)D.fresh[b] * kBlockBytes;
+    *reinterpret_cast<float4*>(blk + v * 4) = make_float4(-1.f, -1.f, -1.f, -1.f);
+    *reinterpret_cast<float4*>(blk + kProbOffset + v * 4) = make_float4(.5f, .5f, .5f, .5f);
+    uint4* cw = reinterpret_cast<uint4*>(blk + kRgbwOffset + v * 4);
+    uint4 c = *cw;
+    c.x &= 0x00FFFFFFu;
+    c.y &= 0x00FFFFFFu;
+    c.z &= 0x00FFFFFFu;
+    c.w &= 0x00FFFFFFu;
+    *cw = c;
+  }
+}
+
+}  // namespace tsdf

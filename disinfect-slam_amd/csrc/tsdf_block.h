@@ -1,0 +1,189 @@
+// tsdf_block.h -- wave / workgroup building blocks shared by the engine kernels (wave64).
+#pragma once
+
+#include "tsdf_device.h"
+
+namespace tsdf {
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int n = __shfl_up(v, o, 64);
+    if (l >= o) v += n;
+  }
+  return v;
+}
+// exclusive workgroup scan; every thread of the block must call it. scratch: blockDim/64 ints.
+__device__ __forceinline__ int block_excl_scan(int v, int* scratch, int* total) {
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int incl = wave_incl_scan(v);
+  if (lane_id() == 63) scratch[w] = incl;
+  __syncthreads();
+  int before = 0, tot = 0;
+  for (int i = 0; i < nw; ++i) {
+    const int s = scratch[i];
+    if (i < w) before += s;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return before + incl - v;
+}
+__device__ __forceinline__ uint64_t mix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Single-workgroup ordered streaming of an unsorted list whose sort keys are unique integers in
+// [0, range): a histogram over <= kMaxWin windows of width <= 1024 groups the list into batches
+// of <= kBatch elements in key order (a window holds at most `width` distinct keys), each batch
+// is gathered into LDS and bitonic-sorted. Used by both resolvers to replay the reference's
+// sequential order without a global sort.
+// ---------------------------------------------------------------------------------------------
+constexpr int kBatch = 2048;
+constexpr int kMaxWin = 8192;
+constexpr int kClaimSlots = 4096;
+
+struct ResolveLds {
+  uint32_t hist[kMaxWin];             // window counts -> exclusive prefix
+  unsigned long long batch[kBatch];   // (sort key << 32) | list index
+  uint32_t ckey[kClaimSlots];         // claim table: bucket + 1 (0 = empty)
+  uint32_t cval[kClaimSlots];         // claim table: smallest claiming rank
+  int scan[16];
+  int count;
+  int first_dirty;
+  int sfree;
+  int nfresh;
+  int base;
+  int nalloc;
+  uint32_t epoch;
+};
+
+__device__ __forceinline__ void lds_bitonic_sort(unsigned long long* a, int m) {
+  int P = 1;
+  while (P < m) P <<= 1;
+  for (int i = m + (int)threadIdx.x; i < P; i += blockDim.x) a[i] = ~0ull;
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long x = a[i], y = a[ixj];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            a[i] = y;
+            a[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// claim table: each key claims buckets; the smallest rank per bucket wins
+__device__ __forceinline__ void claims_clear(ResolveLds& L) {
+  for (int i = threadIdx.x; i < kClaimSlots; i += blockDim.x) {
+    L.ckey[i] = 0u;
+    L.cval[i] = 0xFFFFFFFFu;
+  }
+}
+__device__ __forceinline__ void claim(ResolveLds& L, uint32_t bucket, uint32_t rank) {
+  uint32_t h = mix32(bucket) & (kClaimSlots - 1);
+  const uint32_t k = bucket + 1u;
+  for (int p = 0; p < kClaimSlots; ++p) {
+    const uint32_t prev = atomicCAS(&L.ckey[h], 0u, k);
+    if (prev == 0u || prev == k) {
+      atomicMin(&L.cval[h], rank);
+      return;
+    }
+    h = (h + 1) & (kClaimSlots - 1);
+  }
+}
+__device__ __forceinline__ uint32_t claim_winner(const ResolveLds& L, uint32_t bucket) {
+  uint32_t h = mix32(bucket) & (kClaimSlots - 1);
+  const uint32_t k = bucket + 1u;
+  for (int p = 0; p < kClaimSlots; ++p) {
+    if (L.ckey[h] == k) return L.cval[h];
+    h = (h + 1) & (kClaimSlots - 1);
+  }
+  return 0xFFFFFFFFu;
+}
+
+// Prepare ordered streaming of `n` elements with keys(i) in [0, range); returns the window width.
+// After it, L.hist[w] holds the exclusive prefix count of window w.
+template <typename KeyFn>
+__device__ int stream_prepare(ResolveLds& L, int n, uint32_t range, KeyFn keyf) {
+  uint32_t width = (range + kMaxWin - 1) / kMaxWin;
+  if (width < 1) width = 1;
+  const int nwin = (int)((range + width - 1) / width);
+  if (n <= kBatch) return (int)width;  // single batch: no histogram needed
+  for (int i = threadIdx.x; i < nwin; i += blockDim.x) L.hist[i] = 0u;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&L.hist[keyf(i) / width], 1u);
+  __syncthreads();
+  // exclusive scan of hist[0..nwin) (kMaxWin / blockDim windows per thread)
+  const int per = (nwin + blockDim.x - 1) / blockDim.x;
+  const int w0 = threadIdx.x * per;
+  int local = 0;
+  for (int k = 0; k < per; ++k)
+    if (w0 + k < nwin) local += (int)L.hist[w0 + k];
+  int tot;
+  int run = block_excl_scan(local, L.scan, &tot);
+  for (int k = 0; k < per; ++k)
+    if (w0 + k < nwin) {
+      const int c = (int)L.hist[w0 + k];
+      L.hist[w0 + k] = (uint32_t)run;
+      run += c;
+    }
+  __syncthreads();
+  return (int)width;
+}
+
+// Gather batch `j` (elements whose window prefix >> 10 == j, or all when n <= kBatch) into
+// L.batch sorted ascending by key; returns its size.
+template <typename KeyFn>
+__device__ int stream_batch(ResolveLds& L, int n, int width, int j, KeyFn keyf) {
+  if (threadIdx.x == 0) L.count = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t k = keyf(i);
+    if (n <= kBatch || (int)(L.hist[k / (uint32_t)width] >> 10) == j) {
+      const int pos = atomicAdd(&L.count, 1);
+      if (pos < kBatch) L.batch[pos] = ((unsigned long long)k << 32) | (uint32_t)i;
+    }
+  }
+  __syncthreads();
+  const int m = L.count < kBatch ? L.count : kBatch;  // bounded by construction (width <= 1024)
+  lds_bitonic_sort(L.batch, m);
+  return m;
+}
+
+}  // namespace tsdf

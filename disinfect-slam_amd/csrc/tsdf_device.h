@@ -36,7 +36,10 @@ constexpr int kBlockBytes = kBlockVolume * 12;  // 6 KiB per voxel block
 constexpr int kProbOffset = kBlockVolume * 4;   // byte offsets inside a block record
 constexpr int kRgbwOffset = kBlockVolume * 8;
 constexpr uint32_t kNewKeyCap = 1u << 17;       // unique new blocks per frame
+constexpr int kMaxDdaSamples = 6;               // DDA samples per pixel the ingest kernel supports
+constexpr int64_t kMaxOrderRange = 8192ll * 1024;  // candidate order space the resolver streams
 constexpr int kResolveThreads = 1024;
+constexpr int kIntegrateGrid = 2048;  // k_integrate workgroups (persistent grid-stride)
 
 struct f3 {
   float x, y, z;
@@ -69,13 +72,11 @@ struct alignas(16) VisRec {
 
 struct DevCounters {
   int32_t free_count;     // VoxelMemPool::num_free_blocks_
-  uint32_t lock_epoch;    // current lock epoch
-  uint32_t claim_gen;     // resolver claim generation
+  uint32_t lock_epoch;    // current lock epoch (one per allocate / delete launch)
   int32_t nk_count;       // unique new keys inserted by the DDA this frame
-  int32_t n_sorted;       // ordered new keys (compaction output)
-  int32_t n_fresh;        // blocks acquired this frame
+  int32_t n_fresh;        // blocks acquired by the hash-level test path
   int32_t n_vis;          // visible blocks this frame
-  int32_t n_cand;         // carve candidates this frame (compaction output)
+  int32_t n_cand;         // carve candidates this frame
   uint32_t status;        // TSDF_STATUS_* bits
   int32_t last_alloc;
   int32_t last_deleted;

@@ -86,9 +86,7 @@ struct tsdf_engine {
   bool own_stream = false;
   EngineDev D{};
   int maxs = 3;
-  int64_t obits_bits = 0;
-  int obits_words = 0;
-  int wgcnt_cap = 0;
+  int64_t order_range = 0;  // candidate order space: max_pixels * maxs
   int64_t max_pixels = 0;
   // host-frame staging
   uint8_t* s_rgb = nullptr;
@@ -123,12 +121,12 @@ namespace {
 
 void free_all(tsdf_engine* e) {
   EngineDev& D = e->D;
-  void* ptrs[] = {D.table,  D.lock_tag, D.claim,   D.heap,    D.pool,   D.occ,       D.ctr,
-                  D.nk_key, D.nk_order, D.nk_list, D.obits,   D.order_slot, D.sorted, D.fresh,
-                  D.visbits, D.wgcnt,   D.vis,     D.candbits, D.cand,   D.pix,       e->s_rgb,
-                  e->s_depth, e->s_ht,  e->s_lt,   e->rc_rgba, e->rc_norm, e->q_sel,  e->q_count,
-                  e->q_out, e->t_keys,  e->t_recs, e->t_count, e->t_i32, e->t_u32,    e->t_f0,
-                  e->t_f1,  e->t_s4};
+  void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.fresh_flag, D.occ,
+                  D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs,      D.fresh,
+                  D.vis,     D.cand,     D.wg_upd, D.pixA,     D.pixB,    D.visbits,    D.wgcnt,
+                  e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
+                  e->q_sel,  e->q_count, e->q_out,   e->t_keys, e->t_recs,    e->t_count,
+                  e->t_i32,  e->t_u32,   e->t_f0,    e->t_f1,   e->t_s4};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->h_ctr) (void)hipHostFree(e->h_ctr);
@@ -186,31 +184,11 @@ int ensure_test_cap(tsdf_engine* e, int n) {
   return TSDF_OK;
 }
 
-// ordered compaction of `nwords` 64-bit words into `out`, count to `out_count` (device)
-int launch_compact(tsdf_engine* e, unsigned long long* bits, int nwords, int32_t* out,
-                   int32_t* out_count) {
-  const int nwg = (nwords + 255) / 256;
-  if (nwg > e->wgcnt_cap) {
-    set_error("compaction grid exceeds wgcnt capacity");
-    return TSDF_ERR_INVALID_ARG;
-  }
-  hipLaunchKernelGGL(k_compact_count, dim3(nwg), dim3(256), 0, e->stream, bits, nwords,
-                     e->D.wgcnt);
-  hipLaunchKernelGGL(k_compact_emit, dim3(nwg), dim3(256), 0, e->stream, bits, nwords,
-                     e->D.wgcnt, nwg, out, out_count);
-  LAUNCH_OK("compaction");
-  return TSDF_OK;
-}
-
-// order bits -> resolver -> fresh block init (shared by integrate and the hash_allocate test op)
-int launch_allocate_tail(tsdf_engine* e, int64_t order_bits, int count_stats) {
-  hipLaunchKernelGGL(k_order_mark, dim3(256), dim3(256), 0, e->stream, e->D);
-  const int nwords = (int)((order_bits + 63) / 64);
-  int rc = launch_compact(e, e->D.obits, nwords, e->D.sorted, &e->D.ctr->n_sorted);
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_resolve_alloc, dim3(1), dim3(kResolveThreads), 0, e->stream, e->D,
-                     count_stats);
-  hipLaunchKernelGGL(k_fresh_init, dim3(512), dim3(256), 0, e->stream, e->D);
+int launch_resolve_alloc(tsdf_engine* e, uint32_t range, int frame_mode) {
+  hipLaunchKernelGGL(k_resolve_alloc, dim3(1), dim3(kResolveThreads), 0, e->stream, e->D, range,
+                     frame_mode);
+  if (!frame_mode)
+    hipLaunchKernelGGL(k_fresh_init, dim3(512), dim3(256), 0, e->stream, e->D);
   LAUNCH_OK("allocate");
   return TSDF_OK;
 }
@@ -283,14 +261,13 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   // DDA samples per pixel: step_grid = ceil(max|2 trunc dir / voxel| / 8) + 1 (voxel_tsdf.cu:136)
   e->maxs = (int)std::ceil(2.0 * cfg.truncation / cfg.voxel_size * 1.0001 / kBlockLen) + 1;
   e->max_pixels = (int64_t)cfg.max_width * cfg.max_height;
-  e->obits_bits = e->max_pixels * e->maxs;
-  if (e->obits_bits >= (1ll << 31)) {
+  e->order_range = e->max_pixels * e->maxs;
+  if (e->maxs > kMaxDdaSamples || e->order_range > kMaxOrderRange) {
     delete e;
-    set_error("tsdf_create: image too large for the candidate order space");
+    set_error("tsdf_create: truncation / voxel ratio or image size beyond the supported "
+              "candidate order space (maxs <= 6, width*height*maxs <= 8M)");
     return TSDF_ERR_INVALID_ARG;
   }
-  e->obits_words = (int)((e->obits_bits + 63) / 64);
-  e->wgcnt_cap = std::max<int>((e->obits_words + 255) / 256, (int)(kOccWords / 256)) + 8;
   const int nb = 1 << cfg.num_block_bits;
   EngineDev& D = e->D;
   D.nblocks = nb;
@@ -309,24 +286,23 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   } while (0)
   ALLOC(D.table, kNumEntry);
   ALLOC(D.lock_tag, kNumBucket);
-  ALLOC(D.claim, kNumBucket);
   ALLOC(D.heap, nb);
   ALLOC(D.pool, (size_t)nb * kBlockBytes);
+  ALLOC(D.fresh_flag, nb);
   ALLOC(D.occ, kOccWords);
   ALLOC(D.ctr, 1);
   ALLOC(D.nk_key, kNewKeyCap);
   ALLOC(D.nk_order, kNewKeyCap);
   ALLOC(D.nk_list, kNewKeyCap);
-  ALLOC(D.obits, e->obits_words);
-  ALLOC(D.order_slot, e->obits_bits);
-  ALLOC(D.sorted, kNewKeyCap);
+  ALLOC(D.pairs, kNewKeyCap);
   ALLOC(D.fresh, kNewKeyCap);
-  ALLOC(D.visbits, kOccWords);
-  ALLOC(D.wgcnt, e->wgcnt_cap);
   ALLOC(D.vis, nb);
-  ALLOC(D.candbits, (nb + 63) / 64);
   ALLOC(D.cand, nb);
-  ALLOC(D.pix, e->max_pixels);
+  ALLOC(D.wg_upd, kIntegrateGrid);
+  ALLOC(D.pixA, e->max_pixels);
+  ALLOC(D.pixB, e->max_pixels);
+  ALLOC(D.visbits, kOccWords);
+  ALLOC(D.wgcnt, kOccWords / 256);
   ALLOC(e->s_rgb, e->max_pixels * 3);
   ALLOC(e->s_depth, e->max_pixels);
   ALLOC(e->s_ht, e->max_pixels);
@@ -349,13 +325,11 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   hipStream_t s = e->stream;
   bool ok = true;
   ok &= hipMemsetAsync(D.lock_tag, 0, sizeof(uint32_t) * kNumBucket, s) == hipSuccess;
-  ok &= hipMemsetAsync(D.claim, 0, sizeof(unsigned long long) * kNumBucket, s) == hipSuccess;
   ok &= hipMemsetAsync(D.pool, 0, (size_t)nb * kBlockBytes, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.fresh_flag, 0, (size_t)nb, s) == hipSuccess;
   ok &= hipMemsetAsync(D.occ, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
   ok &= hipMemsetAsync(D.nk_key, 0, sizeof(unsigned long long) * kNewKeyCap, s) == hipSuccess;
   ok &= hipMemsetAsync(D.nk_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
-  ok &= hipMemsetAsync(D.obits, 0, sizeof(unsigned long long) * e->obits_words, s) == hipSuccess;
-  ok &= hipMemsetAsync(D.candbits, 0, sizeof(unsigned long long) * ((nb + 63) / 64), s) == hipSuccess;
   ok &= hipMemsetAsync(D.visbits, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
   DevCounters c0{};
   c0.free_count = nb;
@@ -433,24 +407,20 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
   hipLaunchKernelGGL(k_ingest_dda, dim3((W + 15) / 16, (H + 15) / 16), dim3(256), 0, s, e->D, P,
                      depth, rgb, ht, lt);
   LAUNCH_OK("k_ingest_dda");
-  int rc = launch_allocate_tail(e, (int64_t)np * e->maxs, 1);
+  int rc = launch_resolve_alloc(e, (uint32_t)(np * e->maxs), 1);
   if (rc) return rc;
   if (ev) HIP_OK(hipEventRecord((*ev)[1], s));
   // ---- visibility (voxel_tsdf.cu:388-397) ----
-  hipLaunchKernelGGL(k_vis_count, dim3(kOccWords / 256), dim3(256), 0, s, e->D, P);
-  hipLaunchKernelGGL(k_vis_emit, dim3(kOccWords / 256), dim3(256), 0, s, e->D, e->D.vis,
-                     &e->D.ctr->n_vis);
-  LAUNCH_OK("visibility");
+  hipLaunchKernelGGL(k_vis, dim3(kOccWords / 256), dim3(256), 0, s, e->D, P);
+  LAUNCH_OK("k_vis");
   if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
   // ---- update (voxel_tsdf.cu:474-481) ----
-  hipLaunchKernelGGL(k_integrate, dim3(1024), dim3(256), 0, s, e->D, P);
+  hipLaunchKernelGGL(k_integrate, dim3(kIntegrateGrid), dim3(256), 0, s, e->D, P);
   LAUNCH_OK("k_integrate");
   if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
   // ---- space carving (voxel_tsdf.cu:483-488) ----
-  rc = launch_compact(e, e->D.candbits, (e->D.nblocks + 63) / 64, e->D.cand, &e->D.ctr->n_cand);
-  if (rc) return rc;
   hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kResolveThreads), 0, s, e->D, e->D.cand,
-                     &e->D.ctr->n_cand, e->D.vis, kResolveThreads, 1);
+                     &e->D.ctr->n_cand, 0);
   LAUNCH_OK("k_resolve_delete");
   if (ev) HIP_OK(hipEventRecord((*ev)[4], s));
   return TSDF_OK;
@@ -638,8 +608,7 @@ int tsdf_debug_dump(tsdf_engine* e, int16_t* pos_off, int32_t* idx, int32_t* hea
 }
 
 int tsdf_hash_allocate(tsdf_engine* e, const int16_t* keys, int n) {
-  if (!e || n < 0 || (n > 0 && !keys) || n > (int)kNewKeyCap || (int64_t)n > e->obits_bits)
-    return TSDF_ERR_INVALID_ARG;
+  if (!e || n < 0 || (n > 0 && !keys) || n > (int)kNewKeyCap) return TSDF_ERR_INVALID_ARG;
   if (n == 0) return TSDF_OK;
   HIP_OK(hipSetDevice(e->device));
   int rc = ensure_test_cap(e, n);
@@ -648,7 +617,7 @@ int tsdf_hash_allocate(tsdf_engine* e, const int16_t* keys, int n) {
   hipLaunchKernelGGL(k_keys_to_newset, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->D,
                      e->t_keys, n);
   LAUNCH_OK("k_keys_to_newset");
-  rc = launch_allocate_tail(e, n, 0);
+  rc = launch_resolve_alloc(e, (uint32_t)n, 0);
   if (rc) return rc;
   HIP_OK(hipStreamSynchronize(e->stream));
   return TSDF_OK;
@@ -672,7 +641,7 @@ int tsdf_hash_delete(tsdf_engine* e, const int16_t* keys, int n) {
   HIP_OK(hipMemcpyAsync(e->t_recs, recs.data(), sizeof(VisRec) * n, hipMemcpyHostToDevice, e->stream));
   HIP_OK(hipMemcpyAsync(e->t_count, &n, sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
   hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kResolveThreads), 0, e->stream, e->D,
-                     (const int32_t*)nullptr, e->t_count, e->t_recs, 1, 0);
+                     e->t_recs, e->t_count, 1);
   LAUNCH_OK("k_resolve_delete");
   HIP_OK(hipStreamSynchronize(e->stream));
   return TSDF_OK;

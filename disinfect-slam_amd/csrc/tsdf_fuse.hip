@@ -1,0 +1,313 @@
+// tsdf_fuse.hip -- per-frame visibility, the fused integrate kernel and the space-carving resolver.
+#include "tsdf_block.h"
+#include "tsdf_kernels.h"
+
+namespace tsdf {
+
+// ---------------------------------------------------------------------------------------------
+// k_vis: check_visibility_kernel (voxel_tsdf.cu:82-93) over the 512 KiB occupancy bitmap instead
+// of the 48 MiB table: every allocated block with any corner in view (no depth test) is appended
+// to the visible list (one atomic per wave). Order is irrelevant to the update; the carving
+// resolver restores the reference's entry order for the deletes.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_vis(EngineDev D, FrameParams P) {
+  const int w = blockIdx.x * 256 + threadIdx.x;  // kOccWords == 256 * 256
+  unsigned long long occ = D.occ[w], vis = 0ull;
+  unsigned long long scan = occ;
+  while (scan) {
+    const int b = __ffsll((long long)scan) - 1;
+    scan &= scan - 1;
+    const Ent en = load_ent(D.table, (uint32_t)(w * 64 + b));
+    if (block_visible<false>(P, en.x, en.y, en.z)) vis |= 1ull << b;
+  }
+  // one atomic per workgroup: a single hot counter serialises at ~90 adds/us (MI355X_MICROARCH)
+  __shared__ int s_scan[4];
+  __shared__ int s_base;
+  const int cnt = __popcll(vis);
+  int total;
+  const int excl = block_excl_scan(cnt, s_scan, &total);
+  if (threadIdx.x == 0) s_base = total ? atomicAdd(&D.ctr->n_vis, total) : 0;
+  __syncthreads();
+  int pos = s_base + excl;
+  while (vis) {
+    const int b = __ffsll((long long)vis) - 1;
+    vis &= vis - 1;
+    const uint32_t e = (uint32_t)(w * 64 + b);
+    const Ent en = load_ent(D.table, e);
+    VisRec r;
+    r.x = en.x;
+    r.y = en.y;
+    r.z = en.z;
+    r.pad = 0;
+    r.idx = en.idx;
+    r.entry = (int32_t)e;
+    D.vis[pos++] = r;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_integrate: tsdf_integrate_kernel (voxel_tsdf.cu:149-205) + the space_carving_kernel minimum
+// (:207-230) fused. Two waves per visible 8^3 block, 4 voxels per lane: lane l of wave half h owns
+// voxels v = 256h + 4l .. +3 (x = 4(l&1)+j, y = (l>>1)&7, z = l>>4 + 4h), so each of the three
+// state arrays moves as one 16-B-per-lane, 1-KiB-per-wave access inside the block's contiguous
+// 6-KiB record. Pixel data is two gathers per voxel (16 B + 8 B, L2 resident). Blocks allocated
+// this frame (fresh_flag) start from AquireBlock's state (voxel_mem.cu:43-51) in registers.
+// Carve candidates (min |tsdf| >= 0.9) are appended with their hash-entry index.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float comp(const float4& v, int j) {
+  return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+}
+__device__ __forceinline__ void setc(float4& v, int j, float f) {
+  if (j == 0) v.x = f; else if (j == 1) v.y = f; else if (j == 2) v.z = f; else v.w = f;
+}
+__device__ __forceinline__ uint32_t compu(const uint4& v, int j) {
+  return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+}
+__device__ __forceinline__ void setu(uint4& v, int j, uint32_t f) {
+  if (j == 0) v.x = f; else if (j == 1) v.y = f; else if (j == 2) v.z = f; else v.w = f;
+}
+
+__global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
+  __shared__ float s_min[4];
+  __shared__ int s_upd[4];
+  const int lane = lane_id();
+  const int wave = threadIdx.x >> 6;
+  const int pair = wave >> 1, hf = wave & 1;
+  const int nvis = D.ctr->n_vis;
+  const int rx0 = (lane & 1) * 4, ry = (lane >> 1) & 7, rz = (lane >> 4) + 4 * hf;
+  const int off = (hf * 256 + lane * 4) * 4;
+  const float neg_trunc = -P.trunc;
+  int my_upd = 0;
+  for (int base = blockIdx.x * 2; base < nvis; base += gridDim.x * 2) {
+    const int b = base + pair;
+    float mn = __builtin_inff();
+    bool fresh = false;
+    int32_t pidx = 0;
+    if (b < nvis) {
+      const VisRec r = D.vis[__builtin_amdgcn_readfirstlane(b)];
+      pidx = r.idx;
+      uint8_t* blk = D.pool + (size_t)pidx * kBlockBytes;
+      float4 ts = *reinterpret_cast<const float4*>(blk + off);
+      float4 pr = *reinterpret_cast<const float4*>(blk + kProbOffset + off);
+      uint4 cw = *reinterpret_cast<const uint4*>(blk + kRgbwOffset + off);
+      fresh = D.fresh_flag[pidx] != 0;
+      if (fresh) {
+        ts = make_float4(-1.f, -1.f, -1.f, -1.f);
+        pr = make_float4(.5f, .5f, .5f, .5f);
+        cw.x &= 0x00FFFFFFu;
+        cw.y &= 0x00FFFFFFu;
+        cw.z &= 0x00FFFFFFu;
+        cw.w &= 0x00FFFFFFu;
+      }
+      const int16_t ax0 = (int16_t)(r.x << kBlockLenBits), ay = (int16_t)((r.y << kBlockLenBits) + ry),
+                    az = (int16_t)((r.z << kBlockLenBits) + rz);
+      const float fy = (float)ay * P.voxel, fz = (float)az * P.voxel;
+      int upd_mask = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int16_t ax = (int16_t)(ax0 + rx0 + j);
+        const f3 pw = {(float)ax * P.voxel, fy, fz};
+        const f3 pc = se3_apply(P.cq, P.ct, pw);
+        const float hx = P.fx * pc.x + P.cx * pc.z;
+        const float hy = P.fy * pc.y + P.cy * pc.z;
+        const float hz = pc.z;
+        const int u = f2i(roundf(hx / hz));
+        const int v = f2i(roundf(hy / hz));
+        float tsdf = comp(ts, j);
+        if (u >= 0 && u < P.W && v >= 0 && v < P.H) {
+          const int img = v * P.W + u;
+          const float4 px = D.pixA[img];
+          const float d = px.x;
+          if (!(d == 0 || d > P.max_depth)) {
+            const float sdf = px.y * (d - hz);
+            if (sdf > neg_trunc) {
+              const float2 lg = D.pixB[img];
+              const float tsdf_new = fminf(1.0f, sdf / P.trunc);
+              const uint32_t c_old = compu(cw, j);
+              const uint32_t c_new = __float_as_uint(px.w);
+              const float w_new = px.z;
+              const float w_old = (float)(c_old >> 24);
+              const float wc = w_old + w_new;
+              const float r0 = ((float)(c_old & 0xFF) * w_old + (float)(c_new & 0xFF) * w_new) / wc;
+              const float r1 = ((float)((c_old >> 8) & 0xFF) * w_old +
+                                (float)((c_new >> 8) & 0xFF) * w_new) / wc;
+              const float r2 = ((float)((c_old >> 16) & 0xFF) * w_old +
+                                (float)((c_new >> 16) & 0xFF) * w_new) / wc;
+              tsdf = (tsdf * w_old + tsdf_new * w_new) / wc;
+              const uint32_t wt = f2u8(fminf(roundf(wc), 40.0f));
+              const uint32_t c = (uint32_t)f2u8(roundf(r0)) | ((uint32_t)f2u8(roundf(r1)) << 8) |
+                                 ((uint32_t)f2u8(roundf(r2)) << 16) | (wt << 24);
+              const float p = comp(pr, j);
+              const float pos = expf((w_old * logf(p) + w_new * lg.x) / wc);
+              const float neg = expf((w_old * logf(1.0f - p) + w_new * lg.y) / wc);
+              setc(ts, j, tsdf);
+              setc(pr, j, pos / (pos + neg));
+              setu(cw, j, c);
+              upd_mask |= 1 << j;
+            }
+          }
+        }
+        mn = fminf(mn, fabsf(tsdf));
+      }
+      if (upd_mask || fresh) {
+        *reinterpret_cast<float4*>(blk + off) = ts;
+        *reinterpret_cast<float4*>(blk + kProbOffset + off) = pr;
+        *reinterpret_cast<uint4*>(blk + kRgbwOffset + off) = cw;
+      }
+      my_upd += __popc(upd_mask);
+    }
+    mn = wave_min(mn);
+    if (lane == 0) s_min[wave] = mn;
+    __syncthreads();
+    if (hf == 0 && lane == 0 && b < nvis) {
+      const float m2 = fminf(s_min[wave], s_min[wave + 1]);
+      if (fresh) D.fresh_flag[pidx] = 0;
+      if (m2 >= 0.9f) {  // space_carving_kernel threshold (voxel_tsdf.cu:227, :485)
+        const int k = atomicAdd(&D.ctr->n_cand, 1);
+        D.cand[k] = D.vis[b];
+      }
+    }
+    __syncthreads();
+  }
+  // updated-voxel count: one plain store per workgroup, summed by k_resolve_delete (no atomics)
+  const int tot = wave_sum(my_upd);
+  if (lane == 0) s_upd[wave] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) D.wg_upd[blockIdx.x] = s_upd[0] + s_upd[1] + s_upd[2] + s_upd[3];
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_resolve_delete: VoxelHashTable::Delete (voxel_hash.cu:122-171) for every carve candidate in
+// hash-entry order (the reference deletes from the entry-ordered visible list). Slot-0 deletes are
+// lock free and touch only their own entry; list-head / list-element deletes lock the key's
+// bucket and only the first of them per bucket proceeds. The two kinds modify disjoint entries,
+// so a whole 1024-candidate round commits at once; ReleaseBlock's stack order is a prefix sum.
+// direct: the test path -- recs[0..*count) are keys in list order, one key per round.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
+                                                                    const VisRec* __restrict__ recs,
+                                                                    const int32_t* __restrict__ count,
+                                                                    int direct) {
+  __shared__ ResolveLds L;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    L.epoch = D.ctr->lock_epoch + 1;
+    D.ctr->lock_epoch = L.epoch;
+    L.sfree = D.ctr->free_count;
+    L.nalloc = 0;  // deletions
+  }
+  claims_clear(L);
+  if (!direct) {  // voxels updated by k_integrate: sum of its per-workgroup counts
+    int u = 0;
+    for (int i = t; i < kIntegrateGrid; i += kResolveThreads) u += D.wg_upd[i];
+    int tot;
+    (void)block_excl_scan(u, L.scan, &tot);
+    if (t == 0) D.ctr->last_updated = (unsigned long long)tot;
+  }
+  __syncthreads();
+  const int n = *count;
+  auto keyf = [&](int i) -> uint32_t { return (uint32_t)recs[i].entry; };
+  const int width = direct ? 1 : stream_prepare(L, n, kNumEntry, keyf);
+  const int nbatch = direct ? n : (n <= kBatch ? (n > 0 ? 1 : 0) : ((n - 1) >> 10) + 1);
+  for (int j = 0; j < nbatch; ++j) {
+    int m;
+    if (direct) {
+      if (t == 0) L.batch[0] = (unsigned long long)(uint32_t)j;
+      m = 1;
+      __syncthreads();
+    } else {
+      m = stream_batch(L, n, width, j, keyf);
+    }
+    for (int base = 0; base < m; base += kResolveThreads) {
+      const bool have = base + t < m;
+      int kind = 0;  // 1 slot 0, 2 list head, 3 list element
+      uint32_t A = 0, prev = 0, cur = 0;
+      Ent ecur = {}, eprev = {};
+      if (have) {
+        const VisRec r = recs[(int)(L.batch[base + t] & 0xFFFFFFFFu)];
+        A = hash_block(r.x, r.y, r.z);
+        const Ent s0 = load_ent(D.table, 2 * A);
+        if (s0.x == r.x && s0.y == r.y && s0.z == r.z && s0.idx >= 0) {
+          kind = 1;
+          cur = 2 * A;
+          ecur = s0;
+        } else {
+          const Ent hd = load_ent(D.table, 2 * A + 1);
+          if (hd.x == r.x && hd.y == r.y && hd.z == r.z && hd.idx >= 0) {
+            kind = 2;
+            prev = 2 * A + 1;
+            eprev = hd;
+            cur = (uint32_t)(prev + (int32_t)hd.off) & kEntryMask;  // element moved into the head
+            ecur = load_ent(D.table, cur);
+          } else {
+            uint32_t last = 2 * A + 1;
+            Ent bl = hd;
+            while (bl.off) {
+              const uint32_t c = (uint32_t)(last + (int32_t)bl.off) & kEntryMask;
+              const Ent bc = load_ent(D.table, c);
+              if (bc.x == r.x && bc.y == r.y && bc.z == r.z && bc.idx >= 0) {
+                kind = 3;
+                prev = last;
+                eprev = bl;
+                cur = c;
+                ecur = bc;
+                break;
+              }
+              last = c;
+              bl = bc;
+            }
+          }
+        }
+        if (kind >= 2) claim(L, A, (uint32_t)t);
+      }
+      __syncthreads();
+      bool ok = false;
+      int32_t released = -1;
+      if (kind == 1) {
+        ok = true;
+      } else if (kind >= 2 && claim_winner(L, A) == (uint32_t)t) {
+        ok = D.lock_tag[A] != L.epoch;
+        D.lock_tag[A] = L.epoch;
+      }
+      if (ok) {
+        if (kind == 1) {  // voxel_hash.cu:126-135
+          released = ecur.idx;
+          store_off_idx(D.table, cur, 0, -1);
+        } else if (kind == 2) {  // :137-152 (cur aliases the head when the list is empty)
+          released = eprev.idx;
+          const int16_t noff = ecur.off ? (int16_t)(eprev.off + ecur.off) : (int16_t)0;
+          store_ent(D.table, prev, ecur.x, ecur.y, ecur.z, noff, ecur.idx);
+          store_off_idx(D.table, cur, 0, -1);
+        } else {  // :154-170
+          released = ecur.idx;
+          const int16_t noff = ecur.off ? (int16_t)(eprev.off + ecur.off) : (int16_t)0;
+          store_off(D.table, prev, noff);
+          store_off_idx(D.table, cur, 0, -1);
+        }
+        atomicAnd(&D.occ[cur >> 6], ~(1ull << (cur & 63)));
+      }
+      int nok;
+      const int rank = block_excl_scan(ok ? 1 : 0, L.scan, &nok);
+      if (ok) D.heap[L.sfree + rank] = released;  // ReleaseBlock (voxel_mem.cu:54-59)
+      claims_clear(L);
+      __syncthreads();
+      if (t == 0) {
+        L.sfree += nok;
+        L.nalloc += nok;
+      }
+      __syncthreads();
+    }
+  }
+  if (t == 0) {
+    D.ctr->free_count = L.sfree;
+    if (!direct) {
+      D.ctr->last_deleted = L.nalloc;
+      D.ctr->total_deleted += (unsigned long long)L.nalloc;
+      D.ctr->total_visible += (unsigned long long)D.ctr->n_vis;
+      D.ctr->total_updated += D.ctr->last_updated;
+      D.ctr->frames += 1ull;
+    }
+  }
+}
+
+}  // namespace tsdf

@@ -197,3 +197,84 @@ def render(cam: Camera, frame: int, noise: bool = True, holes: float = 0.02):
 def frames(cam: Camera, start: int, count: int, **kw):
     for f in range(start, start + count):
         yield render(cam, f, **kw)
+
+
+def render_torch(cam: Camera, frame_ids, device="cuda", noise: bool = True, holes: float = 0.02,
+                 seed: int = SEED):
+    """Same scene rendered with torch on `device` (float64 geometry) for benchmark streams.
+
+    Returns dict of stacked tensors: rgb (F,H,W,3) u8, depth/ht/lt (F,H,W) f32, and host numpy
+    q (F,4) / t (F,3) float32 cam_T_world. Noise comes from a torch generator, so the frames are
+    deterministic per (seed, frame) but not bit-identical to render(); parity tests use render().
+    """
+    import torch
+
+    H, W = cam.height, cam.width
+    F = len(frame_ids)
+    dd = dict(device=device, dtype=torch.float64)
+    v, u = torch.meshgrid(torch.arange(H, **dd), torch.arange(W, **dd), indexing="ij")
+    dc = torch.stack([(u - cam.cx) / cam.fx, (v - cam.cy) / cam.fy, torch.ones_like(u)], -1).reshape(-1, 3)
+    out = dict(
+        rgb=torch.empty((F, H, W, 3), dtype=torch.uint8, device=device),
+        depth=torch.empty((F, H, W), dtype=torch.float32, device=device),
+        ht=torch.empty((F, H, W), dtype=torch.float32, device=device),
+        lt=torch.empty((F, H, W), dtype=torch.float32, device=device),
+        q=np.zeros((F, 4), np.float32),
+        t=np.zeros((F, 3), np.float32),
+    )
+    room_min = torch.tensor(ROOM_MIN, **dd)
+    room_max = torch.tensor(ROOM_MAX, **dd)
+    pal = torch.tensor(_PALETTE, **dd)
+    touch = torch.tensor(_TOUCH_BASE, **dd)
+    gen = torch.Generator(device=device)
+    for k, f in enumerate(frame_ids):
+        (R_wc, p), (q, t) = pose(f)
+        out["q"][k], out["t"][k] = q, t
+        d = dc @ torch.tensor(R_wc.T, **dd)
+        o = torch.tensor(p, **dd)
+        inv = torch.where(d.abs() > 1e-12, 1.0 / torch.where(d == 0, torch.ones_like(d), d),
+                          torch.full_like(d, 1e12))
+        t_hi = torch.maximum((room_min - o) * inv, (room_max - o) * inv)
+        best, axis = t_hi.min(dim=1)
+        positive = d.gather(1, axis[:, None])[:, 0] > 0
+        sid = axis * 2 + positive.long()
+        for bmin, bmax, ident in BOXES:
+            t0 = (torch.tensor(bmin, **dd) - o) * inv
+            t1 = (torch.tensor(bmax, **dd) - o) * inv
+            tn = torch.minimum(t0, t1).max(dim=1).values
+            tf = torch.maximum(t0, t1).min(dim=1).values
+            hit = (tn <= tf) & (tn > 1e-6) & (tn < best)
+            best = torch.where(hit, tn, best)
+            sid = torch.where(hit, torch.full_like(sid, ident), sid)
+        for cen, rad, ident in SPHERES:
+            oc = o - torch.tensor(cen, **dd)
+            a = (d * d).sum(1)
+            b = 2.0 * (d @ oc)
+            cc = (oc @ oc) - rad * rad
+            disc = b * b - 4 * a * cc
+            ok = disc >= 0
+            sq = torch.sqrt(torch.where(ok, disc, torch.zeros_like(disc)))
+            s0 = (-b - sq) / (2 * a)
+            hit = ok & (s0 > 1e-6) & (s0 < best)
+            best = torch.where(hit, s0, best)
+            sid = torch.where(hit, torch.full_like(sid, ident), sid)
+        pts = o + best[:, None] * d
+        gen.manual_seed(seed + f)
+        depth = best
+        if noise:
+            depth = depth + 0.001 * torch.randn(depth.shape, generator=gen, **dd)
+        depth = torch.round(depth * DEPTH_FACTOR).clamp(0, 65535).to(torch.float32) / DEPTH_FACTOR
+        depth[depth > MAX_RANGE] = 0.0
+        if holes > 0:
+            depth[torch.rand(depth.shape, generator=gen, **dd) < holes] = 0.0
+        wave = torch.sin(3.1 * pts[:, 0] + 1.7 * pts[:, 1]) * torch.cos(2.3 * pts[:, 2] + 0.4 * pts[:, 0])
+        ht = (touch[sid] + 0.08 * wave).clamp(0.02, 0.98).to(torch.float32)
+        chk = torch.remainder(torch.floor(pts[:, 0] / 0.2) + torch.floor(pts[:, 1] / 0.2)
+                              + torch.floor(pts[:, 2] / 0.2), 2)
+        shade = 0.75 + 0.25 * chk
+        rgb = (pal[sid] * shade[:, None] + 10 * wave[:, None]).clamp(0, 255).to(torch.uint8)
+        out["depth"][k] = depth.reshape(H, W)
+        out["ht"][k] = ht.reshape(H, W)
+        out["lt"][k] = (1.0 - ht).reshape(H, W)
+        out["rgb"][k] = rgb.reshape(H, W, 3)
+    return out

@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Summarise a scripts/profile_integrate.sh run: per-kernel trace stats + PMC HBM bytes.
+
+gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KiB;
+FETCH_SIZE reports half the bytes of wide coalesced reads, so it is doubled.
+Writes <out>/summary.json and prints a table.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import statistics
+import sys
+
+
+def find(pattern):
+    m = glob.glob(pattern, recursive=True)
+    return m[0] if m else None
+
+
+def bench_line(path):
+    try:
+        for line in open(path):
+            line = line.strip()
+            if line.startswith("{") and '"metric"' in line:
+                return json.loads(line)
+    except OSError:
+        pass
+    return None
+
+
+def main(out):
+    res = {"kernels": {}, "pmc": {}}
+    st = find(os.path.join(out, "trace", "**", "*kernel_stats.csv"))
+    if st:
+        for r in csv.DictReader(open(st)):
+            if not re.search(r"tsdf::", r["Name"]):
+                continue
+            name = r["Name"].split("(")[0].replace("tsdf::", "")
+            res["kernels"][name] = {
+                "calls": int(r["Calls"]),
+                "avg_us": float(r["AverageNs"]) / 1e3,
+                "min_us": float(r["MinNs"]) / 1e3,
+                "max_us": float(r["MaxNs"]) / 1e3,
+                "total_ms": float(r["TotalDurationNs"]) / 1e6,
+            }
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        f = find(os.path.join(out, f"pmc_{c}", "**", "*counter_collection.csv"))
+        if not f:
+            continue
+        vals = {}
+        for r in csv.DictReader(open(f)):
+            kn = r.get("Kernel_Name", "")
+            if "tsdf::" not in kn or r.get("Counter_Name") != c:
+                continue
+            name = kn.split("(")[0].replace("tsdf::", "")
+            vals.setdefault(name, []).append(float(r["Counter_Value"]))
+        for name, v in vals.items():
+            kib = statistics.mean(v)
+            corr = 2.0 if c == "FETCH_SIZE" else 1.0
+            res["pmc"].setdefault(name, {})[c] = {"mean_kib_raw": kib, "bytes_per_launch": kib * 1024 * corr,
+                                                   "dispatches": len(v)}
+    b = bench_line(os.path.join(out, "trace_bench.log")) or bench_line(os.path.join(out, "pmc_FETCH_SIZE_bench.log"))
+    if b:
+        res["bench"] = b
+    ki = res["pmc"].get("k_integrate", {})
+    if "FETCH_SIZE" in ki and "WRITE_SIZE" in ki:
+        res["integrate_hbm_bytes_per_launch"] = ki["FETCH_SIZE"]["bytes_per_launch"] + ki["WRITE_SIZE"]["bytes_per_launch"]
+        if b:
+            res["integrate_alg_bytes_per_launch"] = b["roofline"]["alg_bytes_per_launch"]
+    json.dump(res, open(os.path.join(out, "summary.json"), "w"), indent=1)
+    for k, v in sorted(res["kernels"].items(), key=lambda kv: -kv[1]["total_ms"]):
+        p = res["pmc"].get(k, {})
+        fb = p.get("FETCH_SIZE", {}).get("bytes_per_launch")
+        wb = p.get("WRITE_SIZE", {}).get("bytes_per_launch")
+        print(f"{k:22s} calls={v['calls']:6d} avg={v['avg_us']:9.2f}us min={v['min_us']:8.2f} "
+              f"max={v['max_us']:9.2f} fetch={fb and fb / 1e6:.3}MB write={wb and wb / 1e6:.3}MB")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
