@@ -113,17 +113,38 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
     }
   }
   __syncthreads();
-  for (int sl = threadIdx.x; sl < kTileSlots; sl += 256) {
-    const unsigned long long key = s_key[sl];
-    if (!key) continue;
-    int16_t kx, ky, kz;
-    unpack_key(key, kx, ky, kz);
-    if (P.shard_count > 1 &&
-        brick_owner(kx, ky, kz, (uint32_t)P.shard_count) != (uint32_t)P.shard_index)
-      continue;
-    if (!block_visible<true>(P, kx, ky, kz)) continue;
-    if (find_entry(D.table, kx, ky, kz) >= 0) continue;
-    nk_insert(D, key, s_ord[sl]);
+  // Each wave sweeps its 64-slot strips; the few occupied slots of a strip (ballot) are tested
+  // 8 at a time with 8 lanes per key, one block corner per lane (is_block_visible<true>).
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const int grp = lane >> 3, corner = lane & 7;
+  for (int strip = wave; strip < kTileSlots / 64; strip += 4) {
+    const unsigned long long skey = s_key[strip * 64 + lane];
+    const unsigned long long occ = __ballot(skey != 0ull);
+    const int n = __popcll(occ);
+    for (int base = 0; base < n; base += 8) {
+      const int want = base + grp;  // rank of the occupied slot this 8-lane group handles
+      int src = 0;                  // lane holding that slot: binary search on prefix popcounts
+#pragma unroll
+      for (int step = 32; step > 0; step >>= 1)
+        if (src + step < 64 && __popcll(occ & ((1ull << (src + step)) - 1ull)) <= want) src += step;
+      const unsigned long long key = __shfl(skey, src, 64);
+      bool vis = false;
+      int16_t kx = 0, ky = 0, kz = 0;
+      if (want < n) {
+        unpack_key(key, kx, ky, kz);
+        vis = voxel_visible(P, (int16_t)((int16_t)(kx << kBlockLenBits) + ((corner >> 0) & 1) * (kBlockLen - 1)),
+                            (int16_t)((int16_t)(ky << kBlockLenBits) + ((corner >> 1) & 1) * (kBlockLen - 1)),
+                            (int16_t)((int16_t)(kz << kBlockLenBits) + ((corner >> 2) & 1) * (kBlockLen - 1)));
+      }
+      const unsigned long long bal = __ballot(vis);
+      if (want < n && corner == 0 && ((bal >> (lane & ~7)) & 0xFFull) == 0xFFull) {
+        if (P.shard_count > 1 &&
+            brick_owner(kx, ky, kz, (uint32_t)P.shard_count) != (uint32_t)P.shard_index)
+          continue;
+        if (find_entry(D.table, kx, ky, kz) >= 0) continue;
+        nk_insert(D, key, s_ord[strip * 64 + src]);
+      }
+    }
   }
 }
 

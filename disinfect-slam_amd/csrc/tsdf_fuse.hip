@@ -137,9 +137,13 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
               const uint32_t wt = f2u8(fminf(roundf(wc), 40.0f));
               const uint32_t c = (uint32_t)f2u8(roundf(r0)) | ((uint32_t)f2u8(roundf(r1)) << 8) |
                                  ((uint32_t)f2u8(roundf(r2)) << 16) | (wt << 24);
+              // semantic log-odds fusion (voxel_tsdf.cu:196-202): hardware v_log / v_exp and a
+              // v_rcp scale (error ~1e-7 against the 1e-4 probability tolerance); the final
+              // normalisation stays an IEEE divide so p stays exactly 0.5 when ht == lt.
               const float p = comp(pr, j);
-              const float pos = expf((w_old * logf(p) + w_new * lg.x) / wc);
-              const float neg = expf((w_old * logf(1.0f - p) + w_new * lg.y) / wc);
+              const float iwc = __builtin_amdgcn_rcpf(wc);
+              const float pos = __expf((w_old * __logf(p) + w_new * lg.x) * iwc);
+              const float neg = __expf((w_old * __logf(1.0f - p) + w_new * lg.y) * iwc);
               setc(ts, j, tsdf);
               setc(pr, j, pos / (pos + neg));
               setu(cw, j, c);

@@ -74,8 +74,10 @@ def main(out):
         p = res["pmc"].get(k, {})
         fb = p.get("FETCH_SIZE", {}).get("bytes_per_launch")
         wb = p.get("WRITE_SIZE", {}).get("bytes_per_launch")
+        fs = "n/a" if fb is None else f"{fb / 1e6:.3f}MB"
+        ws = "n/a" if wb is None else f"{wb / 1e6:.3f}MB"
         print(f"{k:22s} calls={v['calls']:6d} avg={v['avg_us']:9.2f}us min={v['min_us']:8.2f} "
-              f"max={v['max_us']:9.2f} fetch={fb and fb / 1e6:.3}MB write={wb and wb / 1e6:.3}MB")
+              f"max={v['max_us']:9.2f} fetch={fs} write={ws}")
 
 
 if __name__ == "__main__":
