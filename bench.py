@@ -107,6 +107,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.warmup, nframes):
         step(i)
+    t_enq = time.perf_counter()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist:
@@ -186,6 +187,7 @@ def main():
                 "integrate": round(prof["ms_integrate"] / a.steps, 4),
                 "carve": round(prof["ms_carve"] / a.steps, 4),
             },
+            "host_enqueue_ms_per_step": round((t_enq - t0) / a.steps * 1e3, 4),
             "avg_visible_blocks": round(prof["sum_visible"] / a.steps, 1),
             "avg_updated_voxels": round(prof["sum_updated"] / a.steps, 1),
             "active_blocks": st["active_blocks"],

@@ -53,11 +53,13 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
                                                     const float* __restrict__ lt) {
   __shared__ unsigned long long s_key[kTileSlots];
   __shared__ uint32_t s_ord[kTileSlots];
+  TSDF_STAMP(D, 0, 0);
   for (int i = threadIdx.x; i < kTileSlots; i += 256) {
     s_key[i] = 0ull;
     s_ord[i] = 0xFFFFFFFFu;
   }
   __syncthreads();
+  TSDF_STAMP(D, 0, 1);
   const int x = blockIdx.x * 16 + (threadIdx.x & 15);
   const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
   if (x < P.W && y < P.H) {
@@ -69,17 +71,20 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
     const float l = lt ? lt[i] : 1.0f;
     const f3 pc = pixel_ray(P, x, y);
     const float range = sqrtf(dot3(pc, pc));  // img_depth_to_range (voxel_tsdf.cu:120)
-    const float w_new = (1.0f - d / P.max_depth) * 4.0f;
+    const float w_new = (1.0f - quot_const(d, P.max_depth, P.inv_max_depth)) * 4.0f;
     D.pixA[i] = make_float4(d, range, w_new, __uint_as_float(c));
     D.pixB[i] = make_float2(logf(h), logf(l));
+    TSDF_STAMP(D, 0, 2);
     if (!(d == 0 || d > P.max_depth)) {
       const f3 pcd = {pc.x * d, pc.y * d, pc.z * d};
       const f3 pw = se3_apply(P.wq, P.wt, pcd);
       const f3 dc = {pc.x / range, pc.y / range, pc.z / range};
       const f3 dw = qrot(P.wq, dc);
       const f3 sw = {pw.x - dw.x * P.trunc, pw.y - dw.y * P.trunc, pw.z - dw.z * P.trunc};
-      const f3 dg = {dw.x / P.voxel, dw.y / P.voxel, dw.z / P.voxel};
-      const f3 sg = {sw.x / P.voxel, sw.y / P.voxel, sw.z / P.voxel};
+      const f3 dg = {quot_const(dw.x, P.voxel, P.inv_voxel), quot_const(dw.y, P.voxel, P.inv_voxel),
+                     quot_const(dw.z, P.voxel, P.inv_voxel)};
+      const f3 sg = {quot_const(sw.x, P.voxel, P.inv_voxel), quot_const(sw.y, P.voxel, P.inv_voxel),
+                     quot_const(sw.z, P.voxel, P.inv_voxel)};
       const float two_trunc = 2 * P.trunc;
       const f3 rg = {two_trunc * dg.x, two_trunc * dg.y, two_trunc * dg.z};
       const int step_grid =
@@ -112,7 +117,9 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
       }
     }
   }
+  TSDF_STAMP(D, 0, 3);
   __syncthreads();
+  TSDF_STAMP(D, 0, 4);
   // Each wave sweeps its 64-slot strips; the few occupied slots of a strip (ballot) are tested
   // 8 at a time with 8 lanes per key, one block corner per lane (is_block_visible<true>).
   const int lane = lane_id(), wave = threadIdx.x >> 6;
@@ -146,6 +153,7 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
       }
     }
   }
+  TSDF_STAMP(D, 0, 5);
 }
 
 // test path: keys[n] in list order (one VoxelHashTable::Allocate launch, voxel_hash_test.cu)
@@ -175,6 +183,7 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, 
                                                                    int frame_mode) {
   __shared__ ResolveLds L;
   const int t = threadIdx.x;
+  TSDF_STAMP(D, 1, 0);
   if (t == 0) {
     L.epoch = D.ctr->lock_epoch + 1;
     D.ctr->lock_epoch = L.epoch;
@@ -194,8 +203,10 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, 
   const int width = stream_prepare(L, n, range, keyf);
   const int nbatch = n <= kBatch ? (n > 0 ? 1 : 0) : ((n - 1) >> 10) + 1;
   int rounds = 0;
+  TSDF_STAMP(D, 1, 1);
   for (int j = 0; j < nbatch; ++j) {
     const int m = stream_batch(L, n, width, j, keyf);
+    TSDF_STAMP(D, 1, 2);
     if (t == 0) L.base = 0;
     __syncthreads();
     while (L.base < m) {
@@ -316,6 +327,7 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, 
       __syncthreads();
     }
   }
+  TSDF_STAMP(D, 1, 3);
   if (t == 0) {
     D.ctr->free_count = L.sfree;
     D.ctr->n_fresh = L.nfresh;

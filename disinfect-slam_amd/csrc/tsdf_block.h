@@ -187,3 +187,23 @@ __device__ int stream_batch(ResolveLds& L, int n, int width, int j, KeyFn keyf) 
 }
 
 }  // namespace tsdf
+
+// ---------------------------------------------------------------------------------------------
+// Diagnostic build only (make DIAG=1): per-workgroup s_memrealtime stamps (100 MHz) at phase
+// boundaries, written by thread 0 to D.dbg[((kernel * kDiagMaxWg) + wg) * kDiagStamps + k].
+// ---------------------------------------------------------------------------------------------
+#ifdef TSDF_DIAG_STAMPS
+#define TSDF_STAMP(D, kern, k)                                                                 \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && (D).dbg) {                                                         \
+      const unsigned wg_ = blockIdx.y * gridDim.x + blockIdx.x;                                \
+      if (wg_ < (unsigned)::tsdf::kDiagMaxWg)                                                  \
+        (D).dbg[((kern) * ::tsdf::kDiagMaxWg + wg_) * ::tsdf::kDiagStamps + (k)] =             \
+            __builtin_amdgcn_s_memrealtime();                                                  \
+    }                                                                                          \
+  } while (0)
+#else
+#define TSDF_STAMP(D, kern, k) \
+  do {                         \
+  } while (0)
+#endif

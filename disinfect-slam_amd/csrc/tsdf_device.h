@@ -58,6 +58,7 @@ struct FrameParams {
   quatf wq;                  // world_T_cam
   f3 wt;
   float voxel, trunc, max_depth;
+  float inv_trunc, inv_voxel, inv_max_depth;  // RN(1 / .), host IEEE divides (quot_const)
   int W, H;
   int maxs;                  // DDA samples reserved per pixel in the candidate order space
   int shard_index, shard_count;
@@ -120,22 +121,48 @@ __device__ __forceinline__ f3 se3_apply(quatf q, f3 t, f3 v) {  // SE3::Apply, l
   r.z = r.z + t.z;
   return r;
 }
-__device__ __forceinline__ int32_t f2i(float f) {  // cvt.rzi.s32.f32 semantics
-  if (f != f) return 0;
-  if (f >= 2147483648.0f) return 2147483647;
-  if (f <= -2147483648.0f) return (-2147483647 - 1);
-  return (int32_t)f;
+// float -> integer conversions with PTX cvt.rzi semantics (truncate, saturate, NaN -> 0), which
+// is exactly what v_cvt_i32_f32 / v_cvt_u32_f32 do in hardware.
+__device__ __forceinline__ int32_t f2i(float f) {  // cvt.rzi.s32.f32
+  int32_t r;
+  asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(f));
+  return r;
 }
-__device__ __forceinline__ int16_t f2s(float f) {
-  if (f != f) return 0;
-  if (f >= 32767.0f) return 32767;
-  if (f <= -32768.0f) return -32768;
-  return (int16_t)f;
+__device__ __forceinline__ int16_t f2s(float f) {  // cvt.rzi.s16.f32
+  return (int16_t)min(32767, max(-32768, f2i(f)));
 }
-__device__ __forceinline__ uint8_t f2u8(float f) {
-  if (!(f > 0.0f)) return 0;
-  if (f >= 255.0f) return 255;
-  return (uint8_t)f;
+__device__ __forceinline__ uint8_t f2u8(float f) {  // cvt.rzi.u8.f32
+  uint32_t r;
+  asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(f));
+  return (uint8_t)min(r, 255u);
+}
+
+// ---- exact quotients without the full IEEE divide sequence (11 VALU ops). Both helpers return
+// bit-for-bit what the correctly rounded a / b would give; libtsdf_selfcheck checks them against
+// the IEEE divide exhaustively / on adversarial samples (tests/test_gpu_numerics.py). ----
+
+// roundf(a / b) from the reciprocal estimate rb = v_rcp(b) (1 ulp): |a*rb - RN(a/b)| < 2^-21 |q|,
+// so rounding the estimate gives the same integer unless it lies within 2^-20 |q| of a rounding
+// boundary (k + 1/2), or is not finite and below 2^16 -- those lanes take the IEEE divide.
+__device__ __forceinline__ float round_quot(float a, float b, float rb) {
+  const float q = a * rb;
+  const float fq = fabsf(q);
+  const float frac = fq - truncf(fq);
+  if (__builtin_expect(fq < 65536.0f && fabsf(frac - 0.5f) > fq * 0x1p-20f, 1)) return roundf(q);
+  return roundf(a / b);
+}
+
+// RN(a / b) for a frame-constant divisor b with rb = RN(1 / b) computed on the host: Markstein's
+// correction q + (a - b q) rb (two fma) is the correctly rounded quotient when no intermediate
+// leaves the normal range; |a| outside [2^-100, 2^100] (incl. 0, inf, NaN) takes the IEEE divide.
+__device__ __forceinline__ float quot_const(float a, float b, float rb) {
+  const float fa = fabsf(a);
+  if (__builtin_expect(fa > 0x1p-100f && fa < 0x1p100f, 1)) {
+    const float q = a * rb;
+    const float r = __builtin_fmaf(-q, b, a);
+    return __builtin_fmaf(r, rb, q);
+  }
+  return a / b;
 }
 
 // voxel_hash.cu:31-35

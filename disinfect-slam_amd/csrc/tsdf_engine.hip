@@ -123,7 +123,7 @@ void free_all(tsdf_engine* e) {
   EngineDev& D = e->D;
   void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.fresh_flag, D.occ,
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs,      D.fresh,
-                  D.vis,     D.cand,     D.wg_upd, D.pixA,     D.pixB,    D.visbits,    D.wgcnt,
+                  D.vis,     D.cand,     D.wg_upd, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
                   e->q_sel,  e->q_count, e->q_out,   e->t_keys, e->t_recs,    e->t_count,
                   e->t_i32,  e->t_u32,   e->t_f0,    e->t_f1,   e->t_s4};
@@ -158,6 +158,9 @@ FrameParams make_params(const tsdf_engine* e, const tsdf_intrinsics* K, int W, i
   P.wt = h_qrot(P.wq, nt);
   P.voxel = e->cfg.voxel_size;
   P.trunc = e->cfg.truncation;
+  P.inv_trunc = 1.0f / e->cfg.truncation;
+  P.inv_voxel = 1.0f / e->cfg.voxel_size;
+  P.inv_max_depth = 1.0f / max_depth;
   P.max_depth = max_depth;
   P.W = W;
   P.H = H;
@@ -303,6 +306,9 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.pixB, e->max_pixels);
   ALLOC(D.visbits, kOccWords);
   ALLOC(D.wgcnt, kOccWords / 256);
+  ALLOC(D.dbg, (size_t)kDiagKernels * kDiagMaxWg * kDiagStamps);
+  if (hipMemset(D.dbg, 0, (size_t)kDiagKernels * kDiagMaxWg * kDiagStamps * 8) != hipSuccess)
+    return fail(TSDF_ERR_HIP);
   ALLOC(e->s_rgb, e->max_pixels * 3);
   ALLOC(e->s_depth, e->max_pixels);
   ALLOC(e->s_ht, e->max_pixels);
@@ -546,6 +552,26 @@ int tsdf_profile_end(tsdf_engine* e, tsdf_profile* o) {
   }
   o->sum_visible = (int64_t)(e->h_ctr->total_visible - e->prof_vis0);
   o->sum_updated = (int64_t)(e->h_ctr->total_updated - e->prof_upd0);
+  return TSDF_OK;
+}
+
+int tsdf_debug_stamps(tsdf_engine* e, uint64_t* out, int64_t capacity, int* enabled) {
+  if (!e) return TSDF_ERR_INVALID_ARG;
+  HIP_OK(hipSetDevice(e->device));
+#ifdef TSDF_DIAG_STAMPS
+  if (enabled) *enabled = 1;
+#else
+  if (enabled) *enabled = 0;
+#endif
+  const int64_t n = (int64_t)kDiagKernels * kDiagMaxWg * kDiagStamps;
+  if (!out) return TSDF_OK;
+  if (capacity < n) {
+    set_error("tsdf_debug_stamps: capacity too small");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipStreamSynchronize(e->stream));
+  HIP_OK(hipMemcpy(out, e->D.dbg, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemset(e->D.dbg, 0, n * sizeof(uint64_t)));
   return TSDF_OK;
 }
 

@@ -11,6 +11,7 @@ namespace tsdf {
 // resolver restores the reference's entry order for the deletes.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_vis(EngineDev D, FrameParams P) {
+  TSDF_STAMP(D, 2, 0);
   const int w = blockIdx.x * 256 + threadIdx.x;  // kOccWords == 256 * 256
   unsigned long long occ = D.occ[w], vis = 0ull;
   unsigned long long scan = occ;
@@ -43,6 +44,7 @@ __global__ __launch_bounds__(256) void k_vis(EngineDev D, FrameParams P) {
     r.entry = (int32_t)e;
     D.vis[pos++] = r;
   }
+  TSDF_STAMP(D, 2, 1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -78,6 +80,7 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
   const int off = (hf * 256 + lane * 4) * 4;
   const float neg_trunc = -P.trunc;
   int my_upd = 0;
+  TSDF_STAMP(D, 3, 0);
   for (int base = blockIdx.x * 2; base < nvis; base += gridDim.x * 2) {
     const int b = base + pair;
     float mn = __builtin_inff();
@@ -103,6 +106,12 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
                     az = (int16_t)((r.z << kBlockLenBits) + rz);
       const float fy = (float)ay * P.voxel, fz = (float)az * P.voxel;
       int upd_mask = 0;
+      // pass 1: project the lane's 4 voxels and issue every pixel gather before any is consumed
+      // (the gathers are predicated, not branched around, so all 8 stay in flight together)
+      float hzs[4];
+      float4 px[4];
+      float2 lg[4];
+      bool inb[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int16_t ax = (int16_t)(ax0 + rx0 + j);
@@ -111,44 +120,54 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
         const float hx = P.fx * pc.x + P.cx * pc.z;
         const float hy = P.fy * pc.y + P.cy * pc.z;
         const float hz = pc.z;
-        const int u = f2i(roundf(hx / hz));
-        const int v = f2i(roundf(hy / hz));
-        float tsdf = comp(ts, j);
-        if (u >= 0 && u < P.W && v >= 0 && v < P.H) {
+        const float rz = __builtin_amdgcn_rcpf(hz);
+        const int u = f2i(round_quot(hx, hz, rz));
+        const int v = f2i(round_quot(hy, hz, rz));
+        hzs[j] = hz;
+        inb[j] = u >= 0 && u < P.W && v >= 0 && v < P.H;
+        px[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        lg[j] = make_float2(0.f, 0.f);
+        if (inb[j]) {
           const int img = v * P.W + u;
-          const float4 px = D.pixA[img];
-          const float d = px.x;
-          if (!(d == 0 || d > P.max_depth)) {
-            const float sdf = px.y * (d - hz);
-            if (sdf > neg_trunc) {
-              const float2 lg = D.pixB[img];
-              const float tsdf_new = fminf(1.0f, sdf / P.trunc);
-              const uint32_t c_old = compu(cw, j);
-              const uint32_t c_new = __float_as_uint(px.w);
-              const float w_new = px.z;
-              const float w_old = (float)(c_old >> 24);
-              const float wc = w_old + w_new;
-              const float r0 = ((float)(c_old & 0xFF) * w_old + (float)(c_new & 0xFF) * w_new) / wc;
-              const float r1 = ((float)((c_old >> 8) & 0xFF) * w_old +
-                                (float)((c_new >> 8) & 0xFF) * w_new) / wc;
-              const float r2 = ((float)((c_old >> 16) & 0xFF) * w_old +
-                                (float)((c_new >> 16) & 0xFF) * w_new) / wc;
-              tsdf = (tsdf * w_old + tsdf_new * w_new) / wc;
-              const uint32_t wt = f2u8(fminf(roundf(wc), 40.0f));
-              const uint32_t c = (uint32_t)f2u8(roundf(r0)) | ((uint32_t)f2u8(roundf(r1)) << 8) |
-                                 ((uint32_t)f2u8(roundf(r2)) << 16) | (wt << 24);
-              // semantic log-odds fusion (voxel_tsdf.cu:196-202): hardware v_log / v_exp and a
-              // v_rcp scale (error ~1e-7 against the 1e-4 probability tolerance); the final
-              // normalisation stays an IEEE divide so p stays exactly 0.5 when ht == lt.
-              const float p = comp(pr, j);
-              const float iwc = __builtin_amdgcn_rcpf(wc);
-              const float pos = __expf((w_old * __logf(p) + w_new * lg.x) * iwc);
-              const float neg = __expf((w_old * __logf(1.0f - p) + w_new * lg.y) * iwc);
-              setc(ts, j, tsdf);
-              setc(pr, j, pos / (pos + neg));
-              setu(cw, j, c);
-              upd_mask |= 1 << j;
-            }
+          px[j] = D.pixA[img];
+          lg[j] = D.pixB[img];
+        }
+      }
+      // pass 2: the per-voxel update of tsdf_integrate_kernel (voxel_tsdf.cu:174-203)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float tsdf = comp(ts, j);
+        const float d = px[j].x;
+        if (inb[j] && !(d == 0 || d > P.max_depth)) {
+          const float sdf = px[j].y * (d - hzs[j]);
+          if (sdf > neg_trunc) {
+            const float tsdf_new = fminf(1.0f, quot_const(sdf, P.trunc, P.inv_trunc));
+            const uint32_t c_old = compu(cw, j);
+            const uint32_t c_new = __float_as_uint(px[j].w);
+            const float w_new = px[j].z;
+            const float w_old = (float)(c_old >> 24);
+            const float wc = w_old + w_new;
+            const float iwc = __builtin_amdgcn_rcpf(wc);
+            const float r0 = round_quot((float)(c_old & 0xFF) * w_old + (float)(c_new & 0xFF) * w_new,
+                                        wc, iwc);
+            const float r1 = round_quot((float)((c_old >> 8) & 0xFF) * w_old +
+                                            (float)((c_new >> 8) & 0xFF) * w_new, wc, iwc);
+            const float r2 = round_quot((float)((c_old >> 16) & 0xFF) * w_old +
+                                            (float)((c_new >> 16) & 0xFF) * w_new, wc, iwc);
+            tsdf = (tsdf * w_old + tsdf_new * w_new) / wc;
+            const uint32_t wt = f2u8(fminf(roundf(wc), 40.0f));
+            const uint32_t c = (uint32_t)f2u8(r0) | ((uint32_t)f2u8(r1) << 8) |
+                               ((uint32_t)f2u8(r2) << 16) | (wt << 24);
+            // semantic log-odds fusion (voxel_tsdf.cu:196-202): hardware v_log / v_exp / v_rcp
+            // (error ~1e-7 against the 1e-4 probability tolerance); p stays exactly 0.5 when the
+            // two evidence terms are equal (ht == lt, e.g. depth-only frames).
+            const float p = comp(pr, j);
+            const float pos = __expf((w_old * __logf(p) + w_new * lg[j].x) * iwc);
+            const float neg = __expf((w_old * __logf(1.0f - p) + w_new * lg[j].y) * iwc);
+            setc(ts, j, tsdf);
+            setc(pr, j, pos == neg ? 0.5f : pos * __builtin_amdgcn_rcpf(pos + neg));
+            setu(cw, j, c);
+            upd_mask |= 1 << j;
           }
         }
         mn = fminf(mn, fabsf(tsdf));
@@ -178,6 +197,7 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
   if (lane == 0) s_upd[wave] = tot;
   __syncthreads();
   if (threadIdx.x == 0) D.wg_upd[blockIdx.x] = s_upd[0] + s_upd[1] + s_upd[2] + s_upd[3];
+  TSDF_STAMP(D, 3, 1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -194,6 +214,7 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
                                                                     int direct) {
   __shared__ ResolveLds L;
   const int t = threadIdx.x;
+  TSDF_STAMP(D, 4, 0);
   if (t == 0) {
     L.epoch = D.ctr->lock_epoch + 1;
     D.ctr->lock_epoch = L.epoch;
@@ -302,6 +323,7 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
       __syncthreads();
     }
   }
+  TSDF_STAMP(D, 4, 1);
   if (t == 0) {
     D.ctr->free_count = L.sfree;
     if (!direct) {

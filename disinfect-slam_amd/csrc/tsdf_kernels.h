@@ -5,6 +5,9 @@
 
 namespace tsdf {
 
+// diagnostic stamp buffer geometry (tsdf_debug_stamps, TSDF_STAMP in tsdf_block.h)
+constexpr int kDiagKernels = 8, kDiagMaxWg = 4096, kDiagStamps = 8;
+
 // device pointers of one engine (passed by value to every kernel)
 struct EngineDev {
   int4* table;                  // kNumEntry hash entries
@@ -31,6 +34,7 @@ struct EngineDev {
   // query scratch
   unsigned long long* visbits;  // kOccWords
   int32_t* wgcnt;               // kOccWords / 256
+  unsigned long long* dbg;      // diagnostic stamps (DIAG builds), else unused
 };
 
 __global__ void k_init_table(int4* table);

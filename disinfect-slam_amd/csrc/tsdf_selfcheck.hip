@@ -1,0 +1,141 @@
+// tsdf_selfcheck.hip -- test-only library (libtsdf_selfcheck.so): checks the engine's fast exact
+// quotient helpers (tsdf_device.h: round_quot, quot_const, f2i / f2u8) bit-for-bit against the
+// correctly rounded IEEE divide and the saturating conversions, on the GPU, over exhaustive and
+// adversarial input sets. Not part of the product library; tests/test_gpu_numerics.py drives it.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "tsdf_device.h"
+
+using namespace tsdf;
+
+namespace {
+
+__device__ __forceinline__ uint32_t pcg(uint32_t v) {
+  const uint32_t s = v * 747796405u + 2891336453u;
+  const uint32_t w = ((s >> ((s >> 28u) + 4u)) ^ s) * 277803737u;
+  return (w >> 22u) ^ w;
+}
+
+__device__ __forceinline__ bool same_bits(float a, float b) {
+  return __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b);
+}
+
+// every a with bits in [lo, hi) against divisor b (rb = RN(1/b) computed on the host)
+__global__ void k_quot_const(float b, float rb, uint32_t lo, uint32_t hi,
+                             unsigned long long* bad, uint32_t* first) {
+  const uint64_t n = (uint64_t)hi - lo;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t bits = lo + (uint32_t)i;
+    const float a = __uint_as_float(bits);
+    if (!same_bits(quot_const(a, b, rb), a / b)) {
+      atomicAdd(bad, 1ull);
+      atomicMin(first, bits);
+    }
+  }
+}
+
+// random (a, b) with b in [bmin, bmax) and a = (k + 1/2 + tiny) * b: quotients at and around the
+// rounding boundaries of roundf, plus uniformly random quotients in [-qmax, qmax]
+__global__ void k_round_quot(uint32_t seed, uint64_t n, float bmin, float bmax, float qmax,
+                             unsigned long long* bad, uint32_t* first) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t h0 = pcg((uint32_t)i ^ seed), h1 = pcg(h0 + 0x9e3779b9u), h2 = pcg(h1 ^ 0x85ebca6bu);
+    const float b = bmin + (bmax - bmin) * ((h0 >> 8) * 0x1p-24f);
+    float a;
+    if (h2 & 1u) {
+      const float k = floorf((h1 >> 8) * 0x1p-24f * qmax);
+      const float half = (k + 0.5f) * b;
+      // perturb by up to +-8 ulps around the exact boundary product
+      const int32_t d = (int32_t)((h2 >> 1) & 15u) - 8;
+      a = __uint_as_float(__float_as_uint(half) + d);
+      if (h2 & 0x100u) a = -a;
+    } else {
+      a = ((h1 >> 8) * 0x1p-23f - 1.0f) * qmax * b;
+    }
+    const float rb = __builtin_amdgcn_rcpf(b);
+    const int32_t fast_i = f2i(round_quot(a, b, rb)), ref_i = f2i(roundf(a / b));
+    const uint32_t fast_u = f2u8(round_quot(a, b, rb)), ref_u = f2u8(roundf(a / b));
+    if (fast_i != ref_i || fast_u != ref_u) {
+      atomicAdd(bad, 1ull);
+      atomicMin(first, (uint32_t)i);
+    }
+  }
+}
+
+// conversions on every float bit pattern in [lo, hi) against the reference semantics spelled out
+__global__ void k_convert(uint32_t lo, uint32_t hi, unsigned long long* bad, uint32_t* first) {
+  const uint64_t n = (uint64_t)hi - lo;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t bits = lo + (uint32_t)i;
+    const float f = __uint_as_float(bits);
+    const float t = truncf(f);
+    const int32_t ei = f != f ? 0 : t >= 2147483648.0f ? 2147483647
+                       : t <= -2147483648.0f ? (-2147483647 - 1) : (int32_t)t;
+    const int32_t es = f != f ? 0 : t >= 32767.0f ? 32767 : t <= -32768.0f ? -32768 : (int32_t)t;
+    const uint32_t eu = !(t > 0.0f) ? 0u : t >= 255.0f ? 255u : (uint32_t)t;
+    if (f2i(f) != ei || f2s(f) != es || f2u8(f) != eu) {
+      atomicAdd(bad, 1ull);
+      atomicMin(first, bits);
+    }
+  }
+}
+
+struct Out {
+  unsigned long long bad;
+  uint32_t first;
+};
+
+int finish(Out* d, unsigned long long* bad, uint32_t* first) {
+  Out h{};
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpy(&h, d, sizeof(Out), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  (void)hipFree(d);
+  *bad = h.bad;
+  *first = h.first;
+  return 0;
+}
+
+Out* start() {
+  Out* d = nullptr;
+  if (hipMalloc(&d, sizeof(Out)) != hipSuccess) return nullptr;
+  Out h{0ull, 0xFFFFFFFFu};
+  if (hipMemcpy(d, &h, sizeof(Out), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+  return d;
+}
+
+}  // namespace
+
+extern "C" {
+
+// quot_const(a, b, RN(1/b)) == a / b for every a whose bit pattern lies in [lo, hi)
+int tsdf_selfcheck_quot_const(float b, uint32_t lo, uint32_t hi, unsigned long long* bad,
+                              uint32_t* first) {
+  Out* d = start();
+  if (!d) return -1;
+  const float rb = 1.0f / b;
+  hipLaunchKernelGGL(k_quot_const, dim3(8192), dim3(256), 0, 0, b, rb, lo, hi, &d->bad, &d->first);
+  return finish(d, bad, first);
+}
+
+int tsdf_selfcheck_round_quot(uint32_t seed, uint64_t n, float bmin, float bmax, float qmax,
+                              unsigned long long* bad, uint32_t* first) {
+  Out* d = start();
+  if (!d) return -1;
+  hipLaunchKernelGGL(k_round_quot, dim3(8192), dim3(256), 0, 0, seed, n, bmin, bmax, qmax, &d->bad,
+                     &d->first);
+  return finish(d, bad, first);
+}
+
+int tsdf_selfcheck_convert(uint32_t lo, uint32_t hi, unsigned long long* bad, uint32_t* first) {
+  Out* d = start();
+  if (!d) return -1;
+  hipLaunchKernelGGL(k_convert, dim3(8192), dim3(256), 0, 0, lo, hi, &d->bad, &d->first);
+  return finish(d, bad, first);
+}
+
+}  // extern "C"

@@ -87,7 +87,7 @@ class Profile(C.Structure):
 EXPORTS = [
     "tsdf_config_default", "tsdf_create", "tsdf_destroy", "tsdf_integrate", "tsdf_raycast",
     "tsdf_query", "tsdf_get_stats", "tsdf_synchronize", "tsdf_profile_begin", "tsdf_profile_end",
-    "tsdf_debug_dump", "tsdf_num_entries", "tsdf_num_blocks", "tsdf_hash_allocate",
+    "tsdf_debug_dump", "tsdf_debug_stamps", "tsdf_num_entries", "tsdf_num_blocks", "tsdf_hash_allocate",
     "tsdf_hash_delete", "tsdf_hash_retrieve", "tsdf_hash_assign", "tsdf_num_active_blocks",
     "tsdf_pool_acquire", "tsdf_pool_release", "tsdf_pool_set_weight", "tsdf_pool_get_weights",
     "tsdf_hash_block", "tsdf_block_owner", "tsdf_error_string", "tsdf_last_error",
@@ -101,7 +101,8 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or LIB_PATH
+    # TSDF_AMD_LIB selects an alternative build of the same ABI (e.g. the DIAG=1 stamp variant)
+    path = path or os.environ.get("TSDF_AMD_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise OSError(f"HIP engine library not built: {path} (run __graft_entry__.build())")
     L = C.CDLL(path)
@@ -118,6 +119,7 @@ def load(path: str | None = None):
     L.tsdf_profile_begin.argtypes = [P]
     L.tsdf_profile_end.argtypes = [P, C.POINTER(Profile)]
     L.tsdf_debug_dump.argtypes = [P, P, P, P, P, P, P, P]
+    L.tsdf_debug_stamps.argtypes = [P, P, i64, C.POINTER(i)]
     L.tsdf_num_entries.restype = C.c_int32
     L.tsdf_num_entries.argtypes = []
     L.tsdf_num_blocks.restype = C.c_int32
@@ -141,7 +143,8 @@ def load(path: str | None = None):
     L.tsdf_last_error.argtypes = []
     for name in ("tsdf_create", "tsdf_destroy", "tsdf_integrate", "tsdf_raycast", "tsdf_query",
                  "tsdf_get_stats", "tsdf_synchronize", "tsdf_profile_begin", "tsdf_profile_end",
-                 "tsdf_debug_dump", "tsdf_hash_allocate", "tsdf_hash_delete", "tsdf_hash_retrieve",
+                 "tsdf_debug_dump", "tsdf_debug_stamps", "tsdf_hash_allocate", "tsdf_hash_delete",
+                 "tsdf_hash_retrieve",
                  "tsdf_hash_assign", "tsdf_num_active_blocks", "tsdf_pool_acquire",
                  "tsdf_pool_release", "tsdf_pool_set_weight", "tsdf_pool_get_weights"):
         getattr(L, name).restype = C.c_int

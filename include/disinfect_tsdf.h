@@ -136,6 +136,10 @@ int tsdf_profile_end(tsdf_engine* e, tsdf_profile* out);
  * any NULL pointer is skipped. */
 int tsdf_debug_dump(tsdf_engine* e, int16_t* entry_pos_off, int32_t* entry_idx, int32_t* heap,
                     int32_t* free_count, float* tsdf, float* prob, uint8_t* rgbw);
+/* Diagnostic builds only (make DIAG=1): per-workgroup 100 MHz phase stamps of the last launch of
+ * each frame kernel, [8 kernels][4096 workgroups][8 stamps] u64, cleared after the copy. *enabled
+ * reports whether the library was built with stamps. out == NULL only queries enabled. */
+int tsdf_debug_stamps(tsdf_engine* e, uint64_t* out, int64_t capacity, int* enabled);
 int32_t tsdf_num_entries(void);
 int32_t tsdf_num_blocks(const tsdf_engine* e);
 

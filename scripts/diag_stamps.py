@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Per-workgroup phase timing of the frame kernels from the DIAG=1 library (s_memrealtime, 100 MHz).
+
+Usage (GPU box): make -C disinfect-slam_amd diag && \
+    TSDF_AMD_LIB=disinfect-slam_amd/libdisinfect_tsdf_diag.so python scripts/diag_stamps.py
+Diagnostic only: nothing here is part of the product or the bench.
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "disinfect-slam_amd"))
+
+KERNELS = {0: ("ingest", ["lds_init", "pix_write", "dda", "barrier", "sweep"]),
+           1: ("resolve_alloc", ["prepare", "batch0", "resolve"]),
+           2: ("vis", ["all"]),
+           3: ("integrate", ["all"]),
+           4: ("resolve_delete", ["all"])}
+NK, NWG, NS = 8, 4096, 8
+
+
+def main():
+    import ctypes as C
+    import torch
+    import tsdf_amd
+    from tsdf_amd import _lib, synth
+
+    L = _lib.load()
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    cam = synth.camera(640, 480, synth.TUM_FR1)
+    nwarm, nmeas = 60, 20
+    fr = synth.render_torch(cam, list(range(nwarm + nmeas)), device=dev)
+    torch.cuda.synchronize()
+    eng = tsdf_amd.Engine(0.005, 0.03, max_width=640, max_height=480, num_block_bits=18,
+                          device=0, stream=torch.cuda.current_stream().cuda_stream)
+    en = C.c_int(0)
+    L.tsdf_debug_stamps(eng._h, None, 0, C.byref(en))
+    if not en.value:
+        raise SystemExit("library built without TSDF_DIAG_STAMPS (make diag; set TSDF_AMD_LIB)")
+    buf = np.zeros(NK * NWG * NS, np.uint64)
+
+    def step(i):
+        eng.integrate(fr["rgb"][i], fr["depth"][i], fr["ht"][i], fr["lt"][i], cam.K,
+                      tsdf_amd.SE3(fr["q"][i], fr["t"][i]), 4.0)
+
+    for i in range(nwarm):
+        step(i)
+    torch.cuda.synchronize()
+    L.tsdf_debug_stamps(eng._h, buf.ctypes.data, buf.size, None)
+    acc = {}
+    for i in range(nwarm, nwarm + nmeas):
+        step(i)
+        torch.cuda.synchronize()
+        L.tsdf_debug_stamps(eng._h, buf.ctypes.data, buf.size, None)
+        S = buf.reshape(NK, NWG, NS).astype(np.int64)
+        t0 = None
+        bounds = []
+        for k, (name, phases) in KERNELS.items():
+            s = S[k]
+            valid = s[:, 0] > 0
+            if not valid.any():
+                continue
+            s = s[valid]
+            last = len(phases)
+            start, end = s[:, 0].min(), s[:, last].max()
+            if t0 is None:
+                t0 = start
+            bounds.append((name, start, end))
+            d = acc.setdefault(name, {"n_wg": [], "span": [], "start_skew_p50": [],
+                                      "start_skew_max": [], **{p: [] for p in phases},
+                                      **{p + "_max": [] for p in phases}})
+            d["n_wg"].append(len(s))
+            d["span"].append((end - start) * 10e-3)
+            sk = (s[:, 0] - start) * 10e-3
+            d["start_skew_p50"].append(np.median(sk))
+            d["start_skew_max"].append(sk.max())
+            for j, p in enumerate(phases):
+                dur = (s[:, j + 1] - s[:, j]) * 10e-3
+                d[p].append(np.median(dur))
+                d[p + "_max"].append(dur.max())
+        for (n1, _, e1), (n2, s2, _) in zip(bounds, bounds[1:]):
+            acc.setdefault("gaps", {}).setdefault(f"{n1}->{n2}", []).append((s2 - e1) * 10e-3)
+        acc.setdefault("frame", {}).setdefault("first_start_to_last_end", []).append(
+            (bounds[-1][2] - bounds[0][1]) * 10e-3)
+    print("median over", nmeas, "frames; microseconds (per-WG medians / maxima)")
+    for name, d in acc.items():
+        print(f"[{name}]")
+        for key, v in d.items():
+            print(f"   {key:24s} {np.median(v):9.2f}")
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

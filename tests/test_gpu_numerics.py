@@ -1,0 +1,73 @@
+"""Bit-exactness of the engine's fast quotient / conversion helpers (csrc/tsdf_device.h) on the GPU.
+
+The integrate and ingest kernels replace the 11-op IEEE divide where an exact shortcut exists:
+ - quot_const(a, b, RN(1/b))  -- Markstein-corrected quotient for frame-constant divisors
+   (truncation, voxel size, max depth); checked EXHAUSTIVELY over every float a of both signs in
+   the normal range for the divisors the tests and the bench use;
+ - round_quot(a, b, rcp(b))   -- roundf(a / b) from a reciprocal estimate with an IEEE fallback
+   near rounding boundaries (projection to pixels, colour averages); checked on 2^28 random and
+   boundary-adversarial pairs per divisor range;
+ - f2i / f2s / f2u8 via v_cvt_{i,u}32_f32 -- checked on every float bit pattern.
+Each must agree bit for bit with the correctly rounded divide / cvt.rzi semantics.
+"""
+import ctypes as C
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "disinfect-slam_amd", "libtsdf_selfcheck.so")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    L = C.CDLL(LIB)
+    u32, u64, f = C.c_uint32, C.c_uint64, C.c_float
+    P64, P32 = C.POINTER(C.c_ulonglong), C.POINTER(C.c_uint32)
+    L.tsdf_selfcheck_quot_const.argtypes = [f, u32, u32, P64, P32]
+    L.tsdf_selfcheck_round_quot.argtypes = [u32, u64, f, f, f, P64, P32]
+    L.tsdf_selfcheck_convert.argtypes = [u32, u32, P64, P32]
+    return L
+
+
+def _run(fn, *args):
+    bad, first = C.c_ulonglong(), C.c_uint32()
+    assert fn(*args, C.byref(bad), C.byref(first)) == 0
+    return bad.value, first.value
+
+
+# positive and negative normal floats up to 2^100 (larger |a| takes the IEEE path anyway)
+RANGES = [(0x00800000, 0x71800000), (0x80800000, 0xF1800000)]
+
+
+@pytest.mark.parametrize("b", [0.03, 0.005, 0.02, 0.04, 0.08, 0.01, 4.0, 3.0, 5.0, 0.1])
+def test_quot_const_exhaustive(lib, b):
+    for lo, hi in RANGES:
+        bad, first = _run(lib.tsdf_selfcheck_quot_const, b, lo, hi)
+        assert bad == 0, f"b={b}: {bad} mismatches, first a bits {first:#x}"
+
+
+def test_quot_const_edges(lib):
+    # zero, denormals, huge values, inf, NaN: the helper must route them to the IEEE divide
+    for lo, hi in [(0, 0x00800000), (0x80000000, 0x80800000), (0x71800000, 0x80000000),
+                   (0xF1800000, 0xFFFFFFFF)]:
+        bad, first = _run(lib.tsdf_selfcheck_quot_const, 0.03, lo, hi)
+        assert bad == 0, f"{bad} mismatches, first a bits {first:#x}"
+
+
+@pytest.mark.parametrize("bmin,bmax,qmax", [
+    (0.05, 10.0, 2000.0),     # projection: hz in metres, pixel coordinates
+    (1e-3, 0.05, 2000.0),     # voxels close to the camera plane
+    (1e-4, 44.0, 256.0),      # colour averages: wc = w_old + w_new in (0, 44]
+    (0.5, 44.0, 300.0),
+])
+def test_round_quot_random(lib, bmin, bmax, qmax):
+    bad, first = _run(lib.tsdf_selfcheck_round_quot, 12345, 1 << 28, bmin, bmax, qmax)
+    assert bad == 0, f"{bad} mismatches, first sample {first}"
+
+
+def test_convert_all_floats(lib):
+    bad, first = _run(lib.tsdf_selfcheck_convert, 0, 0xFFFFFFFF)
+    assert bad == 0, f"{bad} mismatches, first bits {first:#x}"
