@@ -141,24 +141,46 @@ __device__ __forceinline__ uint8_t f2u8(float f) {  // cvt.rzi.u8.f32
 // bit-for-bit what the correctly rounded a / b would give; libtsdf_selfcheck checks them against
 // the IEEE divide exhaustively / on adversarial samples (tests/test_gpu_numerics.py). ----
 
-// roundf(a / b) from the reciprocal estimate rb = v_rcp(b) (1 ulp): |a*rb - RN(a/b)| < 2^-21 |q|,
-// so rounding the estimate gives the same integer unless it lies within 2^-20 |q| of a rounding
-// boundary (k + 1/2), or is not finite and below 2^16 -- those lanes take the IEEE divide.
-__device__ __forceinline__ float round_quot(float a, float b, float rb) {
+// f2i(roundf(a / b)) -- the integer the reference gets from roundf of the IEEE quotient followed
+// by a truncating cvt -- from the reciprocal estimate rb = v_rcp(b) (1 ulp). q = a*rb is within
+// 2^-22 |q| of RN(a/b); rounding the two perturbations q (1 +- 2^-20) half away from zero
+// (fma with +-1/2, then the truncating cvt) brackets roundf of every value in between, so when
+// both land on the same integer it is the answer (the fma rounding error is covered for |q| >= 1/7,
+// and below that both give 0). Otherwise -- near k + 1/2, or |b| out of range -- the lane takes
+// the IEEE divide. Saturation and NaN -> 0 match cvt.rzi in both paths.
+__device__ __forceinline__ int32_t round_quot_i(float a, float b, float rb) {
+  const float q = a * rb;
+  const float h = __builtin_copysignf(0.5f, q);
+  const int32_t i1 = f2i(__builtin_fmaf(q, 1.0f + 0x1p-20f, h));
+  const int32_t i2 = f2i(__builtin_fmaf(q, 1.0f - 0x1p-20f, h));
+  if (__builtin_expect(i1 == i2 && fabsf(b) < 0x1p100f, 1)) return i1;
+  return f2i(roundf(a / b));
+}
+// f2u8(roundf(a / b)): the saturating u8 cvt of the same rounded quotient
+__device__ __forceinline__ uint32_t round_quot_u8(float a, float b, float rb) {
+  return (uint32_t)min(255, max(0, round_quot_i(a, b, rb)));
+}
+
+// RN(a / b) where the caller only compares the quotient with 0 and with the float c: the
+// estimate a * rcp(b) is returned when it provably lies on the same side of 0 and of c as the IEEE
+// quotient (distance to c above 2^-20 |q|, |q| and |b| in range), else the IEEE quotient.
+__device__ __forceinline__ float quot_for_cmp(float a, float b, float rb, float c) {
   const float q = a * rb;
   const float fq = fabsf(q);
-  const float frac = fq - truncf(fq);
-  if (__builtin_expect(fq < 65536.0f && fabsf(frac - 0.5f) > fq * 0x1p-20f, 1)) return roundf(q);
-  return roundf(a / b);
+  if (__builtin_expect(fq > 0x1p-100f && fq < 0x1p100f && fabsf(b) < 0x1p100f &&
+                           fabsf(q - c) > fq * 0x1p-20f, 1))
+    return q;
+  return a / b;
 }
 
 // RN(a / b) for a frame-constant divisor b with rb = RN(1 / b) computed on the host: Markstein's
 // correction q + (a - b q) rb (two fma) is the correctly rounded quotient when no intermediate
-// leaves the normal range; |a| outside [2^-100, 2^100] (incl. 0, inf, NaN) takes the IEEE divide.
+// leaves the normal range; |a| or |q| outside [2^-60, 2^60] (incl. 0, inf, NaN) takes the IEEE
+// divide.
 __device__ __forceinline__ float quot_const(float a, float b, float rb) {
-  const float fa = fabsf(a);
-  if (__builtin_expect(fa > 0x1p-100f && fa < 0x1p100f, 1)) {
-    const float q = a * rb;
+  const float q = a * rb;
+  const float fa = fabsf(a), fq = fabsf(q);
+  if (__builtin_expect(fa > 0x1p-60f && fa < 0x1p60f && fq > 0x1p-60f && fq < 0x1p60f, 1)) {
     const float r = __builtin_fmaf(-q, b, a);
     return __builtin_fmaf(r, rb, q);
   }
@@ -252,7 +274,9 @@ __device__ __forceinline__ bool voxel_visible(const FrameParams& P, int16_t gx, 
   const float hx = P.fx * pc.x + P.cx * pc.z;
   const float hy = P.fy * pc.y + P.cy * pc.z;
   const float hz = pc.z;
-  const float u = hx / hz, v = hy / hz;
+  const float rz = __builtin_amdgcn_rcpf(hz);
+  const float u = quot_for_cmp(hx, hz, rz, (float)(P.W - 1));
+  const float v = quot_for_cmp(hy, hz, rz, (float)(P.H - 1));
   return u >= 0 && u <= (float)(P.W - 1) && v >= 0 && v <= (float)(P.H - 1) && hz >= 0;
 }
 // voxel_tsdf.cu:59-80 is_block_visible<Full>

@@ -112,6 +112,7 @@ struct tsdf_engine {
   DevCounters* h_ctr = nullptr;  // pinned readback
   // profiling
   bool profiling = false;
+  int prof_mode = TSDF_PROFILE_PHASES;
   std::vector<std::array<hipEvent_t, 5>> events;
   size_t ev_used = 0;
   unsigned long long prof_vis0 = 0, prof_upd0 = 0;
@@ -123,7 +124,7 @@ void free_all(tsdf_engine* e) {
   EngineDev& D = e->D;
   void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.fresh_flag, D.occ,
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs,      D.fresh,
-                  D.vis,     D.cand,     D.wg_upd, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
+                  D.vis,     D.band,    D.cand,     D.wg_upd, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
                   e->q_sel,  e->q_count, e->q_out,   e->t_keys, e->t_recs,    e->t_count,
                   e->t_i32,  e->t_u32,   e->t_f0,    e->t_f1,   e->t_s4};
@@ -299,9 +300,17 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.nk_list, kNewKeyCap);
   ALLOC(D.pairs, kNewKeyCap);
   ALLOC(D.fresh, kNewKeyCap);
-  ALLOC(D.vis, nb);
+  ALLOC(D.vis, (size_t)kBands * nb);
+  ALLOC(D.band, kBands * kBandStride);
   ALLOC(D.cand, nb);
   ALLOC(D.wg_upd, kIntegrateGrid);
+  {  // one resident wave of k_integrate workgroups: no second-round stragglers
+    int per_cu = 0, ncu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate, 256, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+      return fail(TSDF_ERR_HIP);
+    D.integrate_grid = std::max(8, std::min(kIntegrateGrid, (per_cu * ncu) & ~7));
+  }
   ALLOC(D.pixA, e->max_pixels);
   ALLOC(D.pixB, e->max_pixels);
   ALLOC(D.visbits, kOccWords);
@@ -336,6 +345,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ok &= hipMemsetAsync(D.occ, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
   ok &= hipMemsetAsync(D.nk_key, 0, sizeof(unsigned long long) * kNewKeyCap, s) == hipSuccess;
   ok &= hipMemsetAsync(D.nk_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.band, 0, sizeof(int32_t) * kBands * kBandStride, s) == hipSuccess;
   ok &= hipMemsetAsync(D.visbits, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
   DevCounters c0{};
   c0.free_count = nb;
@@ -407,28 +417,29 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
       e->events.push_back(a);
     }
     ev = &e->events[e->ev_used++];
-    HIP_OK(hipEventRecord((*ev)[0], s));
   }
+  const bool all_ev = ev && e->prof_mode == TSDF_PROFILE_PHASES;
+  if (all_ev) HIP_OK(hipEventRecord((*ev)[0], s));
   // ---- allocate (voxel_tsdf.cu:377-386) ----
   hipLaunchKernelGGL(k_ingest_dda, dim3((W + 15) / 16, (H + 15) / 16), dim3(256), 0, s, e->D, P,
                      depth, rgb, ht, lt);
   LAUNCH_OK("k_ingest_dda");
   int rc = launch_resolve_alloc(e, (uint32_t)(np * e->maxs), 1);
   if (rc) return rc;
-  if (ev) HIP_OK(hipEventRecord((*ev)[1], s));
+  if (all_ev) HIP_OK(hipEventRecord((*ev)[1], s));
   // ---- visibility (voxel_tsdf.cu:388-397) ----
   hipLaunchKernelGGL(k_vis, dim3(kOccWords / 256), dim3(256), 0, s, e->D, P);
   LAUNCH_OK("k_vis");
   if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
   // ---- update (voxel_tsdf.cu:474-481) ----
-  hipLaunchKernelGGL(k_integrate, dim3(kIntegrateGrid), dim3(256), 0, s, e->D, P);
+  hipLaunchKernelGGL(k_integrate, dim3(e->D.integrate_grid), dim3(256), 0, s, e->D, P);
   LAUNCH_OK("k_integrate");
   if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
   // ---- space carving (voxel_tsdf.cu:483-488) ----
   hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kResolveThreads), 0, s, e->D, e->D.cand,
                      &e->D.ctr->n_cand, 0);
   LAUNCH_OK("k_resolve_delete");
-  if (ev) HIP_OK(hipEventRecord((*ev)[4], s));
+  if (all_ev) HIP_OK(hipEventRecord((*ev)[4], s));
   return TSDF_OK;
 }
 
@@ -523,8 +534,10 @@ int tsdf_get_stats(tsdf_engine* e, tsdf_stats* o, int clear_status) {
   return TSDF_OK;
 }
 
-int tsdf_profile_begin(tsdf_engine* e) {
-  if (!e) return TSDF_ERR_INVALID_ARG;
+int tsdf_profile_begin(tsdf_engine* e, int mode) {
+  if (!e || (mode != TSDF_PROFILE_PHASES && mode != TSDF_PROFILE_INTEGRATE))
+    return TSDF_ERR_INVALID_ARG;
+  e->prof_mode = mode;
   int rc = read_counters(e);
   if (rc) return rc;
   e->prof_vis0 = e->h_ctr->total_visible;
@@ -542,9 +555,10 @@ int tsdf_profile_end(tsdf_engine* e, tsdf_profile* o) {
   std::memset(o, 0, sizeof(*o));
   o->frames = (int64_t)e->ev_used;
   for (size_t i = 0; i < e->ev_used; ++i) {
-    float ms[4];
+    float ms[4] = {0.f, 0.f, 0.f, 0.f};
     for (int k = 0; k < 4; ++k)
-      HIP_OK(hipEventElapsedTime(&ms[k], e->events[i][k], e->events[i][k + 1]));
+      if (e->prof_mode == TSDF_PROFILE_PHASES || k == 2)
+        HIP_OK(hipEventElapsedTime(&ms[k], e->events[i][k], e->events[i][k + 1]));
     o->ms_allocate += ms[0];
     o->ms_visible += ms[1];
     o->ms_integrate += ms[2];

@@ -7,34 +7,50 @@ namespace tsdf {
 // ---------------------------------------------------------------------------------------------
 // k_vis: check_visibility_kernel (voxel_tsdf.cu:82-93) over the 512 KiB occupancy bitmap instead
 // of the 48 MiB table: every allocated block with any corner in view (no depth test) is appended
-// to the visible list (one atomic per wave). Order is irrelevant to the update; the carving
-// resolver restores the reference's entry order for the deletes.
+// to the list of the image band its centre projects into (LDS counts, one global atomic per band
+// per workgroup). Order is irrelevant to the update; the carving resolver restores the
+// reference's entry order for the deletes.
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int block_band(const FrameParams& P, int16_t bx, int16_t by, int16_t bz) {
+  const float h = 0.5f * (float)(kBlockLen - 1);
+  const f3 pw = {((float)(bx << kBlockLenBits) + h) * P.voxel, ((float)(by << kBlockLenBits) + h) * P.voxel,
+                 ((float)(bz << kBlockLenBits) + h) * P.voxel};
+  const f3 pc = se3_apply(P.cq, P.ct, pw);
+  const float v = (P.fy * pc.y + P.cy * pc.z) * __builtin_amdgcn_rcpf(pc.z);
+  const float bandf = v * ((float)kBands / (float)P.H);
+  return pc.z > 0.f && bandf > 0.f ? min(kBands - 1, f2i(bandf)) : 0;
+}
+
 __global__ __launch_bounds__(256) void k_vis(EngineDev D, FrameParams P) {
   TSDF_STAMP(D, 2, 0);
+  __shared__ int s_cnt[kBands], s_base[kBands];
+  if (threadIdx.x < kBands) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
   const int w = blockIdx.x * 256 + threadIdx.x;  // kOccWords == 256 * 256
   unsigned long long occ = D.occ[w], vis = 0ull;
-  unsigned long long scan = occ;
-  while (scan) {
-    const int b = __ffsll((long long)scan) - 1;
-    scan &= scan - 1;
+  while (occ) {
+    const int b = __ffsll((long long)occ) - 1;
+    occ &= occ - 1;
     const Ent en = load_ent(D.table, (uint32_t)(w * 64 + b));
-    if (block_visible<false>(P, en.x, en.y, en.z)) vis |= 1ull << b;
+    if (block_visible<false>(P, en.x, en.y, en.z)) {
+      vis |= 1ull << b;
+      atomicAdd(&s_cnt[block_band(P, en.x, en.y, en.z)], 1);
+    }
   }
-  // one atomic per workgroup: a single hot counter serialises at ~90 adds/us (MI355X_MICROARCH)
-  __shared__ int s_scan[4];
-  __shared__ int s_base;
-  const int cnt = __popcll(vis);
-  int total;
-  const int excl = block_excl_scan(cnt, s_scan, &total);
-  if (threadIdx.x == 0) s_base = total ? atomicAdd(&D.ctr->n_vis, total) : 0;
   __syncthreads();
-  int pos = s_base + excl;
+  if (threadIdx.x < kBands) {
+    const int c = s_cnt[threadIdx.x];
+    s_base[threadIdx.x] = c ? atomicAdd(&D.band[threadIdx.x * kBandStride], c) : 0;
+    s_cnt[threadIdx.x] = 0;
+  }
+  __syncthreads();
   while (vis) {
     const int b = __ffsll((long long)vis) - 1;
     vis &= vis - 1;
     const uint32_t e = (uint32_t)(w * 64 + b);
     const Ent en = load_ent(D.table, e);
+    const int band = block_band(P, en.x, en.y, en.z);
+    const int pos = s_base[band] + atomicAdd(&s_cnt[band], 1);
     VisRec r;
     r.x = en.x;
     r.y = en.y;
@@ -42,7 +58,7 @@ __global__ __launch_bounds__(256) void k_vis(EngineDev D, FrameParams P) {
     r.pad = 0;
     r.idx = en.idx;
     r.entry = (int32_t)e;
-    D.vis[pos++] = r;
+    D.vis[(size_t)band * D.nblocks + pos] = r;
   }
   TSDF_STAMP(D, 2, 1);
 }
@@ -75,24 +91,51 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
   const int pair = wave >> 1, hf = wave & 1;
-  const int nvis = D.ctr->n_vis;
+  // concatenated band lists: band i holds visible-block indices [bstart_i, bstart_i + count_i)
+  int bstart[kBands];
+  int nvis = 0;
+#pragma unroll
+  for (int i = 0; i < kBands; ++i) {
+    bstart[i] = nvis;
+    nvis += D.band[i * kBandStride];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) D.ctr->n_vis = nvis;
+  // XCD-aware split (workgroups b and b + 8 share an XCD): group g = blockIdx % 8 takes the g-th
+  // contiguous eighth of the block pairs in band order, a compact image region whose pixel
+  // records stay resident in that XCD's L2.
+  const int npairs = (nvis + 1) >> 1;
+  const int g = blockIdx.x & 7, ngrp = gridDim.x >> 3;
+  const int p_lo = (int)(((long long)npairs * g) >> 3), p_hi = (int)(((long long)npairs * (g + 1)) >> 3);
   const int rx0 = (lane & 1) * 4, ry = (lane >> 1) & 7, rz = (lane >> 4) + 4 * hf;
   const int off = (hf * 256 + lane * 4) * 4;
   const float neg_trunc = -P.trunc;
   int my_upd = 0;
   TSDF_STAMP(D, 3, 0);
-  for (int base = blockIdx.x * 2; base < nvis; base += gridDim.x * 2) {
-    const int b = base + pair;
+  for (int pp = p_lo + (blockIdx.x >> 3); pp < p_hi; pp += ngrp) {
+    const int b = 2 * pp + pair;
     float mn = __builtin_inff();
     bool fresh = false;
     int32_t pidx = 0;
+    VisRec r{};
     if (b < nvis) {
-      const VisRec r = D.vis[__builtin_amdgcn_readfirstlane(b)];
+      int bd = 0, ofs = b;
+#pragma unroll
+      for (int i = 1; i < kBands; ++i)
+        if (b >= bstart[i]) {
+          bd = i;
+          ofs = b - bstart[i];
+        }
+      r = D.vis[(size_t)bd * D.nblocks + __builtin_amdgcn_readfirstlane(ofs)];
       pidx = r.idx;
       uint8_t* blk = D.pool + (size_t)pidx * kBlockBytes;
+#if defined(TSDF_EXP) && (TSDF_EXP & 2)  // experiment build: no pool state loads
+      float4 ts = make_float4(0.5f, 0.5f, 0.5f, 0.5f), pr = ts;
+      uint4 cw = make_uint4(0x05808080u, 0x05808080u, 0x05808080u, 0x05808080u);
+#else
       float4 ts = *reinterpret_cast<const float4*>(blk + off);
       float4 pr = *reinterpret_cast<const float4*>(blk + kProbOffset + off);
       uint4 cw = *reinterpret_cast<const uint4*>(blk + kRgbwOffset + off);
+#endif
       fresh = D.fresh_flag[pidx] != 0;
       if (fresh) {
         ts = make_float4(-1.f, -1.f, -1.f, -1.f);
@@ -121,17 +164,19 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
         const float hy = P.fy * pc.y + P.cy * pc.z;
         const float hz = pc.z;
         const float rz = __builtin_amdgcn_rcpf(hz);
-        const int u = f2i(round_quot(hx, hz, rz));
-        const int v = f2i(round_quot(hy, hz, rz));
+        const int u = round_quot_i(hx, hz, rz);
+        const int v = round_quot_i(hy, hz, rz);
         hzs[j] = hz;
         inb[j] = u >= 0 && u < P.W && v >= 0 && v < P.H;
-        px[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        lg[j] = make_float2(0.f, 0.f);
+#if defined(TSDF_EXP) && (TSDF_EXP & 1)  // experiment build: no pixel gathers
+        if (inb[j]) px[j] = make_float4(hz + 0.01f, 1.0f, 1.0f, __uint_as_float(0x00808080u));
+#else
         if (inb[j]) {
           const int img = v * P.W + u;
           px[j] = D.pixA[img];
           lg[j] = D.pixB[img];
         }
+#endif
       }
       // pass 2: the per-voxel update of tsdf_integrate_kernel (voxel_tsdf.cu:174-203)
 #pragma unroll
@@ -148,22 +193,23 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
             const float w_old = (float)(c_old >> 24);
             const float wc = w_old + w_new;
             const float iwc = __builtin_amdgcn_rcpf(wc);
-            const float r0 = round_quot((float)(c_old & 0xFF) * w_old + (float)(c_new & 0xFF) * w_new,
-                                        wc, iwc);
-            const float r1 = round_quot((float)((c_old >> 8) & 0xFF) * w_old +
-                                            (float)((c_new >> 8) & 0xFF) * w_new, wc, iwc);
-            const float r2 = round_quot((float)((c_old >> 16) & 0xFF) * w_old +
-                                            (float)((c_new >> 16) & 0xFF) * w_new, wc, iwc);
+            const uint32_t r0 = round_quot_u8(
+                (float)(c_old & 0xFF) * w_old + (float)(c_new & 0xFF) * w_new, wc, iwc);
+            const uint32_t r1 = round_quot_u8(
+                (float)((c_old >> 8) & 0xFF) * w_old + (float)((c_new >> 8) & 0xFF) * w_new, wc, iwc);
+            const uint32_t r2 = round_quot_u8(
+                (float)((c_old >> 16) & 0xFF) * w_old + (float)((c_new >> 16) & 0xFF) * w_new, wc, iwc);
             tsdf = (tsdf * w_old + tsdf_new * w_new) / wc;
             const uint32_t wt = f2u8(fminf(roundf(wc), 40.0f));
-            const uint32_t c = (uint32_t)f2u8(r0) | ((uint32_t)f2u8(r1) << 8) |
-                               ((uint32_t)f2u8(r2) << 16) | (wt << 24);
-            // semantic log-odds fusion (voxel_tsdf.cu:196-202): hardware v_log / v_exp / v_rcp
-            // (error ~1e-7 against the 1e-4 probability tolerance); p stays exactly 0.5 when the
-            // two evidence terms are equal (ht == lt, e.g. depth-only frames).
+            const uint32_t c = r0 | (r1 << 8) | (r2 << 16) | (wt << 24);
+            // semantic log-odds fusion (voxel_tsdf.cu:196-202) in base 2: pixB holds log2 ht /
+            // log2 lt, so exp((w_old ln p + w_new ln ht) / wc) = exp2((w_old log2 p + w_new log2 ht)
+            // / wc) with raw v_log_f32 / v_exp_f32 / v_rcp_f32 (~1 ulp each against the 1e-4
+            // probability tolerance); p stays exactly 0.5 when the two terms are equal (ht == lt).
             const float p = comp(pr, j);
-            const float pos = __expf((w_old * __logf(p) + w_new * lg[j].x) * iwc);
-            const float neg = __expf((w_old * __logf(1.0f - p) + w_new * lg[j].y) * iwc);
+            const float pos = __builtin_amdgcn_exp2f((w_old * __builtin_amdgcn_logf(p) + w_new * lg[j].x) * iwc);
+            const float neg =
+                __builtin_amdgcn_exp2f((w_old * __builtin_amdgcn_logf(1.0f - p) + w_new * lg[j].y) * iwc);
             setc(ts, j, tsdf);
             setc(pr, j, pos == neg ? 0.5f : pos * __builtin_amdgcn_rcpf(pos + neg));
             setu(cw, j, c);
@@ -172,7 +218,11 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
         }
         mn = fminf(mn, fabsf(tsdf));
       }
+#if defined(TSDF_EXP) && (TSDF_EXP & 4)  // experiment build: no pool state stores
+      if (upd_mask < 0) {
+#else
       if (upd_mask || fresh) {
+#endif
         *reinterpret_cast<float4*>(blk + off) = ts;
         *reinterpret_cast<float4*>(blk + kProbOffset + off) = pr;
         *reinterpret_cast<uint4*>(blk + kRgbwOffset + off) = cw;
@@ -187,7 +237,7 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
       if (fresh) D.fresh_flag[pidx] = 0;
       if (m2 >= 0.9f) {  // space_carving_kernel threshold (voxel_tsdf.cu:227, :485)
         const int k = atomicAdd(&D.ctr->n_cand, 1);
-        D.cand[k] = D.vis[b];
+        D.cand[k] = r;
       }
     }
     __syncthreads();
@@ -224,7 +274,7 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
   claims_clear(L);
   if (!direct) {  // voxels updated by k_integrate: sum of its per-workgroup counts
     int u = 0;
-    for (int i = t; i < kIntegrateGrid; i += kResolveThreads) u += D.wg_upd[i];
+    for (int i = t; i < D.integrate_grid; i += kResolveThreads) u += D.wg_upd[i];
     int tot;
     (void)block_excl_scan(u, L.scan, &tot);
     if (t == 0) D.ctr->last_updated = (unsigned long long)tot;

@@ -8,6 +8,11 @@ namespace tsdf {
 // diagnostic stamp buffer geometry (tsdf_debug_stamps, TSDF_STAMP in tsdf_block.h)
 constexpr int kDiagKernels = 8, kDiagMaxWg = 4096, kDiagStamps = 8;
 
+// visible-block lists: one per horizontal image band of the block centre's projection, so the
+// integrate kernel can hand each XCD a contiguous, spatially compact slice (its pixel gathers stay
+// in that XCD's L2). Counters 128 B apart; list b holds up to nblocks records at vis + b * nblocks.
+constexpr int kBands = 16, kBandStride = 32;
+
 // device pointers of one engine (passed by value to every kernel)
 struct EngineDev {
   int4* table;                  // kNumEntry hash entries
@@ -18,6 +23,7 @@ struct EngineDev {
   unsigned long long* occ;      // kOccWords occupancy bitmap
   DevCounters* ctr;
   int32_t nblocks;
+  int32_t integrate_grid;       // k_integrate workgroups (resident capacity, multiple of 8)
   // per-frame allocation scratch
   unsigned long long* nk_key;   // kNewKeyCap new-key set
   uint32_t* nk_order;           // kNewKeyCap smallest candidate order per key
@@ -25,12 +31,13 @@ struct EngineDev {
   unsigned long long* pairs;    // kNewKeyCap (order << 32 | slot) resolver scratch
   int32_t* fresh;               // pool indices acquired by the hash-level test path
   // visibility / carving
-  VisRec* vis;                  // visible blocks (any order)
+  VisRec* vis;                  // kBands x nblocks visible blocks (band-major, any order within)
+  int32_t* band;                // kBands x kBandStride: record count of each band list
   VisRec* cand;                 // carve candidates (any order; resolver sorts by entry)
   int32_t* wg_upd;              // kIntegrateGrid per-workgroup updated-voxel counts
   // packed frame
   float4* pixA;                 // {depth, range, w_new, rgb}
-  float2* pixB;                 // {log ht, log lt}
+  float2* pixB;                 // {log2 ht, log2 lt}
   // query scratch
   unsigned long long* visbits;  // kOccWords
   int32_t* wgcnt;               // kOccWords / 256

@@ -1,5 +1,5 @@
 // tsdf_selfcheck.hip -- test-only library (libtsdf_selfcheck.so): checks the engine's fast exact
-// quotient helpers (tsdf_device.h: round_quot, quot_const, f2i / f2u8) bit-for-bit against the
+// quotient helpers (tsdf_device.h: round_quot_i/_u8, quot_const, quot_for_cmp, f2i / f2u8) bit-for-bit against the
 // correctly rounded IEEE divide and the saturating conversions, on the GPU, over exhaustive and
 // adversarial input sets. Not part of the product library; tests/test_gpu_numerics.py drives it.
 #include <hip/hip_runtime.h>
@@ -57,9 +57,37 @@ __global__ void k_round_quot(uint32_t seed, uint64_t n, float bmin, float bmax, 
       a = ((h1 >> 8) * 0x1p-23f - 1.0f) * qmax * b;
     }
     const float rb = __builtin_amdgcn_rcpf(b);
-    const int32_t fast_i = f2i(round_quot(a, b, rb)), ref_i = f2i(roundf(a / b));
-    const uint32_t fast_u = f2u8(round_quot(a, b, rb)), ref_u = f2u8(roundf(a / b));
+    const int32_t fast_i = round_quot_i(a, b, rb), ref_i = f2i(roundf(a / b));
+    const uint32_t fast_u = round_quot_u8(a, b, rb), ref_u = f2u8(roundf(a / b));
     if (fast_i != ref_i || fast_u != ref_u) {
+      atomicAdd(bad, 1ull);
+      atomicMin(first, (uint32_t)i);
+    }
+  }
+}
+
+// voxel_visible's comparisons: RN(a/b) >= 0 and <= c, with a / b near c, near 0 and uniform
+__global__ void k_quot_cmp(uint32_t seed, uint64_t n, float bmin, float bmax, float c,
+                           unsigned long long* bad, uint32_t* first) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t h0 = pcg((uint32_t)i ^ seed), h1 = pcg(h0 + 0x9e3779b9u), h2 = pcg(h1 ^ 0x85ebca6bu);
+    float b = bmin + (bmax - bmin) * ((h0 >> 8) * 0x1p-24f);
+    if (h2 & 0x200u) b = -b;
+    float a;
+    const uint32_t mode = h2 & 3u;
+    if (mode == 0) {
+      a = __uint_as_float(__float_as_uint(c * b) + (int32_t)((h2 >> 2) & 15u) - 8);
+    } else if (mode == 1) {
+      a = ((h1 >> 8) * 0x1p-24f - 0.5f) * 1e-30f * b;
+      if (h2 & 0x400u) a = 0.0f;
+      if (h2 & 0x800u) a = -a;
+    } else {
+      a = ((h1 >> 8) * 0x1p-23f - 1.0f) * 2.0f * c * b;
+    }
+    const float rb = __builtin_amdgcn_rcpf(b);
+    const float qf = quot_for_cmp(a, b, rb, c), qe = a / b;
+    if ((qf >= 0) != (qe >= 0) || (qf <= c) != (qe <= c)) {
       atomicAdd(bad, 1ull);
       atomicMin(first, (uint32_t)i);
     }
@@ -127,6 +155,15 @@ int tsdf_selfcheck_round_quot(uint32_t seed, uint64_t n, float bmin, float bmax,
   Out* d = start();
   if (!d) return -1;
   hipLaunchKernelGGL(k_round_quot, dim3(8192), dim3(256), 0, 0, seed, n, bmin, bmax, qmax, &d->bad,
+                     &d->first);
+  return finish(d, bad, first);
+}
+
+int tsdf_selfcheck_quot_cmp(uint32_t seed, uint64_t n, float bmin, float bmax, float c,
+                            unsigned long long* bad, uint32_t* first) {
+  Out* d = start();
+  if (!d) return -1;
+  hipLaunchKernelGGL(k_quot_cmp, dim3(8192), dim3(256), 0, 0, seed, n, bmin, bmax, c, &d->bad,
                      &d->first);
   return finish(d, bad, first);
 }

@@ -116,7 +116,7 @@ def load(path: str | None = None):
     L.tsdf_query.argtypes = [P, P, P, i64, C.POINTER(i64)]
     L.tsdf_get_stats.argtypes = [P, C.POINTER(Stats), i]
     L.tsdf_synchronize.argtypes = [P]
-    L.tsdf_profile_begin.argtypes = [P]
+    L.tsdf_profile_begin.argtypes = [P, i]
     L.tsdf_profile_end.argtypes = [P, C.POINTER(Profile)]
     L.tsdf_debug_dump.argtypes = [P, P, P, P, P, P, P, P]
     L.tsdf_debug_stamps.argtypes = [P, P, i64, C.POINTER(i)]

@@ -127,7 +127,12 @@ int tsdf_query(tsdf_engine* e, const float* bounds, tsdf_voxel* out, int64_t cap
 
 int tsdf_get_stats(tsdf_engine* e, tsdf_stats* out, int clear_status);
 int tsdf_synchronize(tsdf_engine* e);
-int tsdf_profile_begin(tsdf_engine* e);
+/* mode TSDF_PROFILE_PHASES: HIP events between all four phases of every integrate call;
+ * TSDF_PROFILE_INTEGRATE: only the two events bracketing the fused update kernel (least
+ * perturbation of a timed loop; the other phase times read 0). */
+#define TSDF_PROFILE_PHASES 0
+#define TSDF_PROFILE_INTEGRATE 1
+int tsdf_profile_begin(tsdf_engine* e, int mode);
 int tsdf_profile_end(tsdf_engine* e, tsdf_profile* out);
 
 /* Test-only full state dump (Query exposes only tsdf): the 2^22-entry hash table as

@@ -1,0 +1,103 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures under tests/golden/ (run from the repo root, CPU only).
+
+1. kat_reference.json -- the known-answer vectors the reference's own tests hold for this path,
+   transcribed as data: utils/tests/voxel_hash_test.cu (Single :56-92, Multiple :94-126,
+   Collision :128-180) and utils/tests/voxel_mem_test.cu (Test1 :38-90). They are the only golden
+   facts the reference ships; the reference itself is CUDA + Eigen + OpenCV and
+   cannot be built or run here, so no reference-generated integrate output exists.
+2. integrate_48x36.npz -- a small synthetic stream (inputs stored verbatim: rgb, depth, ht, lt,
+   poses, intrinsics) and the CPU oracle's outputs after every frame (per-frame counters) and at
+   the end (active hash entries, free-block stack, voxel state of every live block, raycast images,
+   Query result). Pins the oracle against drift (tests/test_golden.py) and gives the GPU tests a
+   fixed target that needs no oracle call (tests/test_gpu_golden.py). "Parity unpinned" applies:
+   these outputs are the restatement's, not the reference's.
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "disinfect-slam_amd"))
+
+# ---- 1. reference KATs (data only) ----
+KAT = {
+    "source": "utils/tests/voxel_hash_test.cu, utils/tests/voxel_mem_test.cu (yuzhou42/disinfect-slam)",
+    "num_bucket": 1 << 21,
+    "hash": [  # voxel_hash_test.cu:133-135: three block keys that land in the last bucket
+        {"key": [33, 180, 42], "bucket": (1 << 21) - 1},
+        {"key": [61, 16, 170], "bucket": (1 << 21) - 1},
+        {"key": [63, 171, 45], "bucket": (1 << 21) - 1},
+    ],
+    "collision": {  # voxel_hash_test.cu:137-155: one key per Allocate launch
+        "launches": [[[33, 180, 42]], [[61, 16, 170]], [[63, 171, 45]]],
+        "active_after_each": [2, 3, 4],
+        "preallocated": [[0, 0, 0]],
+    },
+    "single": {  # voxel_hash_test.cu:56-92
+        "allocate": [1, 1, 1], "retrieve_point": [8, 8, 8], "expect_block": [1, 1, 1],
+        "empty_point": [0, 0, 0], "expect_empty_weight": 0,
+        "assign": [[[0, 0, i], [i, i, i, i]] for i in range(8)],
+    },
+    "multiple": {"n": 128},  # voxel_hash_test.cu:94-126: diagonal blocks (i, i, i), voxel (i,i,i,i)
+    "mem_pool": {  # voxel_mem_test.cu:38-90: acquire -> init weight 0; set weight; release
+        "num_blocks_log2": 12, "init_weight": 0, "init_tsdf": -1.0, "init_prob": 0.5,
+    },
+}
+
+
+def make_integrate():
+    from _oracle import OracleGrid
+    from tsdf_amd import synth
+
+    W, H, voxel, trunc, bits, nframes = 48, 36, 0.02, 0.08, 11, 6
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    ora = OracleGrid(voxel, trunc, bits)
+    rgb, depth, ht, lt, q, t, stats = [], [], [], [], [], [], []
+    for f in range(nframes):
+        fr = synth.render(cam, 3 * f)
+        ora.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], 4.0, cam.K, fr["q"], fr["t"])
+        s = ora.stats()
+        stats.append([s["last_num_visible"], s["last_num_updated"], s["last_num_deleted"],
+                      s["active_blocks"]])
+        rgb.append(fr["rgb"]); depth.append(fr["depth"]); ht.append(fr["ht"]); lt.append(fr["lt"])
+        q.append(fr["q"]); t.append(fr["t"])
+    d = ora.dump()
+    live = np.flatnonzero(d["entry_idx"] >= 0)
+    idx = d["entry_idx"][live]
+    blk = lambda a: a.reshape(-1, 512, *a.shape[1:])[idx]
+    rq, rt = q[-1], t[-1]
+    rgba, normal = ora.raycast(cam.K, W, H, rq, rt, 4.0)
+    query = ora.query(None)
+    out = dict(
+        W=W, H=H, voxel=voxel, trunc=trunc, num_block_bits=bits, max_depth=4.0,
+        K=np.asarray(cam.K, np.float32),
+        rgb=np.stack(rgb), depth=np.stack(depth), ht=np.stack(ht), lt=np.stack(lt),
+        q=np.stack(q).astype(np.float32), t=np.stack(t).astype(np.float32),
+        stats=np.asarray(stats, np.int64),
+        live_entry=live.astype(np.int32), live_pos=d["entry_pos"][live], live_idx=idx,
+        heap=d["heap"], free=np.int32(d["free"]),
+        tsdf=blk(d["tsdf"]), prob=blk(d["prob"]), rgbw=blk(d["rgbw"]),
+        rgba=rgba, normal=normal, query_count=np.int64(query.shape[0]),
+        query_sha256=np.frombuffer(hashlib.sha256(np.ascontiguousarray(query)).digest(), np.uint8),
+        query_head=query[:2048],
+    )
+    ora.close()
+    return out
+
+
+def main():
+    json.dump(KAT, open(os.path.join(HERE, "kat_reference.json"), "w"), indent=1)
+    g = make_integrate()
+    np.savez_compressed(os.path.join(HERE, "integrate_48x36.npz"), **g)
+    print("live blocks", g["live_entry"].size, "query voxels", int(g["query_count"]),
+          "stats", g["stats"].tolist())
+
+
+if __name__ == "__main__":
+    main()

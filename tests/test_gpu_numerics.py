@@ -7,6 +7,8 @@ The integrate and ingest kernels replace the 11-op IEEE divide where an exact sh
  - round_quot(a, b, rcp(b))   -- roundf(a / b) from a reciprocal estimate with an IEEE fallback
    near rounding boundaries (projection to pixels, colour averages); checked on 2^28 random and
    boundary-adversarial pairs per divisor range;
+ - quot_for_cmp(a, b, rcp(b), c) -- a / b where only its order against 0 and c matters
+   (voxel_visible's frustum test); adversarial samples at both thresholds;
  - f2i / f2s / f2u8 via v_cvt_{i,u}32_f32 -- checked on every float bit pattern.
 Each must agree bit for bit with the correctly rounded divide / cvt.rzi semantics.
 """
@@ -29,6 +31,7 @@ def lib():
     L.tsdf_selfcheck_quot_const.argtypes = [f, u32, u32, P64, P32]
     L.tsdf_selfcheck_round_quot.argtypes = [u32, u64, f, f, f, P64, P32]
     L.tsdf_selfcheck_convert.argtypes = [u32, u32, P64, P32]
+    L.tsdf_selfcheck_quot_cmp.argtypes = [u32, u64, f, f, f, P64, P32]
     return L
 
 
@@ -71,3 +74,10 @@ def test_round_quot_random(lib, bmin, bmax, qmax):
 def test_convert_all_floats(lib):
     bad, first = _run(lib.tsdf_selfcheck_convert, 0, 0xFFFFFFFF)
     assert bad == 0, f"{bad} mismatches, first bits {first:#x}"
+
+
+@pytest.mark.parametrize("c", [639.0, 479.0, 79.0, 1279.0, 1919.0, 1079.0])
+def test_quot_for_cmp(lib, c):
+    for bmin, bmax in [(1e-3, 0.05), (0.05, 20.0)]:
+        bad, first = _run(lib.tsdf_selfcheck_quot_cmp, 777, 1 << 27, bmin, bmax, c)
+        assert bad == 0, f"c={c}: {bad} mismatches, first sample {first}"
