@@ -58,9 +58,9 @@ def main():
     import numpy as np
     import torch
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from tsdf_amd import dist as tdist
+
+    rank, local, world = tdist.env_rank_world()
     if world != a.gpus and world != 1:
         raise SystemExit(f"WORLD_SIZE={world} but --gpus {a.gpus}")
     dist = None
@@ -81,10 +81,10 @@ def main():
     nphase = min(100, a.steps)  # untimed phase-breakdown pass after the timed region
     nframes = a.warmup + a.steps + nphase
     # streams mode: each rank's camera starts a third of an orbit apart (its own stream)
-    offset = rank * 240 if (world > 1 and a.mode == "streams") else 0
+    offset = tdist.stream_offset(a.mode, rank, world)
     frames = synth.render_torch(cam, list(range(offset, offset + nframes)), device=dev)
     torch.cuda.synchronize()
-    shard_index, shard_count = (rank, world) if (a.mode == "sharded" and world > 1) else (0, 1)
+    shard_index, shard_count = tdist.shard_of(a.mode, rank, world)
     stream = torch.cuda.current_stream()
     eng = tsdf_amd.Engine(a.voxel, a.trunc, max_width=a.width, max_height=a.height,
                           num_block_bits=a.block_bits, device=torch.cuda.current_device(),
@@ -122,14 +122,8 @@ def main():
     phases = eng.profile_end()
     st = eng.stats()
     elapsed = t1 - t0
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        tot = torch.tensor([prof["sum_visible"], prof["sum_updated"]], dtype=torch.float64, device=dev)
-        dist.all_reduce(tot)
-    units = a.steps * (world if a.mode == "streams" else 1)
-    value = units / elapsed
+    elapsed = tdist.max_over_ranks(elapsed, device=dev)
+    value = tdist.units(a.mode, a.steps, world) / elapsed
 
     # ---- roofline of the fused integrate kernel (this rank's launches) ----
     W, H = a.width, a.height

@@ -1,0 +1,66 @@
+"""Multi-GPU plumbing of the TSDF engine: one process per GPU (torch.distributed.run), no data-path
+collective.
+
+ - streams mode (weak scaling): rank r integrates its own camera stream into its own volume;
+ - sharded mode (strong scaling): every rank sees the same frames and owns the blocks whose 4^3
+   brick hashes to it (tsdf_block_owner); a whole-volume Query is the union of the shards.
+
+The functions here are backend-agnostic (RCCL "nccl" on the GPU box, "gloo" in the CPU tests).
+"""
+from __future__ import annotations
+
+import os
+
+
+def env_rank_world():
+    """(rank, local_rank, world_size) from the torch.distributed.run environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def shard_of(mode: str, rank: int, world: int):
+    """(shard_index, shard_count) of this rank's engine."""
+    return (rank, world) if (mode == "sharded" and world > 1) else (0, 1)
+
+
+def stream_offset(mode: str, rank: int, world: int, stride: int = 240) -> int:
+    """First frame of this rank's camera stream (streams mode: a third of an orbit apart)."""
+    return rank * stride if (mode == "streams" and world > 1) else 0
+
+
+def units(mode: str, steps: int, world: int) -> int:
+    """Frames integrated by the whole job in `steps` timed steps."""
+    return steps * (world if mode == "streams" else 1)
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """MAX of a per-rank float over all ranks (identity without an initialised process group)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(values, device=None):
+    """Element-wise SUM of a list of per-rank numbers over all ranks."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [float(v) for v in values]
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    dist.all_reduce(t)
+    return [float(v) for v in t.tolist()]
+
+
+def gather_block_sets(positions, device=None):
+    """All-gather every rank's live block positions (N x 3 int16 numpy) -> list per rank."""
+    import numpy as np
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [np.asarray(positions)]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, np.asarray(positions))
+    return out

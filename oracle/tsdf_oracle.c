@@ -52,6 +52,7 @@ struct ora_grid {
   int range_cap;
   int32_t* vis;    /* visible_blocks_ entry indices (entry order) */
   ora_stats st;
+  int shard_index, shard_count; /* spatial sharding (not in the reference) */
 };
 
 /* ---------------- float math (utils/cuda/camera.cuh, lie_group.cuh, Eigen 3.3) ------------- */
@@ -393,6 +394,22 @@ static void make_params(const ora_grid* g, frame_params* P, const float K[4], in
 }
 
 /* voxel_tsdf.cu:104-147 block_allocate_kernel (one pixel); allocations sequential. */
+/* owner of block b among shard_count GPUs: hash of the 4^3-block brick; must match
+ * tsdf_block_owner / brick_owner in the engine */
+uint32_t ora_block_owner(int16_t x, int16_t y, int16_t z, uint32_t shards) {
+  uint32_t h = ((uint32_t)(int32_t)(x >> 2) * 0x9E3779B1u) ^ ((uint32_t)(int32_t)(y >> 2) * 0x85EBCA77u) ^
+               ((uint32_t)(int32_t)(z >> 2) * 0xC2B2AE3Du);
+  h ^= h >> 16;
+  h *= 0x7FEB352Du;
+  h ^= h >> 15;
+  return shards <= 1 ? 0u : h % shards;
+}
+
+void ora_set_shard(ora_grid* g, int index, int count) {
+  g->shard_index = index;
+  g->shard_count = count;
+}
+
 static void allocate_pixel(ora_grid* g, const frame_params* P, const float* depth, int x, int y) {
   const int idx = y * P->W + x;
   const float d = depth[idx];
@@ -417,7 +434,9 @@ static void allocate_pixel(ora_grid* g, const frame_params* P, const float* dept
   for (int i = 0; i <= step_grid; ++i) {
     s3 p = {f2s(roundf(pos.x)), f2s(roundf(pos.y)), f2s(roundf(pos.z))};
     s3 b = point_to_block(p);
-    if (block_visible(P, b, 1)) {
+    if (block_visible(P, b, 1) &&
+        (g->shard_count <= 1 ||
+         ora_block_owner(b.x, b.y, b.z, (uint32_t)g->shard_count) == (uint32_t)g->shard_index)) {
       const int r2 = hash_allocate(g, b);
       if (r2 != 0) g->st.last_num_candidates++;
       if (r2 > 0) g->st.last_num_alloc++;

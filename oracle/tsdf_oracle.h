@@ -42,6 +42,10 @@ typedef struct ora_stats {
  * (voxel_mem.cuh:11) so tests can run small pools. */
 ora_grid* ora_create(float voxel_size, float truncation, int num_block_bits);
 void ora_destroy(ora_grid* g);
+/* Spatial sharding (not in the reference): the grid allocates only blocks whose
+ * 4^3-block brick hashes to shard index (ora_block_owner == index). count <= 1: unsharded. */
+void ora_set_shard(ora_grid* g, int index, int count);
+uint32_t ora_block_owner(int16_t x, int16_t y, int16_t z, uint32_t shards);
 
 /* voxel_tsdf.cu:347-375 TSDFGrid::Integrate. rgb: HxWx3 u8; depth/ht/lt: HxW f32 (ht/lt may be
  * NULL -> 1.0, tsdf_module.cc:29-33). K = {fx, fy, cx, cy}; cam_T_world = (q xyzw, t). */

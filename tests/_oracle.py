@@ -67,6 +67,9 @@ def lib():
         L.ora_pool_release.argtypes = [P, P, C.c_int]
         L.ora_pool_set_weight.argtypes = [P, C.c_int32, C.c_uint8]
         L.ora_pool_get_weights.argtypes = [P, C.c_int32, P]
+        L.ora_set_shard.argtypes = [P, C.c_int, C.c_int]
+        L.ora_block_owner.restype = C.c_uint32
+        L.ora_block_owner.argtypes = [C.c_int16, C.c_int16, C.c_int16, C.c_uint32]
         L.ora_hash.restype = C.c_uint32
         L.ora_hash.argtypes = [C.c_int16, C.c_int16, C.c_int16]
         _lib = L
@@ -77,6 +80,10 @@ def _p(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
 
 
+def block_owner(x, y, z, shards) -> int:
+    return int(lib().ora_block_owner(x, y, z, shards))
+
+
 def hash_block(x, y, z) -> int:
     return int(lib().ora_hash(x, y, z))
 
@@ -84,12 +91,15 @@ def hash_block(x, y, z) -> int:
 class OracleGrid:
     """CPU restatement of TSDFGrid (voxel_tsdf.cuh:32-124)."""
 
-    def __init__(self, voxel_size: float, truncation: float, num_block_bits: int = 18):
+    def __init__(self, voxel_size: float, truncation: float, num_block_bits: int = 18,
+                 shard_index: int = 0, shard_count: int = 1):
         self.voxel_size = voxel_size
         self.truncation = truncation
         self.h = lib().ora_create(voxel_size, truncation, num_block_bits)
         if not self.h:
             raise MemoryError("ora_create failed")
+        if shard_count > 1:
+            lib().ora_set_shard(self.h, shard_index, shard_count)
         self.num_blocks = lib().ora_num_blocks(self.h)
 
     def close(self):

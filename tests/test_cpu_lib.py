@@ -86,3 +86,12 @@ def test_synth_deterministic():
     assert d.dtype == np.float32 and d.max() <= synth.MAX_RANGE and (d > 0).mean() > 0.9
     assert np.all(a["ht"] >= 0.02) and np.all(a["ht"] <= 0.98)
     assert np.allclose(a["ht"] + a["lt"], 1.0, atol=1e-6)
+
+
+def test_block_owner_matches_oracle():
+    import tsdf_amd
+    from _oracle import block_owner
+    rng = np.random.default_rng(7)
+    for k in rng.integers(-2000, 2000, size=(500, 3)):
+        for n in (2, 3, 8):
+            assert tsdf_amd.block_owner(*map(int, k), n) == block_owner(*map(int, k), n)
