@@ -90,7 +90,7 @@ def main():
                           num_block_bits=a.block_bits, device=torch.cuda.current_device(),
                           shard_index=shard_index, shard_count=shard_count,
                           stream=stream.cuda_stream)
-    K = cam.K
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])  # ctypes struct cached once
     poses = [tsdf_amd.SE3(frames["q"][i], frames["t"][i]) for i in range(nframes)]
 
     def step(i):
@@ -180,6 +180,12 @@ def main():
                 "traffic": traffic,
                 "alg_bytes_per_launch": int(alg_bytes),
                 "us_per_launch": round(t_int * 1e6, 3),
+                # cross-check: first-WG start -> last-WG end from the in-kernel 100 MHz clock
+                # (what rocprofv3's kernel trace measures; the HIP events above also include the
+                # per-launch dispatch / completion overhead)
+                "us_per_launch_device_clock": round(prof["ms_integrate_device"] / a.steps * 1e3, 3),
+                "achieved_device_clock": round(alg_bytes / (prof["ms_integrate_device"] / a.steps / 1e3) / 1e9, 1)
+                if prof["ms_integrate_device"] > 0 else None,
             },
             "cpu_baseline": cpu,
             "phases_ms_per_frame": {  # separate untimed pass of nphase frames

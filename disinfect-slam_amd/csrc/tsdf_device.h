@@ -88,6 +88,7 @@ struct DevCounters {
   unsigned long long total_alloc;
   unsigned long long total_deleted;
   unsigned long long frames;
+  unsigned long long integrate_ticks;  // sum of k_integrate device durations (100 MHz clock)
 };
 
 // ------------------------------------------------------------------------------------------

@@ -115,7 +115,7 @@ struct tsdf_engine {
   int prof_mode = TSDF_PROFILE_PHASES;
   std::vector<std::array<hipEvent_t, 5>> events;
   size_t ev_used = 0;
-  unsigned long long prof_vis0 = 0, prof_upd0 = 0;
+  unsigned long long prof_vis0 = 0, prof_upd0 = 0, prof_ticks0 = 0;
 };
 
 namespace {
@@ -124,7 +124,7 @@ void free_all(tsdf_engine* e) {
   EngineDev& D = e->D;
   void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.fresh_flag, D.occ,
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs,      D.fresh,
-                  D.vis,     D.band,    D.cand,     D.wg_upd, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
+                  D.vis,     D.band,    D.cand,     D.wg_upd, D.wg_end, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
                   e->q_sel,  e->q_count, e->q_out,   e->t_keys, e->t_recs,    e->t_count,
                   e->t_i32,  e->t_u32,   e->t_f0,    e->t_f1,   e->t_s4};
@@ -304,6 +304,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.band, kBands * kBandStride);
   ALLOC(D.cand, nb);
   ALLOC(D.wg_upd, kIntegrateGrid);
+  ALLOC(D.wg_end, kIntegrateGrid + 1);
   {  // one resident wave of k_integrate workgroups: no second-round stragglers
     int per_cu = 0, ncu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate, 256, 0) != hipSuccess ||
@@ -542,6 +543,7 @@ int tsdf_profile_begin(tsdf_engine* e, int mode) {
   if (rc) return rc;
   e->prof_vis0 = e->h_ctr->total_visible;
   e->prof_upd0 = e->h_ctr->total_updated;
+  e->prof_ticks0 = e->h_ctr->integrate_ticks;
   e->ev_used = 0;
   e->profiling = true;
   return TSDF_OK;
@@ -566,6 +568,7 @@ int tsdf_profile_end(tsdf_engine* e, tsdf_profile* o) {
   }
   o->sum_visible = (int64_t)(e->h_ctr->total_visible - e->prof_vis0);
   o->sum_updated = (int64_t)(e->h_ctr->total_updated - e->prof_upd0);
+  o->ms_integrate_device = (double)(e->h_ctr->integrate_ticks - e->prof_ticks0) * 1e-5;
   return TSDF_OK;
 }
 

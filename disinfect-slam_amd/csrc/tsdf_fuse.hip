@@ -8,7 +8,8 @@ namespace tsdf {
 // k_vis: check_visibility_kernel (voxel_tsdf.cu:82-93) over the 512 KiB occupancy bitmap instead
 // of the 48 MiB table: every allocated block with any corner in view (no depth test) is appended
 // to the list of the image band its centre projects into (LDS counts, one global atomic per band
-// per workgroup). Order is irrelevant to the update; the carving resolver restores the
+// per workgroup). Each wave first compacts its live entries into LDS so the corner tests run
+// 8 lanes per block on dense work instead of one lane per bitmap word. Order is irrelevant to the update; the carving resolver restores the
 // reference's entry order for the deletes.
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ int block_band(const FrameParams& P, int16_t bx, int16_t by, int16_t bz) {
@@ -23,34 +24,63 @@ __device__ __forceinline__ int block_band(const FrameParams& P, int16_t bx, int1
 
 __global__ __launch_bounds__(256) void k_vis(EngineDev D, FrameParams P) {
   TSDF_STAMP(D, 2, 0);
+  // per wave: its 64 occupancy words (4096 entries) compacted to a list of live entries, then
+  // filtered in place to the visible ones packed as entry | band << 24
+  __shared__ uint32_t s_list[4][4096];
   __shared__ int s_cnt[kBands], s_base[kBands];
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  uint32_t* L = s_list[wave];
   if (threadIdx.x < kBands) s_cnt[threadIdx.x] = 0;
-  __syncthreads();
   const int w = blockIdx.x * 256 + threadIdx.x;  // kOccWords == 256 * 256
-  unsigned long long occ = D.occ[w], vis = 0ull;
+  unsigned long long occ = D.occ[w];
+  const int c = __popcll(occ);
+  const int incl = wave_incl_scan(c);
+  const int total = __shfl(incl, 63, 64);
+  int p = incl - c;
   while (occ) {
     const int b = __ffsll((long long)occ) - 1;
     occ &= occ - 1;
-    const Ent en = load_ent(D.table, (uint32_t)(w * 64 + b));
-    if (block_visible<false>(P, en.x, en.y, en.z)) {
-      vis |= 1ull << b;
-      atomicAdd(&s_cnt[block_band(P, en.x, en.y, en.z)], 1);
-    }
+    L[p++] = (uint32_t)(w * 64 + b);
   }
   __syncthreads();
-  if (threadIdx.x < kBands) {
-    const int c = s_cnt[threadIdx.x];
-    s_base[threadIdx.x] = c ? atomicAdd(&D.band[threadIdx.x * kBandStride], c) : 0;
+  // any-corner visibility (is_block_visible<false>), 8 lanes per block, one corner each
+  const int grp = lane >> 3, corner = lane & 7;
+  int nvis = 0;
+  for (int base = 0; base < total; base += 8) {
+    const int i = base + grp;
+    bool v = false;
+    uint32_t e = 0;
+    Ent en{};
+    if (i < total) {
+      e = L[i];
+      en = load_ent(D.table, e);
+      v = voxel_visible(P, (int16_t)((int16_t)(en.x << kBlockLenBits) + ((corner >> 0) & 1) * (kBlockLen - 1)),
+                        (int16_t)((int16_t)(en.y << kBlockLenBits) + ((corner >> 1) & 1) * (kBlockLen - 1)),
+                        (int16_t)((int16_t)(en.z << kBlockLenBits) + ((corner >> 2) & 1) * (kBlockLen - 1)));
+    }
+    const unsigned long long bal = __ballot(v);
+    const bool lead = corner == 0 && i < total && ((bal >> (lane & ~7)) & 0xFFull) != 0;
+    const unsigned long long leads = __ballot(lead);
+    if (lead) {  // rank among this round's visible blocks; slots < base + 8 were all read above
+      const int band = block_band(P, en.x, en.y, en.z);
+      L[nvis + __popcll(leads & ((1ull << lane) - 1ull))] = e | ((uint32_t)band << 24);
+      atomicAdd(&s_cnt[band], 1);
+    }
+    nvis += __popcll(leads);
+  }
+  __syncthreads();
+  if (threadIdx.x < kBands) {  // one global atomic per non-empty band per workgroup
+    const int cnt = s_cnt[threadIdx.x];
+    s_base[threadIdx.x] = cnt ? atomicAdd(&D.band[threadIdx.x * kBandStride], cnt) : 0;
     s_cnt[threadIdx.x] = 0;
   }
   __syncthreads();
-  while (vis) {
-    const int b = __ffsll((long long)vis) - 1;
-    vis &= vis - 1;
-    const uint32_t e = (uint32_t)(w * 64 + b);
-    const Ent en = load_ent(D.table, e);
-    const int band = block_band(P, en.x, en.y, en.z);
+  for (int k = lane; k < nvis; k += 64) {
+    const uint32_t pk = L[k];
+    const uint32_t e = pk & 0xFFFFFFu;
+    const int band = (int)(pk >> 24);
     const int pos = s_base[band] + atomicAdd(&s_cnt[band], 1);
+    const Ent en = load_ent(D.table, e);
     VisRec r;
     r.x = en.x;
     r.y = en.y;
@@ -111,6 +141,9 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
   const float neg_trunc = -P.trunc;
   int my_upd = 0;
   TSDF_STAMP(D, 3, 0);
+  // device-clock duration of this launch: start stamp by WG 0 (dispatched first), end stamp per WG;
+  // k_resolve_delete takes the max (bench cross-check of the HIP-event timing)
+  if (blockIdx.x == 0 && threadIdx.x == 0) D.wg_end[kIntegrateGrid] = __builtin_amdgcn_s_memrealtime();
   for (int pp = p_lo + (blockIdx.x >> 3); pp < p_hi; pp += ngrp) {
     const int b = 2 * pp + pair;
     float mn = __builtin_inff();
@@ -246,7 +279,10 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
   const int tot = wave_sum(my_upd);
   if (lane == 0) s_upd[wave] = tot;
   __syncthreads();
-  if (threadIdx.x == 0) D.wg_upd[blockIdx.x] = s_upd[0] + s_upd[1] + s_upd[2] + s_upd[3];
+  if (threadIdx.x == 0) {
+    D.wg_upd[blockIdx.x] = s_upd[0] + s_upd[1] + s_upd[2] + s_upd[3];
+    D.wg_end[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+  }
   TSDF_STAMP(D, 3, 1);
 }
 
@@ -273,11 +309,22 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
   }
   claims_clear(L);
   if (!direct) {  // voxels updated by k_integrate: sum of its per-workgroup counts
+    __shared__ unsigned long long s_tend;
+    if (t == 0) s_tend = 0ull;
+    __syncthreads();
     int u = 0;
-    for (int i = t; i < D.integrate_grid; i += kResolveThreads) u += D.wg_upd[i];
+    unsigned long long te = 0ull;
+    for (int i = t; i < D.integrate_grid; i += kResolveThreads) {
+      u += D.wg_upd[i];
+      te = max(te, D.wg_end[i]);
+    }
+    atomicMax(&s_tend, te);
     int tot;
-    (void)block_excl_scan(u, L.scan, &tot);
-    if (t == 0) D.ctr->last_updated = (unsigned long long)tot;
+    (void)block_excl_scan(u, L.scan, &tot);  // (its barriers also publish s_tend)
+    if (t == 0) {
+      D.ctr->last_updated = (unsigned long long)tot;
+      D.ctr->integrate_ticks += s_tend - D.wg_end[kIntegrateGrid];
+    }
   }
   __syncthreads();
   const int n = *count;

@@ -35,6 +35,7 @@ struct EngineDev {
   int32_t* band;                // kBands x kBandStride: record count of each band list
   VisRec* cand;                 // carve candidates (any order; resolver sorts by entry)
   int32_t* wg_upd;              // kIntegrateGrid per-workgroup updated-voxel counts
+  unsigned long long* wg_end;   // kIntegrateGrid + 1: per-WG end stamps, [kIntegrateGrid] = start
   // packed frame
   float4* pixA;                 // {depth, range, w_new, rgb}
   float2* pixB;                 // {log2 ht, log2 lt}

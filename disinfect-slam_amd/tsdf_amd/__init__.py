@@ -62,7 +62,11 @@ class CameraIntrinsics:
                                 float(-f32(self.cy) * fy_inv))
 
     def _c(self) -> _lib.Intrinsics:
-        return _lib.Intrinsics(self.fx, self.fy, self.cx, self.cy)
+        c = self.__dict__.get("_cc")
+        if c is None:  # frozen dataclass: cache the ctypes struct once
+            c = _lib.Intrinsics(self.fx, self.fy, self.cx, self.cy)
+            object.__setattr__(self, "_cc", c)
+        return c
 
 
 @dataclasses.dataclass(frozen=True)
@@ -131,7 +135,11 @@ class SE3:
         return SE3(_qmul_sse(self.q, other.q), _qrot(self.q, other.t) + self.t)
 
     def _c(self) -> _lib.Pose:
-        return _lib.Pose(*[float(v) for v in self.q], *[float(v) for v in self.t])
+        c = self.__dict__.get("_cc")
+        if c is None:  # SE3 is treated as immutable: cache the ctypes struct once
+            c = _lib.Pose(*[float(v) for v in self.q], *[float(v) for v in self.t])
+            self._cc = c
+        return c
 
 
 @dataclasses.dataclass(frozen=True)

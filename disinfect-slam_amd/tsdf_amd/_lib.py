@@ -81,6 +81,7 @@ class Profile(C.Structure):
         ("ms_carve", C.c_double),
         ("sum_visible", C.c_int64),
         ("sum_updated", C.c_int64),
+        ("ms_integrate_device", C.c_double),
     ]
 
 

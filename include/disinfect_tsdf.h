@@ -100,6 +100,9 @@ typedef struct tsdf_profile { /* device time of the integrate phases between beg
   double ms_carve;     /* space-carving compaction + delete resolve */
   int64_t sum_visible; /* sum of N_vis over the profiled frames */
   int64_t sum_updated; /* sum of updated voxels over the profiled frames */
+  double ms_integrate_device; /* k_integrate first-workgroup start -> last-workgroup end, summed
+                                 over the profiled frames (in-kernel 100 MHz clock; excludes the
+                                 dispatch overhead the HIP events of ms_integrate include) */
 } tsdf_profile;
 
 /* ---- engine lifetime: TSDFGrid::TSDFGrid / ~TSDFGrid (voxel_tsdf.cu:309-345) ---- */

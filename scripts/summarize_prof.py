@@ -45,6 +45,18 @@ def main(out):
                 "max_us": float(r["MaxNs"]) / 1e3,
                 "total_ms": float(r["TotalDurationNs"]) / 1e6,
             }
+    # per-dispatch trace: k_integrate durations inside the bench's timed window (launches
+    # [warmup, warmup + steps) of the kernel), the same launches the bench's HIP events bracket
+    tr = find(os.path.join(out, "trace", "**", "*kernel_trace.csv"))
+    b0 = bench_line(os.path.join(out, "trace_bench.log"))
+    if tr and b0:
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(tr))
+                if r["Kernel_Name"].split("(")[0].endswith("tsdf::k_integrate")]
+        w, k = b0["warmup"], b0["steps"]
+        win = durs[w:w + k]
+        if win:
+            res["integrate_timed_window"] = {"launches": len(win), "avg_us": statistics.mean(win) / 1e3,
+                                             "event_avg_us": b0["roofline"]["us_per_launch"]}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         f = find(os.path.join(out, f"pmc_{c}", "**", "*counter_collection.csv"))
         if not f:
@@ -70,6 +82,19 @@ def main(out):
         if b:
             res["integrate_alg_bytes_per_launch"] = b["roofline"]["alg_bytes_per_launch"]
     json.dump(res, open(os.path.join(out, "summary.json"), "w"), indent=1)
+    if "integrate_hbm_bytes_per_launch" in res and b:
+        # the file bench.py reads for roofline.traffic (same workload only)
+        json.dump({"width": b["config"]["width"], "height": b["config"]["height"],
+                   "hbm_bytes_per_launch": res["integrate_hbm_bytes_per_launch"],
+                   "fetch_bytes_per_launch": ki["FETCH_SIZE"]["bytes_per_launch"],
+                   "write_bytes_per_launch": ki["WRITE_SIZE"]["bytes_per_launch"],
+                   "note": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, separate passes, "
+                           "mean over all k_integrate dispatches of the bench command"},
+                  open(os.path.join(out, "pmc_integrate_latest.json"), "w"), indent=1)
+    if "integrate_timed_window" in res:
+        t = res["integrate_timed_window"]
+        print(f"k_integrate timed window: {t['launches']} launches avg {t['avg_us']:.2f}us "
+              f"(bench HIP events {t['event_avg_us']:.2f}us)")
     for k, v in sorted(res["kernels"].items(), key=lambda kv: -kv[1]["total_ms"]):
         p = res["pmc"].get(k, {})
         fb = p.get("FETCH_SIZE", {}).get("bytes_per_launch")
