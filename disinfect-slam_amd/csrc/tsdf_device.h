@@ -162,6 +162,44 @@ __device__ __forceinline__ uint32_t round_quot_u8(float a, float b, float rb) {
   return (uint32_t)min(255, max(0, round_quot_i(a, b, rb)));
 }
 
+// ---- the same helpers on voxel pairs: ext_vector float2 arithmetic lowers to gfx950's packed
+// v_pk_{mul,add,fma}_f32 (IEEE per element, so results are identical to the scalar forms); lanes
+// with act == false never take the IEEE fallback (their results are discarded by the caller) ----
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2f v2(float a, float b) {
+  v2f r;
+  r.x = a;
+  r.y = b;
+  return r;
+}
+__device__ __forceinline__ v2f vfma(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
+
+__device__ __forceinline__ void round_quot_i2(v2f a, v2f b, v2f rb, bool act0, bool act1,
+                                              int32_t& o0, int32_t& o1) {
+  const v2f q = a * rb;
+  const v2f h = v2(__builtin_copysignf(0.5f, q.x), __builtin_copysignf(0.5f, q.y));
+  const v2f f1 = vfma(q, v2(1.0f + 0x1p-20f, 1.0f + 0x1p-20f), h);
+  const v2f f2 = vfma(q, v2(1.0f - 0x1p-20f, 1.0f - 0x1p-20f), h);
+  o0 = f2i(f1.x);
+  o1 = f2i(f1.y);
+  if (__builtin_expect(act0 && !(o0 == f2i(f2.x) && fabsf(b.x) < 0x1p100f), 0))
+    o0 = f2i(roundf(a.x / b.x));
+  if (__builtin_expect(act1 && !(o1 == f2i(f2.y) && fabsf(b.y) < 0x1p100f), 0))
+    o1 = f2i(roundf(a.y / b.y));
+}
+
+__device__ __forceinline__ v2f quot_const2(v2f a, float b, float rb, bool act0, bool act1) {
+  const v2f q = a * rb;
+  const v2f r = vfma(-q, v2(b, b), a);
+  v2f o = vfma(r, v2(rb, rb), q);
+  const float fa0 = fabsf(a.x), fq0 = fabsf(q.x), fa1 = fabsf(a.y), fq1 = fabsf(q.y);
+  if (__builtin_expect(act0 && !(fa0 > 0x1p-60f && fa0 < 0x1p60f && fq0 > 0x1p-60f && fq0 < 0x1p60f), 0))
+    o.x = a.x / b;
+  if (__builtin_expect(act1 && !(fa1 > 0x1p-60f && fa1 < 0x1p60f && fq1 > 0x1p-60f && fq1 < 0x1p60f), 0))
+    o.y = a.y / b;
+  return o;
+}
+
 // RN(a / b) where the caller only compares the quotient with 0 and with the float c: the
 // estimate a * rcp(b) is returned when it provably lies on the same side of 0 and of c as the IEEE
 // quotient (distance to c above 2^-20 |q|, |q| and |b| in range), else the IEEE quotient.

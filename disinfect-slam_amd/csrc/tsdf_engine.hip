@@ -100,6 +100,12 @@ struct tsdf_engine {
   int32_t* q_count = nullptr;
   float4* q_out = nullptr;
   int64_t q_out_cap = 0;
+  // mesh extraction scratch
+  int32_t* m_counts = nullptr;
+  int32_t* m_offsets = nullptr;
+  int64_t* m_total = nullptr;
+  float* m_out = nullptr;
+  int64_t m_out_cap = 0;  // triangles
   int16_t* t_keys = nullptr;
   VisRec* t_recs = nullptr;
   int32_t* t_count = nullptr;
@@ -126,7 +132,7 @@ void free_all(tsdf_engine* e) {
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs,      D.fresh,
                   D.vis,     D.band,    D.cand,     D.wg_upd, D.wg_end, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
-                  e->q_sel,  e->q_count, e->q_out,   e->t_keys, e->t_recs,    e->t_count,
+                  e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
                   e->t_i32,  e->t_u32,   e->t_f0,    e->t_f1,   e->t_s4};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -327,6 +333,9 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(e->rc_norm, e->max_pixels);
   ALLOC(e->q_sel, nb);
   ALLOC(e->q_count, 1);
+  ALLOC(e->m_counts, nb);
+  ALLOC(e->m_offsets, nb);
+  ALLOC(e->m_total, 1);
   ALLOC(e->t_count, 1);
 #undef ALLOC
   if (hipHostMalloc(reinterpret_cast<void**>(&e->h_ctr), sizeof(DevCounters)) != hipSuccess)
@@ -504,6 +513,66 @@ int tsdf_query(tsdf_engine* e, const float* bounds, tsdf_voxel* out, int64_t cap
                      e->cfg.voxel_size, e->q_out);
   LAUNCH_OK("k_query_download");
   HIP_OK(hipMemcpyAsync(out, e->q_out, (size_t)nvox * sizeof(float4), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return TSDF_OK;
+}
+
+int tsdf_extract_mesh(tsdf_engine* e, const float* bounds, float missing_tsdf, int min_weight,
+                      float* triangles, int64_t capacity, int64_t* num_triangles, int mem_kind) {
+  if (!e || !num_triangles || (mem_kind != TSDF_MEM_HOST && mem_kind != TSDF_MEM_DEVICE)) {
+    set_error("tsdf_extract_mesh: invalid argument");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  short4 lo = make_short4(0, 0, 0, 0), hi = make_short4(0, 0, 0, 0);
+  if (bounds) {  // the Query block selection (voxel_tsdf.cuh:21-26, voxel_tsdf.cu:429)
+    const float scale = (float)(1. / (double)e->cfg.voxel_size);
+    lo = make_short4(h_f2s(bounds[0] * scale), h_f2s(bounds[2] * scale), h_f2s(bounds[4] * scale), 0);
+    hi = make_short4(h_f2s(bounds[1] * scale), h_f2s(bounds[3] * scale), h_f2s(bounds[5] * scale), 0);
+  }
+  hipStream_t s = e->stream;
+  hipLaunchKernelGGL(k_query_count, dim3(kOccWords / 256), dim3(256), 0, s, e->D, bounds ? 1 : 0,
+                     lo, hi);
+  hipLaunchKernelGGL(k_vis_emit, dim3(kOccWords / 256), dim3(256), 0, s, e->D, e->q_sel,
+                     e->q_count);
+  LAUNCH_OK("mesh select");
+  int32_t nsel = 0;
+  HIP_OK(hipMemcpyAsync(&nsel, e->q_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  *num_triangles = 0;
+  if (nsel == 0) return TSDF_OK;
+  const MeshParams M{e->cfg.voxel_size, missing_tsdf, min_weight};
+  hipLaunchKernelGGL(k_mesh<false>, dim3(nsel), dim3(256), 0, s, e->D, e->q_sel, M, e->m_counts,
+                     (const int32_t*)nullptr, (float*)nullptr);
+  hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, e->m_counts, nsel, e->m_offsets,
+                     e->m_total);
+  LAUNCH_OK("mesh count");
+  int64_t ntri = 0;
+  HIP_OK(hipMemcpyAsync(&ntri, e->m_total, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  *num_triangles = ntri;
+  if (!triangles || ntri == 0) return TSDF_OK;
+  if (capacity < ntri) {
+    set_error("tsdf_extract_mesh: capacity too small");
+    return TSDF_ERR_CAPACITY;
+  }
+  float* dst = reinterpret_cast<float*>(triangles);
+  if (mem_kind == TSDF_MEM_HOST) {
+    if (e->m_out_cap < ntri) {
+      if (e->m_out) (void)hipFree(e->m_out);
+      e->m_out = nullptr;
+      e->m_out_cap = 0;
+      HIP_OK(dmalloc(&e->m_out, (size_t)ntri * 9));
+      e->m_out_cap = ntri;
+    }
+    dst = e->m_out;
+  }
+  hipLaunchKernelGGL(k_mesh<true>, dim3(nsel), dim3(256), 0, s, e->D, e->q_sel, M,
+                     (int32_t*)nullptr, (const int32_t*)e->m_offsets, dst);
+  LAUNCH_OK("mesh emit");
+  if (mem_kind == TSDF_MEM_HOST)
+    HIP_OK(hipMemcpyAsync(triangles, e->m_out, (size_t)ntri * 9 * sizeof(float),
+                          hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
   return TSDF_OK;
 }

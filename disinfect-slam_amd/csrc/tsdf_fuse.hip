@@ -182,74 +182,116 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
                     az = (int16_t)((r.z << kBlockLenBits) + rz);
       const float fy = (float)ay * P.voxel, fz = (float)az * P.voxel;
       int upd_mask = 0;
-      // pass 1: project the lane's 4 voxels and issue every pixel gather before any is consumed
-      // (the gathers are predicated, not branched around, so all 8 stay in flight together)
-      float hzs[4];
+      // ---- pass 1: project the lane's 4 voxels (two packed pairs) and issue every pixel gather
+      // before any is consumed (predicated, so all 8 stay in flight together).
+      // cam_T_world * (x voxel, fy, fz) in QuaternionBase::_transformVector's exact order, with the
+      // parts that do not depend on x computed once per lane (identical operations, so identical
+      // results to se3_apply per voxel).
+      const float qx = P.cq.x, qy = P.cq.y, qz = P.cq.z, qw = P.cq.w;
+      const float qx_fz = qx * fz, qx_fy = qx * fy;
+      float uvx = qy * fz - qz * fy;
+      uvx += uvx;
+      const float w_uvx = qw * uvx, qz_uvx = qz * uvx, qy_uvx = qy * uvx;
+      v2f hzs[2];
       float4 px[4];
       float2 lg[4];
       bool inb[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int16_t ax = (int16_t)(ax0 + rx0 + j);
-        const f3 pw = {(float)ax * P.voxel, fy, fz};
-        const f3 pc = se3_apply(P.cq, P.ct, pw);
-        const float hx = P.fx * pc.x + P.cx * pc.z;
-        const float hy = P.fy * pc.y + P.cy * pc.z;
-        const float hz = pc.z;
-        const float rz = __builtin_amdgcn_rcpf(hz);
-        const int u = round_quot_i(hx, hz, rz);
-        const int v = round_quot_i(hy, hz, rz);
-        hzs[j] = hz;
-        inb[j] = u >= 0 && u < P.W && v >= 0 && v < P.H;
-#if defined(TSDF_EXP) && (TSDF_EXP & 1)  // experiment build: no pixel gathers
-        if (inb[j]) px[j] = make_float4(hz + 0.01f, 1.0f, 1.0f, __uint_as_float(0x00808080u));
-#else
-        if (inb[j]) {
-          const int img = v * P.W + u;
-          px[j] = D.pixA[img];
-          lg[j] = D.pixB[img];
-        }
-#endif
-      }
-      // pass 2: the per-voxel update of tsdf_integrate_kernel (voxel_tsdf.cu:174-203)
+      for (int k = 0; k < 2; ++k) {
+        const v2f wx = v2((float)(int16_t)(ax0 + rx0 + 2 * k), (float)(int16_t)(ax0 + rx0 + 2 * k + 1)) * P.voxel;
+        v2f uvy = qz * wx - qx_fz;
+        v2f uvz = qx_fy - qy * wx;
+        uvy += uvy;
+        uvz += uvz;
+        const v2f cx = qy * uvz - qz * uvy;
+        const v2f cy = qz_uvx - qx * uvz;
+        const v2f cz = qx * uvy - qy_uvx;
+        const v2f pcx = ((wx + w_uvx) + cx) + P.ct.x;
+        const v2f pcy = ((fy + qw * uvy) + cy) + P.ct.y;
+        const v2f pcz = ((fz + qw * uvz) + cz) + P.ct.z;
+        const v2f hx = P.fx * pcx + P.cx * pcz;
+        const v2f hy = P.fy * pcy + P.cy * pcz;
+        const v2f rz = v2(__builtin_amdgcn_rcpf(pcz.x), __builtin_amdgcn_rcpf(pcz.y));
+        int u0, u1, v0, v1;
+        round_quot_i2(hx, pcz, rz, true, true, u0, u1);
+        round_quot_i2(hy, pcz, rz, true, true, v0, v1);
+        hzs[k] = pcz;
+        const int uu[2] = {u0, u1}, vv[2] = {v0, v1};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float tsdf = comp(ts, j);
-        const float d = px[j].x;
-        if (inb[j] && !(d == 0 || d > P.max_depth)) {
-          const float sdf = px[j].y * (d - hzs[j]);
-          if (sdf > neg_trunc) {
-            const float tsdf_new = fminf(1.0f, quot_const(sdf, P.trunc, P.inv_trunc));
-            const uint32_t c_old = compu(cw, j);
-            const uint32_t c_new = __float_as_uint(px[j].w);
-            const float w_new = px[j].z;
-            const float w_old = (float)(c_old >> 24);
-            const float wc = w_old + w_new;
-            const float iwc = __builtin_amdgcn_rcpf(wc);
-            const uint32_t r0 = round_quot_u8(
-                (float)(c_old & 0xFF) * w_old + (float)(c_new & 0xFF) * w_new, wc, iwc);
-            const uint32_t r1 = round_quot_u8(
-                (float)((c_old >> 8) & 0xFF) * w_old + (float)((c_new >> 8) & 0xFF) * w_new, wc, iwc);
-            const uint32_t r2 = round_quot_u8(
-                (float)((c_old >> 16) & 0xFF) * w_old + (float)((c_new >> 16) & 0xFF) * w_new, wc, iwc);
-            tsdf = (tsdf * w_old + tsdf_new * w_new) / wc;
-            const uint32_t wt = f2u8(fminf(roundf(wc), 40.0f));
-            const uint32_t c = r0 | (r1 << 8) | (r2 << 16) | (wt << 24);
-            // semantic log-odds fusion (voxel_tsdf.cu:196-202) in base 2: pixB holds log2 ht /
-            // log2 lt, so exp((w_old ln p + w_new ln ht) / wc) = exp2((w_old log2 p + w_new log2 ht)
-            // / wc) with raw v_log_f32 / v_exp_f32 / v_rcp_f32 (~1 ulp each against the 1e-4
-            // probability tolerance); p stays exactly 0.5 when the two terms are equal (ht == lt).
-            const float p = comp(pr, j);
-            const float pos = __builtin_amdgcn_exp2f((w_old * __builtin_amdgcn_logf(p) + w_new * lg[j].x) * iwc);
-            const float neg =
-                __builtin_amdgcn_exp2f((w_old * __builtin_amdgcn_logf(1.0f - p) + w_new * lg[j].y) * iwc);
-            setc(ts, j, tsdf);
-            setc(pr, j, pos == neg ? 0.5f : pos * __builtin_amdgcn_rcpf(pos + neg));
-            setu(cw, j, c);
-            upd_mask |= 1 << j;
+        for (int e = 0; e < 2; ++e) {
+          const int j = 2 * k + e;
+          inb[j] = uu[e] >= 0 && uu[e] < P.W && vv[e] >= 0 && vv[e] < P.H;
+#if defined(TSDF_EXP) && (TSDF_EXP & 1)  // experiment build: no pixel gathers
+          if (inb[j]) px[j] = make_float4(pcz[e] + 0.01f, 1.0f, 1.0f, __uint_as_float(0x00808080u));
+#else
+          if (inb[j]) {
+            const int img = vv[e] * P.W + uu[e];
+            px[j] = D.pixA[img];
+            lg[j] = D.pixB[img];
           }
+#endif
         }
-        mn = fminf(mn, fabsf(tsdf));
+      }
+      // ---- pass 2: tsdf_integrate_kernel's update (voxel_tsdf.cu:174-203), branch-free on
+      // packed pairs; each voxel's result is kept only where it is updated (the reference's
+      // conditions: in image, 0 < d <= max_depth, sdf > -trunc).
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int j0 = 2 * k, j1 = 2 * k + 1;
+        const v2f d = v2(px[j0].x, px[j1].x), rng = v2(px[j0].y, px[j1].y);
+        const v2f w_new = v2(px[j0].z, px[j1].z);
+        const uint32_t n0 = __float_as_uint(px[j0].w), n1 = __float_as_uint(px[j1].w);
+        const v2f sdf = rng * (d - hzs[k]);
+        const bool a0 = inb[j0] && !(d.x == 0 || d.x > P.max_depth) && sdf.x > neg_trunc;
+        const bool a1 = inb[j1] && !(d.y == 0 || d.y > P.max_depth) && sdf.y > neg_trunc;
+        if (a0 || a1) {
+          v2f tn = quot_const2(sdf, P.trunc, P.inv_trunc, a0, a1);
+          tn = v2(fminf(1.0f, tn.x), fminf(1.0f, tn.y));
+          const uint32_t o0 = compu(cw, j0), o1 = compu(cw, j1);
+          const v2f w_old = v2((float)(o0 >> 24), (float)(o1 >> 24));
+          const v2f wc = w_old + w_new;
+          const v2f iwc = v2(__builtin_amdgcn_rcpf(wc.x), __builtin_amdgcn_rcpf(wc.y));
+          uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch) {
+            const v2f num = v2((float)((o0 >> (8 * ch)) & 0xFF), (float)((o1 >> (8 * ch)) & 0xFF)) * w_old +
+                            v2((float)((n0 >> (8 * ch)) & 0xFF), (float)((n1 >> (8 * ch)) & 0xFF)) * w_new;
+            int32_t r0, r1;
+            round_quot_i2(num, wc, iwc, a0, a1, r0, r1);
+            c0 |= (uint32_t)min(255, max(0, r0)) << (8 * ch);
+            c1 |= (uint32_t)min(255, max(0, r1)) << (8 * ch);
+          }
+          const v2f tnum = v2(comp(ts, j0), comp(ts, j1)) * w_old + tn * w_new;
+          const float t0 = tnum.x / wc.x, t1 = tnum.y / wc.y;
+          c0 |= (uint32_t)f2u8(fminf(roundf(wc.x), 40.0f)) << 24;
+          c1 |= (uint32_t)f2u8(fminf(roundf(wc.y), 40.0f)) << 24;
+          // semantic log-odds fusion (voxel_tsdf.cu:196-202) in base 2: pixB holds log2 ht /
+          // log2 lt, so exp((w_old ln p + w_new ln ht) / wc) = exp2((w_old log2 p + w_new log2 ht)
+          // / wc) with raw v_log_f32 / v_exp_f32 / v_rcp_f32 (~1 ulp each against the 1e-4
+          // probability tolerance); p stays exactly 0.5 when the two terms are equal (ht == lt).
+          const v2f p = v2(comp(pr, j0), comp(pr, j1));
+          const v2f q = 1.0f - p;
+          const v2f lp = v2(__builtin_amdgcn_logf(p.x), __builtin_amdgcn_logf(p.y));
+          const v2f lq = v2(__builtin_amdgcn_logf(q.x), __builtin_amdgcn_logf(q.y));
+          const v2f ap = (w_old * lp + w_new * v2(lg[j0].x, lg[j1].x)) * iwc;
+          const v2f an = (w_old * lq + w_new * v2(lg[j0].y, lg[j1].y)) * iwc;
+          const v2f pos = v2(__builtin_amdgcn_exp2f(ap.x), __builtin_amdgcn_exp2f(ap.y));
+          const v2f neg = v2(__builtin_amdgcn_exp2f(an.x), __builtin_amdgcn_exp2f(an.y));
+          const v2f sum = pos + neg;
+          const v2f pn = pos * v2(__builtin_amdgcn_rcpf(sum.x), __builtin_amdgcn_rcpf(sum.y));
+          if (a0) {
+            setc(ts, j0, t0);
+            setc(pr, j0, pos.x == neg.x ? 0.5f : pn.x);
+            setu(cw, j0, c0);
+          }
+          if (a1) {
+            setc(ts, j1, t1);
+            setc(pr, j1, pos.y == neg.y ? 0.5f : pn.y);
+            setu(cw, j1, c1);
+          }
+          upd_mask |= (a0 ? 1 << j0 : 0) | (a1 ? 1 << j1 : 0);
+        }
+        mn = fminf(mn, fminf(fabsf(comp(ts, j0)), fabsf(comp(ts, j1))));
       }
 #if defined(TSDF_EXP) && (TSDF_EXP & 4)  // experiment build: no pool state stores
       if (upd_mask < 0) {

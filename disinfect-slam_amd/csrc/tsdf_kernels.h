@@ -59,6 +59,14 @@ __global__ void k_resolve_delete(EngineDev D, const VisRec* recs, const int32_t*
 __global__ void k_keys_to_newset(EngineDev D, const int16_t* keys, int n);
 __global__ void k_fresh_init(EngineDev D);
 // extraction
+struct MeshParams {
+  float voxel, missing;
+  int min_weight;
+};
+template <bool Emit>
+__global__ void k_mesh(EngineDev D, const VisRec* sel, MeshParams M, int32_t* counts,
+                       const int32_t* offsets, float* out);
+__global__ void k_scan_counts(const int32_t* counts, int n, int32_t* offsets, int64_t* total);
 __global__ void k_raycast(EngineDev D, FrameParams P, float step_size, uchar4* rgba,
                           uchar4* normal);
 __global__ void k_query_count(EngineDev D, int use_bounds, short4 lo, short4 hi);

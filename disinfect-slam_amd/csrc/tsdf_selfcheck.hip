@@ -30,7 +30,10 @@ __global__ void k_quot_const(float b, float rb, uint32_t lo, uint32_t hi,
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t bits = lo + (uint32_t)i;
     const float a = __uint_as_float(bits);
-    if (!same_bits(quot_const(a, b, rb), a / b)) {
+    const v2f a2 = v2(a, __uint_as_float(bits ^ 0x80000000u));  // pair: a and -a
+    const v2f q2 = quot_const2(a2, b, rb, true, true);
+    if (!same_bits(quot_const(a, b, rb), a / b) || !same_bits(q2.x, a / b) ||
+        !same_bits(q2.y, a2.y / b)) {
       atomicAdd(bad, 1ull);
       atomicMin(first, bits);
     }
@@ -59,7 +62,9 @@ __global__ void k_round_quot(uint32_t seed, uint64_t n, float bmin, float bmax, 
     const float rb = __builtin_amdgcn_rcpf(b);
     const int32_t fast_i = round_quot_i(a, b, rb), ref_i = f2i(roundf(a / b));
     const uint32_t fast_u = round_quot_u8(a, b, rb), ref_u = f2u8(roundf(a / b));
-    if (fast_i != ref_i || fast_u != ref_u) {
+    int32_t p0, p1;  // the packed-pair form on (a, b) and (-a, b)
+    round_quot_i2(v2(a, -a), v2(b, b), v2(rb, rb), true, true, p0, p1);
+    if (fast_i != ref_i || fast_u != ref_u || p0 != ref_i || p1 != f2i(roundf(-a / b))) {
       atomicAdd(bad, 1ull);
       atomicMin(first, (uint32_t)i);
     }

@@ -254,6 +254,27 @@ class Engine:
                                             _ptr(normal), TSDF_MEM_HOST), "tsdf_raycast")
         return rgba, normal
 
+    def extract_mesh(self, bounds=None, missing_tsdf: float = 0.99, min_weight: int = 0,
+                     out=None) -> np.ndarray:
+        """Marching-cubes triangles (n, 3, 3) float32 of the selected blocks (tsdf_extract_mesh).
+        out: optional device tensor of >= 9 n floats to receive them on the GPU instead."""
+        L = _lib.load()
+        b = None if bounds is None else np.ascontiguousarray(
+            bounds.as_array() if isinstance(bounds, BoundingCube) else bounds, dtype=np.float32)
+        n = C.c_int64()
+        _lib.check(L.tsdf_extract_mesh(self._h, _ptr(b), missing_tsdf, min_weight, None, 0,
+                                       C.byref(n), TSDF_MEM_HOST), "tsdf_extract_mesh")
+        if out is not None:
+            _lib.check(L.tsdf_extract_mesh(self._h, _ptr(b), missing_tsdf, min_weight, _ptr(out),
+                                           out.numel() // 9, C.byref(n), TSDF_MEM_DEVICE),
+                       "tsdf_extract_mesh")
+            return out[:9 * n.value].view(-1, 3, 3)
+        tris = np.zeros((n.value, 3, 3), np.float32)
+        if n.value:
+            _lib.check(L.tsdf_extract_mesh(self._h, _ptr(b), missing_tsdf, min_weight, _ptr(tris),
+                                           n.value, C.byref(n), TSDF_MEM_HOST), "tsdf_extract_mesh")
+        return tris
+
     def query(self, bounds=None) -> np.ndarray:
         L = _lib.load()
         b = None if bounds is None else np.ascontiguousarray(

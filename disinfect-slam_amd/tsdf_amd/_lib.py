@@ -87,7 +87,7 @@ class Profile(C.Structure):
 
 EXPORTS = [
     "tsdf_config_default", "tsdf_create", "tsdf_destroy", "tsdf_integrate", "tsdf_raycast",
-    "tsdf_query", "tsdf_get_stats", "tsdf_synchronize", "tsdf_profile_begin", "tsdf_profile_end",
+    "tsdf_query", "tsdf_extract_mesh", "tsdf_get_stats", "tsdf_synchronize", "tsdf_profile_begin", "tsdf_profile_end",
     "tsdf_debug_dump", "tsdf_debug_stamps", "tsdf_num_entries", "tsdf_num_blocks", "tsdf_hash_allocate",
     "tsdf_hash_delete", "tsdf_hash_retrieve", "tsdf_hash_assign", "tsdf_num_active_blocks",
     "tsdf_pool_acquire", "tsdf_pool_release", "tsdf_pool_set_weight", "tsdf_pool_get_weights",
@@ -115,6 +115,7 @@ def load(path: str | None = None):
     L.tsdf_integrate.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f]
     L.tsdf_raycast.argtypes = [P, C.POINTER(Intrinsics), i, i, C.POINTER(Pose), f, P, P, i]
     L.tsdf_query.argtypes = [P, P, P, i64, C.POINTER(i64)]
+    L.tsdf_extract_mesh.argtypes = [P, P, f, i, P, i64, C.POINTER(i64), i]
     L.tsdf_get_stats.argtypes = [P, C.POINTER(Stats), i]
     L.tsdf_synchronize.argtypes = [P]
     L.tsdf_profile_begin.argtypes = [P, i]
@@ -143,6 +144,7 @@ def load(path: str | None = None):
     L.tsdf_last_error.restype = C.c_char_p
     L.tsdf_last_error.argtypes = []
     for name in ("tsdf_create", "tsdf_destroy", "tsdf_integrate", "tsdf_raycast", "tsdf_query",
+                 "tsdf_extract_mesh",
                  "tsdf_get_stats", "tsdf_synchronize", "tsdf_profile_begin", "tsdf_profile_end",
                  "tsdf_debug_dump", "tsdf_debug_stamps", "tsdf_hash_allocate", "tsdf_hash_delete",
                  "tsdf_hash_retrieve",

@@ -128,6 +128,18 @@ int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int width, int height
 int tsdf_query(tsdf_engine* e, const float* bounds, tsdf_voxel* out, int64_t capacity,
                int64_t* count);
 
+/* Marching-cubes mesh of the volume (GPU; replaces Query + KrisLibrary
+ * SparseTSDFReconstruction::ExtractMesh in examples/ros_camera_driver/ros_offline.cc:258-318).
+ * bounds as tsdf_query (NULL = every allocated block). Samples sit at voxel centres + half a
+ * voxel (ros_offline.cc:281-283); a voxel of a selected block contributes its tsdf when its
+ * weight >= min_weight (0 = every voxel, like the reference), every other grid point reads
+ * missing_tsdf (KrisLibrary defaultValue = truncation distance; 0.99 ~ the reference's auto
+ * value). Output: triangles[9 * i .. 9 * i + 8] = three xyz vertices, normals (right-hand
+ * rule) toward increasing tsdf; deterministic order (blocks in hash-entry order). Two-call:
+ * triangles == NULL returns the count only. mem_kind: where `triangles` lives. */
+int tsdf_extract_mesh(tsdf_engine* e, const float* bounds, float missing_tsdf, int min_weight,
+                      float* triangles, int64_t capacity, int64_t* num_triangles, int mem_kind);
+
 int tsdf_get_stats(tsdf_engine* e, tsdf_stats* out, int clear_status);
 int tsdf_synchronize(tsdf_engine* e);
 /* mode TSDF_PROFILE_PHASES: HIP events between all four phases of every integrate call;

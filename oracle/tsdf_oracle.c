@@ -11,6 +11,8 @@
  */
 #include "tsdf_oracle.h"
 
+#include "../disinfect-slam_amd/csrc/tsdf_mc_tables.h" /* generated case table (data only) */
+
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -756,4 +758,100 @@ void ora_pool_set_weight(ora_grid* g, int32_t b, uint8_t w) {
 void ora_pool_get_weights(const ora_grid* g, int32_t b, uint8_t* out) {
   const int64_t base = (int64_t)b << BLOCK_VOLUME_BITS;
   for (int v = 0; v < BLOCK_VOLUME; ++v) out[v] = g->rgbw[(base + v) * 4 + 3];
+}
+
+/* ---------------- marching cubes over the selected blocks ----------------
+ * Replaces Query + KrisLibrary SparseTSDFReconstruction::ExtractMesh
+ * (examples/ros_camera_driver/ros_offline.cc:258-318; not vendored -> parity unpinned):
+ *  - samples: every voxel g of a selected block (GatherValid / GatherVoxels selection, see
+ *    ora_query) at (float)g * voxel + voxel / 2 (the caller's +cell/2 offset, :281-283); its value
+ *    is its tsdf when its weight >= min_weight, else `missing` (KrisLibrary defaultValue = the
+ *    truncation distance, :279-280); grid points outside selected blocks are `missing` too;
+ *  - cells: the cube with lower corner c is meshed iff one of its 8 corners lies in a selected
+ *    block; it belongs to the block of the first such corner (corner order i = x | y << 1 | z << 2);
+ *  - order: blocks in hash-entry order, cells of a block by (z, y, x) of c in [8b - 1, 8b + 7]^3,
+ *    triangles in case-table order; vertex on edge (a, b): t = va / (va - vb), p = pa + t (pb - pa)
+ *    along the edge's axis. Output: 9 floats per triangle. */
+static const int8_t kOraMcEdge[12][2] = TSDF_MC_EDGE_INIT;
+static const uint8_t kOraMcNumTri[256] = TSDF_MC_NUM_TRI_INIT;
+static const int8_t kOraMcTri[256][3 * TSDF_MC_MAX_TRI] = TSDF_MC_TRI_INIT;
+
+static int block_selected(const ora_grid* g, s3 blk, const int16_t* bb, int64_t* e_out) {
+  const int64_t e = hash_find(g, blk);
+  if (e_out) *e_out = e;
+  if (e < 0) return 0;
+  if (!bb) return 1;
+  const s3 vg = block_to_point(blk);
+  return vg.x >= bb[0] && vg.y >= bb[2] && vg.z >= bb[4] && vg.x + BLOCK_LEN - 1 <= bb[1] &&
+         vg.y + BLOCK_LEN - 1 <= bb[3] && vg.z + BLOCK_LEN - 1 <= bb[5];
+}
+
+int64_t ora_extract_mesh(const ora_grid* g, const float* bounds, float missing, int min_weight,
+                         float* out, int64_t capacity) {
+  int16_t bbv[6] = {0, 0, 0, 0, 0, 0};
+  const int16_t* bb = NULL;
+  if (bounds) {
+    const float scale = (float)(1. / (double)g->voxel);
+    for (int i = 0; i < 6; ++i) bbv[i] = f2s(bounds[i] * scale);
+    bb = bbv;
+  }
+  const float half = 0.5f * g->voxel;
+  int64_t n = 0;
+  for (int e = 0; e < NUM_ENTRY; ++e) {
+    const entry* b = &g->table[e];
+    if (b->idx < 0 || !block_selected(g, b->pos, bb, NULL)) continue;
+    const s3 base = block_to_point(b->pos);
+    for (int lz = -1; lz < BLOCK_LEN; ++lz)
+      for (int ly = -1; ly < BLOCK_LEN; ++ly)
+        for (int lx = -1; lx < BLOCK_LEN; ++lx) {
+          float val[8];
+          int owner_found = 0, mine = 0;
+          for (int i = 0; i < 8; ++i) {
+            const s3 p = {(int16_t)(base.x + lx + (i & 1)), (int16_t)(base.y + ly + ((i >> 1) & 1)),
+                          (int16_t)(base.z + lz + ((i >> 2) & 1))};
+            const s3 pb = point_to_block(p);
+            int64_t pe = -1;
+            const int sel = block_selected(g, pb, bb, &pe);
+            if (sel && !owner_found) {
+              owner_found = 1;
+              mine = pe == e;
+            }
+            val[i] = missing;
+            if (sel) {
+              const int64_t a = ((int64_t)g->table[pe].idx << BLOCK_VOLUME_BITS) +
+                                offset_to_index(p.x & 7, p.y & 7, p.z & 7);
+              if ((int)g->rgbw[a * 4 + 3] >= min_weight) val[i] = g->tsdf[a];
+            }
+          }
+          if (!mine) continue;
+          int cube = 0;
+          for (int i = 0; i < 8; ++i)
+            if (val[i] < 0) cube |= 1 << i;
+          const int nt = kOraMcNumTri[cube];
+          for (int t = 0; t < nt; ++t) {
+            if (out && n < capacity) {
+              float* w = &out[n * 9];
+              for (int k = 0; k < 3; ++k) {
+                const int ed = kOraMcTri[cube][3 * t + k];
+                const int a = kOraMcEdge[ed][0], bc = kOraMcEdge[ed][1];
+                const int gx = base.x + lx, gy = base.y + ly, gz = base.z + lz;
+                float pa[3] = {(float)(gx + (a & 1)) * g->voxel + half,
+                               (float)(gy + ((a >> 1) & 1)) * g->voxel + half,
+                               (float)(gz + ((a >> 2) & 1)) * g->voxel + half};
+                const float pbv[3] = {(float)(gx + (bc & 1)) * g->voxel + half,
+                                      (float)(gy + ((bc >> 1) & 1)) * g->voxel + half,
+                                      (float)(gz + ((bc >> 2) & 1)) * g->voxel + half};
+                const int axis = (a ^ bc) == 1 ? 0 : (a ^ bc) == 2 ? 1 : 2;
+                const float tt = val[a] / (val[a] - val[bc]);
+                pa[axis] = pa[axis] + tt * (pbv[axis] - pa[axis]);
+                w[3 * k + 0] = pa[0];
+                w[3 * k + 1] = pa[1];
+                w[3 * k + 2] = pa[2];
+              }
+            }
+            ++n;
+          }
+        }
+  }
+  return n;
 }

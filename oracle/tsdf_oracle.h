@@ -45,6 +45,10 @@ void ora_destroy(ora_grid* g);
 /* Spatial sharding (not in the reference): the grid allocates only blocks whose
  * 4^3-block brick hashes to shard index (ora_block_owner == index). count <= 1: unsharded. */
 void ora_set_shard(ora_grid* g, int index, int count);
+/* Marching cubes over the selected blocks (bounds as ora_query, NULL = all); 9 floats per
+ * triangle into out (up to capacity triangles); returns the triangle count. See the .c. */
+int64_t ora_extract_mesh(const ora_grid* g, const float* bounds, float missing, int min_weight,
+                         float* out, int64_t capacity);
 uint32_t ora_block_owner(int16_t x, int16_t y, int16_t z, uint32_t shards);
 
 /* voxel_tsdf.cu:347-375 TSDFGrid::Integrate. rgb: HxWx3 u8; depth/ht/lt: HxW f32 (ht/lt may be

@@ -68,6 +68,8 @@ def lib():
         L.ora_pool_set_weight.argtypes = [P, C.c_int32, C.c_uint8]
         L.ora_pool_get_weights.argtypes = [P, C.c_int32, P]
         L.ora_set_shard.argtypes = [P, C.c_int, C.c_int]
+        L.ora_extract_mesh.restype = C.c_int64
+        L.ora_extract_mesh.argtypes = [P, P, C.c_float, C.c_int, P, C.c_int64]
         L.ora_block_owner.restype = C.c_uint32
         L.ora_block_owner.argtypes = [C.c_int16, C.c_int16, C.c_int16, C.c_uint32]
         L.ora_hash.restype = C.c_uint32
@@ -139,6 +141,14 @@ class OracleGrid:
         out = np.zeros((n, 4), np.float32)
         if n:
             lib().ora_query(self.h, _p(b), _p(out), n)
+        return out
+
+    def extract_mesh(self, bounds=None, missing_tsdf=0.99, min_weight=0):
+        b = None if bounds is None else np.ascontiguousarray(bounds, dtype=np.float32)
+        n = lib().ora_extract_mesh(self.h, _p(b), missing_tsdf, min_weight, None, 0)
+        out = np.zeros((n, 3, 3), np.float32)
+        if n:
+            lib().ora_extract_mesh(self.h, _p(b), missing_tsdf, min_weight, _p(out), n)
         return out
 
     def stats(self) -> dict:
