@@ -16,7 +16,9 @@ only the blocks it owns), value = frames / max rank time, scaling "strong".
 roofline: the fused integrate kernel (k_integrate). Algorithmic bytes per launch:
 N_vis * (512 * 12 + 12) voxel state + block metadata read, N_upd * 12 updated voxel state written,
 15 * W * H frame bytes read -- N_vis and N_upd are counted on device. Average launch duration from
-HIP events recorded on the engine stream around every k_integrate launch of the timed region.
+HIP events recorded on the engine stream around the k_integrate launches of every 8th frame of the
+timed region (--event-every; an event is a queue marker costing the stream ~3 us, so timing every
+launch would slow the loop ~8 %); the in-kernel device clock of every launch is reported beside it.
 cpu_baseline: the single-threaded CPU oracle (oracle/tsdf_oracle.c, a restatement of the
 reference kernels incl. its full-table visibility scan) on a bounded sample of the same stream.
 """
@@ -50,6 +52,10 @@ def parse():
     p.add_argument("--cpu-frames", type=int, default=-1, help="oracle sample size (-1 = auto)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--block-bits", type=int, default=18)
+    p.add_argument("--event-every", type=int, default=8,
+                   help="HIP-event-time k_integrate on every n-th timed frame (events cost ~3 us each)")
+    p.add_argument("--no-events", action="store_true",
+                   help="diagnostic: no HIP events in the timed loop (roofline then unmeasured)")
     return p.parse_args()
 
 
@@ -103,7 +109,10 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    eng.profile_begin(integrate_only=True)  # 2 events per frame around k_integrate only
+    if not a.no_events:
+        # 2 events around k_integrate on every event_every-th frame: each event is a queue marker
+        # that stalls the stream ~3 us, so the loop samples instead of timing every launch
+        eng.profile_begin(integrate_only=True, every=a.event_every)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.warmup, a.warmup + a.steps):
@@ -113,6 +122,8 @@ def main():
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
+    if a.no_events:  # device-clock and counters still come from a profile window
+        eng.profile_begin(integrate_only=True)
     prof = eng.profile_end()
     # phase breakdown (all four phases event-bracketed) on the next frames of the stream, untimed
     eng.profile_begin()
@@ -129,8 +140,8 @@ def main():
     W, H = a.width, a.height
     img_bytes = (12 if a.depth_only else 15) * W * H
     alg_bytes = (prof["sum_visible"] * (512 * 12 + 12) + prof["sum_updated"] * 12) / a.steps + img_bytes
-    t_int = prof["ms_integrate"] / a.steps / 1e3
-    achieved = alg_bytes / t_int / 1e9
+    t_int = prof["ms_integrate"] / max(prof["frames"], 1) / 1e3
+    achieved = alg_bytes / t_int / 1e9 if t_int > 0 else 0.0
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_integrate_latest.json")
     if os.path.exists(pmc_path):
@@ -183,6 +194,7 @@ def main():
                 # cross-check: first-WG start -> last-WG end from the in-kernel 100 MHz clock
                 # (what rocprofv3's kernel trace measures; the HIP events above also include the
                 # per-launch dispatch / completion overhead)
+                "event_timed_launches": prof["frames"],
                 "us_per_launch_device_clock": round(prof["ms_integrate_device"] / a.steps * 1e3, 3),
                 "achieved_device_clock": round(alg_bytes / (prof["ms_integrate_device"] / a.steps / 1e3) / 1e9, 1)
                 if prof["ms_integrate_device"] > 0 else None,

@@ -121,9 +121,13 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
   __syncthreads();
   TSDF_STAMP(D, 0, 4);
   // Each wave sweeps its 64-slot strips; the few occupied slots of a strip (ballot) are tested
-  // 8 at a time with 8 lanes per key, one block corner per lane (is_block_visible<true>).
+  // 8 at a time with 8 lanes per key, one block corner per lane (is_block_visible<true>), and the
+  // fully visible ones are listed in LDS. The table probes and new-key inserts then run one key
+  // per lane over that list, so the wave pays their memory latency once, not once per 8 keys.
+  __shared__ uint16_t s_vis[4][kTileSlots / 4];
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   const int grp = lane >> 3, corner = lane & 7;
+  int nv = 0;
   for (int strip = wave; strip < kTileSlots / 64; strip += 4) {
     const unsigned long long skey = s_key[strip * 64 + lane];
     const unsigned long long occ = __ballot(skey != 0ull);
@@ -136,22 +140,30 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
         if (src + step < 64 && __popcll(occ & ((1ull << (src + step)) - 1ull)) <= want) src += step;
       const unsigned long long key = __shfl(skey, src, 64);
       bool vis = false;
-      int16_t kx = 0, ky = 0, kz = 0;
       if (want < n) {
+        int16_t kx, ky, kz;
         unpack_key(key, kx, ky, kz);
         vis = voxel_visible(P, (int16_t)((int16_t)(kx << kBlockLenBits) + ((corner >> 0) & 1) * (kBlockLen - 1)),
                             (int16_t)((int16_t)(ky << kBlockLenBits) + ((corner >> 1) & 1) * (kBlockLen - 1)),
                             (int16_t)((int16_t)(kz << kBlockLenBits) + ((corner >> 2) & 1) * (kBlockLen - 1)));
       }
       const unsigned long long bal = __ballot(vis);
-      if (want < n && corner == 0 && ((bal >> (lane & ~7)) & 0xFFull) == 0xFFull) {
-        if (P.shard_count > 1 &&
-            brick_owner(kx, ky, kz, (uint32_t)P.shard_count) != (uint32_t)P.shard_index)
-          continue;
-        if (find_entry(D.table, kx, ky, kz) >= 0) continue;
-        nk_insert(D, key, s_ord[strip * 64 + src]);
-      }
+      const bool lead = want < n && corner == 0 && ((bal >> (lane & ~7)) & 0xFFull) == 0xFFull;
+      const unsigned long long leads = __ballot(lead);
+      if (lead) s_vis[wave][nv + __popcll(leads & ((1ull << lane) - 1ull))] = (uint16_t)(strip * 64 + src);
+      nv += __popcll(leads);
     }
+  }
+  for (int i = lane; i < nv; i += 64) {
+    const int slot = s_vis[wave][i];
+    const unsigned long long key = s_key[slot];
+    int16_t kx, ky, kz;
+    unpack_key(key, kx, ky, kz);
+    if (P.shard_count > 1 &&
+        brick_owner(kx, ky, kz, (uint32_t)P.shard_count) != (uint32_t)P.shard_index)
+      continue;
+    if (find_entry(D.table, kx, ky, kz) >= 0) continue;
+    nk_insert(D, key, s_ord[slot]);
   }
   TSDF_STAMP(D, 0, 5);
 }
@@ -197,6 +209,7 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, 
   for (int i = t; i < n; i += kResolveThreads) {
     const int h = D.nk_list[i];
     D.pairs[i] = ((unsigned long long)D.nk_order[h] << 32) | (uint32_t)h;
+    D.pkey[i] = D.nk_key[h];
   }
   __syncthreads();
   auto keyf = [&](int i) -> uint32_t { return (uint32_t)(D.pairs[i] >> 32); };
@@ -223,7 +236,7 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, 
       if (have) {
         const int li = (int)(L.batch[base + t] & 0xFFFFFFFFu);
         h = (int)(D.pairs[li] & 0xFFFFFFFFu);
-        unpack_key(D.nk_key[h], kx, ky, kz);
+        unpack_key(D.pkey[li], kx, ky, kz);
         B = hash_block(kx, ky, kz);
         const Ent s0 = load_ent(D.table, 2 * B);
         const Ent s1 = load_ent(D.table, 2 * B + 1);

@@ -70,6 +70,8 @@ constexpr int kBatch = 2048;
 constexpr int kMaxWin = 8192;
 constexpr int kClaimSlots = 4096;
 
+constexpr int kRankSortMax = 512;  // single-batch sizes sorted by rank (<= blockDim, <= kMaxWin / 2)
+
 struct ResolveLds {
   uint32_t hist[kMaxWin];             // window counts -> exclusive prefix
   unsigned long long batch[kBatch];   // (sort key << 32) | list index
@@ -182,7 +184,23 @@ __device__ int stream_batch(ResolveLds& L, int n, int width, int j, KeyFn keyf) 
   }
   __syncthreads();
   const int m = L.count < kBatch ? L.count : kBatch;  // bounded by construction (width <= 1024)
-  lds_bitonic_sort(L.batch, m);
+  if (n <= kBatch && m <= kRankSortMax) {
+    // single batch (hist unused): rank sort -- every element counts the smaller ones with
+    // broadcast LDS reads, one barrier instead of bitonic's log^2 stages (keys are unique)
+    unsigned long long* tmp = reinterpret_cast<unsigned long long*>(L.hist);
+    unsigned long long x = 0ull;
+    int rank = 0;
+    if ((int)threadIdx.x < m) {
+      x = L.batch[threadIdx.x];
+      for (int j = 0; j < m; ++j) rank += L.batch[j] < x;
+      tmp[rank] = x;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < m) L.batch[threadIdx.x] = tmp[threadIdx.x];
+    __syncthreads();
+  } else {
+    lds_bitonic_sort(L.batch, m);
+  }
   return m;
 }
 

@@ -119,6 +119,8 @@ struct tsdf_engine {
   // profiling
   bool profiling = false;
   int prof_mode = TSDF_PROFILE_PHASES;
+  int prof_every = 1;        // event-time every n-th integrate call
+  int64_t prof_calls = 0;    // integrate calls since profile_begin
   std::vector<std::array<hipEvent_t, 5>> events;
   size_t ev_used = 0;
   unsigned long long prof_vis0 = 0, prof_upd0 = 0, prof_ticks0 = 0;
@@ -129,7 +131,7 @@ namespace {
 void free_all(tsdf_engine* e) {
   EngineDev& D = e->D;
   void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.fresh_flag, D.occ,
-                  D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs,      D.fresh,
+                  D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs, D.pkey,      D.fresh,
                   D.vis,     D.band,    D.cand,     D.wg_upd, D.wg_end, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
                   e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
@@ -305,6 +307,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.nk_order, kNewKeyCap);
   ALLOC(D.nk_list, kNewKeyCap);
   ALLOC(D.pairs, kNewKeyCap);
+  ALLOC(D.pkey, kNewKeyCap);
   ALLOC(D.fresh, kNewKeyCap);
   ALLOC(D.vis, (size_t)kBands * nb);
   ALLOC(D.band, kBands * kBandStride);
@@ -420,7 +423,7 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
   }
   const FrameParams P = make_params(e, K, W, H, pose, max_depth);
   std::array<hipEvent_t, 5>* ev = nullptr;
-  if (e->profiling) {
+  if (e->profiling && (e->prof_calls++ % e->prof_every) == 0) {
     if (e->ev_used == e->events.size()) {
       std::array<hipEvent_t, 5> a{};
       for (auto& x : a) HIP_OK(hipEventCreate(&x));
@@ -604,10 +607,12 @@ int tsdf_get_stats(tsdf_engine* e, tsdf_stats* o, int clear_status) {
   return TSDF_OK;
 }
 
-int tsdf_profile_begin(tsdf_engine* e, int mode) {
-  if (!e || (mode != TSDF_PROFILE_PHASES && mode != TSDF_PROFILE_INTEGRATE))
+int tsdf_profile_begin(tsdf_engine* e, int mode, int every) {
+  if (!e || (mode != TSDF_PROFILE_PHASES && mode != TSDF_PROFILE_INTEGRATE) || every < 1)
     return TSDF_ERR_INVALID_ARG;
   e->prof_mode = mode;
+  e->prof_every = every;
+  e->prof_calls = 0;
   int rc = read_counters(e);
   if (rc) return rc;
   e->prof_vis0 = e->h_ctr->total_visible;
@@ -625,6 +630,7 @@ int tsdf_profile_end(tsdf_engine* e, tsdf_profile* o) {
   if (rc) return rc;
   std::memset(o, 0, sizeof(*o));
   o->frames = (int64_t)e->ev_used;
+  o->calls = e->prof_calls;
   for (size_t i = 0; i < e->ev_used; ++i) {
     float ms[4] = {0.f, 0.f, 0.f, 0.f};
     for (int k = 0; k < 4; ++k)

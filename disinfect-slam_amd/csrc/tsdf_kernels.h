@@ -29,6 +29,7 @@ struct EngineDev {
   uint32_t* nk_order;           // kNewKeyCap smallest candidate order per key
   int32_t* nk_list;             // kNewKeyCap occupied slots
   unsigned long long* pairs;    // kNewKeyCap (order << 32 | slot) resolver scratch
+  unsigned long long* pkey;     // kNewKeyCap packed key of pairs[i] (one load in the rounds)
   int32_t* fresh;               // pool indices acquired by the hash-level test path
   // visibility / carving
   VisRec* vis;                  // kBands x nblocks visible blocks (band-major, any order within)

@@ -292,9 +292,10 @@ class Engine:
         _lib.check(_lib.load().tsdf_get_stats(self._h, C.byref(s), int(clear_status)), "tsdf_get_stats")
         return {k: getattr(s, k) for k, _ in _lib.Stats._fields_}
 
-    def profile_begin(self, integrate_only: bool = False):
-        """HIP-event timing of the following integrate calls (all phases, or only k_integrate)."""
-        _lib.check(_lib.load().tsdf_profile_begin(self._h, 1 if integrate_only else 0),
+    def profile_begin(self, integrate_only: bool = False, every: int = 1):
+        """HIP-event timing of every `every`-th following integrate call (all phases, or only
+        k_integrate)."""
+        _lib.check(_lib.load().tsdf_profile_begin(self._h, 1 if integrate_only else 0, every),
                    "tsdf_profile_begin")
 
     def profile_end(self) -> dict:

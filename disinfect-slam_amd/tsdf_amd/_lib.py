@@ -82,6 +82,7 @@ class Profile(C.Structure):
         ("sum_visible", C.c_int64),
         ("sum_updated", C.c_int64),
         ("ms_integrate_device", C.c_double),
+        ("calls", C.c_int64),
     ]
 
 
@@ -118,7 +119,7 @@ def load(path: str | None = None):
     L.tsdf_extract_mesh.argtypes = [P, P, f, i, P, i64, C.POINTER(i64), i]
     L.tsdf_get_stats.argtypes = [P, C.POINTER(Stats), i]
     L.tsdf_synchronize.argtypes = [P]
-    L.tsdf_profile_begin.argtypes = [P, i]
+    L.tsdf_profile_begin.argtypes = [P, i, i]
     L.tsdf_profile_end.argtypes = [P, C.POINTER(Profile)]
     L.tsdf_debug_dump.argtypes = [P, P, P, P, P, P, P, P]
     L.tsdf_debug_stamps.argtypes = [P, P, i64, C.POINTER(i)]

@@ -93,7 +93,7 @@ typedef struct tsdf_stats {
 } tsdf_stats;
 
 typedef struct tsdf_profile { /* device time of the integrate phases between begin/end */
-  int64_t frames;
+  int64_t frames;      /* integrate calls that were event-timed (every `every`-th call) */
   double ms_allocate;  /* DDA + new-key ordering + allocation resolve + block init */
   double ms_visible;   /* visibility compaction */
   double ms_integrate; /* the fused TSDF/RGB/weight/semantic update kernel (+ carve minimum) */
@@ -103,6 +103,8 @@ typedef struct tsdf_profile { /* device time of the integrate phases between beg
   double ms_integrate_device; /* k_integrate first-workgroup start -> last-workgroup end, summed
                                  over the profiled frames (in-kernel 100 MHz clock; excludes the
                                  dispatch overhead the HIP events of ms_integrate include) */
+  int64_t calls;       /* all integrate calls between begin and end (sum_* and the device
+                          clock cover all of them; the ms_* event times only `frames`) */
 } tsdf_profile;
 
 /* ---- engine lifetime: TSDFGrid::TSDFGrid / ~TSDFGrid (voxel_tsdf.cu:309-345) ---- */
@@ -142,12 +144,13 @@ int tsdf_extract_mesh(tsdf_engine* e, const float* bounds, float missing_tsdf, i
 
 int tsdf_get_stats(tsdf_engine* e, tsdf_stats* out, int clear_status);
 int tsdf_synchronize(tsdf_engine* e);
-/* mode TSDF_PROFILE_PHASES: HIP events between all four phases of every integrate call;
- * TSDF_PROFILE_INTEGRATE: only the two events bracketing the fused update kernel (least
- * perturbation of a timed loop; the other phase times read 0). */
+/* mode TSDF_PROFILE_PHASES: HIP events between all four phases of an integrate call;
+ * TSDF_PROFILE_INTEGRATE: only the two events bracketing the fused update kernel (the other
+ * phase times read 0). Events are recorded on every `every`-th integrate call (1 = all): each
+ * event is a queue marker that costs the stream ~3 us, so a timed loop samples. */
 #define TSDF_PROFILE_PHASES 0
 #define TSDF_PROFILE_INTEGRATE 1
-int tsdf_profile_begin(tsdf_engine* e, int mode);
+int tsdf_profile_begin(tsdf_engine* e, int mode, int every);
 int tsdf_profile_end(tsdf_engine* e, tsdf_profile* out);
 
 /* Test-only full state dump (Query exposes only tsdf): the 2^22-entry hash table as

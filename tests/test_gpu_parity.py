@@ -200,7 +200,7 @@ def test_sharded_engines_match_sharded_oracles():
             eng.close(), ora.close()
 
 
-@pytest.mark.parametrize("min_weight,bounded", [(0, False), (1, False), (2, True)])
+@pytest.mark.parametrize("min_weight,bounded", [(0, False), (1, False), (1, True)])
 def test_marching_cubes_matches_oracle(min_weight, bounded):
     """GPU marching cubes (tsdf_extract_mesh) == the oracle's restatement, bit for bit and in
     the same order (KrisLibrary itself is absent: parity unpinned)."""
@@ -211,11 +211,11 @@ def test_marching_cubes_matches_oracle(min_weight, bounded):
         if bounded:
             d = ora.dump(pool=False)
             pos = d["entry_pos"][d["entry_idx"] >= 0, :3].astype(np.float32) * 8 * 0.01
-            lo, hi = np.percentile(pos, 25, axis=0), np.percentile(pos, 75, axis=0)
+            lo, hi = np.percentile(pos, 5, axis=0), np.percentile(pos, 95, axis=0) + 0.08
             bounds = np.array([lo[0], hi[0], lo[1], hi[1], lo[2], hi[2]], np.float32)
         got = eng.extract_mesh(bounds, 0.99, min_weight)
         exp = ora.extract_mesh(bounds, 0.99, min_weight)
-        assert exp.shape[0] > 100
+        assert exp.shape[0] > (20 if bounded else 100)
         assert got.shape == exp.shape
         np.testing.assert_array_equal(got.view(np.uint32), exp.view(np.uint32))
     finally:
