@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void k_vis(EngineDev D, FrameParams P) {
     r.x = en.x;
     r.y = en.y;
     r.z = en.z;
-    r.pad = 0;
+    r.pad = (int16_t)D.fresh_flag[en.idx];  // allocated this frame: integrate starts it from AquireBlock's state
     r.idx = en.idx;
     r.entry = (int32_t)e;
     D.vis[(size_t)band * D.nblocks + pos] = r;
@@ -119,7 +119,9 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
   __shared__ float s_min[4];
   __shared__ int s_upd[4];
   const int lane = lane_id();
-  const int wave = threadIdx.x >> 6;
+  // wave-uniform (scalar) loop state: the band search, the list record and the fresh flag are
+  // SALU / scalar loads instead of per-lane selects
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pair = wave >> 1, hf = wave & 1;
   // concatenated band lists: band i holds visible-block indices [bstart_i, bstart_i + count_i)
   int bstart[kBands];
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
       float4 pr = *reinterpret_cast<const float4*>(blk + kProbOffset + off);
       uint4 cw = *reinterpret_cast<const uint4*>(blk + kRgbwOffset + off);
 #endif
-      fresh = D.fresh_flag[pidx] != 0;
+      fresh = r.pad != 0;
       if (fresh) {
         ts = make_float4(-1.f, -1.f, -1.f, -1.f);
         pr = make_float4(.5f, .5f, .5f, .5f);
@@ -224,11 +226,11 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
 #if defined(TSDF_EXP) && (TSDF_EXP & 1)  // experiment build: no pixel gathers
           if (inb[j]) px[j] = make_float4(pcz[e] + 0.01f, 1.0f, 1.0f, __uint_as_float(0x00808080u));
 #else
-          if (inb[j]) {
-            const int img = vv[e] * P.W + uu[e];
-            px[j] = D.pixA[img];
-            lg[j] = D.pixB[img];
-          }
+          // unconditional gathers at a clamped index (pixel 0 when out of the image): no exec-
+          // masked region around the loads, so all 8 stay in flight until pass 2
+          const int img = inb[j] ? vv[e] * P.W + uu[e] : 0;
+          px[j] = D.pixA[img];
+          lg[j] = D.pixB[img];
 #endif
         }
       }
