@@ -37,7 +37,7 @@ __device__ void nk_insert(const EngineDev& D, uint64_t key, uint32_t order) {
 // k_ingest_dda: 16x16 pixel tile per workgroup.
 //  1. pack the frame into per-pixel records the integrate kernel gathers:
 //       pixA = {depth, range = |K^-1 [x y 1]|, w_new = (1 - d / max_depth) * 4, rgb}
-//       pixB = {log2 ht, log2 lt}
+//       pixB = log2 ht - log2 lt
 //     (exactly the values tsdf_integrate_kernel recomputes per voxel, voxel_tsdf.cu:174-201)
 //  2. DDA of [p - trunc dir, p + trunc dir] (voxel_tsdf.cu:116-146); block keys deduplicated in
 //     an LDS hash set with their smallest candidate order (y*W + x)*maxs + i
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
     const float range = sqrtf(dot3(pc, pc));  // img_depth_to_range (voxel_tsdf.cu:120)
     const float w_new = (1.0f - quot_const(d, P.max_depth, P.inv_max_depth)) * 4.0f;
     D.pixA[i] = make_float4(d, range, w_new, __uint_as_float(c));
-    D.pixB[i] = make_float2(log2f(h), log2f(l));  // base-2 log-odds terms (k_integrate)
+    D.pixB[i] = log2f(h) - log2f(l);  // base-2 log-odds of the pixel (k_integrate)
     TSDF_STAMP(D, 0, 2);
     if (!(d == 0 || d > P.max_depth)) {
       const f3 pcd = {pc.x * d, pc.y * d, pc.z * d};

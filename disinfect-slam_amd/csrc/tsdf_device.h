@@ -200,6 +200,50 @@ __device__ __forceinline__ v2f quot_const2(v2f a, float b, float rb, bool act0, 
   return o;
 }
 
+// f2i(roundf(a / b)) on voxel pairs for a >= 0 and 0 < b < 2^100 (or the NaN of 0 / 0, which
+// both paths turn into 0): round_quot_i2 with the half-away offset fixed at +1/2 and no |b| test
+__device__ __forceinline__ void round_quot_pos2(v2f a, v2f b, v2f rb, bool act0, bool act1,
+                                                int32_t& o0, int32_t& o1) {
+  const v2f q = a * rb;
+  const v2f f1 = vfma(q, v2(1.0f + 0x1p-20f, 1.0f + 0x1p-20f), v2(0.5f, 0.5f));
+  const v2f f2 = vfma(q, v2(1.0f - 0x1p-20f, 1.0f - 0x1p-20f), v2(0.5f, 0.5f));
+  o0 = f2i(f1.x);
+  o1 = f2i(f1.y);
+  if (__builtin_expect(act0 && o0 != f2i(f2.x), 0)) o0 = f2i(roundf(a.x / b.x));
+  if (__builtin_expect(act1 && o1 != f2i(f2.y), 0)) o1 = f2i(roundf(a.y / b.y));
+}
+
+// RN(a / b) on voxel pairs with y = v_rcp(b): the compiler's IEEE f32 division expansion
+// (Newton-refined reciprocal, quotient, two residual corrections) without its v_div_scale /
+// v_div_fmas / v_div_fixup range handling, which are identities while |a| and |b| lie in
+// [2^-40, 2^40] (every residual is then a normal float or 0); lanes outside that range take the
+// IEEE divide. Checked against a / b by libtsdf_selfcheck (tests/test_gpu_numerics.py).
+__device__ __forceinline__ v2f div_pair(v2f a, v2f b, v2f y, bool act0, bool act1) {
+  const v2f e = vfma(-b, y, v2(1.0f, 1.0f));
+  const v2f y1 = vfma(e, y, y);
+  const v2f q = a * y1;
+  const v2f r = vfma(-b, q, a);
+  const v2f q1 = vfma(r, y1, q);
+  const v2f r1 = vfma(-b, q1, a);
+  v2f o = vfma(r1, y1, q1);
+  const float fa0 = fabsf(a.x), fb0 = fabsf(b.x), fa1 = fabsf(a.y), fb1 = fabsf(b.y);
+  if (__builtin_expect(act0 && !(fa0 >= 0x1p-40f && fa0 <= 0x1p40f && fb0 >= 0x1p-40f && fb0 <= 0x1p40f), 0))
+    o.x = a.x / b.x;
+  if (__builtin_expect(act1 && !(fa1 >= 0x1p-40f && fa1 <= 0x1p40f && fb1 >= 0x1p-40f && fb1 <= 0x1p40f), 0))
+    o.y = a.y / b.y;
+  return o;
+}
+
+// min(roundf(w), 40) as an integer for 0 <= w < 2^23 (the weight update, voxel_tsdf.cu:188):
+// floor(RN(w + pred(1/2))) == roundf(w) on that whole range (pred(1/2) = 0x1.fffffep-2 keeps
+// RN(0.49999997 + 1/2) below 1; at every larger w the sum's rounding never crosses an integer
+// the exact sum does not reach). Exhaustively checked by tests/test_cpu_lib.py.
+__device__ __forceinline__ uint32_t weight_round_cap(float w, uint32_t cap) {
+  uint32_t r;
+  asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(w));
+  return min(r, cap);
+}
+
 // RN(a / b) where the caller only compares the quotient with 0 and with the float c: the
 // estimate a * rcp(b) is returned when it provably lies on the same side of 0 and of c as the IEEE
 // quotient (distance to c above 2^-20 |q|, |q| and |b| in range), else the IEEE quotient.

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
       const float w_uvx = qw * uvx, qz_uvx = qz * uvx, qy_uvx = qy * uvx;
       v2f hzs[2];
       float4 px[4];
-      float2 lg[4];
+      float lg[4];
       bool inb[4];
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
@@ -251,44 +251,43 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
           tn = v2(fminf(1.0f, tn.x), fminf(1.0f, tn.y));
           const uint32_t o0 = compu(cw, j0), o1 = compu(cw, j1);
           const v2f w_old = v2((float)(o0 >> 24), (float)(o1 >> 24));
-          const v2f wc = w_old + w_new;
+          const v2f wc = w_old + w_new;  // >= 0: both weights are
           const v2f iwc = v2(__builtin_amdgcn_rcpf(wc.x), __builtin_amdgcn_rcpf(wc.y));
           uint32_t c0 = 0, c1 = 0;
 #pragma unroll
-          for (int ch = 0; ch < 3; ++ch) {
+          for (int ch = 0; ch < 3; ++ch) {  // rgb running average, numerators >= 0
             const v2f num = v2((float)((o0 >> (8 * ch)) & 0xFF), (float)((o1 >> (8 * ch)) & 0xFF)) * w_old +
                             v2((float)((n0 >> (8 * ch)) & 0xFF), (float)((n1 >> (8 * ch)) & 0xFF)) * w_new;
             int32_t r0, r1;
-            round_quot_i2(num, wc, iwc, a0, a1, r0, r1);
-            c0 |= (uint32_t)min(255, max(0, r0)) << (8 * ch);
-            c1 |= (uint32_t)min(255, max(0, r1)) << (8 * ch);
+            round_quot_pos2(num, wc, iwc, a0, a1, r0, r1);
+            c0 |= (uint32_t)min(255, r0) << (8 * ch);
+            c1 |= (uint32_t)min(255, r1) << (8 * ch);
           }
           const v2f tnum = v2(comp(ts, j0), comp(ts, j1)) * w_old + tn * w_new;
-          const float t0 = tnum.x / wc.x, t1 = tnum.y / wc.y;
-          c0 |= (uint32_t)f2u8(fminf(roundf(wc.x), 40.0f)) << 24;
-          c1 |= (uint32_t)f2u8(fminf(roundf(wc.y), 40.0f)) << 24;
-          // semantic log-odds fusion (voxel_tsdf.cu:196-202) in base 2: pixB holds log2 ht /
-          // log2 lt, so exp((w_old ln p + w_new ln ht) / wc) = exp2((w_old log2 p + w_new log2 ht)
-          // / wc) with raw v_log_f32 / v_exp_f32 / v_rcp_f32 (~1 ulp each against the 1e-4
-          // probability tolerance); p stays exactly 0.5 when the two terms are equal (ht == lt).
+          const v2f tq = div_pair(tnum, wc, iwc, a0, a1);
+          const v2f wr = wc + v2(0x1.fffffep-2f, 0x1.fffffep-2f);
+          c0 |= weight_round_cap(wr.x, 40u) << 24;
+          c1 |= weight_round_cap(wr.y, 40u) << 24;
+          // semantic log-odds fusion (voxel_tsdf.cu:196-202) as a logistic in base 2:
+          //   P / (P + N) with P = exp((w_old ln p + w_new ln ht) / wc), N likewise with 1 - p, lt
+          //   = 1 / (1 + 2^-x),  x = (w_old log2(p / (1 - p)) + w_new log2(ht / lt)) / wc
+          // (pixB holds log2 ht - log2 lt); raw v_log / v_exp / v_rcp are ~1 ulp each against the
+          // 1e-4 probability tolerance, and p stays exactly 0.5 when ht == lt (x == 0).
           const v2f p = v2(comp(pr, j0), comp(pr, j1));
           const v2f q = 1.0f - p;
-          const v2f lp = v2(__builtin_amdgcn_logf(p.x), __builtin_amdgcn_logf(p.y));
-          const v2f lq = v2(__builtin_amdgcn_logf(q.x), __builtin_amdgcn_logf(q.y));
-          const v2f ap = (w_old * lp + w_new * v2(lg[j0].x, lg[j1].x)) * iwc;
-          const v2f an = (w_old * lq + w_new * v2(lg[j0].y, lg[j1].y)) * iwc;
-          const v2f pos = v2(__builtin_amdgcn_exp2f(ap.x), __builtin_amdgcn_exp2f(ap.y));
-          const v2f neg = v2(__builtin_amdgcn_exp2f(an.x), __builtin_amdgcn_exp2f(an.y));
-          const v2f sum = pos + neg;
-          const v2f pn = pos * v2(__builtin_amdgcn_rcpf(sum.x), __builtin_amdgcn_rcpf(sum.y));
+          const v2f odds = p * v2(__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y));
+          const v2f lo = v2(__builtin_amdgcn_logf(odds.x), __builtin_amdgcn_logf(odds.y));
+          const v2f x = (w_old * lo + w_new * v2(lg[j0], lg[j1])) * iwc;
+          const v2f den = 1.0f + v2(__builtin_amdgcn_exp2f(-x.x), __builtin_amdgcn_exp2f(-x.y));
+          const v2f pn = v2(__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y));
           if (a0) {
-            setc(ts, j0, t0);
-            setc(pr, j0, pos.x == neg.x ? 0.5f : pn.x);
+            setc(ts, j0, tq.x);
+            setc(pr, j0, pn.x);
             setu(cw, j0, c0);
           }
           if (a1) {
-            setc(ts, j1, t1);
-            setc(pr, j1, pos.y == neg.y ? 0.5f : pn.y);
+            setc(ts, j1, tq.y);
+            setc(pr, j1, pn.y);
             setu(cw, j1, c1);
           }
           upd_mask |= (a0 ? 1 << j0 : 0) | (a1 ? 1 << j1 : 0);

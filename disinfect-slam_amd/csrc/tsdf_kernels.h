@@ -39,7 +39,7 @@ struct EngineDev {
   unsigned long long* wg_end;   // kIntegrateGrid + 1: per-WG end stamps, [kIntegrateGrid] = start
   // packed frame
   float4* pixA;                 // {depth, range, w_new, rgb}
-  float2* pixB;                 // {log2 ht, log2 lt}
+  float* pixB;                  // log2 ht - log2 lt (base-2 log-odds of the pixel)
   // query scratch
   unsigned long long* visbits;  // kOccWords
   int32_t* wgcnt;               // kOccWords / 256

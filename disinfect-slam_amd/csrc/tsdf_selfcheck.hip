@@ -1,5 +1,6 @@
 // tsdf_selfcheck.hip -- test-only library (libtsdf_selfcheck.so): checks the engine's fast exact
-// quotient helpers (tsdf_device.h: round_quot_i/_u8, quot_const, quot_for_cmp, f2i / f2u8) bit-for-bit against the
+// quotient helpers (tsdf_device.h: round_quot_i/_u8/_pos2, div_pair, quot_const, quot_for_cmp,
+// f2i / f2u8) bit-for-bit against the
 // correctly rounded IEEE divide and the saturating conversions, on the GPU, over exhaustive and
 // adversarial input sets. Not part of the product library; tests/test_gpu_numerics.py drives it.
 #include <hip/hip_runtime.h>
@@ -64,9 +65,41 @@ __global__ void k_round_quot(uint32_t seed, uint64_t n, float bmin, float bmax, 
     const uint32_t fast_u = round_quot_u8(a, b, rb), ref_u = f2u8(roundf(a / b));
     int32_t p0, p1;  // the packed-pair form on (a, b) and (-a, b)
     round_quot_i2(v2(a, -a), v2(b, b), v2(rb, rb), true, true, p0, p1);
-    if (fast_i != ref_i || fast_u != ref_u || p0 != ref_i || p1 != f2i(roundf(-a / b))) {
+    int32_t n0, n1;  // the non-negative form on (|a|, b) twice
+    const float fa = fabsf(a);
+    round_quot_pos2(v2(fa, fa), v2(b, b), v2(rb, rb), true, true, n0, n1);
+    const int32_t ref_pos = f2i(roundf(fa / b));
+    if (fast_i != ref_i || fast_u != ref_u || p0 != ref_i || p1 != f2i(roundf(-a / b)) ||
+        n0 != ref_pos || n1 != ref_pos) {
       atomicAdd(bad, 1ull);
       atomicMin(first, (uint32_t)i);
+    }
+  }
+}
+
+// div_pair(a, b, v_rcp(b)) == a / b: every a with bits in [lo, hi) (both signs) against a fixed
+// divisor b, or (lo == hi) n random pairs with b log-uniform in [bmin, bmax) and a log-uniform in
+// [2^-44, 2^44] of random sign (covers the fast range and both edges of it)
+__global__ void k_div_pair(float b, uint32_t lo, uint32_t hi, uint32_t seed, uint64_t n, float bmin,
+                           float bmax, unsigned long long* bad, uint32_t* first) {
+  const bool sweep = hi > lo;
+  const uint64_t cnt = sweep ? (uint64_t)hi - lo : n;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cnt;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    float a, bb = b;
+    if (sweep) {
+      a = __uint_as_float(lo + (uint32_t)i);
+    } else {
+      const uint32_t h0 = pcg((uint32_t)i ^ seed), h1 = pcg(h0 + 0x9e3779b9u);
+      bb = bmin * exp2f(log2f(bmax / bmin) * ((h0 >> 8) * 0x1p-24f));
+      a = exp2f(-44.0f + 88.0f * ((h1 >> 8) * 0x1p-24f));
+      if (h1 & 1u) a = -a;
+    }
+    const float y = __builtin_amdgcn_rcpf(bb);
+    const v2f q = div_pair(v2(a, -a), v2(bb, bb), v2(y, y), true, true);
+    if (!same_bits(q.x, a / bb) || !same_bits(q.y, -a / bb)) {
+      atomicAdd(bad, 1ull);
+      atomicMin(first, sweep ? lo + (uint32_t)i : (uint32_t)i);
     }
   }
 }
@@ -170,6 +203,16 @@ int tsdf_selfcheck_quot_cmp(uint32_t seed, uint64_t n, float bmin, float bmax, f
   if (!d) return -1;
   hipLaunchKernelGGL(k_quot_cmp, dim3(8192), dim3(256), 0, 0, seed, n, bmin, bmax, c, &d->bad,
                      &d->first);
+  return finish(d, bad, first);
+}
+
+// div_pair == IEEE a / b: sweep (lo < hi, fixed b) or random (lo == hi, n pairs, b in [bmin, bmax))
+int tsdf_selfcheck_div_pair(float b, uint32_t lo, uint32_t hi, uint32_t seed, uint64_t n, float bmin,
+                            float bmax, unsigned long long* bad, uint32_t* first) {
+  Out* d = start();
+  if (!d) return -1;
+  hipLaunchKernelGGL(k_div_pair, dim3(8192), dim3(256), 0, 0, b, lo, hi, seed, n, bmin, bmax,
+                     &d->bad, &d->first);
   return finish(d, bad, first);
 }
 

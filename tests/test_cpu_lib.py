@@ -95,3 +95,18 @@ def test_block_owner_matches_oracle():
     for k in rng.integers(-2000, 2000, size=(500, 3)):
         for n in (2, 3, 8):
             assert tsdf_amd.block_owner(*map(int, k), n) == block_owner(*map(int, k), n)
+
+
+def test_weight_rounding_identity():
+    """k_integrate's weight update min(roundf(wc), 40) (voxel_tsdf.cu:188) is computed as
+    trunc(RN(wc + 0x1.fffffep-2)) (csrc/tsdf_device.h weight_round_cap): exhaustive over every
+    float wc in [0, 64) -- weights are at most 40 + 4 -- against roundf (half away from zero)."""
+    c = np.float32(float.fromhex("0x1.fffffep-2"))
+    hi = int(np.float32(64.0).view(np.uint32))
+    step = 1 << 24
+    for lo in range(0, hi, step):
+        w = np.arange(lo, min(hi, lo + step), dtype=np.uint32).view(np.float32)
+        fast = (w + c).astype(np.uint32)  # float32 add (RN), truncating convert
+        ref = np.floor(w.astype(np.float64) + 0.5).astype(np.uint32)  # roundf for w >= 0
+        bad = np.nonzero(fast != ref)[0]
+        assert bad.size == 0, f"mismatch at w={w[bad[0]]!r}"

@@ -9,6 +9,8 @@ The integrate and ingest kernels replace the 11-op IEEE divide where an exact sh
    boundary-adversarial pairs per divisor range;
  - quot_for_cmp(a, b, rcp(b), c) -- a / b where only its order against 0 and c matters
    (voxel_visible's frustum test); adversarial samples at both thresholds;
+ - div_pair(a, b, rcp(b))     -- the IEEE divide expansion without its range scaling (tsdf
+   running average); every a in the fast range against fixed divisors, 2^28 random pairs;
  - f2i / f2s / f2u8 via v_cvt_{i,u}32_f32 -- checked on every float bit pattern.
 Each must agree bit for bit with the correctly rounded divide / cvt.rzi semantics.
 """
@@ -32,6 +34,7 @@ def lib():
     L.tsdf_selfcheck_round_quot.argtypes = [u32, u64, f, f, f, P64, P32]
     L.tsdf_selfcheck_convert.argtypes = [u32, u32, P64, P32]
     L.tsdf_selfcheck_quot_cmp.argtypes = [u32, u64, f, f, f, P64, P32]
+    L.tsdf_selfcheck_div_pair.argtypes = [f, u32, u32, u32, u64, f, f, P64, P32]
     return L
 
 
@@ -81,3 +84,20 @@ def test_quot_for_cmp(lib, c):
     for bmin, bmax in [(1e-3, 0.05), (0.05, 20.0)]:
         bad, first = _run(lib.tsdf_selfcheck_quot_cmp, 777, 1 << 27, bmin, bmax, c)
         assert bad == 0, f"c={c}: {bad} mismatches, first sample {first}"
+
+
+# |a| in [2^-44, 2^44] both signs: the whole fast range plus 4 binades of fallback on either side
+DIV_RANGES = [(0x29800000, 0x55800000), (0xA9800000, 0xD5800000)]
+
+
+@pytest.mark.parametrize("b", [4.0, 1.0, 3.9999998, 40.5, 44.0, 7.3125, 0.0137, 2.3841858e-7, 1.5e-12])
+def test_div_pair_sweep(lib, b):
+    for lo, hi in DIV_RANGES:
+        bad, first = _run(lib.tsdf_selfcheck_div_pair, b, lo, hi, 0, 0, 0.0, 0.0)
+        assert bad == 0, f"b={b}: {bad} mismatches, first a bits {first:#x}"
+
+
+@pytest.mark.parametrize("bmin,bmax", [(2.0**-22, 44.0), (2.0**-44, 2.0**44)])
+def test_div_pair_random(lib, bmin, bmax):
+    bad, first = _run(lib.tsdf_selfcheck_div_pair, 0.0, 0, 0, 4242, 1 << 28, bmin, bmax)
+    assert bad == 0, f"{bad} mismatches, first sample {first}"
