@@ -45,14 +45,123 @@ __device__ void nk_insert(const EngineDev& D, uint64_t key, uint32_t order) {
 //     table probe; missing keys go to the global new-key set.
 // ---------------------------------------------------------------------------------------------
 constexpr int kTileSlots = 2048;  // > 256 pixels x maxs (<= 6, checked by tsdf_create)
+constexpr int kVisChunk = 1024;   // visibility sweep: 16 occupancy words x 64 entries per wave
+static_assert(kBands == 16, "ResolveLds band arrays");
 
+// the two roles of k_ingest_dda share one LDS allocation
+union IngestLds {
+  struct {
+    unsigned long long key[kTileSlots];
+    uint32_t ord[kTileSlots];
+    uint16_t vis[4][kTileSlots / 4];
+  } tile;
+  struct {
+    uint32_t list[4][kVisChunk];
+    int cnt[kBands], base[kBands];
+  } sweep;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Visibility sweep (check_visibility_kernel + GatherVisible, voxel_tsdf.cu:82-93,388-397) over
+// the 512 KiB occupancy bitmap instead of the 48 MiB table: every allocated block with any corner
+// in view (no depth test) is appended to the list of the image band its centre projects into
+// (LDS counts, one global atomic per band per pass). Workgroup `wg` covers occupancy words
+// [256 wg, 256 wg + 256); each wave compacts 16 words at a time into LDS so the corner tests run
+// 8 lanes per block on dense work. It runs inside k_ingest_dda, before allocation: it sees the
+// blocks that existed after the previous frame's carving, and k_resolve_alloc appends the
+// blocks it creates. Order within a list is irrelevant to the update; the carving resolver
+// restores the reference's entry order for the deletes.
+// ---------------------------------------------------------------------------------------------
+__device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, IngestLds& S) {
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  uint32_t* L = S.sweep.list[wave];
+  int* s_cnt = S.sweep.cnt;
+  int* s_base = S.sweep.base;
+  const int grp = lane >> 3, corner = lane & 7;
+  for (int pass = 0; pass < 4; ++pass) {
+    if (threadIdx.x < kBands) s_cnt[threadIdx.x] = 0;
+    const int w = wg * 256 + wave * 64 + pass * 16 + (lane & 15);
+    unsigned long long occ = lane < 16 ? D.occ[w] : 0ull;
+    const int c = __popcll(occ);
+    const int incl = wave_incl_scan(c);
+    const int total = __shfl(incl, 63, 64);
+    int p = incl - c;
+    while (occ) {
+      const int b = __ffsll((long long)occ) - 1;
+      occ &= occ - 1;
+      L[p++] = (uint32_t)(w * 64 + b);
+    }
+    __syncthreads();
+    // any-corner visibility (is_block_visible<false>), 8 lanes per block, one corner each; the
+    // visible ones are packed in place as entry | band << 24
+    int nvis = 0;
+    for (int base = 0; base < total; base += 8) {
+      const int i = base + grp;
+      bool v = false;
+      uint32_t e = 0;
+      Ent en{};
+      if (i < total) {
+        e = L[i];
+        en = load_ent(D.table, e);
+        v = voxel_visible(P, (int16_t)((int16_t)(en.x << kBlockLenBits) + ((corner >> 0) & 1) * (kBlockLen - 1)),
+                          (int16_t)((int16_t)(en.y << kBlockLenBits) + ((corner >> 1) & 1) * (kBlockLen - 1)),
+                          (int16_t)((int16_t)(en.z << kBlockLenBits) + ((corner >> 2) & 1) * (kBlockLen - 1)));
+      }
+      const unsigned long long bal = __ballot(v);
+      const bool lead = corner == 0 && i < total && ((bal >> (lane & ~7)) & 0xFFull) != 0;
+      const unsigned long long leads = __ballot(lead);
+      if (lead) {  // rank among this round's visible blocks; slots < base + 8 were all read above
+        const int band = block_band(P, en.x, en.y, en.z);
+        L[nvis + __popcll(leads & ((1ull << lane) - 1ull))] = e | ((uint32_t)band << 24);
+        atomicAdd(&s_cnt[band], 1);
+      }
+      nvis += __popcll(leads);
+    }
+    __syncthreads();
+    if (threadIdx.x < kBands) {  // one global atomic per non-empty band per pass
+      const int cnt = s_cnt[threadIdx.x];
+      s_base[threadIdx.x] = cnt ? atomicAdd(&D.band[threadIdx.x * kBandStride], cnt) : 0;
+      s_cnt[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    for (int k = lane; k < nvis; k += 64) {
+      const uint32_t pk = L[k];
+      const uint32_t e = pk & 0xFFFFFFu;
+      const int band = (int)(pk >> 24);
+      const int pos = s_base[band] + atomicAdd(&s_cnt[band], 1);
+      const Ent en = load_ent(D.table, e);
+      VisRec r;
+      r.x = en.x;
+      r.y = en.y;
+      r.z = en.z;
+      r.pad = 0;  // existed before this frame (not fresh)
+      r.idx = en.idx;
+      r.entry = (int32_t)e;
+      D.vis[(size_t)band * D.nblocks + pos] = r;
+    }
+    __syncthreads();  // L and the band counts are reused by the next pass
+  }
+}
+
+// grid: kVisWorkgroups sweep workgroups first (dispatched first, they overlap the tiles), then
+// one workgroup per 16x16 pixel tile (tiles_x per row, `tiles` in all)
 __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
                                                     const float* __restrict__ depth,
                                                     const uint8_t* __restrict__ rgb,
                                                     const float* __restrict__ ht,
-                                                    const float* __restrict__ lt) {
-  __shared__ unsigned long long s_key[kTileSlots];
-  __shared__ uint32_t s_ord[kTileSlots];
+                                                    const float* __restrict__ lt, int tiles_x,
+                                                    int tiles) {
+  __shared__ IngestLds S;
+  if ((int)blockIdx.x < kVisWorkgroups) {
+    TSDF_STAMP(D, 2, 0);
+    vis_sweep(D, P, blockIdx.x, S);
+    TSDF_STAMP(D, 2, 1);
+    return;
+  }
+  const int tile = (int)blockIdx.x - kVisWorkgroups;
+  if (tile >= tiles) return;
+  unsigned long long* s_key = S.tile.key;
+  uint32_t* s_ord = S.tile.ord;
   TSDF_STAMP(D, 0, 0);
   for (int i = threadIdx.x; i < kTileSlots; i += 256) {
     s_key[i] = 0ull;
@@ -60,8 +169,8 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
   }
   __syncthreads();
   TSDF_STAMP(D, 0, 1);
-  const int x = blockIdx.x * 16 + (threadIdx.x & 15);
-  const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+  const int x = (tile % tiles_x) * 16 + (threadIdx.x & 15);
+  const int y = (tile / tiles_x) * 16 + (threadIdx.x >> 4);
   if (x < P.W && y < P.H) {
     const int i = y * P.W + x;
     const float d = depth[i];
@@ -124,7 +233,7 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
   // 8 at a time with 8 lanes per key, one block corner per lane (is_block_visible<true>), and the
   // fully visible ones are listed in LDS. The table probes and new-key inserts then run one key
   // per lane over that list, so the wave pays their memory latency once, not once per 8 keys.
-  __shared__ uint16_t s_vis[4][kTileSlots / 4];
+  uint16_t(*s_vis)[kTileSlots / 4] = S.tile.vis;
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   const int grp = lane >> 3, corner = lane & 7;
   int nv = 0;
@@ -188,11 +297,11 @@ __global__ void k_keys_to_newset(EngineDev D, const int16_t* __restrict__ keys, 
 // buckets in an LDS table (smallest rank wins), and the longest prefix whose keys won all their
 // claims commits in parallel. The first key always wins, so each round commits >= 1 key.
 // Pool blocks are popped in commit order by prefix sum (AquireBlock, voxel_mem.cu:37-52).
-// fresh_mode 1: mark new blocks in fresh_flag (integrate initialises them), 0: list them in
-// D.fresh for k_fresh_init.
+// frame_mode 1: append new blocks to this frame's visible-block lists flagged fresh (integrate
+// initialises them), 0: list them in D.fresh for k_fresh_init.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, uint32_t range,
-                                                                   int frame_mode) {
+__global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, FrameParams P,
+                                                                   uint32_t range, int frame_mode) {
   __shared__ ResolveLds L;
   const int t = threadIdx.x;
   TSDF_STAMP(D, 1, 0);
@@ -204,6 +313,7 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, 
     L.nalloc = 0;
   }
   claims_clear(L);
+  if (t < kBands) L.bcnt[t] = 0;
   const int n = D.ctr->nk_count;
   // (order, slot) pairs in a compact scratch array so every batch pass is one coalesced read
   for (int i = t; i < n; i += kResolveThreads) {
@@ -301,6 +411,8 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, 
       int nok;
       const int rank = block_excl_scan(ok ? 1 : 0, L.scan, &nok);
       const int free_now = L.sfree;
+      VisRec vr{};
+      int vband = -1, vrank = 0;
       if (ok) {
         const int hi = free_now - 1 - rank;
         if (hi < 0) {
@@ -317,10 +429,21 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, 
           }
           store_ent(D.table, e, kx, ky, kz, 0, idx);
           atomicOr(&D.occ[e >> 6], 1ull << (e & 63));
-          if (frame_mode)
-            D.fresh_flag[idx] = 1;
-          else
+          if (frame_mode) {
+            // a new block has all 8 corners in view, so it is visible this frame: appended to
+            // its band list below (the sweep in k_ingest_dda saw only the blocks that existed
+            // before), flagged fresh so k_integrate starts it from AquireBlock's state
+            vr.x = kx;
+            vr.y = ky;
+            vr.z = kz;
+            vr.pad = 1;
+            vr.idx = idx;
+            vr.entry = (int32_t)e;
+            vband = block_band(P, kx, ky, kz);
+            vrank = atomicAdd(&L.bcnt[vband], 1);
+          } else {
             D.fresh[L.nfresh + rank] = idx;
+          }
         }
       }
       if (commit) {
@@ -329,6 +452,11 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, 
       }
       claims_clear(L);
       __syncthreads();
+      if (frame_mode && t < kBands) {  // one global append per non-empty band per round
+        const int c = L.bcnt[t];
+        L.bbase[t] = c ? atomicAdd(&D.band[t * kBandStride], c) : 0;
+        L.bcnt[t] = 0;
+      }
       if (t == 0) {
         const int used = nok < free_now ? nok : (free_now > 0 ? free_now : 0);
         L.sfree = free_now - used;
@@ -338,6 +466,7 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, 
         L.base = base + (first_dirty < span ? first_dirty : span);
       }
       __syncthreads();
+      if (vband >= 0) D.vis[(size_t)vband * D.nblocks + L.bbase[vband] + vrank] = vr;
     }
   }
   TSDF_STAMP(D, 1, 3);
@@ -351,10 +480,8 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, 
       D.ctr->total_alloc += (unsigned long long)L.nalloc;
       D.ctr->last_updated = 0ull;
       D.ctr->n_vis = 0;
-      D.ctr->n_cand = 0;
     }
   }
-  if (frame_mode && t < kBands) D.band[t * kBandStride] = 0;
 }
 
 // AquireBlock's initialisation (voxel_mem.cu:43-51) for the hash-level test path

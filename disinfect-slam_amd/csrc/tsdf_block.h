@@ -85,6 +85,8 @@ struct ResolveLds {
   int base;
   int nalloc;
   uint32_t epoch;
+  int bcnt[16];                       // new blocks per visible-list band this round (frame mode)
+  int bbase[16];                      // their base in the band list
 };
 
 __device__ __forceinline__ void lds_bitonic_sort(unsigned long long* a, int m) {

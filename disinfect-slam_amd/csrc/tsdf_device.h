@@ -39,7 +39,10 @@ constexpr uint32_t kNewKeyCap = 1u << 17;       // unique new blocks per frame
 constexpr int kMaxDdaSamples = 6;               // DDA samples per pixel the ingest kernel supports
 constexpr int64_t kMaxOrderRange = 8192ll * 1024;  // candidate order space the resolver streams
 constexpr int kResolveThreads = 1024;
-constexpr int kIntegrateGrid = 2048;  // k_integrate workgroups (persistent grid-stride)
+constexpr int kIntegrateGrid = 2048;  // k_integrate workgroups (persistent grid-stride) at most
+// k_integrate workgroup size: 4 waves, two per visible block (1024-thread workgroups measured
+// slower: 24.3 against 17.5 us)
+constexpr int kIntegrateThreads = 256;
 
 struct f3 {
   float x, y, z;
@@ -268,6 +271,44 @@ __device__ __forceinline__ float quot_const(float a, float b, float rb) {
     return __builtin_fmaf(r, rb, q);
   }
   return a / b;
+}
+
+// 16-B pool-state accesses: plain cached loads and stores. TSDF_STREAM_STORES / _LOADS build
+// nontemporal forms for timing studies (measured slower on MI355X: 18.3 / 20.2 us against 17.8 us
+// for k_integrate at the bench workload).
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 pool_ld(const uint8_t* p) {
+#if !defined(TSDF_STREAM_LOADS)
+  return *reinterpret_cast<const float4*>(p);
+#else
+  const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+#endif
+}
+__device__ __forceinline__ uint4 pool_ldu(const uint8_t* p) {
+#if !defined(TSDF_STREAM_LOADS)
+  return *reinterpret_cast<const uint4*>(p);
+#else
+  const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+#endif
+}
+__device__ __forceinline__ void pool_st(uint8_t* p, float4 v) {
+#if !defined(TSDF_STREAM_STORES)
+  *reinterpret_cast<float4*>(p) = v;
+#else
+  const v4f t = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(t, reinterpret_cast<v4f*>(p));
+#endif
+}
+__device__ __forceinline__ void pool_stu(uint8_t* p, uint4 v) {
+#if !defined(TSDF_STREAM_STORES)
+  *reinterpret_cast<uint4*>(p) = v;
+#else
+  const v4u t = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(t, reinterpret_cast<v4u*>(p));
+#endif
 }
 
 // voxel_hash.cu:31-35

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -130,7 +131,7 @@ namespace {
 
 void free_all(tsdf_engine* e) {
   EngineDev& D = e->D;
-  void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.fresh_flag, D.occ,
+  void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.occ,
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs, D.pkey,      D.fresh,
                   D.vis,     D.band,    D.cand,     D.wg_upd, D.wg_end, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
@@ -196,8 +197,8 @@ int ensure_test_cap(tsdf_engine* e, int n) {
   return TSDF_OK;
 }
 
-int launch_resolve_alloc(tsdf_engine* e, uint32_t range, int frame_mode) {
-  hipLaunchKernelGGL(k_resolve_alloc, dim3(1), dim3(kResolveThreads), 0, e->stream, e->D, range,
+int launch_resolve_alloc(tsdf_engine* e, const FrameParams& P, uint32_t range, int frame_mode) {
+  hipLaunchKernelGGL(k_resolve_alloc, dim3(1), dim3(kResolveThreads), 0, e->stream, e->D, P, range,
                      frame_mode);
   if (!frame_mode)
     hipLaunchKernelGGL(k_fresh_init, dim3(512), dim3(256), 0, e->stream, e->D);
@@ -300,7 +301,6 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.lock_tag, kNumBucket);
   ALLOC(D.heap, nb);
   ALLOC(D.pool, (size_t)nb * kBlockBytes);
-  ALLOC(D.fresh_flag, nb);
   ALLOC(D.occ, kOccWords);
   ALLOC(D.ctr, 1);
   ALLOC(D.nk_key, kNewKeyCap);
@@ -316,9 +316,10 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.wg_end, kIntegrateGrid + 1);
   {  // one resident wave of k_integrate workgroups: no second-round stragglers
     int per_cu = 0, ncu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate, kIntegrateThreads, 0) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
       return fail(TSDF_ERR_HIP);
+    if (const char* v = std::getenv("TSDF_INTEGRATE_WG_PER_CU")) per_cu = std::min(per_cu, std::atoi(v));  // tuning
     D.integrate_grid = std::max(8, std::min(kIntegrateGrid, (per_cu * ncu) & ~7));
   }
   ALLOC(D.pixA, e->max_pixels);
@@ -354,7 +355,6 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   bool ok = true;
   ok &= hipMemsetAsync(D.lock_tag, 0, sizeof(uint32_t) * kNumBucket, s) == hipSuccess;
   ok &= hipMemsetAsync(D.pool, 0, (size_t)nb * kBlockBytes, s) == hipSuccess;
-  ok &= hipMemsetAsync(D.fresh_flag, 0, (size_t)nb, s) == hipSuccess;
   ok &= hipMemsetAsync(D.occ, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
   ok &= hipMemsetAsync(D.nk_key, 0, sizeof(unsigned long long) * kNewKeyCap, s) == hipSuccess;
   ok &= hipMemsetAsync(D.nk_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
@@ -433,19 +433,19 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
   }
   const bool all_ev = ev && e->prof_mode == TSDF_PROFILE_PHASES;
   if (all_ev) HIP_OK(hipEventRecord((*ev)[0], s));
-  // ---- allocate (voxel_tsdf.cu:377-386) ----
-  hipLaunchKernelGGL(k_ingest_dda, dim3((W + 15) / 16, (H + 15) / 16), dim3(256), 0, s, e->D, P,
-                     depth, rgb, ht, lt);
+  // ---- allocate (voxel_tsdf.cu:377-386) + visibility (:388-397) ----
+  // k_ingest_dda sweeps the blocks that already exist for visibility beside the DDA; the
+  // resolver inserts the new keys and appends the blocks it creates to the visible lists
+  const int tiles_x = (W + 15) / 16, tiles = tiles_x * ((H + 15) / 16);
+  hipLaunchKernelGGL(k_ingest_dda, dim3(kVisWorkgroups + tiles), dim3(256), 0, s, e->D, P, depth,
+                     rgb, ht, lt, tiles_x, tiles);
   LAUNCH_OK("k_ingest_dda");
-  int rc = launch_resolve_alloc(e, (uint32_t)(np * e->maxs), 1);
+  int rc = launch_resolve_alloc(e, P, (uint32_t)(np * e->maxs), 1);
   if (rc) return rc;
   if (all_ev) HIP_OK(hipEventRecord((*ev)[1], s));
-  // ---- visibility (voxel_tsdf.cu:388-397) ----
-  hipLaunchKernelGGL(k_vis, dim3(kOccWords / 256), dim3(256), 0, s, e->D, P);
-  LAUNCH_OK("k_vis");
   if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
   // ---- update (voxel_tsdf.cu:474-481) ----
-  hipLaunchKernelGGL(k_integrate, dim3(e->D.integrate_grid), dim3(256), 0, s, e->D, P);
+  hipLaunchKernelGGL(k_integrate, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s, e->D, P);
   LAUNCH_OK("k_integrate");
   if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
   // ---- space carving (voxel_tsdf.cu:483-488) ----
@@ -735,7 +735,7 @@ int tsdf_hash_allocate(tsdf_engine* e, const int16_t* keys, int n) {
   hipLaunchKernelGGL(k_keys_to_newset, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->D,
                      e->t_keys, n);
   LAUNCH_OK("k_keys_to_newset");
-  rc = launch_resolve_alloc(e, (uint32_t)n, 0);
+  rc = launch_resolve_alloc(e, FrameParams{}, (uint32_t)n, 0);
   if (rc) return rc;
   HIP_OK(hipStreamSynchronize(e->stream));
   return TSDF_OK;

@@ -1,105 +1,17 @@
-// tsdf_fuse.hip -- per-frame visibility, the fused integrate kernel and the space-carving resolver.
+// tsdf_fuse.hip -- the fused integrate kernel and the space-carving resolver.
 #include "tsdf_block.h"
 #include "tsdf_kernels.h"
 
 namespace tsdf {
 
 // ---------------------------------------------------------------------------------------------
-// k_vis: check_visibility_kernel (voxel_tsdf.cu:82-93) over the 512 KiB occupancy bitmap instead
-// of the 48 MiB table: every allocated block with any corner in view (no depth test) is appended
-// to the list of the image band its centre projects into (LDS counts, one global atomic per band
-// per workgroup). Each wave first compacts its live entries into LDS so the corner tests run
-// 8 lanes per block on dense work instead of one lane per bitmap word. Order is irrelevant to the update; the carving resolver restores the
-// reference's entry order for the deletes.
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ int block_band(const FrameParams& P, int16_t bx, int16_t by, int16_t bz) {
-  const float h = 0.5f * (float)(kBlockLen - 1);
-  const f3 pw = {((float)(bx << kBlockLenBits) + h) * P.voxel, ((float)(by << kBlockLenBits) + h) * P.voxel,
-                 ((float)(bz << kBlockLenBits) + h) * P.voxel};
-  const f3 pc = se3_apply(P.cq, P.ct, pw);
-  const float v = (P.fy * pc.y + P.cy * pc.z) * __builtin_amdgcn_rcpf(pc.z);
-  const float bandf = v * ((float)kBands / (float)P.H);
-  return pc.z > 0.f && bandf > 0.f ? min(kBands - 1, f2i(bandf)) : 0;
-}
-
-__global__ __launch_bounds__(256) void k_vis(EngineDev D, FrameParams P) {
-  TSDF_STAMP(D, 2, 0);
-  // per wave: its 64 occupancy words (4096 entries) compacted to a list of live entries, then
-  // filtered in place to the visible ones packed as entry | band << 24
-  __shared__ uint32_t s_list[4][4096];
-  __shared__ int s_cnt[kBands], s_base[kBands];
-  const int lane = lane_id(), wave = threadIdx.x >> 6;
-  uint32_t* L = s_list[wave];
-  if (threadIdx.x < kBands) s_cnt[threadIdx.x] = 0;
-  const int w = blockIdx.x * 256 + threadIdx.x;  // kOccWords == 256 * 256
-  unsigned long long occ = D.occ[w];
-  const int c = __popcll(occ);
-  const int incl = wave_incl_scan(c);
-  const int total = __shfl(incl, 63, 64);
-  int p = incl - c;
-  while (occ) {
-    const int b = __ffsll((long long)occ) - 1;
-    occ &= occ - 1;
-    L[p++] = (uint32_t)(w * 64 + b);
-  }
-  __syncthreads();
-  // any-corner visibility (is_block_visible<false>), 8 lanes per block, one corner each
-  const int grp = lane >> 3, corner = lane & 7;
-  int nvis = 0;
-  for (int base = 0; base < total; base += 8) {
-    const int i = base + grp;
-    bool v = false;
-    uint32_t e = 0;
-    Ent en{};
-    if (i < total) {
-      e = L[i];
-      en = load_ent(D.table, e);
-      v = voxel_visible(P, (int16_t)((int16_t)(en.x << kBlockLenBits) + ((corner >> 0) & 1) * (kBlockLen - 1)),
-                        (int16_t)((int16_t)(en.y << kBlockLenBits) + ((corner >> 1) & 1) * (kBlockLen - 1)),
-                        (int16_t)((int16_t)(en.z << kBlockLenBits) + ((corner >> 2) & 1) * (kBlockLen - 1)));
-    }
-    const unsigned long long bal = __ballot(v);
-    const bool lead = corner == 0 && i < total && ((bal >> (lane & ~7)) & 0xFFull) != 0;
-    const unsigned long long leads = __ballot(lead);
-    if (lead) {  // rank among this round's visible blocks; slots < base + 8 were all read above
-      const int band = block_band(P, en.x, en.y, en.z);
-      L[nvis + __popcll(leads & ((1ull << lane) - 1ull))] = e | ((uint32_t)band << 24);
-      atomicAdd(&s_cnt[band], 1);
-    }
-    nvis += __popcll(leads);
-  }
-  __syncthreads();
-  if (threadIdx.x < kBands) {  // one global atomic per non-empty band per workgroup
-    const int cnt = s_cnt[threadIdx.x];
-    s_base[threadIdx.x] = cnt ? atomicAdd(&D.band[threadIdx.x * kBandStride], cnt) : 0;
-    s_cnt[threadIdx.x] = 0;
-  }
-  __syncthreads();
-  for (int k = lane; k < nvis; k += 64) {
-    const uint32_t pk = L[k];
-    const uint32_t e = pk & 0xFFFFFFu;
-    const int band = (int)(pk >> 24);
-    const int pos = s_base[band] + atomicAdd(&s_cnt[band], 1);
-    const Ent en = load_ent(D.table, e);
-    VisRec r;
-    r.x = en.x;
-    r.y = en.y;
-    r.z = en.z;
-    r.pad = (int16_t)D.fresh_flag[en.idx];  // allocated this frame: integrate starts it from AquireBlock's state
-    r.idx = en.idx;
-    r.entry = (int32_t)e;
-    D.vis[(size_t)band * D.nblocks + pos] = r;
-  }
-  TSDF_STAMP(D, 2, 1);
-}
-
-// ---------------------------------------------------------------------------------------------
 // k_integrate: tsdf_integrate_kernel (voxel_tsdf.cu:149-205) + the space_carving_kernel minimum
 // (:207-230) fused. Two waves per visible 8^3 block, 4 voxels per lane: lane l of wave half h owns
 // voxels v = 256h + 4l .. +3 (x = 4(l&1)+j, y = (l>>1)&7, z = l>>4 + 4h), so each of the three
 // state arrays moves as one 16-B-per-lane, 1-KiB-per-wave access inside the block's contiguous
-// 6-KiB record. Pixel data is two gathers per voxel (16 B + 8 B, L2 resident). Blocks allocated
-// this frame (fresh_flag) start from AquireBlock's state (voxel_mem.cu:43-51) in registers.
+// 6-KiB record. Pixel data is two gathers per voxel (16 B + 4 B, L2 resident). Blocks allocated
+// this frame (VisRec.pad, set by the allocation resolver) start from AquireBlock's state
+// (voxel_mem.cu:43-51) in registers.
 // Carve candidates (min |tsdf| >= 0.9) are appended with their hash-entry index.
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ float comp(const float4& v, int j) {
@@ -115,7 +27,7 @@ __device__ __forceinline__ void setu(uint4& v, int j, uint32_t f) {
   if (j == 0) v.x = f; else if (j == 1) v.y = f; else if (j == 2) v.z = f; else v.w = f;
 }
 
-__global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
+__global__ __launch_bounds__(kIntegrateThreads) void k_integrate(EngineDev D, FrameParams P) {
   __shared__ float s_min[4];
   __shared__ int s_upd[4];
   const int lane = lane_id();
@@ -167,9 +79,9 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
       float4 ts = make_float4(0.5f, 0.5f, 0.5f, 0.5f), pr = ts;
       uint4 cw = make_uint4(0x05808080u, 0x05808080u, 0x05808080u, 0x05808080u);
 #else
-      float4 ts = *reinterpret_cast<const float4*>(blk + off);
-      float4 pr = *reinterpret_cast<const float4*>(blk + kProbOffset + off);
-      uint4 cw = *reinterpret_cast<const uint4*>(blk + kRgbwOffset + off);
+      float4 ts = pool_ld(blk + off);
+      float4 pr = pool_ld(blk + kProbOffset + off);
+      uint4 cw = pool_ldu(blk + kRgbwOffset + off);
 #endif
       fresh = r.pad != 0;
       if (fresh) {
@@ -299,9 +211,9 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
 #else
       if (upd_mask || fresh) {
 #endif
-        *reinterpret_cast<float4*>(blk + off) = ts;
-        *reinterpret_cast<float4*>(blk + kProbOffset + off) = pr;
-        *reinterpret_cast<uint4*>(blk + kRgbwOffset + off) = cw;
+        pool_st(blk + off, ts);
+        pool_st(blk + kProbOffset + off, pr);
+        pool_stu(blk + kRgbwOffset + off, cw);
       }
       my_upd += __popc(upd_mask);
     }
@@ -310,7 +222,6 @@ __global__ __launch_bounds__(256) void k_integrate(EngineDev D, FrameParams P) {
     __syncthreads();
     if (hf == 0 && lane == 0 && b < nvis) {
       const float m2 = fminf(s_min[wave], s_min[wave + 1]);
-      if (fresh) D.fresh_flag[pidx] = 0;
       if (m2 >= 0.9f) {  // space_carving_kernel threshold (voxel_tsdf.cu:227, :485)
         const int k = atomicAdd(&D.ctr->n_cand, 1);
         D.cand[k] = r;
@@ -374,6 +285,7 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
   auto keyf = [&](int i) -> uint32_t { return (uint32_t)recs[i].entry; };
   const int width = direct ? 1 : stream_prepare(L, n, kNumEntry, keyf);
   const int nbatch = direct ? n : (n <= kBatch ? (n > 0 ? 1 : 0) : ((n - 1) >> 10) + 1);
+  TSDF_STAMP(D, 4, 1);
   for (int j = 0; j < nbatch; ++j) {
     int m;
     if (direct) {
@@ -463,7 +375,7 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
       __syncthreads();
     }
   }
-  TSDF_STAMP(D, 4, 1);
+  TSDF_STAMP(D, 4, 2);
   if (t == 0) {
     D.ctr->free_count = L.sfree;
     if (!direct) {
@@ -472,8 +384,10 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
       D.ctr->total_visible += (unsigned long long)D.ctr->n_vis;
       D.ctr->total_updated += D.ctr->last_updated;
       D.ctr->frames += 1ull;
+      D.ctr->n_cand = 0;  // the next frame's lists start empty (its sweep runs before allocation)
     }
   }
+  if (!direct && t < kBands) D.band[t * kBandStride] = 0;
 }
 
 }  // namespace tsdf

@@ -13,13 +13,23 @@ constexpr int kDiagKernels = 8, kDiagMaxWg = 4096, kDiagStamps = 8;
 // in that XCD's L2). Counters 128 B apart; list b holds up to nblocks records at vis + b * nblocks.
 constexpr int kBands = 16, kBandStride = 32;
 
+// band of a block: the image band its centre projects into (0 when behind the camera)
+__device__ __forceinline__ int block_band(const FrameParams& P, int16_t bx, int16_t by, int16_t bz) {
+  const float h = 0.5f * (float)(kBlockLen - 1);
+  const f3 pw = {((float)(bx << kBlockLenBits) + h) * P.voxel, ((float)(by << kBlockLenBits) + h) * P.voxel,
+                 ((float)(bz << kBlockLenBits) + h) * P.voxel};
+  const f3 pc = se3_apply(P.cq, P.ct, pw);
+  const float v = (P.fy * pc.y + P.cy * pc.z) * __builtin_amdgcn_rcpf(pc.z);
+  const float bandf = v * ((float)kBands / (float)P.H);
+  return pc.z > 0.f && bandf > 0.f ? min(kBands - 1, f2i(bandf)) : 0;
+}
+
 // device pointers of one engine (passed by value to every kernel)
 struct EngineDev {
   int4* table;                  // kNumEntry hash entries
   uint32_t* lock_tag;           // kNumBucket bucket locks (== epoch: locked)
   int32_t* heap;                // free-block stack
   uint8_t* pool;                // nblocks x kBlockBytes
-  uint8_t* fresh_flag;          // nblocks: allocated this frame, not yet initialised
   unsigned long long* occ;      // kOccWords occupancy bitmap
   DevCounters* ctr;
   int32_t nblocks;
@@ -48,11 +58,11 @@ struct EngineDev {
 
 __global__ void k_init_table(int4* table);
 __global__ void k_init_heap(int32_t* heap, int n);
-// per frame (5 launches)
+// per frame (4 launches)
+constexpr int kVisWorkgroups = kOccWords / 256;  // visibility-sweep workgroups of k_ingest_dda
 __global__ void k_ingest_dda(EngineDev D, FrameParams P, const float* depth, const uint8_t* rgb,
-                             const float* ht, const float* lt);
-__global__ void k_resolve_alloc(EngineDev D, uint32_t range, int frame_mode);
-__global__ void k_vis(EngineDev D, FrameParams P);
+                             const float* ht, const float* lt, int tiles_x, int tiles);
+__global__ void k_resolve_alloc(EngineDev D, FrameParams P, uint32_t range, int frame_mode);
 __global__ void k_integrate(EngineDev D, FrameParams P);
 __global__ void k_resolve_delete(EngineDev D, const VisRec* recs, const int32_t* count,
                                  int direct);

@@ -94,8 +94,9 @@ typedef struct tsdf_stats {
 
 typedef struct tsdf_profile { /* device time of the integrate phases between begin/end */
   int64_t frames;      /* integrate calls that were event-timed (every `every`-th call) */
-  double ms_allocate;  /* DDA + new-key ordering + allocation resolve + block init */
-  double ms_visible;   /* visibility compaction */
+  double ms_allocate;  /* DDA + visibility sweep of the existing blocks (one kernel) + ordered
+                          allocation resolve, which lists the new blocks as visible */
+  double ms_visible;   /* ~0: visibility runs inside the allocate phase (kept for the layout) */
   double ms_integrate; /* the fused TSDF/RGB/weight/semantic update kernel (+ carve minimum) */
   double ms_carve;     /* space-carving compaction + delete resolve */
   int64_t sum_visible; /* sum of N_vis over the profiled frames */

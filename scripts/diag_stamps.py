@@ -15,9 +15,9 @@ sys.path.insert(0, os.path.join(ROOT, "disinfect-slam_amd"))
 
 KERNELS = {0: ("ingest", ["lds_init", "pix_write", "dda", "barrier", "sweep"]),
            1: ("resolve_alloc", ["prepare", "batch0", "resolve"]),
-           2: ("vis", ["all"]),
+           2: ("vis (in ingest)", ["all"]),
            3: ("integrate", ["all"]),
-           4: ("resolve_delete", ["all"])}
+           4: ("resolve_delete", ["sum+prepare", "rounds"])}
 NK, NWG, NS = 8, 4096, 8
 
 
@@ -58,7 +58,7 @@ def main():
         S = buf.reshape(NK, NWG, NS).astype(np.int64)
         t0 = None
         bounds = []
-        for k, (name, phases) in KERNELS.items():
+        for k, (name, phases) in sorted(KERNELS.items(), key=lambda kv: (kv[0] != 2, kv[0])):
             s = S[k]
             valid = s[:, 0] > 0
             if not valid.any():
@@ -77,6 +77,13 @@ def main():
             sk = (s[:, 0] - start) * 10e-3
             d["start_skew_p50"].append(np.median(sk))
             d["start_skew_max"].append(sk.max())
+            for q in (10, 90, 99):
+                d.setdefault(f"start_skew_p{q}", []).append(np.percentile(sk, q))
+            ek = (s[:, last] - start) * 10e-3
+            for q in (10, 50, 90, 99):
+                d.setdefault(f"end_p{q}", []).append(np.percentile(ek, q))
+            late = s[sk > 5.0]
+            d.setdefault("n_start_after_5us", []).append(len(late))
             for j, p in enumerate(phases):
                 dur = (s[:, j + 1] - s[:, j]) * 10e-3
                 d[p].append(np.median(dur))
