@@ -11,14 +11,18 @@ N>1 (launched by torch.distributed.run, one rank per GPU): default --mode stream
 stream per GPU into that GPU's own volume (a multi-camera rig; no data-path collective), value =
 all frames integrated by all ranks / max rank time, scaling "weak". --mode sharded integrates ONE
 stream with the volume spatially sharded by 4^3-block bricks (each rank allocates and integrates
-only the blocks it owns), value = frames / max rank time, scaling "strong".
+only the blocks it owns), value = frames / max rank time, scaling "strong". --mode routed shards the
+same way but splits the block-allocation DDA by pixel-tile rows across ranks and routes each
+visible key to its owner with one RCCL all-to-all per frame (SURVEY.md 8e option 2), "strong".
 
 roofline: the fused integrate kernel (k_integrate). Algorithmic bytes per launch:
 N_vis * (512 * 12 + 12) voxel state + block metadata read, N_upd * 12 updated voxel state written,
 15 * W * H frame bytes read -- N_vis and N_upd are counted on device. Average launch duration from
-HIP events recorded on the engine stream around the k_integrate launches of every 8th frame of the
-timed region (--event-every; an event is a queue marker costing the stream ~3 us, so timing every
-launch would slow the loop ~8 %); the in-kernel device clock of every launch is reported beside it.
+HIP start/stop events bound to every k_integrate launch of the timed region on the engine stream
+(hipExtLaunchKernel: the dispatch's own begin/end timestamps, the interval a rocprofv3 kernel
+trace reports); --marker-events times with marker events recorded around the launch instead (each
+carries a system-scope release, i.e. an L2 writeback, so it reads a few us longer). The in-kernel
+device clock of every launch is reported beside it.
 cpu_baseline: the single-threaded CPU oracle (oracle/tsdf_oracle.c, a restatement of the
 reference kernels incl. its full-table visibility scan) on a bounded sample of the same stream.
 """
@@ -48,12 +52,19 @@ def parse():
     p.add_argument("--trunc", type=float, default=0.03)
     p.add_argument("--max-depth", type=float, default=4.0)
     p.add_argument("--depth-only", action="store_true", help="config C2: ht = lt = NULL (ones)")
-    p.add_argument("--mode", choices=("streams", "sharded"), default="streams")
+    p.add_argument("--mode", choices=("streams", "sharded", "routed"), default="streams")
+    p.add_argument("--route-cap", type=int, default=8192,
+                   help="routed mode: keys per destination rank per frame (outbox slot size)")
     p.add_argument("--cpu-frames", type=int, default=-1, help="oracle sample size (-1 = auto)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--block-bits", type=int, default=18)
     p.add_argument("--event-every", type=int, default=8,
-                   help="HIP-event-time k_integrate on every n-th timed frame (events cost ~3 us each)")
+                   help="HIP-event-time k_integrate on every n-th timed frame (a profiled dispatch "
+                        "runs ~1 us slower, so the loop samples)")
+    p.add_argument("--marker-events", action="store_true",
+                   help="time k_integrate with marker events recorded around the launch (each is a "
+                        "queue marker with a system-scope release: ~3 us of cache writeback each) "
+                        "instead of events bound to the kernel's dispatch")
     p.add_argument("--no-events", action="store_true",
                    help="diagnostic: no HIP events in the timed loop (roofline then unmeasured)")
     return p.parse_args()
@@ -99,10 +110,22 @@ def main():
     K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])  # ctypes struct cached once
     poses = [tsdf_amd.SE3(frames["q"][i], frames["t"][i]) for i in range(nframes)]
 
+    routed = a.mode == "routed" and shard_count > 1
+    if routed:  # one outbox / inbox slot per rank; exchanged by an RCCL all-to-all each frame
+        nbytes = tsdf_amd.Engine.route_buffer_bytes(world, a.route_cap)
+        outbox = torch.zeros((world, nbytes // world), dtype=torch.uint8, device=dev)
+        inbox = torch.zeros_like(outbox)
+
     def step(i):
         ht = None if a.depth_only else frames["ht"][i]
         lt = None if a.depth_only else frames["lt"][i]
-        eng.integrate(frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i], a.max_depth)
+        if routed:
+            eng.integrate_route_begin(frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i],
+                                      a.max_depth, rank, world, outbox, a.route_cap)
+            tdist.route_exchange(outbox, inbox)
+            eng.integrate_route_end(inbox, a.route_cap)
+        else:
+            eng.integrate(frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i], a.max_depth)
 
     for i in range(a.warmup):
         step(i)
@@ -110,9 +133,10 @@ def main():
     if dist:
         dist.barrier()
     if not a.no_events:
-        # 2 events around k_integrate on every event_every-th frame: each event is a queue marker
-        # that stalls the stream ~3 us, so the loop samples instead of timing every launch
-        eng.profile_begin(integrate_only=True, every=a.event_every)
+        # default: start/stop events bound to every k_integrate dispatch (hipExtLaunchKernel) --
+        # the kernel's begin/end timestamps on the engine stream, nothing added to the stream.
+        # --marker-events: 2 marker events around the launch on every event_every-th frame
+        eng.profile_begin(integrate_only=True, every=a.event_every, kernel_events=not a.marker_events)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.warmup, a.warmup + a.steps):
@@ -178,8 +202,7 @@ def main():
                             f"{a.max_depth:g} m max depth, TUM fr1 intrinsics, orbit 1 cm + 0.5 deg/frame",
                 "width": W, "height": H, "voxel_m": a.voxel, "truncation_m": a.trunc,
                 "pool_blocks": 1 << a.block_bits,
-                "parallelism": (f"streams{world}" if a.mode == "streams" else f"sharded{world}")
-                if world > 1 else "single",
+                "parallelism": f"{a.mode}{world}" if world > 1 else "single",
             },
             "roofline": {
                 "kernel": "k_integrate",
@@ -195,6 +218,7 @@ def main():
                 # (what rocprofv3's kernel trace measures; the HIP events above also include the
                 # per-launch dispatch / completion overhead)
                 "event_timed_launches": prof["frames"],
+                "event_kind": "marker" if a.marker_events else "kernel-dispatch",
                 "us_per_launch_device_clock": round(prof["ms_integrate_device"] / a.steps * 1e3, 3),
                 "achieved_device_clock": round(alg_bytes / (prof["ms_integrate_device"] / a.steps / 1e3) / 1e9, 1)
                 if prof["ms_integrate_device"] > 0 else None,

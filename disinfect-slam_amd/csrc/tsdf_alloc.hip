@@ -13,24 +13,32 @@ namespace tsdf {
 // ---------------------------------------------------------------------------------------------
 // per-frame new-key set: open addressing on 64-bit packed keys, min candidate order per key
 // ---------------------------------------------------------------------------------------------
-__device__ void nk_insert(const EngineDev& D, uint64_t key, uint32_t order) {
+__device__ void keyset_insert(unsigned long long* keys, uint32_t* orders, int32_t* list,
+                              int32_t* count, uint32_t* status, uint64_t key, uint32_t order) {
   uint32_t h = (uint32_t)mix64(key) & (kNewKeyCap - 1);
   for (int p = 0; p < 256; ++p) {
-    unsigned long long cur = D.nk_key[h];
-    if (cur == 0ull) cur = atomicCAS(&D.nk_key[h], 0ull, (unsigned long long)key);
+    unsigned long long cur = keys[h];
+    if (cur == 0ull) cur = atomicCAS(&keys[h], 0ull, (unsigned long long)key);
     if (cur == 0ull) {
-      const int s = atomicAdd(&D.ctr->nk_count, 1);
-      D.nk_list[s] = (int32_t)h;
-      atomicMin(&D.nk_order[h], order);
+      const int s = atomicAdd(count, 1);
+      list[s] = (int32_t)h;
+      atomicMin(&orders[h], order);
       return;
     }
     if (cur == key) {
-      atomicMin(&D.nk_order[h], order);
+      atomicMin(&orders[h], order);
       return;
     }
     h = (h + 1) & (kNewKeyCap - 1);
   }
-  atomicOr(&D.ctr->status, 2u);  // TSDF_STATUS_NEWKEY_OVERFLOW
+  atomicOr(status, 2u);  // TSDF_STATUS_NEWKEY_OVERFLOW
+}
+__device__ void nk_insert(const EngineDev& D, uint64_t key, uint32_t order) {
+  keyset_insert(D.nk_key, D.nk_order, D.nk_list, &D.ctr->nk_count, &D.ctr->status, key, order);
+}
+// routed frames: a visible key another shard owns, kept once with its smallest candidate order
+__device__ void rt_insert(const EngineDev& D, uint64_t key, uint32_t order) {
+  keyset_insert(D.rt_key, D.rt_order, D.rt_list, &D.ctr->rt_count, &D.ctr->status, key, order);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -43,6 +51,9 @@ __device__ void nk_insert(const EngineDev& D, uint64_t key, uint32_t order) {
 //     an LDS hash set with their smallest candidate order (y*W + x)*maxs + i
 //  3. each unique key once: all-8-corners visibility (is_block_visible<true>), shard ownership,
 //     table probe; missing keys go to the global new-key set.
+// Steps 2-3 run only for tiles in [P.tile_lo, P.tile_hi) (a routed frame's pixel slice; every
+// tile otherwise). In a routed frame visible keys owned by another shard go to the route set
+// (k_route_pack sends them to their owner) instead of being dropped.
 // ---------------------------------------------------------------------------------------------
 constexpr int kTileSlots = 2048;  // > 256 pixels x maxs (<= 6, checked by tsdf_create)
 constexpr int kVisChunk = 1024;   // visibility sweep: 16 occupancy words x 64 entries per wave
@@ -184,7 +195,7 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
     D.pixA[i] = make_float4(d, range, w_new, __uint_as_float(c));
     D.pixB[i] = log2f(h) - log2f(l);  // base-2 log-odds of the pixel (k_integrate)
     TSDF_STAMP(D, 0, 2);
-    if (!(d == 0 || d > P.max_depth)) {
+    if (tile >= P.tile_lo && tile < P.tile_hi && !(d == 0 || d > P.max_depth)) {
       const f3 pcd = {pc.x * d, pc.y * d, pc.z * d};
       const f3 pw = se3_apply(P.wq, P.wt, pcd);
       const f3 dc = {pc.x / range, pc.y / range, pc.z / range};
@@ -228,6 +239,7 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
   }
   TSDF_STAMP(D, 0, 3);
   __syncthreads();
+  if (tile < P.tile_lo || tile >= P.tile_hi) return;  // pixel records only (workgroup-uniform)
   TSDF_STAMP(D, 0, 4);
   // Each wave sweeps its 64-slot strips; the few occupied slots of a strip (ballot) are tested
   // 8 at a time with 8 lanes per key, one block corner per lane (is_block_visible<true>), and the
@@ -269,12 +281,79 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
     int16_t kx, ky, kz;
     unpack_key(key, kx, ky, kz);
     if (P.shard_count > 1 &&
-        brick_owner(kx, ky, kz, (uint32_t)P.shard_count) != (uint32_t)P.shard_index)
+        brick_owner(kx, ky, kz, (uint32_t)P.shard_count) != (uint32_t)P.shard_index) {
+      if (P.route) rt_insert(D, key, s_ord[slot]);
       continue;
+    }
     if (find_entry(D.table, kx, ky, kz) >= 0) continue;
     nk_insert(D, key, s_ord[slot]);
   }
   TSDF_STAMP(D, 0, 5);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Routed frames (SURVEY.md 8e option 2). k_route_pack drains the route set into the outbox, one
+// slot of `cap` records per destination shard (record order within a slot is irrelevant: the
+// owner keeps the smallest candidate order per key); k_route_ingest merges an inbox -- slot s
+// holding what shard s sent here -- into this shard's new-key set after the same table probe
+// the local keys get. Keys, visibility and candidate orders are those of the unsharded DDA, so
+// a routed frame allocates exactly what the replicated-frame (option 1) shard would.
+// ---------------------------------------------------------------------------------------------
+constexpr int kMaxShards = 64;
+__global__ __launch_bounds__(1024) void k_route_pack(EngineDev D, RouteRec* __restrict__ out, int cap,
+                                                     int nshard) {
+  __shared__ int s_cnt[kMaxShards];
+  const int t = threadIdx.x;
+  if (t < nshard) s_cnt[t] = 0;
+  __syncthreads();
+  const int n = D.ctr->rt_count;
+  for (int i = t; i < n; i += blockDim.x) {
+    const int h = D.rt_list[i];
+    const unsigned long long key = D.rt_key[h];
+    const uint32_t ord = D.rt_order[h];
+    D.rt_key[h] = 0ull;  // the set starts empty next frame
+    D.rt_order[h] = 0xFFFFFFFFu;
+    int16_t x, y, z;
+    unpack_key(key, x, y, z);
+    const int o = (int)brick_owner(x, y, z, (uint32_t)nshard);
+    const int s = atomicAdd(&s_cnt[o], 1);
+    if (s < cap) {
+      RouteRec r;
+      r.x = x;
+      r.y = y;
+      r.z = z;
+      r.pad = 0;
+      r.order = ord;
+      r.zero = 0u;
+      out[(size_t)o * (cap + 1) + 1 + s] = r;
+    }
+  }
+  __syncthreads();
+  if (t < nshard) {
+    const int c = s_cnt[t];
+    RouteRec h{};
+    h.order = (uint32_t)min(c, cap);
+    out[(size_t)t * (cap + 1)] = h;
+    if (c > cap) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_ROUTE_OVERFLOW
+  }
+  if (t == 0) D.ctr->rt_count = 0;
+}
+
+// grid (ceil(cap / 256), nshard): workgroup row s reads the slot shard s sent
+__global__ __launch_bounds__(256) void k_route_ingest(EngineDev D, FrameParams P,
+                                                      const RouteRec* __restrict__ in, int cap) {
+  const int src = blockIdx.y;
+  const RouteRec* slot = in + (size_t)src * (cap + 1);
+  const int n = min((int)slot[0].order, cap);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const RouteRec r = slot[1 + i];
+  if (brick_owner(r.x, r.y, r.z, (uint32_t)P.shard_count) != (uint32_t)P.shard_index) {
+    atomicOr(&D.ctr->status, 32u);  // TSDF_STATUS_ROUTE_MISROUTED: inbox not from this layout
+    return;
+  }
+  if (find_entry(D.table, r.x, r.y, r.z) >= 0) return;
+  nk_insert(D, pack_key(r.x, r.y, r.z), r.order);
 }
 
 // test path: keys[n] in list order (one VoxelHashTable::Allocate launch, voxel_hash_test.cu)
@@ -492,7 +571,7 @@ __global__ __launch_bounds__(256) void k_fresh_init(EngineDev D) {
     const int b = q >> 7, v = (q & 127) * 4;
     uint8_t* blk = D.pool + (size_t)D.fresh[b] * kBlockBytes;
     *reinterpret_cast<float4*>(blk + v * 4) = make_float4(-1.f, -1.f, -1.f, -1.f);
-    *reinterpret_cast<float4*>(blk + kProbOffset + v * 4) = make_float4(.5f, .5f, .5f, .5f);
+    *reinterpret_cast<float4*>(blk + kProbOffset + v * 4) = make_float4(0.f, 0.f, 0.f, 0.f);  // p = 0.5
     uint4* cw = reinterpret_cast<uint4*>(blk + kRgbwOffset + v * 4);
     uint4 c = *cw;
     c.x &= 0x00FFFFFFu;

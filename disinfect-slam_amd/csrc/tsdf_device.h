@@ -6,9 +6,12 @@
 //              voxel_mem.cuh:73-93; NUM_BUCKET 2^21 x 2, voxel_hash.cuh:12-25).
 //   lock_tag : 2^21 u32 bucket locks, "locked" == current lock epoch (no per-launch reset pass;
 //              reference resets 8 MiB twice per frame, voxel_tsdf.cu:385,487).
-//   pool     : 2^bits voxel blocks x 6 KiB, block-major {f32 tsdf[512] | f32 prob[512] |
+//   pool     : 2^bits voxel blocks x 6 KiB, block-major {f32 tsdf[512] | f32 logodds[512] |
 //              u8x4 rgbw[512]} so one block's state is one contiguous 6 KiB run (reference: three
-//              SoA arrays of 2^27 voxels, voxel_mem.cu:13-27).
+//              SoA arrays of 2^27 voxels, voxel_mem.cu:13-27). The semantic state is kept as the
+//              base-2 log-odds L = log2(p / (1 - p)) of the reference's probability p
+//              (VoxelSEGM, voxel_types.cuh): its update is linear in L (see k_integrate), and
+//              every reader converts with prob_of_logodds (p = 0.5 <-> L = 0, p = 0 <-> L = -inf).
 //   occ      : 2^22-bit occupancy bitmap of the table (replaces the full 48 MiB table scans of
 //              check_visibility_kernel / check_valid_kernel with a 512 KiB bitmap sweep).
 //
@@ -33,7 +36,7 @@ constexpr uint32_t kNumEntry = kNumBucket * 2;
 constexpr uint32_t kEntryMask = kNumEntry - 1;
 constexpr uint32_t kOccWords = kNumEntry / 64;
 constexpr int kBlockBytes = kBlockVolume * 12;  // 6 KiB per voxel block
-constexpr int kProbOffset = kBlockVolume * 4;   // byte offsets inside a block record
+constexpr int kProbOffset = kBlockVolume * 4;   // byte offsets inside a block record (log-odds)
 constexpr int kRgbwOffset = kBlockVolume * 8;
 constexpr uint32_t kNewKeyCap = 1u << 17;       // unique new blocks per frame
 constexpr int kMaxDdaSamples = 6;               // DDA samples per pixel the ingest kernel supports
@@ -65,6 +68,16 @@ struct FrameParams {
   int W, H;
   int maxs;                  // DDA samples reserved per pixel in the candidate order space
   int shard_index, shard_count;
+  int tile_lo, tile_hi;      // pixel tiles whose DDA this engine runs (all of them unless routed)
+  int route;                 // 1: keys owned by other shards go to the route set (SURVEY 8e opt. 2)
+};
+
+// one routed candidate key (16 B); record 0 of each destination slot is a header whose `order`
+// holds the record count. Route buffer = shard_count slots x (cap + 1) records.
+struct alignas(16) RouteRec {
+  int16_t x, y, z, pad;
+  uint32_t order;
+  uint32_t zero;
 };
 
 // one visible block: snapshot of its hash entry (gather_visible_blocks_kernel copies entries)
@@ -92,11 +105,19 @@ struct DevCounters {
   unsigned long long total_deleted;
   unsigned long long frames;
   unsigned long long integrate_ticks;  // sum of k_integrate device durations (100 MHz clock)
+  int32_t rt_count;       // unique keys in the route set (routed frames)
+  int32_t rt_pad;
 };
 
 // ------------------------------------------------------------------------------------------
 // float math (bit-exact restatement; see header comment)
 // ------------------------------------------------------------------------------------------
+// VoxelSEGM::probability from the stored base-2 log-odds: 1 / (1 + 2^-L) on the raw v_exp /
+// v_rcp (~1 ulp each; exact at L = 0, 0 at L = -inf, 1 at large L)
+__device__ __forceinline__ float prob_of_logodds(float L) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-L));
+}
+
 __device__ __forceinline__ f3 cross3(f3 a, f3 b) {  // Eigen MatrixBase::cross
   f3 r;
   r.x = a.y * b.z - a.z * b.y;

@@ -1,6 +1,7 @@
 // tsdf_engine.hip -- host side of the MI355X TSDF engine: buffers, launch sequence and the C ABI
 // declared in include/disinfect_tsdf.h. No HIP type crosses the ABI.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <array>
@@ -125,6 +126,10 @@ struct tsdf_engine {
   std::vector<std::array<hipEvent_t, 5>> events;
   size_t ev_used = 0;
   unsigned long long prof_vis0 = 0, prof_upd0 = 0, prof_ticks0 = 0;
+  // routed frame between tsdf_integrate_route_begin and _end
+  bool route_pending = false;
+  FrameParams route_P{};
+  std::array<hipEvent_t, 5>* route_ev = nullptr;
 };
 
 namespace {
@@ -133,6 +138,7 @@ void free_all(tsdf_engine* e) {
   EngineDev& D = e->D;
   void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.occ,
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs, D.pkey,      D.fresh,
+                  D.rt_key,  D.rt_order, D.rt_list,
                   D.vis,     D.band,    D.cand,     D.wg_upd, D.wg_end, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
                   e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
@@ -177,6 +183,9 @@ FrameParams make_params(const tsdf_engine* e, const tsdf_intrinsics* K, int W, i
   P.maxs = e->maxs;
   P.shard_index = e->cfg.shard_index;
   P.shard_count = e->cfg.shard_count;
+  P.tile_lo = 0;
+  P.tile_hi = 1 << 30;
+  P.route = 0;
   return P;
 }
 
@@ -307,6 +316,11 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.nk_order, kNewKeyCap);
   ALLOC(D.nk_list, kNewKeyCap);
   ALLOC(D.pairs, kNewKeyCap);
+  if (cfg.shard_count > 1) {  // route set of routed frames
+    ALLOC(D.rt_key, kNewKeyCap);
+    ALLOC(D.rt_order, kNewKeyCap);
+    ALLOC(D.rt_list, kNewKeyCap);
+  }
   ALLOC(D.pkey, kNewKeyCap);
   ALLOC(D.fresh, kNewKeyCap);
   ALLOC(D.vis, (size_t)kBands * nb);
@@ -358,6 +372,10 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ok &= hipMemsetAsync(D.occ, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
   ok &= hipMemsetAsync(D.nk_key, 0, sizeof(unsigned long long) * kNewKeyCap, s) == hipSuccess;
   ok &= hipMemsetAsync(D.nk_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
+  if (D.rt_key) {
+    ok &= hipMemsetAsync(D.rt_key, 0, sizeof(unsigned long long) * kNewKeyCap, s) == hipSuccess;
+    ok &= hipMemsetAsync(D.rt_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
+  }
   ok &= hipMemsetAsync(D.band, 0, sizeof(int32_t) * kBands * kBandStride, s) == hipSuccess;
   ok &= hipMemsetAsync(D.visbits, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
   DevCounters c0{};
@@ -365,6 +383,8 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ok &= hipMemcpyAsync(D.ctr, &c0, sizeof(c0), hipMemcpyHostToDevice, s) == hipSuccess;
   hipLaunchKernelGGL(k_init_table, dim3(kNumEntry / 256), dim3(256), 0, s, D.table);
   hipLaunchKernelGGL(k_init_heap, dim3((nb + 255) / 256), dim3(256), 0, s, D.heap, nb);
+  hipLaunchKernelGGL(k_init_logodds, dim3((unsigned)(((size_t)nb * (kBlockVolume / 4) + 255) / 256)), dim3(256),
+                     0, s, D.pool, nb);
   ok &= hipGetLastError() == hipSuccess;
   ok &= hipStreamSynchronize(s) == hipSuccess;
   if (!ok) {
@@ -390,11 +410,18 @@ int tsdf_synchronize(tsdf_engine* e) {
   return TSDF_OK;
 }
 
-int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
-                   const tsdf_pose* pose, float max_depth) {
+namespace {
+
+// Phase 1 of a frame: stage host inputs, then k_ingest_dda (pixel records for the whole frame, the
+// DDA over tiles [tile_lo, tile_hi), visibility of the existing blocks). *P / *ev carry the frame
+// to frame_finish.
+int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, const tsdf_pose* pose,
+                 float max_depth, int slice_index, int slice_count, int route, FrameParams* P,
+                 std::array<hipEvent_t, 5>** ev_out) {
   if (!e || !f || !K || !pose || !f->depth || !f->rgb || f->width <= 0 || f->height <= 0 ||
       (int64_t)f->width * f->height > e->max_pixels || f->width > e->cfg.max_width ||
-      f->height > e->cfg.max_height || (f->ht == nullptr) != (f->lt == nullptr)) {
+      f->height > e->cfg.max_height || (f->ht == nullptr) != (f->lt == nullptr) ||
+      slice_count < 1 || slice_index < 0 || slice_index >= slice_count) {
     set_error("tsdf_integrate: invalid argument");
     return TSDF_ERR_INVALID_ARG;
   }
@@ -421,7 +448,14 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
     set_error("tsdf_integrate: bad mem_kind");
     return TSDF_ERR_INVALID_ARG;
   }
-  const FrameParams P = make_params(e, K, W, H, pose, max_depth);
+  *P = make_params(e, K, W, H, pose, max_depth);
+  const int tiles_x = (W + 15) / 16, tiles_y = (H + 15) / 16, tiles = tiles_x * tiles_y;
+  if (slice_count > 1) {  // contiguous bands of tile rows
+    const int rows = (tiles_y + slice_count - 1) / slice_count;
+    P->tile_lo = std::min(tiles_y, slice_index * rows) * tiles_x;
+    P->tile_hi = std::min(tiles_y, (slice_index + 1) * rows) * tiles_x;
+  }
+  P->route = route;
   std::array<hipEvent_t, 5>* ev = nullptr;
   if (e->profiling && (e->prof_calls++ % e->prof_every) == 0) {
     if (e->ev_used == e->events.size()) {
@@ -431,29 +465,95 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
     }
     ev = &e->events[e->ev_used++];
   }
-  const bool all_ev = ev && e->prof_mode == TSDF_PROFILE_PHASES;
-  if (all_ev) HIP_OK(hipEventRecord((*ev)[0], s));
+  *ev_out = ev;
+  if (ev && e->prof_mode == TSDF_PROFILE_PHASES) HIP_OK(hipEventRecord((*ev)[0], s));
   // ---- allocate (voxel_tsdf.cu:377-386) + visibility (:388-397) ----
   // k_ingest_dda sweeps the blocks that already exist for visibility beside the DDA; the
   // resolver inserts the new keys and appends the blocks it creates to the visible lists
-  const int tiles_x = (W + 15) / 16, tiles = tiles_x * ((H + 15) / 16);
-  hipLaunchKernelGGL(k_ingest_dda, dim3(kVisWorkgroups + tiles), dim3(256), 0, s, e->D, P, depth,
+  hipLaunchKernelGGL(k_ingest_dda, dim3(kVisWorkgroups + tiles), dim3(256), 0, s, e->D, *P, depth,
                      rgb, ht, lt, tiles_x, tiles);
   LAUNCH_OK("k_ingest_dda");
-  int rc = launch_resolve_alloc(e, P, (uint32_t)(np * e->maxs), 1);
+  return TSDF_OK;
+}
+
+// Phase 2: ordered allocation of the new keys -> fused update -> space carving.
+int frame_finish(tsdf_engine* e, const FrameParams& P, std::array<hipEvent_t, 5>* ev) {
+  hipStream_t s = e->stream;
+  const bool all_ev = ev && e->prof_mode == TSDF_PROFILE_PHASES;
+  int rc = launch_resolve_alloc(e, P, (uint32_t)((size_t)P.W * P.H * e->maxs), 1);
   if (rc) return rc;
   if (all_ev) HIP_OK(hipEventRecord((*ev)[1], s));
-  if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
   // ---- update (voxel_tsdf.cu:474-481) ----
-  hipLaunchKernelGGL(k_integrate, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s, e->D, P);
+  if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
+    // the two events are bound to the kernel's own dispatch packet (its begin / end timestamps,
+    // the interval rocprofv3's kernel trace reports): no marker packets enter the stream
+    hipExtLaunchKernelGGL(k_integrate, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
+                          (*ev)[2], (*ev)[3], 0, e->D, P);
+  } else {
+    if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
+    hipLaunchKernelGGL(k_integrate, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s, e->D, P);
+    if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
+  }
   LAUNCH_OK("k_integrate");
-  if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
   // ---- space carving (voxel_tsdf.cu:483-488) ----
   hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kResolveThreads), 0, s, e->D, e->D.cand,
                      &e->D.ctr->n_cand, 0);
   LAUNCH_OK("k_resolve_delete");
   if (all_ev) HIP_OK(hipEventRecord((*ev)[4], s));
   return TSDF_OK;
+}
+
+}  // namespace
+
+int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
+                   const tsdf_pose* pose, float max_depth) {
+  if (e && e->route_pending) {
+    set_error("tsdf_integrate: a routed frame is pending (tsdf_integrate_route_end)");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  FrameParams P;
+  std::array<hipEvent_t, 5>* ev = nullptr;
+  int rc = frame_ingest(e, f, K, pose, max_depth, 0, 1, 0, &P, &ev);
+  if (rc) return rc;
+  return frame_finish(e, P, ev);
+}
+
+int64_t tsdf_route_buffer_bytes(int32_t shard_count, int32_t route_cap) {
+  if (shard_count < 1 || route_cap < 1) return 0;
+  return (int64_t)shard_count * (route_cap + 1) * (int64_t)sizeof(RouteRec);
+}
+
+int tsdf_integrate_route_begin(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
+                               const tsdf_pose* pose, float max_depth, int32_t slice_index,
+                               int32_t slice_count, void* outbox, int32_t route_cap) {
+  if (!e || e->cfg.shard_count < 2 || e->route_pending || !outbox || route_cap < 1) {
+    set_error("tsdf_integrate_route_begin: invalid argument");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  FrameParams P;
+  std::array<hipEvent_t, 5>* ev = nullptr;
+  int rc = frame_ingest(e, f, K, pose, max_depth, slice_index, slice_count, 1, &P, &ev);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_route_pack, dim3(1), dim3(1024), 0, e->stream, e->D,
+                     reinterpret_cast<RouteRec*>(outbox), route_cap, e->cfg.shard_count);
+  LAUNCH_OK("k_route_pack");
+  e->route_P = P;
+  e->route_ev = ev;
+  e->route_pending = true;
+  return TSDF_OK;
+}
+
+int tsdf_integrate_route_end(tsdf_engine* e, const void* inbox, int32_t route_cap) {
+  if (!e || !e->route_pending || !inbox || route_cap < 1) {
+    set_error("tsdf_integrate_route_end: invalid argument");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  e->route_pending = false;
+  hipLaunchKernelGGL(k_route_ingest, dim3((route_cap + 255) / 256, e->cfg.shard_count), dim3(256), 0,
+                     e->stream, e->D, e->route_P, reinterpret_cast<const RouteRec*>(inbox), route_cap);
+  LAUNCH_OK("k_route_ingest");
+  return frame_finish(e, e->route_P, e->route_ev);
 }
 
 int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const tsdf_pose* pose,
@@ -608,7 +708,8 @@ int tsdf_get_stats(tsdf_engine* e, tsdf_stats* o, int clear_status) {
 }
 
 int tsdf_profile_begin(tsdf_engine* e, int mode, int every) {
-  if (!e || (mode != TSDF_PROFILE_PHASES && mode != TSDF_PROFILE_INTEGRATE) || every < 1)
+  if (!e || (mode != TSDF_PROFILE_PHASES && mode != TSDF_PROFILE_INTEGRATE &&
+             mode != TSDF_PROFILE_KERNEL) || every < 1)
     return TSDF_ERR_INVALID_ARG;
   e->prof_mode = mode;
   e->prof_every = every;

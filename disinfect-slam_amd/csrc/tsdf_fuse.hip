@@ -27,7 +27,7 @@ __device__ __forceinline__ void setu(uint4& v, int j, uint32_t f) {
   if (j == 0) v.x = f; else if (j == 1) v.y = f; else if (j == 2) v.z = f; else v.w = f;
 }
 
-__global__ __launch_bounds__(kIntegrateThreads) void k_integrate(EngineDev D, FrameParams P) {
+__global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_integrate(EngineDev D, FrameParams P) {
   __shared__ float s_min[4];
   __shared__ int s_upd[4];
   const int lane = lane_id();
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(kIntegrateThreads) void k_integrate(EngineDev D, Fr
       fresh = r.pad != 0;
       if (fresh) {
         ts = make_float4(-1.f, -1.f, -1.f, -1.f);
-        pr = make_float4(.5f, .5f, .5f, .5f);
+        pr = make_float4(0.f, 0.f, 0.f, 0.f);  // log-odds of AquireBlock's p = 0.5
         cw.x &= 0x00FFFFFFu;
         cw.y &= 0x00FFFFFFu;
         cw.z &= 0x00FFFFFFu;
@@ -180,18 +180,13 @@ __global__ __launch_bounds__(kIntegrateThreads) void k_integrate(EngineDev D, Fr
           const v2f wr = wc + v2(0x1.fffffep-2f, 0x1.fffffep-2f);
           c0 |= weight_round_cap(wr.x, 40u) << 24;
           c1 |= weight_round_cap(wr.y, 40u) << 24;
-          // semantic log-odds fusion (voxel_tsdf.cu:196-202) as a logistic in base 2:
-          //   P / (P + N) with P = exp((w_old ln p + w_new ln ht) / wc), N likewise with 1 - p, lt
-          //   = 1 / (1 + 2^-x),  x = (w_old log2(p / (1 - p)) + w_new log2(ht / lt)) / wc
-          // (pixB holds log2 ht - log2 lt); raw v_log / v_exp / v_rcp are ~1 ulp each against the
-          // 1e-4 probability tolerance, and p stays exactly 0.5 when ht == lt (x == 0).
-          const v2f p = v2(comp(pr, j0), comp(pr, j1));
-          const v2f q = 1.0f - p;
-          const v2f odds = p * v2(__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y));
-          const v2f lo = v2(__builtin_amdgcn_logf(odds.x), __builtin_amdgcn_logf(odds.y));
-          const v2f x = (w_old * lo + w_new * v2(lg[j0], lg[j1])) * iwc;
-          const v2f den = 1.0f + v2(__builtin_amdgcn_exp2f(-x.x), __builtin_amdgcn_exp2f(-x.y));
-          const v2f pn = v2(__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y));
+          // semantic fusion (voxel_tsdf.cu:196-202): p' = P / (P + N) with
+          //   P = exp((w_old ln p + w_new ln ht) / wc), N = exp((w_old ln(1 - p) + w_new ln lt) / wc)
+          // is exactly the logistic of  L' = (w_old L + w_new log2(ht / lt)) / wc  in the base-2
+          // log-odds L = log2(p / (1 - p)) the pool stores (pixB holds log2 ht - log2 lt), so the
+          // update is two products and a sum; readers convert with prob_of_logodds (within 1e-4
+          // of the reference's float chain, and L stays exactly 0 -- p 0.5 -- when ht == lt)
+          const v2f pn = (w_old * v2(comp(pr, j0), comp(pr, j1)) + w_new * v2(lg[j0], lg[j1])) * iwc;
           if (a0) {
             setc(ts, j0, tq.x);
             setc(pr, j0, pn.x);

@@ -41,6 +41,10 @@ struct EngineDev {
   unsigned long long* pairs;    // kNewKeyCap (order << 32 | slot) resolver scratch
   unsigned long long* pkey;     // kNewKeyCap packed key of pairs[i] (one load in the rounds)
   int32_t* fresh;               // pool indices acquired by the hash-level test path
+  // routed frames (shard_count > 1): visible keys other shards own, min candidate order per key
+  unsigned long long* rt_key;   // kNewKeyCap
+  uint32_t* rt_order;           // kNewKeyCap
+  int32_t* rt_list;             // kNewKeyCap
   // visibility / carving
   VisRec* vis;                  // kBands x nblocks visible blocks (band-major, any order within)
   int32_t* band;                // kBands x kBandStride: record count of each band list
@@ -58,6 +62,7 @@ struct EngineDev {
 
 __global__ void k_init_table(int4* table);
 __global__ void k_init_heap(int32_t* heap, int n);
+__global__ void k_init_logodds(uint8_t* pool, int nb);
 // per frame (4 launches)
 constexpr int kVisWorkgroups = kOccWords / 256;  // visibility-sweep workgroups of k_ingest_dda
 __global__ void k_ingest_dda(EngineDev D, FrameParams P, const float* depth, const uint8_t* rgb,
@@ -68,6 +73,9 @@ __global__ void k_resolve_delete(EngineDev D, const VisRec* recs, const int32_t*
                                  int direct);
 // hash-level test path
 __global__ void k_keys_to_newset(EngineDev D, const int16_t* keys, int n);
+// routed frames (SURVEY 8e option 2)
+__global__ void k_route_pack(EngineDev D, RouteRec* out, int cap, int nshard);
+__global__ void k_route_ingest(EngineDev D, FrameParams P, const RouteRec* in, int cap);
 __global__ void k_fresh_init(EngineDev D);
 // extraction
 struct MeshParams {

@@ -19,7 +19,8 @@ import numpy as np
 
 from . import _lib
 from ._lib import (STATUS_DDA_OVERFLOW, STATUS_NEWKEY_OVERFLOW, STATUS_POOL_EXHAUSTED,
-                   TSDF_MEM_DEVICE, TSDF_MEM_HOST, TSDFError)
+                   STATUS_ROUTE_MISROUTED, STATUS_ROUTE_OVERFLOW, TSDF_MEM_DEVICE, TSDF_MEM_HOST,
+                   TSDFError)
 
 NUM_ENTRY = 1 << 22
 NUM_BUCKET = 1 << 21
@@ -195,6 +196,8 @@ class Engine:
         self.truncation = truncation
         self.num_blocks = int(L.tsdf_num_blocks(h))
         self.device = device
+        self.shard_index = shard_index
+        self.shard_count = shard_count
 
     def close(self):
         if getattr(self, "_h", None):
@@ -214,6 +217,53 @@ class Engine:
         self.close()
 
     # ---- hot path ----
+    def _frame(self, rgb, depth, ht, lt):
+        dev = _is_torch_cuda(depth)
+        if dev:
+            H, W = int(depth.shape[0]), int(depth.shape[1])
+            for a in (rgb, depth, ht, lt):
+                if a is not None and not a.is_contiguous():
+                    raise ValueError("device frames must be contiguous")
+        else:
+            rgb = _np(rgb, np.uint8)
+            depth = _np(depth, np.float32)
+            ht = _np(ht, np.float32)
+            lt = _np(lt, np.float32)
+            H, W = depth.shape
+        if tuple(rgb.shape[:2]) != (H, W):
+            raise ValueError("rgb / depth size mismatch (voxel_tsdf.cu:352-353)")
+        # the arrays stay referenced by the caller for the duration of the call
+        return _lib.Frame(W, H, _ptr(rgb), _ptr(depth), _ptr(ht), _ptr(lt),
+                          TSDF_MEM_DEVICE if dev else TSDF_MEM_HOST), (rgb, depth, ht, lt)
+
+    @staticmethod
+    def route_buffer_bytes(shard_count: int, route_cap: int) -> int:
+        """Bytes of one routed-frame outbox / inbox (shard_count slots of route_cap + 1 records)."""
+        return int(_lib.load().tsdf_route_buffer_bytes(shard_count, route_cap))
+
+    def integrate_route_begin(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float,
+                              slice_index: int, slice_count: int, outbox, route_cap: int):
+        """Routed frame, phase 1 (SURVEY 8e option 2): DDA over this slice of pixel-tile rows; keys
+        other shards own are written to `outbox` (device tensor of route_buffer_bytes)."""
+        if not _is_torch_cuda(outbox) or outbox.numel() * outbox.element_size() < \
+                self.route_buffer_bytes(self.shard_count, route_cap):
+            raise ValueError("outbox must be a device tensor of route_buffer_bytes(shard_count, route_cap)")
+        fr, keep = self._frame(rgb, depth, ht, lt)
+        Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        _lib.check(_lib.load().tsdf_integrate_route_begin(self._h, C.byref(fr), C.byref(Kc),
+                                                          C.byref(cam_T_world._c()), max_depth,
+                                                          slice_index, slice_count, _ptr(outbox),
+                                                          route_cap), "tsdf_integrate_route_begin")
+        del keep
+
+    def integrate_route_end(self, inbox, route_cap: int):
+        """Routed frame, phase 2: merge the exchanged keys and finish the frame."""
+        if not _is_torch_cuda(inbox) or inbox.numel() * inbox.element_size() < \
+                self.route_buffer_bytes(self.shard_count, route_cap):
+            raise ValueError("inbox must be a device tensor of route_buffer_bytes(shard_count, route_cap)")
+        _lib.check(_lib.load().tsdf_integrate_route_end(self._h, _ptr(inbox), route_cap),
+                   "tsdf_integrate_route_end")
+
     def integrate(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float):
         dev = _is_torch_cuda(depth)
         if dev:
@@ -292,11 +342,12 @@ class Engine:
         _lib.check(_lib.load().tsdf_get_stats(self._h, C.byref(s), int(clear_status)), "tsdf_get_stats")
         return {k: getattr(s, k) for k, _ in _lib.Stats._fields_}
 
-    def profile_begin(self, integrate_only: bool = False, every: int = 1):
-        """HIP-event timing of every `every`-th following integrate call (all phases, or only
-        k_integrate)."""
-        _lib.check(_lib.load().tsdf_profile_begin(self._h, 1 if integrate_only else 0, every),
-                   "tsdf_profile_begin")
+    def profile_begin(self, integrate_only: bool = False, every: int = 1, kernel_events: bool = False):
+        """HIP-event timing of every `every`-th following integrate call: all phases (marker
+        events between them), only k_integrate (marker events around it), or -- kernel_events --
+        k_integrate's own dispatch timestamps (start/stop events bound to the launch)."""
+        mode = 2 if kernel_events else (1 if integrate_only else 0)
+        _lib.check(_lib.load().tsdf_profile_begin(self._h, mode, every), "tsdf_profile_begin")
 
     def profile_end(self) -> dict:
         p = _lib.Profile()

@@ -18,6 +18,9 @@ TSDF_MEM_DEVICE = 1
 STATUS_POOL_EXHAUSTED = 1
 STATUS_NEWKEY_OVERFLOW = 2
 STATUS_DDA_OVERFLOW = 4
+STATUS_RESOLVE_ABORT = 8
+STATUS_ROUTE_OVERFLOW = 16
+STATUS_ROUTE_MISROUTED = 32
 
 
 class Config(C.Structure):
@@ -93,6 +96,7 @@ EXPORTS = [
     "tsdf_hash_delete", "tsdf_hash_retrieve", "tsdf_hash_assign", "tsdf_num_active_blocks",
     "tsdf_pool_acquire", "tsdf_pool_release", "tsdf_pool_set_weight", "tsdf_pool_get_weights",
     "tsdf_hash_block", "tsdf_block_owner", "tsdf_error_string", "tsdf_last_error",
+    "tsdf_route_buffer_bytes", "tsdf_integrate_route_begin", "tsdf_integrate_route_end",
 ]
 
 _lib = None
@@ -115,6 +119,11 @@ def load(path: str | None = None):
     L.tsdf_destroy.argtypes = [P]
     L.tsdf_integrate.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f]
     L.tsdf_raycast.argtypes = [P, C.POINTER(Intrinsics), i, i, C.POINTER(Pose), f, P, P, i]
+    L.tsdf_route_buffer_bytes.restype = C.c_int64
+    L.tsdf_route_buffer_bytes.argtypes = [C.c_int32, C.c_int32]
+    L.tsdf_integrate_route_begin.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f,
+                                             C.c_int32, C.c_int32, P, C.c_int32]
+    L.tsdf_integrate_route_end.argtypes = [P, P, C.c_int32]
     L.tsdf_query.argtypes = [P, P, P, i64, C.POINTER(i64)]
     L.tsdf_extract_mesh.argtypes = [P, P, f, i, P, i64, C.POINTER(i64), i]
     L.tsdf_get_stats.argtypes = [P, C.POINTER(Stats), i]
@@ -145,6 +154,7 @@ def load(path: str | None = None):
     L.tsdf_last_error.restype = C.c_char_p
     L.tsdf_last_error.argtypes = []
     for name in ("tsdf_create", "tsdf_destroy", "tsdf_integrate", "tsdf_raycast", "tsdf_query",
+                 "tsdf_integrate_route_begin", "tsdf_integrate_route_end",
                  "tsdf_extract_mesh",
                  "tsdf_get_stats", "tsdf_synchronize", "tsdf_profile_begin", "tsdf_profile_end",
                  "tsdf_debug_dump", "tsdf_debug_stamps", "tsdf_hash_allocate", "tsdf_hash_delete",

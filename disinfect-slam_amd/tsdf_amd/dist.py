@@ -1,9 +1,13 @@
-"""Multi-GPU plumbing of the TSDF engine: one process per GPU (torch.distributed.run), no data-path
-collective.
+"""Multi-GPU plumbing of the TSDF engine: one process per GPU (torch.distributed.run).
 
- - streams mode (weak scaling): rank r integrates its own camera stream into its own volume;
- - sharded mode (strong scaling): every rank sees the same frames and owns the blocks whose 4^3
-   brick hashes to it (tsdf_block_owner); a whole-volume Query is the union of the shards.
+ - streams mode (weak scaling): rank r integrates its own camera stream into its own volume; no
+   data-path collective;
+ - sharded mode (strong scaling, SURVEY 8e option 1): every rank sees the same frames, runs the
+   whole DDA and owns the blocks whose 4^3 brick hashes to it (tsdf_block_owner); no data-path
+   collective; a whole-volume Query is the union of the shards;
+ - routed mode (strong scaling, SURVEY 8e option 2): same ownership, but rank r runs the DDA only
+   over its slice of pixel-tile rows and routes the keys other ranks own with one all-to-all per
+   frame (route_exchange: RCCL over xGMI on the GPU box).
 
 The functions here are backend-agnostic (RCCL "nccl" on the GPU box, "gloo" in the CPU tests).
 """
@@ -20,7 +24,21 @@ def env_rank_world():
 
 def shard_of(mode: str, rank: int, world: int):
     """(shard_index, shard_count) of this rank's engine."""
-    return (rank, world) if (mode == "sharded" and world > 1) else (0, 1)
+    return (rank, world) if (mode in ("sharded", "routed") and world > 1) else (0, 1)
+
+
+def route_exchange(outbox, inbox):
+    """Routed frames: inbox slot s <- rank s's outbox slot <this rank> (all-to-all, equal splits).
+
+    outbox / inbox: contiguous (world, slot_bytes) tensors (tsdf_route_buffer_bytes in all). On the
+    GPU box this is one RCCL all-to-all ordered on the current stream (the engine's stream), so the
+    frame stays asynchronous; without a process group it is the identity (one shard)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        inbox.copy_(outbox)
+        return inbox
+    dist.all_to_all_single(inbox, outbox)
+    return inbox
 
 
 def stream_offset(mode: str, rank: int, world: int, stride: int = 240) -> int:

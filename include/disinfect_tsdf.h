@@ -36,6 +36,8 @@ extern "C" {
 #define TSDF_STATUS_NEWKEY_OVERFLOW 2u /* more new blocks in one frame than the key set holds */
 #define TSDF_STATUS_DDA_OVERFLOW 4u    /* a DDA ray took more samples than sized for */
 #define TSDF_STATUS_RESOLVE_ABORT 8u   /* allocation resolver made no progress (internal error) */
+#define TSDF_STATUS_ROUTE_OVERFLOW 16u /* a routed frame had more keys for one shard than route_cap */
+#define TSDF_STATUS_ROUTE_MISROUTED 32u /* an inbox record belongs to another shard */
 
 typedef struct tsdf_engine tsdf_engine;
 
@@ -118,6 +120,27 @@ int tsdf_destroy(tsdf_engine* e);
 int tsdf_integrate(tsdf_engine* e, const tsdf_frame* frame, const tsdf_intrinsics* K,
                    const tsdf_pose* cam_T_world, float max_depth);
 
+/* Routed frames (SURVEY.md 8e option 2, shard_count > 1): TSDFGrid::Integrate split across the
+ * shards of one volume. Every shard gets the whole frame (its pixel records feed the update) but
+ * runs the block-allocation DDA (block_allocate_kernel, voxel_tsdf.cu:104-147) only over its slice
+ * of pixel-tile rows; visible keys another shard owns are routed to it:
+ *   1. tsdf_integrate_route_begin: DDA over slice `slice_index` of `slice_count`, then writes the
+ *      outbox -- device memory of tsdf_route_buffer_bytes(shard_count, route_cap) bytes: one slot
+ *      of (route_cap + 1) 16-B records per destination shard (record 0 = count header).
+ *   2. the caller exchanges the buffers (an all-to-all with equal splits, e.g. RCCL over xGMI):
+ *      inbox slot s = what shard s's outbox holds in slot <this shard>. The exchange must be
+ *      ordered after begin and before end on the engine stream (or synchronised around).
+ *   3. tsdf_integrate_route_end: merges the inbox and finishes the frame (ordered allocation,
+ *      update, carving).
+ * Keys, candidate orders and allocation outcomes equal the replicated-frame sharded integrate
+ * (tsdf_integrate on the same shard engine). More than route_cap keys for one destination sets
+ * TSDF_STATUS_ROUTE_OVERFLOW (the excess is dropped). No other engine call may come between. */
+int64_t tsdf_route_buffer_bytes(int32_t shard_count, int32_t route_cap);
+int tsdf_integrate_route_begin(tsdf_engine* e, const tsdf_frame* frame, const tsdf_intrinsics* K,
+                               const tsdf_pose* cam_T_world, float max_depth, int32_t slice_index,
+                               int32_t slice_count, void* outbox, int32_t route_cap);
+int tsdf_integrate_route_end(tsdf_engine* e, const void* inbox, int32_t route_cap);
+
 /* TSDFGrid::RayCast (voxel_tsdf.cu:490-506; ray_cast_kernel :232-307). rgba / normal are
  * height x width x 4 u8 (either may be NULL), host or device memory per mem_kind. */
 int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int width, int height,
@@ -151,6 +174,10 @@ int tsdf_synchronize(tsdf_engine* e);
  * event is a queue marker that costs the stream ~3 us, so a timed loop samples. */
 #define TSDF_PROFILE_PHASES 0
 #define TSDF_PROFILE_INTEGRATE 1
+/* TSDF_PROFILE_KERNEL: ms_integrate from two events bound to the k_integrate dispatch itself
+ * (hipExtLaunchKernel start/stop events = the kernel's begin/end timestamps, as a kernel trace
+ * reports them); adds nothing to the stream, so `every` = 1 times every launch. */
+#define TSDF_PROFILE_KERNEL 2
 int tsdf_profile_begin(tsdf_engine* e, int mode, int every);
 int tsdf_profile_end(tsdf_engine* e, tsdf_profile* out);
 

@@ -1,7 +1,7 @@
 """Multi-rank (world_size 2, gloo, CPU) coverage of the N>1 path.
 
  - the bench's rank bookkeeping (tsdf_amd.dist): max-over-ranks timing, whole-job units, stream
-   offsets, shard assignment;
+   offsets, shard assignment, and the routed-frame key exchange (all-to-all of the outboxes);
  - spatial sharding semantics on the CPU oracle: two shard engines fed the same frames own
    disjoint block sets, each block lives on its owner, and the union equals the unsharded volume
    with bit-identical voxels (integration of a block reads only its own state + the frame).
@@ -57,6 +57,15 @@ def _worker(rank, world, port):
         assert tdist.units("sharded", 300, world) == 300
         assert tdist.shard_of("sharded", rank, world) == (rank, world)
         assert tdist.shard_of("streams", rank, world) == (0, 1)
+        assert tdist.units("routed", 300, world) == 300
+        assert tdist.shard_of("routed", rank, world) == (rank, world)
+        # routed frames' key exchange (bench --mode routed): inbox slot s = rank s's outbox slot rank
+        import torch
+        slot = 48
+        out = torch.stack([torch.full((slot,), rank * world + j, dtype=torch.uint8) for j in range(world)])
+        inbox = tdist.route_exchange(out, torch.empty_like(out))
+        for src in range(world):
+            assert bool((inbox[src] == src * world + rank).all()), (rank, src, inbox[src][:4])
         offs = [None] * world
         dist.all_gather_object(offs, tdist.stream_offset("streams", rank, world))
         assert len(set(offs)) == world

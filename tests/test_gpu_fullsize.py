@@ -1,0 +1,114 @@
+"""Parity at BASELINE.json's full frame sizes (SURVEY.md 8d "parity gate ... a digest check at full
+size"): C3 640x480 depth + ht/lt, C2 640x480 depth-only and C4 1280x720 (L515 intrinsics) against
+the CPU oracle frame by frame, and the bench workload itself (the GPU-rendered 640x480 stream, 2^18
+block pool, warmup + timed frames) through size-independent properties: the hash table / free
+stack stay a consistent structure, every block is reachable from its bucket, voxel values stay in
+range, and two engines fed the same stream end bit-identical.
+"""
+import numpy as np
+import pytest
+
+from test_gpu_parity import compare, np_hash, run_sequence
+
+pytestmark = pytest.mark.gpu
+
+ENTRY_MASK = (1 << 22) - 1
+
+
+def test_c3_640x480_semantic_parity():
+    """BASELINE configs[2]: the bench's frame shape, oracle-exact over the first frames."""
+    eng, ora, cam = run_sequence(640, 480, 0.005, 0.03, 5, nb_bits=16, check_every=5)
+    st = eng.stats()
+    assert st["active_blocks"] > 3000 and st["last_num_updated"] > 500000
+    eng.close(), ora.close()
+
+
+def test_c2_640x480_depth_only_parity():
+    """BASELINE configs[1]: ht = lt = NULL."""
+    eng, ora, cam = run_sequence(640, 480, 0.005, 0.03, 3, nb_bits=16, semantic=False, check_every=3,
+                                 start=40)
+    eng.close(), ora.close()
+
+
+def test_c4_1280x720_l515_parity():
+    """BASELINE configs[3] frame shape (1280x720, L515 full-resolution intrinsics), one GPU."""
+    from tsdf_amd import synth
+    eng, ora, cam = run_sequence(1280, 720, 0.005, 0.03, 3, nb_bits=16, check_every=3,
+                                 intrinsics=synth.L515_FULL, start=7)
+    assert eng.stats()["last_num_updated"] > 1000000
+    eng.close(), ora.close()
+
+
+def check_structure(d, nb):
+    """The hash table + free stack invariants VoxelHashTable / VoxelMemPool maintain
+    (voxel_hash.cu:58-171, voxel_mem.cu:37-61)."""
+    pos, idx, heap, free = d["entry_pos"], d["entry_idx"], d["heap"], d["free"]
+    live = np.flatnonzero(idx >= 0)
+    assert live.size == nb - free
+    # pool indices: live blocks and the free stack partition [0, nb)
+    owned = np.concatenate([idx[live], heap[:free]])
+    assert np.array_equal(np.sort(owned), np.arange(nb, dtype=owned.dtype))
+    # keys are unique
+    keys = pos[live, :3].astype(np.int64)
+    packed = ((keys[:, 0] & 0xFFFF) << 32) | ((keys[:, 1] & 0xFFFF) << 16) | (keys[:, 2] & 0xFFFF)
+    assert np.unique(packed).size == live.size
+    # every live entry is its bucket's slot 0 or on the chain hanging off the bucket's slot 1
+    A = np_hash(keys).astype(np.int64)
+    found = live == 2 * A
+    cur = 2 * A + 1
+    found |= cur == live
+    for _ in range(256):
+        off = pos[cur, 3].astype(np.int64)
+        step = ~found & (off != 0)
+        if not step.any():
+            break
+        cur = np.where(step, (cur + off) & ENTRY_MASK, cur)
+        found |= step & (cur == live)
+    assert found.all(), f"{(~found).sum()} live entries unreachable from their bucket"
+    # empty entries carry no chain link unless they are a bucket's (possibly empty) head
+    return live
+
+
+def test_bench_stream_full_size_invariants_and_determinism():
+    """The bench workload at full size (GPU-rendered 640x480 orbit, 2^18 pool, 130 frames):
+    structure invariants + value ranges, and two engines end bit-identical (a digest of the full
+    state, since the oracle would need minutes for this many frames)."""
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    cam = synth.camera(640, 480, synth.TUM_FR1)
+    n = 130
+    frames = synth.render_torch(cam, list(range(n)), device="cuda")
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    dumps = []
+    for rep in range(2):
+        eng = tsdf_amd.Engine(0.005, 0.03, max_width=640, max_height=480, num_block_bits=18)
+        try:
+            for i in range(n):
+                eng.integrate(frames["rgb"][i], frames["depth"][i], frames["ht"][i], frames["lt"][i], K,
+                              tsdf_amd.SE3(frames["q"][i], frames["t"][i]), 4.0)
+            torch.cuda.synchronize()
+            st = eng.stats()
+            assert st["status"] == 0, st
+            assert st["total_alloc"] - st["total_deleted"] == st["active_blocks"] > 10000
+            dumps.append(eng.dump())
+        finally:
+            eng.close()
+    a, b = dumps
+    live = check_structure(a, 1 << 18)
+    for k in ("entry_pos", "entry_idx", "heap"):
+        assert np.array_equal(a[k], b[k]), k
+    assert a["free"] == b["free"]
+    pidx = a["entry_idx"][live]
+    ts = a["tsdf"].reshape(-1, 512)[pidx]
+    pr = a["prob"].reshape(-1, 512)[pidx]
+    cw = a["rgbw"].reshape(-1, 512, 4)[pidx]
+    assert np.isfinite(ts).all() and (ts >= -1).all() and (ts <= 1).all()
+    assert np.isfinite(pr).all() and (pr > 0).all() and (pr < 1).all()
+    assert cw[..., 3].max() <= 40
+    assert (cw[..., 3] > 0).mean() > 0.05
+    for k in ("tsdf", "prob"):
+        assert np.array_equal(a[k].reshape(-1, 512)[pidx].view(np.uint32),
+                              b[k].reshape(-1, 512)[pidx].view(np.uint32)), k
+    assert np.array_equal(cw, b["rgbw"].reshape(-1, 512, 4)[pidx])
