@@ -130,6 +130,14 @@ struct tsdf_engine {
   bool route_pending = false;
   FrameParams route_P{};
   std::array<hipEvent_t, 5>* route_ev = nullptr;
+  // feed_rgbd_frame staging: raw full-size inputs (host frames) and the half-size outputs
+  uint8_t* fe_rgb = nullptr;
+  uint16_t* fe_depth = nullptr;
+  uint8_t* fe_mask = nullptr;
+  int64_t fe_in_cap = 0;  // pixels
+  uint8_t* fe_out_rgb = nullptr;
+  float* fe_out_depth = nullptr;
+  int64_t fe_out_cap = 0;
 };
 
 namespace {
@@ -139,6 +147,7 @@ void free_all(tsdf_engine* e) {
   void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.occ,
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs, D.pkey,      D.fresh,
                   D.rt_key,  D.rt_order, D.rt_list,
+                  e->fe_rgb, e->fe_depth, e->fe_mask, e->fe_out_rgb, e->fe_out_depth,
                   D.vis,     D.band,    D.cand,     D.wg_upd, D.wg_end, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
                   e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
@@ -554,6 +563,110 @@ int tsdf_integrate_route_end(tsdf_engine* e, const void* inbox, int32_t route_ca
                      e->stream, e->D, e->route_P, reinterpret_cast<const RouteRec*>(inbox), route_cap);
   LAUNCH_OK("k_route_ingest");
   return frame_finish(e, e->route_P, e->route_ev);
+}
+
+namespace {
+
+// cv::resize x0.5 + convertTo + mask (k_rgbd_half) of a W x H frame into device rgb_out / depth_out
+int rgbd_half(tsdf_engine* e, const uint8_t* rgb, const uint16_t* depth, const uint8_t* mask, int W,
+              int H, float depth_factor, uint8_t* rgb_out, float* depth_out, int mem_kind) {
+  hipStream_t s = e->stream;
+  const size_t np = (size_t)W * H;
+  if (mem_kind == TSDF_MEM_HOST) {
+    if ((int64_t)np > e->fe_in_cap) {
+      (void)hipFree(e->fe_rgb);
+      (void)hipFree(e->fe_depth);
+      (void)hipFree(e->fe_mask);
+      e->fe_rgb = nullptr;
+      e->fe_depth = nullptr;
+      e->fe_mask = nullptr;
+      e->fe_in_cap = 0;
+      HIP_OK(dmalloc(&e->fe_rgb, np * 3));
+      HIP_OK(dmalloc(&e->fe_depth, np));
+      HIP_OK(dmalloc(&e->fe_mask, np));
+      e->fe_in_cap = (int64_t)np;
+    }
+    HIP_OK(hipMemcpyAsync(e->fe_rgb, rgb, np * 3, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(e->fe_depth, depth, np * 2, hipMemcpyHostToDevice, s));
+    if (mask) HIP_OK(hipMemcpyAsync(e->fe_mask, mask, np, hipMemcpyHostToDevice, s));
+    rgb = e->fe_rgb;
+    depth = e->fe_depth;
+    mask = mask ? e->fe_mask : nullptr;
+  }
+  const float alpha = (float)(1. / (double)depth_factor);  // convertTo(CV_32FC1, 1. / factor)
+  const int w = W / 2, h = H / 2;
+  hipLaunchKernelGGL(k_rgbd_half, dim3((w + 63) / 64, (h + 3) / 4), dim3(256), 0, s, rgb, depth, mask,
+                     W, H, alpha, rgb_out, depth_out);
+  LAUNCH_OK("k_rgbd_half");
+  return TSDF_OK;
+}
+
+bool rgbd_args_ok(const uint8_t* rgb, const uint16_t* depth, int W, int H, float depth_factor,
+                  int mem_kind) {
+  return rgb && depth && W >= 2 && H >= 2 && W % 2 == 0 && H % 2 == 0 && depth_factor > 0.0f &&
+         (mem_kind == TSDF_MEM_HOST || mem_kind == TSDF_MEM_DEVICE);
+}
+
+int ensure_fe_out(tsdf_engine* e, int64_t npix) {
+  if (npix <= e->fe_out_cap) return TSDF_OK;
+  (void)hipFree(e->fe_out_rgb);
+  (void)hipFree(e->fe_out_depth);
+  e->fe_out_rgb = nullptr;
+  e->fe_out_depth = nullptr;
+  e->fe_out_cap = 0;
+  HIP_OK(dmalloc(&e->fe_out_rgb, (size_t)npix * 3));
+  HIP_OK(dmalloc(&e->fe_out_depth, (size_t)npix));
+  e->fe_out_cap = npix;
+  return TSDF_OK;
+}
+
+}  // namespace
+
+int tsdf_rgbd_half(tsdf_engine* e, const uint8_t* rgb, const uint16_t* depth, const uint8_t* mask,
+                   int width, int height, float depth_factor, uint8_t* rgb_out, float* depth_out,
+                   int mem_kind) {
+  if (!e || !rgbd_args_ok(rgb, depth, width, height, depth_factor, mem_kind) || !rgb_out || !depth_out) {
+    set_error("tsdf_rgbd_half: invalid argument (even width / height, depth_factor > 0)");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  const int64_t nout = (int64_t)(width / 2) * (height / 2);
+  if (mem_kind == TSDF_MEM_DEVICE)
+    return rgbd_half(e, rgb, depth, mask, width, height, depth_factor, rgb_out, depth_out, mem_kind);
+  int rc = ensure_fe_out(e, nout);
+  if (rc) return rc;
+  rc = rgbd_half(e, rgb, depth, mask, width, height, depth_factor, e->fe_out_rgb, e->fe_out_depth, mem_kind);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(rgb_out, e->fe_out_rgb, (size_t)nout * 3, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipMemcpyAsync(depth_out, e->fe_out_depth, (size_t)nout * 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return TSDF_OK;
+}
+
+int tsdf_feed_rgbd_frame(tsdf_engine* e, const uint8_t* rgb, const uint16_t* depth,
+                         const uint8_t* mask, int width, int height, float depth_factor,
+                         const tsdf_intrinsics* K, const tsdf_pose* cam_T_world, float max_depth,
+                         int mem_kind) {
+  if (!e || !rgbd_args_ok(rgb, depth, width, height, depth_factor, mem_kind)) {
+    set_error("tsdf_feed_rgbd_frame: invalid argument (even width / height, depth_factor > 0)");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  const int w = width / 2, h = height / 2;
+  int rc = ensure_fe_out(e, (int64_t)w * h);
+  if (rc) return rc;
+  rc = rgbd_half(e, rgb, depth, mask, width, height, depth_factor, e->fe_out_rgb, e->fe_out_depth, mem_kind);
+  if (rc) return rc;
+  // TSDFSystem::Integrate without ht / lt (disinfect_slam.cc:66; ones, tsdf_module.cc:29-33)
+  tsdf_frame f{};
+  f.width = w;
+  f.height = h;
+  f.rgb = e->fe_out_rgb;
+  f.depth = e->fe_out_depth;
+  f.ht = nullptr;
+  f.lt = nullptr;
+  f.mem_kind = TSDF_MEM_DEVICE;
+  return tsdf_integrate(e, &f, K, cam_T_world, max_depth);
 }
 
 int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const tsdf_pose* pose,

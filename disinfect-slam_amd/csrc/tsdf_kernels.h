@@ -76,6 +76,9 @@ __global__ void k_keys_to_newset(EngineDev D, const int16_t* keys, int n);
 // routed frames (SURVEY 8e option 2)
 __global__ void k_route_pack(EngineDev D, RouteRec* out, int cap, int nshard);
 __global__ void k_route_ingest(EngineDev D, FrameParams P, const RouteRec* in, int cap);
+// DISINFSystem::feed_rgbd_frame preprocessing (tsdf_frontend.hip); grid (ceil(w / 64), ceil(h / 4))
+__global__ void k_rgbd_half(const uint8_t* rgb, const uint16_t* depth, const uint8_t* mask, int W,
+                            int H, float alpha, uint8_t* rgb_out, float* depth_out);
 __global__ void k_fresh_init(EngineDev D);
 // extraction
 struct MeshParams {

@@ -41,6 +41,18 @@ void TSDFSystem::Integrate(const SE3<float>& posecam_T_world, const Mat& img_rgb
     in = std::make_unique<TSDFSystemInput>(cam_T_posecam_ * posecam_T_world, img_rgb.clone(),
                                            img_depth.clone(), img_ht.clone(), img_lt.clone());
   }
+  Enqueue(std::move(in));
+}
+
+void TSDFSystem::IntegrateRaw(const SE3<float>& posecam_T_world, const Mat& img_rgb,
+                              const Mat& img_depth_raw, const Mat& mask, float depth_factor) {
+  if (!(depth_factor > 0.0f)) throw std::invalid_argument("TSDFSystem::IntegrateRaw: depth_factor <= 0");
+  Enqueue(std::make_unique<TSDFSystemInput>(cam_T_posecam_ * posecam_T_world, img_rgb.clone(),
+                                            img_depth_raw.clone(), mask.empty() ? Mat() : mask.clone(),
+                                            Mat(), depth_factor));
+}
+
+void TSDFSystem::Enqueue(std::unique_ptr<TSDFSystemInput> in) {
   {
     std::lock_guard<std::mutex> lock(mtx_queue_);
     inputs_.push(std::move(in));
@@ -85,8 +97,12 @@ void TSDFSystem::Run() {
     }
     try {
       std::lock_guard<std::mutex> lock(mtx_read_);
-      tsdf_.Integrate(input->img_rgb, input->img_depth, input->img_ht, input->img_lt, max_depth_,
-                      intrinsics_, input->cam_T_world);
+      if (input->depth_factor > 0.0f)
+        tsdf_.FeedRGBD(input->img_rgb, input->img_depth, input->img_ht, input->depth_factor, max_depth_,
+                       intrinsics_, input->cam_T_world);
+      else
+        tsdf_.Integrate(input->img_rgb, input->img_depth, input->img_ht, input->img_lt, max_depth_,
+                        intrinsics_, input->cam_T_world);
     } catch (const std::exception& ex) {  // never let an engine error kill the worker
       std::fprintf(stderr, "[TSDF System] integrate failed: %s\n", ex.what());
     }

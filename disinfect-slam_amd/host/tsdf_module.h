@@ -22,13 +22,14 @@ struct TSDFSystemInput {
   SE3<float> cam_T_world;
   Mat img_rgb;
   Mat img_depth;
-  Mat img_ht;
+  Mat img_ht;   // raw frames: the mask
   Mat img_lt;
+  float depth_factor = 0.0f;  // > 0: a raw sensor frame (FeedRGBD) with depth in sensor units
 
   TSDFSystemInput(const SE3<float>& cam_T_world, const Mat& img_rgb, const Mat& img_depth,
-                  const Mat& img_ht, const Mat& img_lt)
+                  const Mat& img_ht, const Mat& img_lt, float depth_factor = 0.0f)
       : cam_T_world(cam_T_world), img_rgb(img_rgb), img_depth(img_depth), img_ht(img_ht),
-        img_lt(img_lt) {}
+        img_lt(img_lt), depth_factor(depth_factor) {}
 };
 
 class TSDFSystem {
@@ -44,6 +45,10 @@ class TSDFSystem {
 
   void Integrate(const SE3<float>& posecam_T_world, const Mat& img_rgb, const Mat& img_depth,
                  const Mat& img_ht = {}, const Mat& img_lt = {});
+  // a raw full-size sensor frame (CV_8UC3 rgb, CV_16UC1 depth, optional CV_8UC1 mask): the GPU
+  // runs DISINFSystem::feed_rgbd_frame's resize / depth scale / mask before integrating
+  void IntegrateRaw(const SE3<float>& posecam_T_world, const Mat& img_rgb, const Mat& img_depth_raw,
+                    const Mat& mask, float depth_factor);
   std::vector<VoxelSpatialTSDF> Query(const BoundingCube<float>& volumn);
   void Render(const CameraParams& virtual_cam, const SE3<float> cam_T_world, Mat* img_normal);
 
@@ -53,6 +58,7 @@ class TSDFSystem {
 
  private:
   void Run();
+  void Enqueue(std::unique_ptr<TSDFSystemInput> in);
   TSDFGrid tsdf_;
   float max_depth_;
   const CameraIntrinsics<float> intrinsics_;

@@ -59,6 +59,21 @@ void TSDFGrid::Integrate(const Mat& img_rgb, const Mat& img_depth, const Mat& im
   check_tsdf(tsdf_integrate(engine_, &f, &K, &P, max_depth), "tsdf_integrate");
 }
 
+void TSDFGrid::FeedRGBD(const Mat& img_rgb, const Mat& img_depth_raw, const Mat& mask, float depth_factor,
+                        float max_depth, const CameraIntrinsics<float>& intrinsics,
+                        const SE3<float>& cam_T_world) {
+  if (img_rgb.type() != CV_8UC3 || img_depth_raw.type() != CV_16UC1 || img_rgb.cols != img_depth_raw.cols ||
+      img_rgb.rows != img_depth_raw.rows ||
+      (!mask.empty() && (mask.type() != CV_8UC1 || mask.total() != img_depth_raw.total())))
+    throw std::invalid_argument("TSDFGrid::FeedRGBD: expects CV_8UC3 rgb, CV_16UC1 depth, CV_8UC1 mask");
+  const tsdf_intrinsics K{intrinsics.fx, intrinsics.fy, intrinsics.cx, intrinsics.cy};
+  const tsdf_pose P = to_pose(cam_T_world);
+  check_tsdf(tsdf_feed_rgbd_frame(engine_, img_rgb.ptr<uint8_t>(), img_depth_raw.ptr<uint16_t>(),
+                                  mask.empty() ? nullptr : mask.ptr<uint8_t>(), img_depth_raw.cols,
+                                  img_depth_raw.rows, depth_factor, &K, &P, max_depth, TSDF_MEM_HOST),
+             "tsdf_feed_rgbd_frame");
+}
+
 void TSDFGrid::RayCast(float max_depth, const CameraParams& cam, const SE3<float>& cam_T_world,
                        Mat* rgba, Mat* normal) {
   if (rgba && (rgba->rows != cam.img_h || rgba->cols != cam.img_w || rgba->type() != CV_8UC4))

@@ -24,6 +24,13 @@ class TSDFGrid {
                  float max_depth, const CameraIntrinsics<float>& intrinsics,
                  const SE3<float>& cam_T_world);
 
+  // DISINFSystem::feed_rgbd_frame's preprocessing + Integrate on the GPU (disinfect_slam.cc:31-67):
+  // full-size rgb CV_8UC3, raw depth CV_16UC1, optional mask CV_8UC1 (empty = none), all of even
+  // size; intrinsics are those of the half-size image the volume integrates
+  void FeedRGBD(const Mat& img_rgb, const Mat& img_depth_raw, const Mat& mask, float depth_factor,
+                float max_depth, const CameraIntrinsics<float>& intrinsics,
+                const SE3<float>& cam_T_world);
+
   // voxel_tsdf.cu:490-506: renders into CV_8UC4 images (either may be null; the reference writes
   // into GL textures, utils/gl/image.h)
   void RayCast(float max_depth, const CameraParams& virtual_cam, const SE3<float>& cam_T_world,

@@ -236,6 +236,48 @@ class Engine:
         return _lib.Frame(W, H, _ptr(rgb), _ptr(depth), _ptr(ht), _ptr(lt),
                           TSDF_MEM_DEVICE if dev else TSDF_MEM_HOST), (rgb, depth, ht, lt)
 
+    def _rgbd_inputs(self, rgb, depth_u16, mask):
+        dev = _is_torch_cuda(depth_u16)
+        if dev:
+            for a in (rgb, depth_u16, mask):
+                if a is not None and not a.is_contiguous():
+                    raise ValueError("device frames must be contiguous")
+        else:
+            rgb = _np(rgb, np.uint8)
+            depth_u16 = _np(depth_u16, np.uint16)
+            mask = _np(mask, np.uint8)
+        H, W = int(depth_u16.shape[0]), int(depth_u16.shape[1])
+        if tuple(rgb.shape[:2]) != (H, W) or (mask is not None and tuple(mask.shape[:2]) != (H, W)):
+            raise ValueError("rgb / depth / mask size mismatch")
+        return dev, rgb, depth_u16, mask, W, H
+
+    def rgbd_half(self, rgb, depth_u16, mask, depth_factor: float):
+        """DISINFSystem::feed_rgbd_frame preprocessing alone (x0.5 resize, depth scale, mask):
+        returns (rgb (H/2, W/2, 3) u8, depth (H/2, W/2) f32), host arrays or device tensors."""
+        dev, rgb, depth_u16, mask, W, H = self._rgbd_inputs(rgb, depth_u16, mask)
+        if dev:
+            import torch
+            ro = torch.empty((H // 2, W // 2, 3), dtype=torch.uint8, device=depth_u16.device)
+            do = torch.empty((H // 2, W // 2), dtype=torch.float32, device=depth_u16.device)
+        else:
+            ro = np.zeros((H // 2, W // 2, 3), np.uint8)
+            do = np.zeros((H // 2, W // 2), np.float32)
+        _lib.check(_lib.load().tsdf_rgbd_half(self._h, _ptr(rgb), _ptr(depth_u16), _ptr(mask), W, H,
+                                              depth_factor, _ptr(ro), _ptr(do),
+                                              TSDF_MEM_DEVICE if dev else TSDF_MEM_HOST), "tsdf_rgbd_half")
+        return ro, do
+
+    def feed_rgbd_frame(self, rgb, depth_u16, mask, depth_factor: float, K, cam_T_world: SE3,
+                        max_depth: float):
+        """DISINFSystem::feed_rgbd_frame after its pose lookup: preprocessing + Integrate on the GPU
+        (K = intrinsics of the half-size image)."""
+        dev, rgb, depth_u16, mask, W, H = self._rgbd_inputs(rgb, depth_u16, mask)
+        Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        _lib.check(_lib.load().tsdf_feed_rgbd_frame(self._h, _ptr(rgb), _ptr(depth_u16), _ptr(mask), W, H,
+                                                    depth_factor, C.byref(Kc), C.byref(cam_T_world._c()),
+                                                    max_depth, TSDF_MEM_DEVICE if dev else TSDF_MEM_HOST),
+                   "tsdf_feed_rgbd_frame")
+
     @staticmethod
     def route_buffer_bytes(shard_count: int, route_cap: int) -> int:
         """Bytes of one routed-frame outbox / inbox (shard_count slots of route_cap + 1 records)."""

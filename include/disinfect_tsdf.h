@@ -141,6 +141,22 @@ int tsdf_integrate_route_begin(tsdf_engine* e, const tsdf_frame* frame, const ts
                                int32_t slice_count, void* outbox, int32_t route_cap);
 int tsdf_integrate_route_end(tsdf_engine* e, const void* inbox, int32_t route_cap);
 
+/* DISINFSystem::feed_rgbd_frame (disinfect_slam/disinfect_slam.cc:31-67) after the pose lookup:
+ * cv::resize(x0.5) of rgb (height x width x 3 u8), depth (height x width u16 raw sensor units) and
+ * the optional mask (height x width u8, NULL = none), depth.convertTo(CV_32FC1, 1 / depth_factor),
+ * depth = 0 where the resized mask is 0, then TSDFGrid::Integrate of the (width/2 x height/2)
+ * frame with ht = lt = ones, all on the GPU. width and height must be even (OpenCV's fast 2x2 area
+ * path; see csrc/tsdf_frontend.hip). K is the intrinsics of the half-size image. */
+int tsdf_feed_rgbd_frame(tsdf_engine* e, const uint8_t* rgb, const uint16_t* depth,
+                         const uint8_t* mask, int width, int height, float depth_factor,
+                         const tsdf_intrinsics* K, const tsdf_pose* cam_T_world, float max_depth,
+                         int mem_kind);
+/* The preprocessing step alone: rgb_out (height/2 x width/2 x 3 u8), depth_out (f32), in host or
+ * device memory like the inputs (mem_kind). */
+int tsdf_rgbd_half(tsdf_engine* e, const uint8_t* rgb, const uint16_t* depth, const uint8_t* mask,
+                   int width, int height, float depth_factor, uint8_t* rgb_out, float* depth_out,
+                   int mem_kind);
+
 /* TSDFGrid::RayCast (voxel_tsdf.cu:490-506; ray_cast_kernel :232-307). rgba / normal are
  * height x width x 4 u8 (either may be NULL), host or device memory per mem_kind. */
 int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int width, int height,

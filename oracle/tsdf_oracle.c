@@ -855,3 +855,34 @@ int64_t ora_extract_mesh(const ora_grid* g, const float* bounds, float missing, 
   }
   return n;
 }
+
+/* ---------------------------------------------------------------------------------------------
+ * DISINFSystem::feed_rgbd_frame preprocessing (disinfect_slam/disinfect_slam.cc:31-64).
+ * OpenCV 4.x cv::resize (modules/imgproc/src/resize.cpp), not vendored here -- parity unpinned
+ * beyond this restatement of its published algorithm: with fx = fy = 0.5 and INTER_LINEAR on an
+ * even-sized image, resize() switches to INTER_AREA ("interpolation == INTER_LINEAR &&
+ * is_area_fast && iscale_x == 2 && iscale_y == 2"), whose fast path (resizeAreaFast_ with
+ * ResizeAreaFastVec, fast_mode for 1 / 3 channels) writes (a + b + c + d + 2) >> 2 of each 2x2
+ * block per channel for both CV_8U and CV_16U. convertTo(CV_32FC1, alpha) is
+ * (float)src * (float)alpha + 0 (cvtScale_, one rounding). The mask loop zeroes depth where the
+ * resized mask is 0 (:46-58).
+ * --------------------------------------------------------------------------------------------- */
+void ora_rgbd_half(const uint8_t* rgb, const uint16_t* depth, const uint8_t* mask, int W, int H,
+                   float depth_factor, uint8_t* rgb_out, float* depth_out) {
+  const int w = W / 2, h = H / 2;
+  const float alpha = (float)(1. / (double)depth_factor);
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      const size_t i0 = (size_t)(2 * y) * W + 2 * x, i1 = i0 + W;
+      for (int c = 0; c < 3; ++c)
+        rgb_out[((size_t)y * w + x) * 3 + c] =
+            (uint8_t)((rgb[i0 * 3 + c] + rgb[(i0 + 1) * 3 + c] + rgb[i1 * 3 + c] + rgb[(i1 + 1) * 3 + c] + 2) >> 2);
+      const int dv = (depth[i0] + depth[i0 + 1] + depth[i1] + depth[i1 + 1] + 2) >> 2;
+      float d = (float)(uint16_t)dv * alpha;
+      if (mask) {
+        const int mv = (mask[i0] + mask[i0 + 1] + mask[i1] + mask[i1 + 1] + 2) >> 2;
+        if (mv == 0) d = 0.0f;
+      }
+      depth_out[(size_t)y * w + x] = d;
+    }
+}

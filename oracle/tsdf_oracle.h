@@ -95,6 +95,13 @@ void ora_pool_set_weight(ora_grid* g, int32_t block_idx, uint8_t weight);
 void ora_pool_get_weights(const ora_grid* g, int32_t block_idx, uint8_t* out512);
 uint32_t ora_hash(int16_t x, int16_t y, int16_t z);
 
+/* DISINFSystem::feed_rgbd_frame preprocessing (disinfect_slam/disinfect_slam.cc:31-64):
+ * cv::resize(.., 0.5, 0.5) of rgb (HxWx3 u8), depth (HxW u16) and the optional mask (HxW u8),
+ * depth.convertTo(CV_32FC1, 1. / depth_factor), depth = 0 where the resized mask is 0. W and H
+ * must be even. OpenCV is not vendored: see the .c for the published algorithm restated. */
+void ora_rgbd_half(const uint8_t* rgb, const uint16_t* depth, const uint8_t* mask, int W, int H,
+                   float depth_factor, uint8_t* rgb_out, float* depth_out);
+
 #ifdef __cplusplus
 }
 #endif

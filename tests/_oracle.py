@@ -74,6 +74,7 @@ def lib():
         L.ora_block_owner.argtypes = [C.c_int16, C.c_int16, C.c_int16, C.c_uint32]
         L.ora_hash.restype = C.c_uint32
         L.ora_hash.argtypes = [C.c_int16, C.c_int16, C.c_int16]
+        L.ora_rgbd_half.argtypes = [P, P, P, C.c_int, C.c_int, C.c_float, P, P]
         _lib = L
     return _lib
 
@@ -88,6 +89,18 @@ def block_owner(x, y, z, shards) -> int:
 
 def hash_block(x, y, z) -> int:
     return int(lib().ora_hash(x, y, z))
+
+
+def rgbd_half(rgb, depth_u16, mask, depth_factor):
+    """DISINFSystem::feed_rgbd_frame preprocessing (disinfect_slam.cc:31-64) -> (rgb, depth f32)."""
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    depth_u16 = np.ascontiguousarray(depth_u16, np.uint16)
+    mask = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+    H, W = depth_u16.shape
+    ro = np.zeros((H // 2, W // 2, 3), np.uint8)
+    do = np.zeros((H // 2, W // 2), np.float32)
+    lib().ora_rgbd_half(_p(rgb), _p(depth_u16), _p(mask), W, H, depth_factor, _p(ro), _p(do))
+    return ro, do
 
 
 class OracleGrid:

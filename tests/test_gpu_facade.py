@@ -47,3 +47,48 @@ def test_tsdf_system_matches_oracle(tmp_path, semantic):
     got_n = np.fromfile(tmp_path / "out_render.bin", np.uint8).reshape(H, W, 4)
     assert np.abs(got_n.astype(int) - nrm).max() <= 1
     ora.close()
+
+
+def test_disinf_system_feed_rgbd_frame(tmp_path):
+    """DISINFSystem (host/disinfect_slam.h): poses registered at tracker timestamps, raw 16-bit
+    sensor frames fed at their own timestamps (nearest pose, pose_manager.cc) and preprocessed on the
+    GPU (x0.5 resize, depth scale, mask) == the oracle fed the same preprocessing + poses."""
+    from tsdf_amd import synth
+    from _oracle import OracleGrid, rgbd_half
+    from test_host_cpu import ref_query
+    W, H, n, voxel, trunc, nb, factor = 192, 144, 5, 0.01, 0.04, 13, 5000.0
+    full = synth.camera(W, H)
+    half = synth.camera(W // 2, H // 2)
+    rng = np.random.default_rng(5)
+    reg = []
+    for i in range(2 * n + 2):  # tracker poses every 33 ms
+        (_, _), (q, t) = synth.pose(i)
+        reg.append((1000 + 33 * i, tuple(float(v) for v in list(q) + list(t))))
+    ora = OracleGrid(voxel, trunc, nb)
+    k32 = " ".join(repr(float(v)) for v in half.K)
+    lines = [f"{W} {H} {n} {len(reg)} {k32} {voxel} {trunc} 4.0 {factor} {nb}"]
+    lines += [f"{ts} " + " ".join(repr(v) for v in p) for ts, p in reg]
+    for i in range(n):
+        ts = 1000 + 66 * i + int(rng.integers(-14, 15))  # the depth stream's own clock
+        fr = synth.render(full, 2 * i)
+        d16 = np.round(fr["depth"] * factor).astype(np.uint16)
+        mask = (rng.random((H, W)) < 0.85).astype(np.uint8) if i % 2 else None
+        fr["rgb"].tofile(tmp_path / f"f{i}_rgb.bin")
+        d16.tofile(tmp_path / f"f{i}_depth.bin")
+        if mask is not None:
+            mask.tofile(tmp_path / f"f{i}_mask.bin")
+        lines.append(f"{ts} {int(mask is not None)}")
+        p = ref_query(reg, ts)
+        r2, dd = rgbd_half(fr["rgb"], d16, mask, factor)
+        ora.integrate(r2, dd, None, None, 4.0, half.K, np.float32(p[:4]), np.float32(p[4:]))
+    (tmp_path / "meta.txt").write_text("\n".join(lines) + "\n")
+    binp = os.path.join(ROOT, "disinfect-slam_amd", "disinfect_main")
+    r = subprocess.run([binp, str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.fromfile(tmp_path / "out_query.bin", np.float32).reshape(-1, 4)
+    exp = ora.query(np.array([-1e4, 1e4, -1e4, 1e4, -1e4, 1e4], np.float32))
+    assert got.shape == exp.shape and got.shape[0] > 0
+    np.testing.assert_array_equal(got.view(np.uint32), exp.view(np.uint32))
+    frames, active, status = map(int, (tmp_path / "out_stats.txt").read_text().split())
+    assert (frames, active, status) == (n, ora.stats()["active_blocks"], 0)
+    ora.close()
