@@ -53,6 +53,11 @@ def parse():
     p.add_argument("--max-depth", type=float, default=4.0)
     p.add_argument("--depth-only", action="store_true", help="config C2: ht = lt = NULL (ones)")
     p.add_argument("--mode", choices=("streams", "sharded", "routed"), default="streams")
+    p.add_argument("--loop", choices=("c3", "c5"), default="c3",
+                   help="c5: BASELINE config C5 -- per frame one hipGraph launch (integrate + raycast of "
+                        "the frame's camera), marching cubes of the whole volume every 30 frames")
+    p.add_argument("--graph", action="store_true",
+                   help="c3 loop through the graph-captured frame (one hipGraph launch per frame)")
     p.add_argument("--route-cap", type=int, default=8192,
                    help="routed mode: keys per destination rank per frame (outbox slot size)")
     p.add_argument("--cpu-frames", type=int, default=-1, help="oracle sample size (-1 = auto)")
@@ -116,10 +121,27 @@ def main():
         outbox = torch.zeros((world, nbytes // world), dtype=torch.uint8, device=dev)
         inbox = torch.zeros_like(outbox)
 
+    use_graph = a.loop == "c5" or a.graph
+    if use_graph and routed:
+        raise SystemExit("--graph / --loop c5 take streams or sharded mode")
+    graph = None
+    mesh_tris = []
+    if use_graph:
+        rw, rh = (a.width, a.height) if a.loop == "c5" else (0, 0)
+        graph = eng.frame_graph(a.width, a.height, rw, rh)
+        rgba = torch.zeros((a.height, a.width, 4), dtype=torch.uint8, device=dev) if rw else None
+        normal = torch.zeros_like(rgba) if rw else None
+        mesh_buf = torch.empty(9 * (8 << 20), dtype=torch.float32, device=dev) if a.loop == "c5" else None
+
     def step(i):
         ht = None if a.depth_only else frames["ht"][i]
         lt = None if a.depth_only else frames["lt"][i]
-        if routed:
+        if graph is not None:
+            graph.frame(frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i], a.max_depth,
+                        K if rgba is not None else None, poses[i] if rgba is not None else None, rgba, normal)
+            if a.loop == "c5" and (i + 1) % 30 == 0:  # marching cubes of the whole volume (on device)
+                mesh_tris.append(int(eng.extract_mesh(None, 0.99, 0, out=mesh_buf).shape[0]))
+        elif routed:
             eng.integrate_route_begin(frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i],
                                       a.max_depth, rank, world, outbox, a.route_cap)
             tdist.route_exchange(outbox, inbox)
@@ -152,7 +174,11 @@ def main():
     # phase breakdown (all four phases event-bracketed) on the next frames of the stream, untimed
     eng.profile_begin()
     for i in range(a.warmup + a.steps, nframes):
-        step(i)
+        if graph is not None:  # graph frames carry no events: the eager calls of the same frame
+            eng.integrate(frames["rgb"][i], frames["depth"][i], None if a.depth_only else frames["ht"][i],
+                          None if a.depth_only else frames["lt"][i], K, poses[i], a.max_depth)
+        else:
+            step(i)
     torch.cuda.synchronize()
     phases = eng.profile_end()
     st = eng.stats()
@@ -165,6 +191,10 @@ def main():
     img_bytes = (12 if a.depth_only else 15) * W * H
     alg_bytes = (prof["sum_visible"] * (512 * 12 + 12) + prof["sum_updated"] * 12) / a.steps + img_bytes
     t_int = prof["ms_integrate"] / max(prof["frames"], 1) / 1e3
+    event_kind = "marker" if a.marker_events else "kernel-dispatch"
+    if graph is not None:  # graph frames carry no events: the in-kernel device clock
+        t_int = prof["ms_integrate_device"] / a.steps / 1e3
+        event_kind = "none (graph frames): device clock"
     achieved = alg_bytes / t_int / 1e9 if t_int > 0 else 0.0
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_integrate_latest.json")
@@ -184,8 +214,15 @@ def main():
         workload = ("C2: 640x480 depth-only" if a.depth_only else "C3: 640x480 depth + ht/lt semantic")
         if (W, H) != (640, 480):
             workload = f"{W}x{H} depth{'' if a.depth_only else ' + ht/lt semantic'}"
+        metric = "TSDF integrate frames/s (640x480 depth+label, 5mm voxel)"
+        if a.loop == "c5":
+            metric = ("C5 frame loop frames/s (integrate + raycast every frame, marching cubes every 30 "
+                      "frames, one hipGraph launch per frame)")
+            workload = "C5: " + workload
+        elif graph is not None:
+            workload += " (hipGraph frame)"
         out = {
-            "metric": "TSDF integrate frames/s (640x480 depth+label, 5mm voxel)",
+            "metric": metric,
             "value": round(value, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -218,7 +255,7 @@ def main():
                 # (what rocprofv3's kernel trace measures; the HIP events above also include the
                 # per-launch dispatch / completion overhead)
                 "event_timed_launches": prof["frames"],
-                "event_kind": "marker" if a.marker_events else "kernel-dispatch",
+                "event_kind": event_kind,
                 "us_per_launch_device_clock": round(prof["ms_integrate_device"] / a.steps * 1e3, 3),
                 "achieved_device_clock": round(alg_bytes / (prof["ms_integrate_device"] / a.steps / 1e3) / 1e9, 1)
                 if prof["ms_integrate_device"] > 0 else None,
@@ -233,11 +270,14 @@ def main():
             },
             "host_enqueue_ms_per_step": round((t_enq - t0) / a.steps * 1e3, 4),
             "avg_visible_blocks": round(prof["sum_visible"] / a.steps, 1),
+            "mesh_triangles": mesh_tris[-1] if mesh_tris else None,
             "avg_updated_voxels": round(prof["sum_updated"] / a.steps, 1),
             "active_blocks": st["active_blocks"],
             "status": st["status"],
         }
         print(json.dumps(out), flush=True)
+    if graph is not None:
+        graph.close()
     eng.close()
     if dist:
         dist.destroy_process_group()

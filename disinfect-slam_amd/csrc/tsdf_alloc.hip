@@ -156,12 +156,11 @@ __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, Inge
 
 // grid: kVisWorkgroups sweep workgroups first (dispatched first, they overlap the tiles), then
 // one workgroup per 16x16 pixel tile (tiles_x per row, `tiles` in all)
-__global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
-                                                    const float* __restrict__ depth,
-                                                    const uint8_t* __restrict__ rgb,
-                                                    const float* __restrict__ ht,
-                                                    const float* __restrict__ lt, int tiles_x,
-                                                    int tiles) {
+__device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
+                                           const float* __restrict__ depth,
+                                           const uint8_t* __restrict__ rgb,
+                                           const float* __restrict__ ht,
+                                           const float* __restrict__ lt, int tiles_x, int tiles) {
   __shared__ IngestLds S;
   if ((int)blockIdx.x < kVisWorkgroups) {
     TSDF_STAMP(D, 2, 0);
@@ -290,6 +289,18 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
   }
   TSDF_STAMP(D, 0, 5);
 }
+__global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
+                                                    const float* __restrict__ depth,
+                                                    const uint8_t* __restrict__ rgb,
+                                                    const float* __restrict__ ht,
+                                                    const float* __restrict__ lt, int tiles_x,
+                                                    int tiles) {
+  ingest_dda(D, P, depth, rgb, ht, lt, tiles_x, tiles);
+}
+__global__ __launch_bounds__(256) void k_ingest_dda_g(EngineDev D, const FrameArgs* __restrict__ A) {
+  const FrameParams P = A->P;
+  ingest_dda(D, P, A->depth, A->rgb, A->ht, A->lt, A->tiles_x, A->tiles);
+}
 
 // ---------------------------------------------------------------------------------------------
 // Routed frames (SURVEY.md 8e option 2). k_route_pack drains the route set into the outbox, one
@@ -379,8 +390,8 @@ __global__ void k_keys_to_newset(EngineDev D, const int16_t* __restrict__ keys, 
 // frame_mode 1: append new blocks to this frame's visible-block lists flagged fresh (integrate
 // initialises them), 0: list them in D.fresh for k_fresh_init.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, FrameParams P,
-                                                                   uint32_t range, int frame_mode) {
+__device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32_t range,
+                                              int frame_mode) {
   __shared__ ResolveLds L;
   const int t = threadIdx.x;
   TSDF_STAMP(D, 1, 0);
@@ -561,6 +572,16 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, 
       D.ctr->n_vis = 0;
     }
   }
+}
+
+__global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, FrameParams P,
+                                                                   uint32_t range, int frame_mode) {
+  resolve_alloc(D, P, range, frame_mode);
+}
+__global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc_g(EngineDev D,
+                                                                     const FrameArgs* __restrict__ A) {
+  const FrameParams P = A->P;
+  resolve_alloc(D, P, A->range, 1);
 }
 
 // AquireBlock's initialisation (voxel_mem.cu:43-51) for the hash-level test path

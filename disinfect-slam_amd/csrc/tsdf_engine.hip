@@ -339,7 +339,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.wg_end, kIntegrateGrid + 1);
   {  // one resident wave of k_integrate workgroups: no second-round stragglers
     int per_cu = 0, ncu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate, kIntegrateThreads, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate_t<false>, kIntegrateThreads, 0) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
       return fail(TSDF_ERR_HIP);
     if (const char* v = std::getenv("TSDF_INTEGRATE_WG_PER_CU")) per_cu = std::min(per_cu, std::atoi(v));  // tuning
@@ -496,11 +496,12 @@ int frame_finish(tsdf_engine* e, const FrameParams& P, std::array<hipEvent_t, 5>
   if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
     // the two events are bound to the kernel's own dispatch packet (its begin / end timestamps,
     // the interval rocprofv3's kernel trace reports): no marker packets enter the stream
-    hipExtLaunchKernelGGL(k_integrate, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
-                          (*ev)[2], (*ev)[3], 0, e->D, P);
+    hipExtLaunchKernelGGL(k_integrate_t<false>, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
+                          (*ev)[2], (*ev)[3], 0, e->D, P, (const FrameArgs*)nullptr);
   } else {
     if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
-    hipLaunchKernelGGL(k_integrate, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s, e->D, P);
+    hipLaunchKernelGGL(k_integrate_t<false>, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s, e->D, P,
+                       (const FrameArgs*)nullptr);
     if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
   }
   LAUNCH_OK("k_integrate");
@@ -563,6 +564,144 @@ int tsdf_integrate_route_end(tsdf_engine* e, const void* inbox, int32_t route_ca
                      e->stream, e->D, e->route_P, reinterpret_cast<const RouteRec*>(inbox), route_cap);
   LAUNCH_OK("k_route_ingest");
   return frame_finish(e, e->route_P, e->route_ev);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Graph-captured frame loop (BASELINE config C5): the whole per-frame sequence -- argument upload,
+// k_ingest_dda, k_resolve_alloc, k_integrate, k_resolve_delete and (optionally) k_raycast -- is one
+// hipGraph launch. The graph's first node copies a FrameArgs block (cameras, frame and output
+// pointers) from a pinned host slot, so one instantiated graph serves every frame; kSlots graphs
+// with their own slots let the host fill frame i+1 while frame i runs.
+// ---------------------------------------------------------------------------------------------
+struct tsdf_graph {
+  static constexpr int kSlots = 4;
+  tsdf_engine* e = nullptr;
+  int W = 0, H = 0, RW = 0, RH = 0;
+  hipStream_t cap = nullptr;  // capture stream (the engine stream may be a legacy default stream)
+  FrameArgs* d_args = nullptr;
+  FrameArgs* h_args = nullptr;  // pinned
+  hipGraph_t graph[kSlots] = {};
+  hipGraphExec_t exec[kSlots] = {};
+  hipEvent_t done[kSlots] = {};
+  bool used[kSlots] = {};
+  int next = 0;
+};
+
+namespace {
+
+void graph_free(tsdf_graph* g) {
+  for (int i = 0; i < tsdf_graph::kSlots; ++i) {
+    if (g->exec[i]) (void)hipGraphExecDestroy(g->exec[i]);
+    if (g->graph[i]) (void)hipGraphDestroy(g->graph[i]);
+    if (g->done[i]) (void)hipEventDestroy(g->done[i]);
+  }
+  if (g->d_args) (void)hipFree(g->d_args);
+  if (g->h_args) (void)hipHostFree(g->h_args);
+  if (g->cap) (void)hipStreamDestroy(g->cap);
+  delete g;
+}
+
+}  // namespace
+
+int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, int render_height,
+                      tsdf_graph** out) {
+  if (!e || !out || width <= 0 || height <= 0 || width > e->cfg.max_width || height > e->cfg.max_height ||
+      render_width < 0 || render_height < 0 || (int64_t)render_width * render_height > e->max_pixels ||
+      (render_width == 0) != (render_height == 0)) {
+    set_error("tsdf_graph_create: invalid argument");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  auto* g = new tsdf_graph();
+  g->e = e;
+  g->W = width;
+  g->H = height;
+  g->RW = render_width;
+  g->RH = render_height;
+  auto fail = [&](hipError_t err, const char* what) {
+    set_error(what, err);
+    graph_free(g);
+    return TSDF_ERR_HIP;
+  };
+  hipError_t err;
+  if ((err = hipStreamCreateWithFlags(&g->cap, hipStreamNonBlocking)) != hipSuccess) return fail(err, "graph stream");
+  if ((err = hipMalloc(&g->d_args, sizeof(FrameArgs) * tsdf_graph::kSlots)) != hipSuccess) return fail(err, "graph args");
+  if ((err = hipHostMalloc(&g->h_args, sizeof(FrameArgs) * tsdf_graph::kSlots)) != hipSuccess)
+    return fail(err, "graph host args");
+  std::memset(g->h_args, 0, sizeof(FrameArgs) * tsdf_graph::kSlots);
+  const int tiles = ((width + 15) / 16) * ((height + 15) / 16);
+  // the engine's queued work must be done before the capture stream records anything
+  if ((err = hipStreamSynchronize(e->stream)) != hipSuccess) return fail(err, "graph sync");
+  for (int k = 0; k < tsdf_graph::kSlots; ++k) {
+    const FrameArgs* A = g->d_args + k;
+    if ((err = hipEventCreateWithFlags(&g->done[k], hipEventDisableTiming)) != hipSuccess) return fail(err, "graph event");
+    if ((err = hipStreamBeginCapture(g->cap, hipStreamCaptureModeThreadLocal)) != hipSuccess)
+      return fail(err, "hipStreamBeginCapture");
+    if (std::getenv("TSDF_GRAPH_MEMCPY_NODE"))  // A/B: a memcpy node instead of the copy kernel
+      (void)hipMemcpyAsync(g->d_args + k, g->h_args + k, sizeof(FrameArgs), hipMemcpyHostToDevice, g->cap);
+    else  // one wave reads the pinned slot over the fabric: a kernel node, no DMA engine in the graph
+      hipLaunchKernelGGL(k_copy_words, dim3(1), dim3(64), 0, g->cap, reinterpret_cast<uint32_t*>(g->d_args + k),
+                         reinterpret_cast<const uint32_t*>(g->h_args + k), (int)(sizeof(FrameArgs) / 4));
+    hipLaunchKernelGGL(k_ingest_dda_g, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
+    hipLaunchKernelGGL(k_resolve_alloc_g, dim3(1), dim3(kResolveThreads), 0, g->cap, e->D, A);
+    hipLaunchKernelGGL(k_integrate_t<true>, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, g->cap, e->D,
+                       FrameParams{}, A);
+    hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kResolveThreads), 0, g->cap, e->D, e->D.cand,
+                       &e->D.ctr->n_cand, 0);
+    if (render_width)
+      hipLaunchKernelGGL(k_raycast_g, dim3((render_width + 15) / 16, (render_height + 15) / 16), dim3(256), 0,
+                         g->cap, e->D, A);
+    if ((err = hipStreamEndCapture(g->cap, &g->graph[k])) != hipSuccess) return fail(err, "hipStreamEndCapture");
+    if ((err = hipGraphInstantiate(&g->exec[k], g->graph[k], nullptr, nullptr, 0)) != hipSuccess)
+      return fail(err, "hipGraphInstantiate");
+  }
+  *out = g;
+  return TSDF_OK;
+}
+
+int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* K, const tsdf_pose* pose,
+                     float max_depth, const tsdf_intrinsics* render_K, const tsdf_pose* render_pose,
+                     uint8_t* rgba, uint8_t* normal) {
+  if (!g || !f || !K || !pose || f->mem_kind != TSDF_MEM_DEVICE || f->width != g->W || f->height != g->H ||
+      !f->depth || !f->rgb || (f->ht == nullptr) != (f->lt == nullptr) ||
+      (g->RW && (!render_K || !render_pose))) {
+    set_error("tsdf_graph_frame: invalid argument (device frame of the graph's size)");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  tsdf_engine* e = g->e;
+  if (e->route_pending) {
+    set_error("tsdf_graph_frame: a routed frame is pending");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  const int k = g->next;
+  g->next = (k + 1) % tsdf_graph::kSlots;
+  if (g->used[k]) HIP_OK(hipEventSynchronize(g->done[k]));  // slot k's upload has run
+  FrameArgs& a = g->h_args[k];
+  a.P = make_params(e, K, f->width, f->height, pose, max_depth);
+  if (g->RW) a.R = make_params(e, render_K, g->RW, g->RH, render_pose, max_depth);
+  a.depth = f->depth;
+  a.rgb = f->rgb;
+  a.ht = f->ht;
+  a.lt = f->lt;
+  a.rgba = reinterpret_cast<uchar4*>(rgba);
+  a.normal = reinterpret_cast<uchar4*>(normal);
+  a.step_size = e->cfg.truncation / 2;
+  a.range = (uint32_t)((size_t)f->width * f->height * e->maxs);
+  a.tiles_x = (f->width + 15) / 16;
+  a.tiles = a.tiles_x * ((f->height + 15) / 16);
+  HIP_OK(hipGraphLaunch(g->exec[k], e->stream));
+  HIP_OK(hipEventRecord(g->done[k], e->stream));
+  g->used[k] = true;
+  return TSDF_OK;
+}
+
+int tsdf_graph_destroy(tsdf_graph* g) {
+  if (!g) return TSDF_ERR_INVALID_ARG;
+  (void)hipSetDevice(g->e->device);
+  (void)hipStreamSynchronize(g->e->stream);
+  graph_free(g);
+  return TSDF_OK;
 }
 
 namespace {

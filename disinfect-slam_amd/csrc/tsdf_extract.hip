@@ -16,6 +16,10 @@ __global__ void k_init_heap(int32_t* heap, int n) {  // voxel_mem.cu:6-11
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) heap[i] = i;
 }
+// graph frames: the FrameArgs upload (pinned host slot -> device), one wave
+__global__ void k_copy_words(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = __builtin_nontemporal_load(src + i);
+}
 // never-acquired blocks read like the reference's zeroed probability array: log-odds -inf (p 0)
 __global__ void k_init_logodds(uint8_t* pool, int nb) {
   const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // one float4 per thread
@@ -128,9 +132,8 @@ __device__ __forceinline__ float retrieve_tsdf(const EngineDev& D, int16_t x, in
   return reinterpret_cast<const float*>(r.blk)[r.o];
 }
 
-__global__ __launch_bounds__(256) void k_raycast(EngineDev D, FrameParams P, float step_size,
-                                                 uchar4* __restrict__ rgba,
-                                                 uchar4* __restrict__ normal) {
+__device__ __forceinline__ void raycast(EngineDev D, FrameParams P, float step_size,
+                                        uchar4* __restrict__ rgba, uchar4* __restrict__ normal) {
   const int x = blockIdx.x * 16 + (threadIdx.x & 15);
   const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
   if (x >= P.W || y >= P.H) return;
@@ -199,6 +202,15 @@ __global__ __launch_bounds__(256) void k_raycast(EngineDev D, FrameParams P, flo
   }
   if (rgba) rgba[idx] = make_uchar4(0, 0, 0, 0);
   if (normal) normal[idx] = make_uchar4(0, 0, 0, 0);
+}
+__global__ __launch_bounds__(256) void k_raycast(EngineDev D, FrameParams P, float step_size,
+                                                 uchar4* __restrict__ rgba,
+                                                 uchar4* __restrict__ normal) {
+  raycast(D, P, step_size, rgba, normal);
+}
+__global__ __launch_bounds__(256) void k_raycast_g(EngineDev D, const FrameArgs* __restrict__ A) {
+  const FrameParams R = A->R;
+  raycast(D, R, A->step_size, A->rgba, A->normal);
 }
 
 // download_tsdf_kernel (voxel_tsdf.cu:34-46): one workgroup of 512 threads per selected block

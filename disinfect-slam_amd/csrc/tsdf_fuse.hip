@@ -27,7 +27,12 @@ __device__ __forceinline__ void setu(uint4& v, int j, uint32_t f) {
   if (j == 0) v.x = f; else if (j == 1) v.y = f; else if (j == 2) v.z = f; else v.w = f;
 }
 
-__global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_integrate(EngineDev D, FrameParams P) {
+// 64 VGPRs: 8 waves per SIMD (65 without the bound: 7). Graph: the graph-captured form reads its
+// camera from the FrameArgs block the graph's first node uploads (k_integrate_g).
+template <bool Graph>
+__global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_integrate_t(
+    EngineDev D, FrameParams Pv, const FrameArgs* __restrict__ A) {
+  const FrameParams P = Graph ? A->P : Pv;
   __shared__ float s_min[4];
   __shared__ int s_upd[4];
   const int lane = lane_id();
@@ -234,6 +239,8 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
   }
   TSDF_STAMP(D, 3, 1);
 }
+template __global__ void k_integrate_t<false>(EngineDev, FrameParams, const FrameArgs*);
+template __global__ void k_integrate_t<true>(EngineDev, FrameParams, const FrameArgs*);
 
 // ---------------------------------------------------------------------------------------------
 // k_resolve_delete: VoxelHashTable::Delete (voxel_hash.cu:122-171) for every carve candidate in

@@ -60,7 +60,24 @@ struct EngineDev {
   unsigned long long* dbg;      // diagnostic stamps (DIAG builds), else unused
 };
 
+// per-frame arguments of the graph-captured frame loop (tsdf_graph_*): the graph's first node
+// copies them from a pinned host slot, every graph kernel reads its camera / frame pointers here
+struct FrameArgs {
+  FrameParams P;  // integrate camera (cam_T_world, intrinsics, frame size)
+  FrameParams R;  // render camera of the raycast node
+  const float* depth;
+  const uint8_t* rgb;
+  const float* ht;
+  const float* lt;
+  uchar4* rgba;
+  uchar4* normal;
+  float step_size;  // raycast step (truncation / 2)
+  uint32_t range;   // candidate order space W * H * maxs
+  int tiles_x, tiles;
+};
+
 __global__ void k_init_table(int4* table);
+__global__ void k_copy_words(uint32_t* dst, const uint32_t* src, int n);
 __global__ void k_init_heap(int32_t* heap, int n);
 __global__ void k_init_logodds(uint8_t* pool, int nb);
 // per frame (4 launches)
@@ -68,7 +85,12 @@ constexpr int kVisWorkgroups = kOccWords / 256;  // visibility-sweep workgroups 
 __global__ void k_ingest_dda(EngineDev D, FrameParams P, const float* depth, const uint8_t* rgb,
                              const float* ht, const float* lt, int tiles_x, int tiles);
 __global__ void k_resolve_alloc(EngineDev D, FrameParams P, uint32_t range, int frame_mode);
-__global__ void k_integrate(EngineDev D, FrameParams P);
+template <bool Graph>
+__global__ void k_integrate_t(EngineDev D, FrameParams P, const FrameArgs* A);
+// graph-captured forms of the frame kernels: identical bodies, arguments from FrameArgs
+__global__ void k_ingest_dda_g(EngineDev D, const FrameArgs* A);
+__global__ void k_resolve_alloc_g(EngineDev D, const FrameArgs* A);
+__global__ void k_raycast_g(EngineDev D, const FrameArgs* A);
 __global__ void k_resolve_delete(EngineDev D, const VisRec* recs, const int32_t* count,
                                  int direct);
 // hash-level test path

@@ -173,6 +173,49 @@ def _np(a, dtype):
     return None if a is None else np.ascontiguousarray(a, dtype=dtype)
 
 
+
+class FrameGraph:
+    """One instantiated per-frame hipGraph of an Engine (tsdf_graph_create). frame() takes device
+    tensors only; rgba / normal are device tensors (render_height, render_width, 4) u8 or None."""
+
+    def __init__(self, eng, width, height, render_width=0, render_height=0):
+        self._eng = eng
+        self.width, self.height = width, height
+        self.render_width, self.render_height = render_width, render_height
+        h = C.c_void_p()
+        _lib.check(_lib.load().tsdf_graph_create(eng._h, width, height, render_width, render_height,
+                                                 C.byref(h)), "tsdf_graph_create")
+        self._g = h
+
+    def frame(self, rgb, depth, ht, lt, K, cam_T_world, max_depth, render_K=None,
+              render_cam_T_world=None, rgba=None, normal=None):
+        for a in (rgb, depth, ht, lt, rgba, normal):
+            if a is not None and (not _is_torch_cuda(a) or not a.is_contiguous()):
+                raise ValueError("graph frames take contiguous device tensors")
+        H, W = int(depth.shape[0]), int(depth.shape[1])
+        fr = _lib.Frame(W, H, _ptr(rgb), _ptr(depth), _ptr(ht), _ptr(lt), TSDF_MEM_DEVICE)
+        Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        Rk = None
+        if render_K is not None:
+            Rk = render_K._c() if isinstance(render_K, CameraIntrinsics) else \
+                _lib.Intrinsics(*[float(v) for v in render_K])
+        _lib.check(_lib.load().tsdf_graph_frame(
+            self._g, C.byref(fr), C.byref(Kc), C.byref(cam_T_world._c()), max_depth,
+            C.byref(Rk) if Rk is not None else None,
+            C.byref(render_cam_T_world._c()) if render_cam_T_world is not None else None,
+            _ptr(rgba), _ptr(normal)), "tsdf_graph_frame")
+
+    def close(self):
+        if getattr(self, "_g", None):
+            _lib.load().tsdf_graph_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
 class Engine:
     """One MI355X TSDF volume (one GPU shard). Thin owner of a tsdf_engine* handle."""
 
@@ -277,6 +320,11 @@ class Engine:
                                                     depth_factor, C.byref(Kc), C.byref(cam_T_world._c()),
                                                     max_depth, TSDF_MEM_DEVICE if dev else TSDF_MEM_HOST),
                    "tsdf_feed_rgbd_frame")
+
+    def frame_graph(self, width: int, height: int, render_width: int = 0, render_height: int = 0):
+        """Graph-captured frame loop (tsdf_graph_*, BASELINE config C5): integrate (+ raycast of
+        a render camera) as one hipGraph launch per frame."""
+        return FrameGraph(self, width, height, render_width, render_height)
 
     @staticmethod
     def route_buffer_bytes(shard_count: int, route_cap: int) -> int:

@@ -97,7 +97,7 @@ EXPORTS = [
     "tsdf_pool_acquire", "tsdf_pool_release", "tsdf_pool_set_weight", "tsdf_pool_get_weights",
     "tsdf_hash_block", "tsdf_block_owner", "tsdf_error_string", "tsdf_last_error",
     "tsdf_route_buffer_bytes", "tsdf_integrate_route_begin", "tsdf_integrate_route_end",
-    "tsdf_feed_rgbd_frame", "tsdf_rgbd_half",
+    "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame", "tsdf_graph_destroy",
 ]
 
 _lib = None
@@ -127,6 +127,10 @@ def load(path: str | None = None):
     L.tsdf_integrate_route_end.argtypes = [P, P, C.c_int32]
     L.tsdf_feed_rgbd_frame.argtypes = [P, P, P, P, i, i, f, C.POINTER(Intrinsics), C.POINTER(Pose), f, i]
     L.tsdf_rgbd_half.argtypes = [P, P, P, P, i, i, f, P, P, i]
+    L.tsdf_graph_create.argtypes = [P, i, i, i, i, C.POINTER(P)]
+    L.tsdf_graph_frame.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f,
+                                   C.POINTER(Intrinsics), C.POINTER(Pose), P, P]
+    L.tsdf_graph_destroy.argtypes = [P]
     L.tsdf_query.argtypes = [P, P, P, i64, C.POINTER(i64)]
     L.tsdf_extract_mesh.argtypes = [P, P, f, i, P, i64, C.POINTER(i64), i]
     L.tsdf_get_stats.argtypes = [P, C.POINTER(Stats), i]
@@ -158,7 +162,8 @@ def load(path: str | None = None):
     L.tsdf_last_error.argtypes = []
     for name in ("tsdf_create", "tsdf_destroy", "tsdf_integrate", "tsdf_raycast", "tsdf_query",
                  "tsdf_integrate_route_begin", "tsdf_integrate_route_end",
-                 "tsdf_feed_rgbd_frame", "tsdf_rgbd_half",
+                 "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame",
+                 "tsdf_graph_destroy",
                  "tsdf_extract_mesh",
                  "tsdf_get_stats", "tsdf_synchronize", "tsdf_profile_begin", "tsdf_profile_end",
                  "tsdf_debug_dump", "tsdf_debug_stamps", "tsdf_hash_allocate", "tsdf_hash_delete",

@@ -40,6 +40,7 @@ extern "C" {
 #define TSDF_STATUS_ROUTE_MISROUTED 32u /* an inbox record belongs to another shard */
 
 typedef struct tsdf_engine tsdf_engine;
+typedef struct tsdf_graph tsdf_graph;
 
 typedef struct tsdf_config {
   float voxel_size;   /* [m] TSDFGrid(voxel_size, truncation), voxel_tsdf.cuh:40 */
@@ -156,6 +157,20 @@ int tsdf_feed_rgbd_frame(tsdf_engine* e, const uint8_t* rgb, const uint16_t* dep
 int tsdf_rgbd_half(tsdf_engine* e, const uint8_t* rgb, const uint16_t* depth, const uint8_t* mask,
                    int width, int height, float depth_factor, uint8_t* rgb_out, float* depth_out,
                    int mem_kind);
+
+/* Graph-captured frame loop (BASELINE config C5): TSDFGrid::Integrate (+ optionally RayCast of a
+ * render camera into device buffers) as ONE hipGraph launch per frame, with the same results as
+ * tsdf_integrate + tsdf_raycast(TSDF_MEM_DEVICE). A graph is bound to one engine, one frame size and
+ * one render size (0 x 0 = no raycast). tsdf_graph_frame takes device frames (TSDF_MEM_DEVICE) that
+ * must stay valid until the frame has run (tsdf_synchronize); rgba / normal are device buffers of
+ * render_height x render_width x 4 u8 (either may be NULL). Asynchronous; profiling events are
+ * not recorded for graph frames. */
+int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, int render_height,
+                      tsdf_graph** out);
+int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* frame, const tsdf_intrinsics* K,
+                     const tsdf_pose* cam_T_world, float max_depth, const tsdf_intrinsics* render_K,
+                     const tsdf_pose* render_cam_T_world, uint8_t* rgba, uint8_t* normal);
+int tsdf_graph_destroy(tsdf_graph* g);
 
 /* TSDFGrid::RayCast (voxel_tsdf.cu:490-506; ray_cast_kernel :232-307). rgba / normal are
  * height x width x 4 u8 (either may be NULL), host or device memory per mem_kind. */

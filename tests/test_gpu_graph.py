@@ -1,0 +1,65 @@
+"""Graph-captured frame loop (tsdf_graph_*, BASELINE config C5): one hipGraph launch per frame
+(argument upload, DDA / allocation, update, carving, raycast of a render camera) must give exactly
+what tsdf_integrate + tsdf_raycast give on the same device frames, frame after frame."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("semantic", [True, False])
+def test_graph_loop_matches_eager_calls(semantic):
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H, n = 160, 120, 9
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    fr = synth.render_torch(cam, list(range(n + 3)), device="cuda")
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    a = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=15)
+    b = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=15)
+    g = b.frame_graph(W, H, W, H)
+    try:
+        img = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(4)]
+        hits = 0
+        for i in range(n):
+            pose = tsdf_amd.SE3(fr["q"][i], fr["t"][i])
+            rpose = tsdf_amd.SE3(fr["q"][i + 3], fr["t"][i + 3])
+            ht = fr["ht"][i] if semantic else None
+            lt = fr["lt"][i] if semantic else None
+            a.integrate(fr["rgb"][i], fr["depth"][i], ht, lt, K, pose, 4.0)
+            a.raycast(K, W, H, rpose, 4.0, rgba=img[0], normal=img[1])
+            g.frame(fr["rgb"][i], fr["depth"][i], ht, lt, K, pose, 4.0, K, rpose, img[2], img[3])
+            a.synchronize()
+            b.synchronize()
+            assert torch.equal(img[0], img[2]) and torch.equal(img[1], img[3]), f"frame {i}"
+            hits += int((img[2][..., 3] == 255).sum())
+            sa, sb = a.stats(), b.stats()
+            for k in ("active_blocks", "last_num_visible", "last_num_updated", "last_num_deleted", "status"):
+                assert sa[k] == sb[k], (i, k, sa[k], sb[k])
+        assert hits > W * H  # the render camera sees the surface
+        da, db = a.dump(), b.dump()
+        for k in ("entry_pos", "entry_idx", "heap", "rgbw"):
+            assert np.array_equal(da[k], db[k]), k
+        for k in ("tsdf", "prob"):
+            assert np.array_equal(da[k].view(np.uint32), db[k].view(np.uint32)), k
+    finally:
+        g.close()
+        a.close(), b.close()
+
+
+def test_graph_rejects_host_frames_and_wrong_size():
+    import tsdf_amd
+    from tsdf_amd import synth
+    cam = synth.camera(64, 48, synth.TUM_FR1)
+    fr = synth.render(cam, 0)
+    with tsdf_amd.Engine(0.01, 0.04, max_width=64, max_height=48, num_block_bits=10) as e:
+        g = e.frame_graph(64, 48)
+        try:
+            with pytest.raises(ValueError):
+                g.frame(fr["rgb"], fr["depth"], None, None, cam.K, tsdf_amd.SE3(fr["q"], fr["t"]), 4.0)
+        finally:
+            g.close()
+        with pytest.raises(tsdf_amd.TSDFError):
+            e.frame_graph(128, 48)
