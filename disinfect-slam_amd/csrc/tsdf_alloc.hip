@@ -395,16 +395,23 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
   __shared__ ResolveLds L;
   const int t = threadIdx.x;
   TSDF_STAMP(D, 1, 0);
+  // the counters are loaded together (one memory round trip) before anything waits on them
+  const int n = D.ctr->nk_count;
+  uint32_t epoch0 = 0u;
+  int free0 = 0;
   if (t == 0) {
-    L.epoch = D.ctr->lock_epoch + 1;
-    D.ctr->lock_epoch = L.epoch;
-    L.sfree = D.ctr->free_count;
-    L.nfresh = 0;
-    L.nalloc = 0;
+    epoch0 = D.ctr->lock_epoch;
+    free0 = D.ctr->free_count;
   }
   claims_clear(L);
   if (t < kBands) L.bcnt[t] = 0;
-  const int n = D.ctr->nk_count;
+  if (t == 0) {
+    L.epoch = epoch0 + 1;
+    D.ctr->lock_epoch = L.epoch;
+    L.sfree = free0;
+    L.nfresh = 0;
+    L.nalloc = 0;
+  }
   // (order, slot) pairs in a compact scratch array so every batch pass is one coalesced read
   for (int i = t; i < n; i += kResolveThreads) {
     const int h = D.nk_list[i];

@@ -255,35 +255,48 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
                                                                     const int32_t* __restrict__ count,
                                                                     int direct) {
   __shared__ ResolveLds L;
+  __shared__ unsigned long long s_te[kResolveThreads / 64];
   const int t = threadIdx.x;
   TSDF_STAMP(D, 4, 0);
+  // every global value the prologue needs is loaded up front, so they share one memory round
+  // trip instead of four dependent ones (counters, per-workgroup sums, candidate count)
+  const int n = *count;
+  uint32_t epoch0 = 0u;
+  int free0 = 0;
+  unsigned long long t_start = 0ull;
   if (t == 0) {
-    L.epoch = D.ctr->lock_epoch + 1;
-    D.ctr->lock_epoch = L.epoch;
-    L.sfree = D.ctr->free_count;
-    L.nalloc = 0;  // deletions
+    epoch0 = D.ctr->lock_epoch;
+    free0 = D.ctr->free_count;
+    if (!direct) t_start = D.wg_end[kIntegrateGrid];
   }
-  claims_clear(L);
-  if (!direct) {  // voxels updated by k_integrate: sum of its per-workgroup counts
-    __shared__ unsigned long long s_tend;
-    if (t == 0) s_tend = 0ull;
-    __syncthreads();
-    int u = 0;
-    unsigned long long te = 0ull;
+  int u = 0;
+  unsigned long long te = 0ull;
+  if (!direct)  // voxels updated by k_integrate: sum of its per-workgroup counts
     for (int i = t; i < D.integrate_grid; i += kResolveThreads) {
       u += D.wg_upd[i];
       te = max(te, D.wg_end[i]);
     }
-    atomicMax(&s_tend, te);
+  claims_clear(L);
+  if (t == 0) {
+    L.epoch = epoch0 + 1;
+    D.ctr->lock_epoch = L.epoch;
+    L.sfree = free0;
+    L.nalloc = 0;  // deletions
+  }
+  if (!direct) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) te = max(te, (unsigned long long)__shfl_xor(te, o, 64));
+    if ((t & 63) == 0) s_te[t >> 6] = te;
     int tot;
-    (void)block_excl_scan(u, L.scan, &tot);  // (its barriers also publish s_tend)
+    (void)block_excl_scan(u, L.scan, &tot);  // (its barriers also publish s_te)
     if (t == 0) {
+      unsigned long long tend = 0ull;
+      for (int w = 0; w < kResolveThreads / 64; ++w) tend = max(tend, s_te[w]);
       D.ctr->last_updated = (unsigned long long)tot;
-      D.ctr->integrate_ticks += s_tend - D.wg_end[kIntegrateGrid];
+      D.ctr->integrate_ticks += tend - t_start;
     }
   }
   __syncthreads();
-  const int n = *count;
   auto keyf = [&](int i) -> uint32_t { return (uint32_t)recs[i].entry; };
   const int width = direct ? 1 : stream_prepare(L, n, kNumEntry, keyf);
   const int nbatch = direct ? n : (n <= kBatch ? (n > 0 ? 1 : 0) : ((n - 1) >> 10) + 1);

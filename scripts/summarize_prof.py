@@ -30,6 +30,14 @@ def bench_line(path):
     return None
 
 
+def kname(full):
+    """Short kernel name: 'tsdf::k_x(args)' / 'void tsdf::k_integrate_t<false>(args)' -> 'k_x' /
+    'k_integrate' (the eager instantiation; the graph one is 'k_integrate_graph')."""
+    n = full.split("(")[0].replace("tsdf::", "")
+    n = re.sub(r"^void ", "", n)
+    return n.replace("k_integrate_t<false>", "k_integrate").replace("k_integrate_t<true>", "k_integrate_graph")
+
+
 def main(out):
     res = {"kernels": {}, "pmc": {}}
     st = find(os.path.join(out, "trace", "**", "*kernel_stats.csv"))
@@ -37,7 +45,7 @@ def main(out):
         for r in csv.DictReader(open(st)):
             if not re.search(r"tsdf::", r["Name"]):
                 continue
-            name = r["Name"].split("(")[0].replace("tsdf::", "")
+            name = kname(r["Name"])
             res["kernels"][name] = {
                 "calls": int(r["Calls"]),
                 "avg_us": float(r["AverageNs"]) / 1e3,
@@ -51,7 +59,7 @@ def main(out):
     b0 = bench_line(os.path.join(out, "trace_bench.log"))
     if tr and b0:
         durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(tr))
-                if r["Kernel_Name"].split("(")[0].endswith("tsdf::k_integrate")]
+                if kname(r["Kernel_Name"]) == "k_integrate"]
         w, k = b0["warmup"], b0["steps"]
         win = durs[w:w + k]
         if win:
@@ -66,7 +74,7 @@ def main(out):
             kn = r.get("Kernel_Name", "")
             if "tsdf::" not in kn or r.get("Counter_Name") != c:
                 continue
-            name = kn.split("(")[0].replace("tsdf::", "")
+            name = kname(kn)
             vals.setdefault(name, []).append(float(r["Counter_Value"]))
         for name, v in vals.items():
             kib = statistics.mean(v)

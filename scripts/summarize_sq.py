@@ -6,6 +6,7 @@ import csv
 import glob
 import json
 import os
+import re
 import statistics
 import sys
 
@@ -17,7 +18,7 @@ def main(out):
             kn = r.get("Kernel_Name", "")
             if "tsdf::" not in kn:
                 continue
-            name = kn.split("(")[0].replace("tsdf::", "")
+            name = re.sub(r"^void ", "", kn.split("(")[0].replace("tsdf::", "")).replace("k_integrate_t<false>", "k_integrate")
             vals.setdefault(name, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     res = {k: {c: statistics.mean(v) for c, v in cs.items()} for k, cs in vals.items()}
     for k, c in res.items():

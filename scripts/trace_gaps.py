@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-frame kernel timeline of a `rocprofv3 --kernel-trace` run of bench.py:
-   scripts/trace_gaps.py <trace dir> [frames]
-Takes the last `frames` occurrences of the per-frame kernel sequence (the bench's timed window)
+   scripts/trace_gaps.py <trace dir> [frames] [first]
+Takes `frames` occurrences from frame index `first` (default: the last `frames`) of the per-frame kernel sequence (the bench's timed window)
 and prints each kernel's average duration and the average idle gap before it, plus the frame
 period -- where the frame time goes beyond the kernels themselves (launch gaps)."""
 import csv
@@ -11,14 +11,15 @@ import sys
 from collections import defaultdict
 
 
-def main(d, frames=200):
+def main(d, frames=200, first=None):
     f = glob.glob(d + "/**/*kernel_trace.csv", recursive=True)[0]
     rows = [r for r in csv.DictReader(open(f)) if "tsdf::" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    name = lambda r: r["Kernel_Name"].split("(")[0].replace("tsdf::", "").split("<")[0]
+    name = lambda r: r["Kernel_Name"].split("(")[0].replace("tsdf::", "").replace("void ", "").split("<")[0].replace(
+        "k_integrate_t", "k_integrate")
     # the frame starts with k_ingest_dda
     starts = [i for i, r in enumerate(rows) if name(r) == "k_ingest_dda"]
-    starts = starts[-(frames + 1):]
+    starts = starts[-(frames + 1):] if first is None else starts[first:first + frames + 1]
     dur, gap = defaultdict(list), defaultdict(list)
     periods = []
     for a, b in zip(starts, starts[1:]):
@@ -41,4 +42,5 @@ def main(d, frames=200):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 200)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 200,
+         int(sys.argv[3]) if len(sys.argv) > 3 else None)

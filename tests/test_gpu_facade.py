@@ -92,3 +92,31 @@ def test_disinf_system_feed_rgbd_frame(tmp_path):
     frames, active, status = map(int, (tmp_path / "out_stats.txt").read_text().split())
     assert (frames, active, status) == (n, ora.stats()["active_blocks"], 0)
     ora.close()
+
+
+@pytest.mark.parametrize("semantic", [True, False])
+def test_offline_replay_matches_oracle(tmp_path, semantic):
+    """examples/tsdf/offline.cc's loop (host/offline_log.cc + TSDFGrid via offline_main): a log
+    directory of PNG frames + trajectory.txt replayed on the GPU == the oracle fed the decoded
+    frames (absent ht maps read as ht = 0, lt = 1, offline.cc:80-81)."""
+    from _oracle import OracleGrid
+    from _png import se3_from_matrix
+    from test_host_cpu import _write_log, expected_frame
+    cam, frames = _write_log(tmp_path, n=4, W=96, H=72, semantic=semantic)
+    ora = OracleGrid(0.01, 0.04, 13)
+    for f in frames:
+        rgb, depth, ht, lt = expected_frame(f)
+        q, t = se3_from_matrix(f["m"])
+        ora.integrate(rgb, depth, ht, lt, 4.0, cam.K, q, t)
+    binp = os.path.join(ROOT, "disinfect-slam_amd", "offline_main")
+    K = [repr(float(v)) for v in cam.K]
+    r = subprocess.run([binp, str(tmp_path), *K, "5000", "0.01", "0.04", "13"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.fromfile(tmp_path / "out_query.bin", np.float32).reshape(-1, 4)
+    exp = ora.query(None)
+    assert got.shape == exp.shape and got.shape[0] > 0
+    np.testing.assert_array_equal(got.view(np.uint32), exp.view(np.uint32))
+    frames_n, active, status = map(int, (tmp_path / "out_stats.txt").read_text().split())
+    assert (frames_n, active, status) == (len(frames), ora.stats()["active_blocks"], 0)
+    ora.close()
