@@ -55,16 +55,19 @@ __device__ void rt_insert(const EngineDev& D, uint64_t key, uint32_t order) {
 // tile otherwise). In a routed frame visible keys owned by another shard go to the route set
 // (k_route_pack sends them to their owner) instead of being dropped.
 // ---------------------------------------------------------------------------------------------
-constexpr int kTileSlots = 2048;  // > 256 pixels x maxs (<= 6, checked by tsdf_create)
+// LDS key-set slots per 16x16 tile: TS > 256 pixels x maxs. 1024 for maxs <= 3 (the reference's
+// 6x truncation / voxel ratio: 2-3 samples per pixel) keeps the workgroup at 16.5 KiB of LDS, so 9
+// workgroups fit a CU and the whole 640x480 grid is resident at once; 2048 up to maxs = 6.
 constexpr int kVisChunk = 1024;   // visibility sweep: 16 occupancy words x 64 entries per wave
 static_assert(kBands == 16, "ResolveLds band arrays");
 
 // the two roles of k_ingest_dda share one LDS allocation
+template <int TS>
 union IngestLds {
   struct {
-    unsigned long long key[kTileSlots];
-    uint32_t ord[kTileSlots];
-    uint16_t vis[4][kTileSlots / 4];
+    unsigned long long key[TS];
+    uint32_t ord[TS];
+    uint16_t vis[4][TS / 4];
   } tile;
   struct {
     uint32_t list[4][kVisChunk];
@@ -83,7 +86,8 @@ union IngestLds {
 // blocks it creates. Order within a list is irrelevant to the update; the carving resolver
 // restores the reference's entry order for the deletes.
 // ---------------------------------------------------------------------------------------------
-__device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, IngestLds& S) {
+template <int TS>
+__device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, IngestLds<TS>& S) {
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   uint32_t* L = S.sweep.list[wave];
   int* s_cnt = S.sweep.cnt;
@@ -156,12 +160,13 @@ __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, Inge
 
 // grid: kVisWorkgroups sweep workgroups first (dispatched first, they overlap the tiles), then
 // one workgroup per 16x16 pixel tile (tiles_x per row, `tiles` in all)
+template <int TS>
 __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
                                            const float* __restrict__ depth,
                                            const uint8_t* __restrict__ rgb,
                                            const float* __restrict__ ht,
                                            const float* __restrict__ lt, int tiles_x, int tiles) {
-  __shared__ IngestLds S;
+  __shared__ IngestLds<TS> S;
   if ((int)blockIdx.x < kVisWorkgroups) {
     TSDF_STAMP(D, 2, 0);
     vis_sweep(D, P, blockIdx.x, S);
@@ -173,7 +178,7 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
   unsigned long long* s_key = S.tile.key;
   uint32_t* s_ord = S.tile.ord;
   TSDF_STAMP(D, 0, 0);
-  for (int i = threadIdx.x; i < kTileSlots; i += 256) {
+  for (int i = threadIdx.x; i < TS; i += 256) {
     s_key[i] = 0ull;
     s_ord[i] = 0xFFFFFFFFu;
   }
@@ -224,14 +229,14 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
         pos.z += st.z;
         const unsigned long long key = pack_key(kx, ky, kz);
         const uint32_t order = (uint32_t)i * (uint32_t)P.maxs + (uint32_t)s;
-        uint32_t hs = (uint32_t)mix64(key) & (kTileSlots - 1);
-        for (int p = 0; p < kTileSlots; ++p) {
+        uint32_t hs = (uint32_t)mix64(key) & (TS - 1);
+        for (int p = 0; p < TS; ++p) {
           const unsigned long long prev = atomicCAS(&s_key[hs], 0ull, key);
           if (prev == 0ull || prev == key) {
             atomicMin(&s_ord[hs], order);
             break;
           }
-          hs = (hs + 1) & (kTileSlots - 1);
+          hs = (hs + 1) & (TS - 1);
         }
       }
     }
@@ -244,11 +249,11 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
   // 8 at a time with 8 lanes per key, one block corner per lane (is_block_visible<true>), and the
   // fully visible ones are listed in LDS. The table probes and new-key inserts then run one key
   // per lane over that list, so the wave pays their memory latency once, not once per 8 keys.
-  uint16_t(*s_vis)[kTileSlots / 4] = S.tile.vis;
+  uint16_t(*s_vis)[TS / 4] = S.tile.vis;
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   const int grp = lane >> 3, corner = lane & 7;
   int nv = 0;
-  for (int strip = wave; strip < kTileSlots / 64; strip += 4) {
+  for (int strip = wave; strip < TS / 64; strip += 4) {
     const unsigned long long skey = s_key[strip * 64 + lane];
     const unsigned long long occ = __ballot(skey != 0ull);
     const int n = __popcll(occ);
@@ -289,18 +294,26 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
   }
   TSDF_STAMP(D, 0, 5);
 }
+template <int TS>
 __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
                                                     const float* __restrict__ depth,
                                                     const uint8_t* __restrict__ rgb,
                                                     const float* __restrict__ ht,
                                                     const float* __restrict__ lt, int tiles_x,
                                                     int tiles) {
-  ingest_dda(D, P, depth, rgb, ht, lt, tiles_x, tiles);
+  ingest_dda<TS>(D, P, depth, rgb, ht, lt, tiles_x, tiles);
 }
+template <int TS>
 __global__ __launch_bounds__(256) void k_ingest_dda_g(EngineDev D, const FrameArgs* __restrict__ A) {
   const FrameParams P = A->P;
-  ingest_dda(D, P, A->depth, A->rgb, A->ht, A->lt, A->tiles_x, A->tiles);
+  ingest_dda<TS>(D, P, A->depth, A->rgb, A->ht, A->lt, A->tiles_x, A->tiles);
 }
+template __global__ void k_ingest_dda<1024>(EngineDev, FrameParams, const float*, const uint8_t*, const float*,
+                                            const float*, int, int);
+template __global__ void k_ingest_dda<2048>(EngineDev, FrameParams, const float*, const uint8_t*, const float*,
+                                            const float*, int, int);
+template __global__ void k_ingest_dda_g<1024>(EngineDev, const FrameArgs*);
+template __global__ void k_ingest_dda_g<2048>(EngineDev, const FrameArgs*);
 
 // ---------------------------------------------------------------------------------------------
 // Routed frames (SURVEY.md 8e option 2). k_route_pack drains the route set into the outbox, one

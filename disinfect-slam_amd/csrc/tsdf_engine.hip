@@ -479,8 +479,12 @@ int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, 
   // ---- allocate (voxel_tsdf.cu:377-386) + visibility (:388-397) ----
   // k_ingest_dda sweeps the blocks that already exist for visibility beside the DDA; the
   // resolver inserts the new keys and appends the blocks it creates to the visible lists
-  hipLaunchKernelGGL(k_ingest_dda, dim3(kVisWorkgroups + tiles), dim3(256), 0, s, e->D, *P, depth,
-                     rgb, ht, lt, tiles_x, tiles);
+  if (e->maxs <= 3)
+    hipLaunchKernelGGL(k_ingest_dda<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, s, e->D, *P, depth,
+                       rgb, ht, lt, tiles_x, tiles);
+  else
+    hipLaunchKernelGGL(k_ingest_dda<2048>, dim3(kVisWorkgroups + tiles), dim3(256), 0, s, e->D, *P, depth,
+                       rgb, ht, lt, tiles_x, tiles);
   LAUNCH_OK("k_ingest_dda");
   return TSDF_OK;
 }
@@ -642,7 +646,10 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
     else  // one wave reads the pinned slot over the fabric: a kernel node, no DMA engine in the graph
       hipLaunchKernelGGL(k_copy_words, dim3(1), dim3(64), 0, g->cap, reinterpret_cast<uint32_t*>(g->d_args + k),
                          reinterpret_cast<const uint32_t*>(g->h_args + k), (int)(sizeof(FrameArgs) / 4));
-    hipLaunchKernelGGL(k_ingest_dda_g, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
+    if (e->maxs <= 3)
+      hipLaunchKernelGGL(k_ingest_dda_g<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
+    else
+      hipLaunchKernelGGL(k_ingest_dda_g<2048>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
     hipLaunchKernelGGL(k_resolve_alloc_g, dim3(1), dim3(kResolveThreads), 0, g->cap, e->D, A);
     hipLaunchKernelGGL(k_integrate_t<true>, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, g->cap, e->D,
                        FrameParams{}, A);

@@ -82,12 +82,14 @@ __global__ void k_init_heap(int32_t* heap, int n);
 __global__ void k_init_logodds(uint8_t* pool, int nb);
 // per frame (4 launches)
 constexpr int kVisWorkgroups = kOccWords / 256;  // visibility-sweep workgroups of k_ingest_dda
+template <int TS>  // LDS key-set slots per tile (tsdf_alloc.hip): 1024 for maxs <= 3, else 2048
 __global__ void k_ingest_dda(EngineDev D, FrameParams P, const float* depth, const uint8_t* rgb,
                              const float* ht, const float* lt, int tiles_x, int tiles);
 __global__ void k_resolve_alloc(EngineDev D, FrameParams P, uint32_t range, int frame_mode);
 template <bool Graph>
 __global__ void k_integrate_t(EngineDev D, FrameParams P, const FrameArgs* A);
 // graph-captured forms of the frame kernels: identical bodies, arguments from FrameArgs
+template <int TS>
 __global__ void k_ingest_dda_g(EngineDev D, const FrameArgs* A);
 __global__ void k_resolve_alloc_g(EngineDev D, const FrameArgs* A);
 __global__ void k_raycast_g(EngineDev D, const FrameArgs* A);
