@@ -72,6 +72,7 @@ union IngestLds {
   struct {
     uint32_t list[4][kVisChunk];
     int cnt[kBands], base[kBands];
+    int npass;
   } sweep;
 };
 
@@ -80,8 +81,10 @@ union IngestLds {
 // the 512 KiB occupancy bitmap instead of the 48 MiB table: every allocated block with any corner
 // in view (no depth test) is appended to the list of the image band its centre projects into
 // (LDS counts, one global atomic per band per pass). Workgroup `wg` covers occupancy words
-// [256 wg, 256 wg + 256); each wave compacts 16 words at a time into LDS so the corner tests run
-// 8 lanes per block on dense work. It runs inside k_ingest_dda, before allocation: it sees the
+// [256 wg, 256 wg + 256), 64 per wave, one per lane; each wave compacts the live entries of its
+// words into LDS so the corner tests run 8 lanes per block on dense work, in passes of at most
+// kVisChunk entries (one pass at the bench's ~1 % table occupancy; each pass costs three dependent
+// global round trips). It runs inside k_ingest_dda, before allocation: it sees the
 // blocks that existed after the previous frame's carving, and k_resolve_alloc appends the
 // blocks it creates. Order within a list is irrelevant to the update; the carving resolver
 // restores the reference's entry order for the deletes.
@@ -93,18 +96,29 @@ __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, Inge
   int* s_cnt = S.sweep.cnt;
   int* s_base = S.sweep.base;
   const int grp = lane >> 3, corner = lane & 7;
-  for (int pass = 0; pass < 4; ++pass) {
+  const int w = wg * 256 + wave * 64 + lane;
+  const unsigned long long occ_all = D.occ[w];
+  const int cw = __popcll(occ_all);
+  const int incl = wave_incl_scan(cw);
+  const int excl = incl - cw;
+  const int wave_total = __shfl(incl, 63, 64);
+  if (threadIdx.x == 0) S.sweep.npass = 0;
+  __syncthreads();
+  if (lane == 0) atomicMax(&S.sweep.npass, (wave_total + kVisChunk - 1) / kVisChunk);
+  __syncthreads();
+  const int npass = S.sweep.npass;
+  for (int pass = 0; pass < npass; ++pass) {
     if (threadIdx.x < kBands) s_cnt[threadIdx.x] = 0;
-    const int w = wg * 256 + wave * 64 + pass * 16 + (lane & 15);
-    unsigned long long occ = lane < 16 ? D.occ[w] : 0ull;
-    const int c = __popcll(occ);
-    const int incl = wave_incl_scan(c);
-    const int total = __shfl(incl, 63, 64);
-    int p = incl - c;
-    while (occ) {
-      const int b = __ffsll((long long)occ) - 1;
-      occ &= occ - 1;
-      L[p++] = (uint32_t)(w * 64 + b);
+    // this pass lists the wave's live entries of rank [lo, lo + kVisChunk)
+    const int lo = pass * kVisChunk;
+    const int total = min(max(wave_total - lo, 0), kVisChunk);
+    if (excl < lo + kVisChunk && incl > lo) {
+      unsigned long long occ = occ_all;
+      for (int r = excl; occ; ++r) {
+        const int b = __ffsll((long long)occ) - 1;
+        occ &= occ - 1;
+        if (r >= lo && r < lo + kVisChunk) L[r - lo] = (uint32_t)(w * 64 + b);
+      }
     }
     __syncthreads();
     // any-corner visibility (is_block_visible<false>), 8 lanes per block, one corner each; the
