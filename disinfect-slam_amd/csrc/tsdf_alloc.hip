@@ -424,12 +424,9 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
   TSDF_STAMP(D, 1, 0);
   // the counters are loaded together (one memory round trip) before anything waits on them
   const int n = D.ctr->nk_count;
+  const int free0 = D.ctr->free_count;  // every thread: the pops index the stack top by it
   uint32_t epoch0 = 0u;
-  int free0 = 0;
-  if (t == 0) {
-    epoch0 = D.ctr->lock_epoch;
-    free0 = D.ctr->free_count;
-  }
+  if (t == 0) epoch0 = D.ctr->lock_epoch;
   claims_clear(L);
   if (t < kBands) L.bcnt[t] = 0;
   if (t == 0) {
@@ -439,20 +436,41 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
     L.nfresh = 0;
     L.nalloc = 0;
   }
-  // (order, slot) pairs in a compact scratch array so every batch pass is one coalesced read
-  for (int i = t; i < n; i += kResolveThreads) {
-    const int h = D.nk_list[i];
-    D.pairs[i] = ((unsigned long long)D.nk_order[h] << 32) | (uint32_t)h;
-    D.pkey[i] = D.nk_key[h];
+  // One batch (the common case): (candidate order, list index) straight into the LDS batch, keys
+  // and set slots into LDS, plus the free-stack top the pops will read -- all in one round trip.
+  // Otherwise (order, slot) pairs go to a compact scratch array so every batch pass is one
+  // coalesced read.
+  const bool single = n <= kBatch;
+  if (single) {
+    const int npre = min(n, free0);
+    for (int i = t; i < npre; i += kResolveThreads) L.heap_top[i] = D.heap[free0 - 1 - i];
+    for (int i = t; i < n; i += kResolveThreads) {
+      const int h = D.nk_list[i];
+      L.batch[i] = ((unsigned long long)D.nk_order[h] << 32) | (uint32_t)i;
+      L.skey[i] = D.nk_key[h];
+      L.sslot[i] = h;
+    }
+  } else {
+    for (int i = t; i < n; i += kResolveThreads) {
+      const int h = D.nk_list[i];
+      D.pairs[i] = ((unsigned long long)D.nk_order[h] << 32) | (uint32_t)h;
+      D.pkey[i] = D.nk_key[h];
+    }
   }
   __syncthreads();
   auto keyf = [&](int i) -> uint32_t { return (uint32_t)(D.pairs[i] >> 32); };
-  const int width = stream_prepare(L, n, range, keyf);
-  const int nbatch = n <= kBatch ? (n > 0 ? 1 : 0) : ((n - 1) >> 10) + 1;
+  const int width = single ? 1 : stream_prepare(L, n, range, keyf);
+  const int nbatch = single ? (n > 0 ? 1 : 0) : ((n - 1) >> 10) + 1;
   int rounds = 0;
   TSDF_STAMP(D, 1, 1);
   for (int j = 0; j < nbatch; ++j) {
-    const int m = stream_batch(L, n, width, j, keyf);
+    int m;
+    if (single) {
+      m = n;
+      batch_sort(L, m, true);
+    } else {
+      m = stream_batch(L, n, width, j, keyf);
+    }
     TSDF_STAMP(D, 1, 2);
     if (t == 0) L.base = 0;
     __syncthreads();
@@ -469,8 +487,13 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
       int16_t kx = 0, ky = 0, kz = 0;
       if (have) {
         const int li = (int)(L.batch[base + t] & 0xFFFFFFFFu);
-        h = (int)(D.pairs[li] & 0xFFFFFFFFu);
-        unpack_key(D.pkey[li], kx, ky, kz);
+        if (single) {
+          h = L.sslot[li];
+          unpack_key(L.skey[li], kx, ky, kz);
+        } else {
+          h = (int)(D.pairs[li] & 0xFFFFFFFFu);
+          unpack_key(D.pkey[li], kx, ky, kz);
+        }
         B = hash_block(kx, ky, kz);
         const Ent s0 = load_ent(D.table, 2 * B);
         const Ent s1 = load_ent(D.table, 2 * B + 1);
@@ -542,7 +565,8 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
         if (hi < 0) {
           atomicOr(&D.ctr->status, 1u);  // TSDF_STATUS_POOL_EXHAUSTED: insert dropped
         } else {
-          const int32_t idx = D.heap[hi];
+          const int top = free0 - 1 - hi;  // pops so far this launch + rank
+          const int32_t idx = single ? L.heap_top[top] : D.heap[hi];
           uint32_t e;
           if (kind == 1) {
             e = 2 * B + (uint32_t)slot;

@@ -87,6 +87,11 @@ struct ResolveLds {
   uint32_t epoch;
   int bcnt[16];                       // new blocks per visible-list band this round (frame mode)
   int bbase[16];                      // their base in the band list
+  // single-batch allocation resolves (n <= kBatch): the new keys, their key-set slots and the
+  // free-stack top, loaded once by the prologue instead of re-read from HBM every round
+  unsigned long long skey[kBatch];
+  int32_t sslot[kBatch];
+  int32_t heap_top[kBatch];           // heap_top[i] = heap[free - 1 - i]
 };
 
 __device__ __forceinline__ void lds_bitonic_sort(unsigned long long* a, int m) {
@@ -171,6 +176,7 @@ __device__ int stream_prepare(ResolveLds& L, int n, uint32_t range, KeyFn keyf) 
   return (int)width;
 }
 
+__device__ __forceinline__ void batch_sort(ResolveLds& L, int m, bool single);
 // Gather batch `j` (elements whose window prefix >> 10 == j, or all when n <= kBatch) into
 // L.batch sorted ascending by key; returns its size.
 template <typename KeyFn>
@@ -186,7 +192,14 @@ __device__ int stream_batch(ResolveLds& L, int n, int width, int j, KeyFn keyf) 
   }
   __syncthreads();
   const int m = L.count < kBatch ? L.count : kBatch;  // bounded by construction (width <= 1024)
-  if (n <= kBatch && m <= kRankSortMax) {
+  batch_sort(L, m, n <= kBatch);
+  return m;
+}
+
+// Sort L.batch[0..m) ascending (unique keys); single: the list is one batch, so L.hist is free
+// as the rank sort's scratch.
+__device__ __forceinline__ void batch_sort(ResolveLds& L, int m, bool single) {
+  if (single && m <= kRankSortMax) {
     // single batch (hist unused): rank sort -- every element counts the smaller ones with
     // broadcast LDS reads, one barrier instead of bitonic's log^2 stages (keys are unique)
     unsigned long long* tmp = reinterpret_cast<unsigned long long*>(L.hist);
@@ -203,7 +216,6 @@ __device__ int stream_batch(ResolveLds& L, int n, int width, int j, KeyFn keyf) 
   } else {
     lds_bitonic_sort(L.batch, m);
   }
-  return m;
 }
 
 }  // namespace tsdf
