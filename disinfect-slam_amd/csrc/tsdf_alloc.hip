@@ -428,7 +428,6 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
   uint32_t epoch0 = 0u;
   if (t == 0) epoch0 = D.ctr->lock_epoch;
   claims_clear(L);
-  if (t < kBands) L.bcnt[t] = 0;
   if (t == 0) {
     L.epoch = epoch0 + 1;
     D.ctr->lock_epoch = L.epoch;
@@ -558,8 +557,6 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
       int nok;
       const int rank = block_excl_scan(ok ? 1 : 0, L.scan, &nok);
       const int free_now = L.sfree;
-      VisRec vr{};
-      int vband = -1, vrank = 0;
       if (ok) {
         const int hi = free_now - 1 - rank;
         if (hi < 0) {
@@ -578,17 +575,17 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
           store_ent(D.table, e, kx, ky, kz, 0, idx);
           atomicOr(&D.occ[e >> 6], 1ull << (e & 63));
           if (frame_mode) {
-            // a new block has all 8 corners in view, so it is visible this frame: appended to
-            // its band list below (the sweep in k_ingest_dda saw only the blocks that existed
-            // before), flagged fresh so k_integrate starts it from AquireBlock's state
+            // a new block has all 8 corners in view, so it is visible this frame: listed for the
+            // fresh-block integrate launch (the sweep in k_ingest_dda listed only the blocks that
+            // existed before), flagged fresh so it starts from AquireBlock's state
+            VisRec vr;
             vr.x = kx;
             vr.y = ky;
             vr.z = kz;
             vr.pad = 1;
             vr.idx = idx;
             vr.entry = (int32_t)e;
-            vband = block_band(P, kx, ky, kz);
-            vrank = atomicAdd(&L.bcnt[vband], 1);
+            D.fresh_vis[L.nfresh + rank] = vr;
           } else {
             D.fresh[L.nfresh + rank] = idx;
           }
@@ -600,11 +597,6 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
       }
       claims_clear(L);
       __syncthreads();
-      if (frame_mode && t < kBands) {  // one global append per non-empty band per round
-        const int c = L.bcnt[t];
-        L.bbase[t] = c ? atomicAdd(&D.band[t * kBandStride], c) : 0;
-        L.bcnt[t] = 0;
-      }
       if (t == 0) {
         const int used = nok < free_now ? nok : (free_now > 0 ? free_now : 0);
         L.sfree = free_now - used;
@@ -614,10 +606,10 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
         L.base = base + (first_dirty < span ? first_dirty : span);
       }
       __syncthreads();
-      if (vband >= 0) D.vis[(size_t)vband * D.nblocks + L.bbase[vband] + vrank] = vr;
     }
   }
   TSDF_STAMP(D, 1, 3);
+  __syncthreads();  // every thread's table / list writes precede the release below
   if (t == 0) {
     D.ctr->free_count = L.sfree;
     D.ctr->n_fresh = L.nfresh;
@@ -626,8 +618,6 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
       D.ctr->last_alloc = L.nalloc;
       D.ctr->last_new_keys = n;
       D.ctr->total_alloc += (unsigned long long)L.nalloc;
-      D.ctr->last_updated = 0ull;
-      D.ctr->n_vis = 0;
     }
   }
 }

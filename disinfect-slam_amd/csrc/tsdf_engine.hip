@@ -335,11 +335,12 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.vis, (size_t)kBands * nb);
   ALLOC(D.band, kBands * kBandStride);
   ALLOC(D.cand, nb);
-  ALLOC(D.wg_upd, kIntegrateGrid);
-  ALLOC(D.wg_end, kIntegrateGrid + 1);
+  ALLOC(D.wg_upd, 2 * kIntegrateGrid);
+  ALLOC(D.wg_end, 2 * kIntegrateGrid + 1);
+  ALLOC(D.fresh_vis, kNewKeyCap);
   {  // one resident wave of k_integrate workgroups: no second-round stragglers
     int per_cu = 0, ncu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate_t<false>, kIntegrateThreads, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate_t<false, false>, kIntegrateThreads, 0) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
       return fail(TSDF_ERR_HIP);
     if (const char* v = std::getenv("TSDF_INTEGRATE_WG_PER_CU")) per_cu = std::min(per_cu, std::atoi(v));  // tuning
@@ -490,6 +491,10 @@ int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, 
 }
 
 // Phase 2: ordered allocation of the new keys -> fused update -> space carving.
+// (Measured and not kept: running the update of the existing blocks beside k_resolve_alloc, on a
+// second stream or as a dispatch without the AQL barrier bit that waits on a release flag for the
+// new blocks. The resolver's chain of dependent HBM round trips slows ~2.5x under the update's
+// memory load, and the stream fork / join costs more than it hides: 15-16k frames/s against 18k.)
 int frame_finish(tsdf_engine* e, const FrameParams& P, std::array<hipEvent_t, 5>* ev) {
   hipStream_t s = e->stream;
   const bool all_ev = ev && e->prof_mode == TSDF_PROFILE_PHASES;
@@ -500,12 +505,12 @@ int frame_finish(tsdf_engine* e, const FrameParams& P, std::array<hipEvent_t, 5>
   if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
     // the two events are bound to the kernel's own dispatch packet (its begin / end timestamps,
     // the interval rocprofv3's kernel trace reports): no marker packets enter the stream
-    hipExtLaunchKernelGGL(k_integrate_t<false>, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
+    hipExtLaunchKernelGGL(k_integrate_t<false, false>, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
                           (*ev)[2], (*ev)[3], 0, e->D, P, (const FrameArgs*)nullptr);
   } else {
     if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
-    hipLaunchKernelGGL(k_integrate_t<false>, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s, e->D, P,
-                       (const FrameArgs*)nullptr);
+    hipLaunchKernelGGL((k_integrate_t<false, false>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
+                       e->D, P, (const FrameArgs*)nullptr);
     if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
   }
   LAUNCH_OK("k_integrate");
@@ -651,8 +656,8 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
     else
       hipLaunchKernelGGL(k_ingest_dda_g<2048>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
     hipLaunchKernelGGL(k_resolve_alloc_g, dim3(1), dim3(kResolveThreads), 0, g->cap, e->D, A);
-    hipLaunchKernelGGL(k_integrate_t<true>, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, g->cap, e->D,
-                       FrameParams{}, A);
+    hipLaunchKernelGGL((k_integrate_t<true, false>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, g->cap,
+                       e->D, FrameParams{}, A);
     hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kResolveThreads), 0, g->cap, e->D, e->D.cand,
                        &e->D.ctr->n_cand, 0);
     if (render_width)

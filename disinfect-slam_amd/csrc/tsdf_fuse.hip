@@ -28,8 +28,10 @@ __device__ __forceinline__ void setu(uint4& v, int j, uint32_t f) {
 }
 
 // 64 VGPRs: 8 waves per SIMD (65 without the bound: 7). Graph: the graph-captured form reads its
-// camera from the FrameArgs block the graph's first node uploads (k_integrate_g).
-template <bool Graph>
+// camera from the FrameArgs block the graph's first node uploads.
+// The visible blocks are the sweep's band lists (blocks that existed before the frame) followed by
+// the blocks k_resolve_alloc created (D.fresh_vis, flagged fresh).
+template <bool Graph, bool Fresh>
 __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_integrate_t(
     EngineDev D, FrameParams Pv, const FrameArgs* __restrict__ A) {
   const FrameParams P = Graph ? A->P : Pv;
@@ -48,13 +50,10 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
     bstart[i] = nvis;
     nvis += D.band[i * kBandStride];
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) D.ctr->n_vis = nvis;
-  // XCD-aware split (workgroups b and b + 8 share an XCD): group g = blockIdx % 8 takes the g-th
-  // contiguous eighth of the block pairs in band order, a compact image region whose pixel
-  // records stay resident in that XCD's L2.
-  const int npairs = (nvis + 1) >> 1;
+  const int nband = nvis;
+  nvis += D.ctr->n_fresh;
+  const int wgb = Fresh ? kIntegrateGrid : 0;  // this launch's per-workgroup slots
   const int g = blockIdx.x & 7, ngrp = gridDim.x >> 3;
-  const int p_lo = (int)(((long long)npairs * g) >> 3), p_hi = (int)(((long long)npairs * (g + 1)) >> 3);
   const int rx0 = (lane & 1) * 4, ry = (lane >> 1) & 7, rz = (lane >> 4) + 4 * hf;
   const int off = (hf * 256 + lane * 4) * 4;
   const float neg_trunc = -P.trunc;
@@ -62,7 +61,12 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
   TSDF_STAMP(D, 3, 0);
   // device-clock duration of this launch: start stamp by WG 0 (dispatched first), end stamp per WG;
   // k_resolve_delete takes the max (bench cross-check of the HIP-event timing)
-  if (blockIdx.x == 0 && threadIdx.x == 0) D.wg_end[kIntegrateGrid] = __builtin_amdgcn_s_memrealtime();
+  if (!Fresh && blockIdx.x == 0 && threadIdx.x == 0) D.wg_end[2 * kIntegrateGrid] = __builtin_amdgcn_s_memrealtime();
+  // XCD-aware split (workgroups b and b + 8 share an XCD): group g = blockIdx % 8 takes the g-th
+  // contiguous eighth of the block pairs in band order, a compact image region whose pixel
+  // records stay resident in that XCD's L2.
+  const int npairs = (nvis + 1) >> 1;
+  const int p_lo = (int)(((long long)npairs * g) >> 3), p_hi = (int)(((long long)npairs * (g + 1)) >> 3);
   for (int pp = p_lo + (blockIdx.x >> 3); pp < p_hi; pp += ngrp) {
     const int b = 2 * pp + pair;
     float mn = __builtin_inff();
@@ -70,14 +74,18 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
     int32_t pidx = 0;
     VisRec r{};
     if (b < nvis) {
-      int bd = 0, ofs = b;
+      if (b >= nband) {
+        r = D.fresh_vis[b - nband];
+      } else {
+        int bd = 0, ofs = b;
 #pragma unroll
-      for (int i = 1; i < kBands; ++i)
-        if (b >= bstart[i]) {
-          bd = i;
-          ofs = b - bstart[i];
-        }
-      r = D.vis[(size_t)bd * D.nblocks + __builtin_amdgcn_readfirstlane(ofs)];
+        for (int i = 1; i < kBands; ++i)
+          if (b >= bstart[i]) {
+            bd = i;
+            ofs = b - bstart[i];
+          }
+        r = D.vis[(size_t)bd * D.nblocks + __builtin_amdgcn_readfirstlane(ofs)];
+      }
       pidx = r.idx;
       uint8_t* blk = D.pool + (size_t)pidx * kBlockBytes;
 #if defined(TSDF_EXP) && (TSDF_EXP & 2)  // experiment build: no pool state loads
@@ -234,13 +242,13 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
   if (lane == 0) s_upd[wave] = tot;
   __syncthreads();
   if (threadIdx.x == 0) {
-    D.wg_upd[blockIdx.x] = s_upd[0] + s_upd[1] + s_upd[2] + s_upd[3];
-    D.wg_end[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    D.wg_upd[wgb + blockIdx.x] = s_upd[0] + s_upd[1] + s_upd[2] + s_upd[3];
+    D.wg_end[wgb + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   }
   TSDF_STAMP(D, 3, 1);
 }
-template __global__ void k_integrate_t<false>(EngineDev, FrameParams, const FrameArgs*);
-template __global__ void k_integrate_t<true>(EngineDev, FrameParams, const FrameArgs*);
+template __global__ void k_integrate_t<false, false>(EngineDev, FrameParams, const FrameArgs*);
+template __global__ void k_integrate_t<true, false>(EngineDev, FrameParams, const FrameArgs*);
 
 // ---------------------------------------------------------------------------------------------
 // k_resolve_delete: VoxelHashTable::Delete (voxel_hash.cu:122-171) for every carve candidate in
@@ -264,18 +272,24 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
   uint32_t epoch0 = 0u;
   int free0 = 0;
   unsigned long long t_start = 0ull;
+  int nfresh = 0;
   if (t == 0) {
     epoch0 = D.ctr->lock_epoch;
     free0 = D.ctr->free_count;
-    if (!direct) t_start = D.wg_end[kIntegrateGrid];
+    if (!direct) {
+      t_start = D.wg_end[2 * kIntegrateGrid];
+      nfresh = D.ctr->n_fresh;
+    }
   }
-  int u = 0;
+  int u = 0, bc = 0;
   unsigned long long te = 0ull;
-  if (!direct)  // voxels updated by k_integrate: sum of its per-workgroup counts
+  if (!direct) {  // voxels updated by both k_integrate launches: sum of their per-workgroup counts
     for (int i = t; i < D.integrate_grid; i += kResolveThreads) {
       u += D.wg_upd[i];
-      te = max(te, D.wg_end[i]);
+      te = max(te, D.wg_end[i]);  // device clock of the main launch
     }
+    if (t < kBands) bc = D.band[t * kBandStride];  // visible = listed by the sweep + created
+  }
   claims_clear(L);
   if (t == 0) {
     L.epoch = epoch0 + 1;
@@ -287,13 +301,15 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) te = max(te, (unsigned long long)__shfl_xor(te, o, 64));
     if ((t & 63) == 0) s_te[t >> 6] = te;
-    int tot;
+    int tot, nband;
     (void)block_excl_scan(u, L.scan, &tot);  // (its barriers also publish s_te)
+    (void)block_excl_scan(bc, L.scan, &nband);
     if (t == 0) {
       unsigned long long tend = 0ull;
       for (int w = 0; w < kResolveThreads / 64; ++w) tend = max(tend, s_te[w]);
       D.ctr->last_updated = (unsigned long long)tot;
       D.ctr->integrate_ticks += tend - t_start;
+      D.ctr->n_vis = nband + nfresh;
     }
   }
   __syncthreads();

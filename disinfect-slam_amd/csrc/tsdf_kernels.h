@@ -50,7 +50,8 @@ struct EngineDev {
   int32_t* band;                // kBands x kBandStride: record count of each band list
   VisRec* cand;                 // carve candidates (any order; resolver sorts by entry)
   int32_t* wg_upd;              // kIntegrateGrid per-workgroup updated-voxel counts
-  unsigned long long* wg_end;   // kIntegrateGrid + 1: per-WG end stamps, [kIntegrateGrid] = start
+  unsigned long long* wg_end;   // 2 x kIntegrateGrid + 1: per-WG end stamps, [2 kIntegrateGrid] = start
+  VisRec* fresh_vis;            // kNewKeyCap blocks created this frame (k_resolve_alloc frame mode)
   // packed frame
   float4* pixA;                 // {depth, range, w_new, rgb}
   float* pixB;                  // log2 ht - log2 lt (base-2 log-odds of the pixel)
@@ -86,7 +87,7 @@ template <int TS>  // LDS key-set slots per tile (tsdf_alloc.hip): 1024 for maxs
 __global__ void k_ingest_dda(EngineDev D, FrameParams P, const float* depth, const uint8_t* rgb,
                              const float* ht, const float* lt, int tiles_x, int tiles);
 __global__ void k_resolve_alloc(EngineDev D, FrameParams P, uint32_t range, int frame_mode);
-template <bool Graph>
+template <bool Graph, bool Fresh>
 __global__ void k_integrate_t(EngineDev D, FrameParams P, const FrameArgs* A);
 // graph-captured forms of the frame kernels: identical bodies, arguments from FrameArgs
 template <int TS>
