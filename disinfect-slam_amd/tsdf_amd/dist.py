@@ -82,3 +82,30 @@ def gather_block_sets(positions, device=None):
     out = [None] * dist.get_world_size()
     dist.all_gather_object(out, np.asarray(positions))
     return out
+
+
+def gather_query(voxels, device=None):
+    """Whole-volume Query of a sharded volume: every rank passes its shard's
+    tsdf_query result, all ranks get the union -- an all-gather of the counts, then one padded
+    all-gather of the (x, y, z, tsdf) rows (RCCL on the GPU box, gloo in the CPU tests). Shards own
+    disjoint blocks, so the union is the unsharded Query as a set of voxels; rows come rank by
+    rank, each rank's in its own entry order."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    arr = np.ascontiguousarray(np.asarray(voxels).view(np.float32).reshape(-1, 4))
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return arr
+    world = dist.get_world_size()
+    n = torch.tensor([arr.shape[0]], dtype=torch.int64, device=device)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n)
+    counts = [int(c.item()) for c in counts]
+    cap = max(max(counts), 1)
+    mine = torch.zeros((cap, 4), dtype=torch.float32, device=device)
+    if arr.shape[0]:
+        mine[:arr.shape[0]] = torch.from_numpy(arr).to(mine.device)
+    allrows = torch.empty((world * cap, 4), dtype=torch.float32, device=device)
+    dist.all_gather_into_tensor(allrows, mine)
+    allrows = allrows.cpu().numpy()
+    return np.concatenate([allrows[r * cap:r * cap + counts[r]] for r in range(world)])

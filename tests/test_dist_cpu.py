@@ -78,6 +78,13 @@ def _worker(rank, world, port):
         pos, tsdf, rgbw = _live(shard)
         shard.close()
         assert all(block_owner(*map(int, p), world) == rank for p in pos)
+        # whole-volume Query of the sharded volume = union of the shard queries (SURVEY 8e gather)
+        qshard = OracleGrid(VOXEL, TRUNC, NB, shard_index=rank, shard_count=world)
+        for f in range(FRAMES):
+            fr = synth.render(cam, 2 * f)
+            qshard.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], 4.0, cam.K, fr["q"], fr["t"])
+        union = tdist.gather_query(qshard.query(None))
+        qshard.close()
         sets = tdist.gather_block_sets(pos)
         tsdfs = [None] * world
         dist.all_gather_object(tsdfs, (tsdf, rgbw))
@@ -89,7 +96,11 @@ def _worker(rank, world, port):
                 fr = synth.render(cam, 2 * f)
                 full.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], 4.0, cam.K, fr["q"], fr["t"])
             fpos, ftsdf, frgbw = _live(full)
+            fq = full.query(None)
             full.close()
+            srt = lambda a: a[np.lexsort(a.view(np.uint32).T[::-1])]
+            assert union.shape == fq.shape and fq.shape[0] > 0
+            np.testing.assert_array_equal(srt(union).view(np.uint32), srt(fq).view(np.uint32))
             fkeys = list(map(tuple, fpos.tolist()))
             assert set(fkeys) == keys[0] | keys[1]
             where = {k: i for i, k in enumerate(fkeys)}

@@ -105,3 +105,30 @@ def test_route_overflow_and_misuse():
                                     torch.zeros(64, dtype=torch.uint8, device="cuda"), 1)
     finally:
         u.close()
+
+
+def test_sharded_query_union_equals_unsharded_query():
+    """SURVEY 8e Query gather on the engine: the shard engines' Query results, concatenated the way
+    tsdf_amd.dist.gather_query concatenates ranks, equal the unsharded engine's Query as a set."""
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H, G = 96, 72, 3
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    full = tsdf_amd.Engine(0.01, 0.04, max_width=W, max_height=H, num_block_bits=13)
+    shards = [tsdf_amd.Engine(0.01, 0.04, max_width=W, max_height=H, num_block_bits=13, shard_index=i,
+                              shard_count=G) for i in range(G)]
+    try:
+        for f in range(5):
+            fr = synth.render(cam, 2 * f)
+            for e in [full] + shards:
+                e.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, tsdf_amd.SE3(fr["q"], fr["t"]), 4.0)
+        srt = lambda a: a[np.lexsort(a.view(np.uint32).T[::-1])]
+        for bounds in (None, np.array([0.5, 4.0, 0.5, 3.5, 0.2, 2.0], np.float32)):
+            exp = full.query(bounds).view(np.float32).reshape(-1, 4)
+            got = np.concatenate([e.query(bounds).view(np.float32).reshape(-1, 4) for e in shards])
+            assert got.shape == exp.shape and exp.shape[0] > 0
+            np.testing.assert_array_equal(srt(got).view(np.uint32), srt(exp).view(np.uint32))
+    finally:
+        full.close()
+        for e in shards:
+            e.close()
