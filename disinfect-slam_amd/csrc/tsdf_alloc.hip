@@ -441,6 +441,7 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
   // coalesced read.
   const bool single = n <= kBatch;
   if (single) {
+    for (int i = t; i < kLockSlots; i += kResolveThreads) L.lkey[i] = 0u;
     const int npre = min(n, free0);
     for (int i = t; i < npre; i += kResolveThreads) L.heap_top[i] = D.heap[free0 - 1 - i];
     for (int i = t; i < n; i += kResolveThreads) {
@@ -539,7 +540,12 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
       const int first_dirty = L.first_dirty;
       const bool commit = have && t < first_dirty;
       bool ok = false;
-      if (commit) {
+      if (commit && single) {  // the launch's locks in LDS (<= 2 x 2048 of the 8192 slots)
+        if (kind == 1)
+          ok = lock_take(L, B);
+        else if (lock_take(L, Lb))
+          ok = lock_take(L, C);
+      } else if (commit) {
         const uint32_t ep = L.epoch;
         if (kind == 1) {
           if (D.lock_tag[B] != ep) {

@@ -71,6 +71,7 @@ constexpr int kMaxWin = 8192;
 constexpr int kClaimSlots = 4096;
 
 constexpr int kRankSortMax = 512;  // single-batch sizes sorted by rank (<= blockDim, <= kMaxWin / 2)
+constexpr int kLockSlots = 8192;   // buckets locked by one single-batch allocation launch (<= 2 per key)
 
 struct ResolveLds {
   uint32_t hist[kMaxWin];             // window counts -> exclusive prefix
@@ -92,6 +93,9 @@ struct ResolveLds {
   unsigned long long skey[kBatch];
   int32_t sslot[kBatch];
   int32_t heap_top[kBatch];           // heap_top[i] = heap[free - 1 - i]
+  // single-batch allocation resolves: the bucket locks this launch has taken (bucket + 1; 0 =
+  // empty), instead of the epoch-tagged lock words in HBM -- a lock only matters within its launch
+  uint32_t lkey[kLockSlots];
 };
 
 __device__ __forceinline__ void lds_bitonic_sort(unsigned long long* a, int m) {
@@ -117,6 +121,18 @@ __device__ __forceinline__ void lds_bitonic_sort(unsigned long long* a, int m) {
   }
 }
 
+// VoxelHashTable's bucket lock within one launch: true if this call took it (it was free)
+__device__ __forceinline__ bool lock_take(ResolveLds& L, uint32_t bucket) {
+  uint32_t h = mix32(bucket ^ 0x9E3779B9u) & (kLockSlots - 1);
+  const uint32_t k = bucket + 1u;
+  for (int p = 0; p < kLockSlots; ++p) {
+    const uint32_t prev = atomicCAS(&L.lkey[h], 0u, k);
+    if (prev == 0u) return true;
+    if (prev == k) return false;
+    h = (h + 1) & (kLockSlots - 1);
+  }
+  return false;
+}
 // claim table: each key claims buckets; the smallest rank per bucket wins
 __device__ __forceinline__ void claims_clear(ResolveLds& L) {
   for (int i = threadIdx.x; i < kClaimSlots; i += blockDim.x) {

@@ -123,7 +123,9 @@ def test_sharded_query_union_equals_unsharded_query():
             for e in [full] + shards:
                 e.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, tsdf_amd.SE3(fr["q"], fr["t"]), 4.0)
         srt = lambda a: a[np.lexsort(a.view(np.uint32).T[::-1])]
-        for bounds in (None, np.array([0.5, 4.0, 0.5, 3.5, 0.2, 2.0], np.float32)):
+        xyz = full.query(None).view(np.float32).reshape(-1, 4)[:, :3]
+        lo, hi = np.percentile(xyz, 10, axis=0), np.percentile(xyz, 90, axis=0)
+        for bounds in (None, np.array([lo[0], hi[0], lo[1], hi[1], lo[2], hi[2]], np.float32)):
             exp = full.query(bounds).view(np.float32).reshape(-1, 4)
             got = np.concatenate([e.query(bounds).view(np.float32).reshape(-1, 4) for e in shards])
             assert got.shape == exp.shape and exp.shape[0] > 0
