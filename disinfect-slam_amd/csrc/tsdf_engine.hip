@@ -1032,6 +1032,99 @@ int tsdf_debug_stamps(tsdf_engine* e, uint64_t* out, int64_t capacity, int* enab
   return TSDF_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Snapshot / restore (SURVEY.md 5 checkpoint / resume; the reference only dumps GatherValid to a
+// file, examples/tsdf/offline.cc:181-187). The whole engine state between frames -- hash table,
+// occupancy bitmap, free-block stack, voxel pool (free blocks included: a re-acquired block keeps
+// its old colour, voxel_mem.cu:43-51) and counters -- so a restored engine continues a stream bit
+// for bit. Layout: header | counters | table | occ | heap | pool.
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct SnapshotHeader {
+  char magic[8];  // "TSDFSNAP"
+  uint32_t version;
+  int32_t nblocks;
+  float voxel, truncation;
+  int64_t bytes;
+};
+constexpr uint32_t kSnapshotVersion = 1;
+
+int64_t snapshot_bytes(const tsdf_engine* e) {
+  return (int64_t)sizeof(SnapshotHeader) + (int64_t)sizeof(DevCounters) + (int64_t)kNumEntry * 16 +
+         (int64_t)kOccWords * 8 + (int64_t)e->D.nblocks * 4 + (int64_t)e->D.nblocks * kBlockBytes;
+}
+}  // namespace
+
+int tsdf_snapshot_bytes(tsdf_engine* e, int64_t* bytes) {
+  if (!e || !bytes) return TSDF_ERR_INVALID_ARG;
+  *bytes = snapshot_bytes(e);
+  return TSDF_OK;
+}
+
+int tsdf_snapshot_save(tsdf_engine* e, void* out, int64_t capacity) {
+  if (!e || !out) return TSDF_ERR_INVALID_ARG;
+  if (e->route_pending) {
+    set_error("tsdf_snapshot_save: a routed frame is pending");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  const int64_t need = snapshot_bytes(e);
+  if (capacity < need) {
+    set_error("tsdf_snapshot_save: buffer smaller than tsdf_snapshot_bytes");
+    return TSDF_ERR_CAPACITY;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  uint8_t* p = static_cast<uint8_t*>(out);
+  SnapshotHeader h{};
+  std::memcpy(h.magic, "TSDFSNAP", 8);
+  h.version = kSnapshotVersion;
+  h.nblocks = e->D.nblocks;
+  h.voxel = e->cfg.voxel_size;
+  h.truncation = e->cfg.truncation;
+  h.bytes = need;
+  std::memcpy(p, &h, sizeof(h));
+  p += sizeof(h);
+  HIP_OK(hipMemcpyAsync(p, e->D.ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
+  p += sizeof(DevCounters);
+  HIP_OK(hipMemcpyAsync(p, e->D.table, (size_t)kNumEntry * 16, hipMemcpyDeviceToHost, s));
+  p += (size_t)kNumEntry * 16;
+  HIP_OK(hipMemcpyAsync(p, e->D.occ, (size_t)kOccWords * 8, hipMemcpyDeviceToHost, s));
+  p += (size_t)kOccWords * 8;
+  HIP_OK(hipMemcpyAsync(p, e->D.heap, (size_t)e->D.nblocks * 4, hipMemcpyDeviceToHost, s));
+  p += (size_t)e->D.nblocks * 4;
+  HIP_OK(hipMemcpyAsync(p, e->D.pool, (size_t)e->D.nblocks * kBlockBytes, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return TSDF_OK;
+}
+
+int tsdf_snapshot_load(tsdf_engine* e, const void* in, int64_t size) {
+  if (!e || !in || size < (int64_t)sizeof(SnapshotHeader)) return TSDF_ERR_INVALID_ARG;
+  SnapshotHeader h;
+  std::memcpy(&h, in, sizeof(h));
+  if (std::memcmp(h.magic, "TSDFSNAP", 8) != 0 || h.version != kSnapshotVersion || h.nblocks != e->D.nblocks ||
+      h.voxel != e->cfg.voxel_size || h.truncation != e->cfg.truncation || h.bytes != snapshot_bytes(e) ||
+      size < h.bytes || e->route_pending) {
+    set_error("tsdf_snapshot_load: not a snapshot of an engine with this configuration");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  const uint8_t* p = static_cast<const uint8_t*>(in) + sizeof(h);
+  HIP_OK(hipMemcpyAsync(e->D.ctr, p, sizeof(DevCounters), hipMemcpyHostToDevice, s));
+  p += sizeof(DevCounters);
+  HIP_OK(hipMemcpyAsync(e->D.table, p, (size_t)kNumEntry * 16, hipMemcpyHostToDevice, s));
+  p += (size_t)kNumEntry * 16;
+  HIP_OK(hipMemcpyAsync(e->D.occ, p, (size_t)kOccWords * 8, hipMemcpyHostToDevice, s));
+  p += (size_t)kOccWords * 8;
+  HIP_OK(hipMemcpyAsync(e->D.heap, p, (size_t)e->D.nblocks * 4, hipMemcpyHostToDevice, s));
+  p += (size_t)e->D.nblocks * 4;
+  HIP_OK(hipMemcpyAsync(e->D.pool, p, (size_t)e->D.nblocks * kBlockBytes, hipMemcpyHostToDevice, s));
+  // lock words hold older epochs than the restored counter's (launches lock with epoch + 1)
+  HIP_OK(hipMemsetAsync(e->D.lock_tag, 0, sizeof(uint32_t) * kNumBucket, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return TSDF_OK;
+}
+
 int tsdf_debug_dump(tsdf_engine* e, int16_t* pos_off, int32_t* idx, int32_t* heap,
                     int32_t* free_count, float* tsdf_out, float* prob, uint8_t* rgbw) {
   if (!e) return TSDF_ERR_INVALID_ARG;

@@ -427,6 +427,20 @@ class Engine:
                                     C.byref(n)), "tsdf_query")
         return out
 
+    def snapshot(self) -> np.ndarray:
+        """The whole volume between frames as bytes (tsdf_snapshot_save): restore() on an engine
+        of the same voxel size, truncation and pool size continues the stream bit for bit."""
+        L = _lib.load()
+        n = C.c_int64()
+        _lib.check(L.tsdf_snapshot_bytes(self._h, C.byref(n)), "tsdf_snapshot_bytes")
+        buf = np.empty(n.value, np.uint8)
+        _lib.check(L.tsdf_snapshot_save(self._h, _ptr(buf), n.value), "tsdf_snapshot_save")
+        return buf
+
+    def restore(self, snapshot):
+        buf = np.ascontiguousarray(snapshot, dtype=np.uint8)
+        _lib.check(_lib.load().tsdf_snapshot_load(self._h, _ptr(buf), buf.size), "tsdf_snapshot_load")
+
     def stats(self, clear_status=False) -> dict:
         s = _lib.Stats()
         _lib.check(_lib.load().tsdf_get_stats(self._h, C.byref(s), int(clear_status)), "tsdf_get_stats")

@@ -98,6 +98,7 @@ EXPORTS = [
     "tsdf_hash_block", "tsdf_block_owner", "tsdf_error_string", "tsdf_last_error",
     "tsdf_route_buffer_bytes", "tsdf_integrate_route_begin", "tsdf_integrate_route_end",
     "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame", "tsdf_graph_destroy",
+    "tsdf_snapshot_bytes", "tsdf_snapshot_save", "tsdf_snapshot_load",
 ]
 
 _lib = None
@@ -131,6 +132,9 @@ def load(path: str | None = None):
     L.tsdf_graph_frame.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f,
                                    C.POINTER(Intrinsics), C.POINTER(Pose), P, P]
     L.tsdf_graph_destroy.argtypes = [P]
+    L.tsdf_snapshot_bytes.argtypes = [P, C.POINTER(i64)]
+    L.tsdf_snapshot_save.argtypes = [P, P, i64]
+    L.tsdf_snapshot_load.argtypes = [P, P, i64]
     L.tsdf_query.argtypes = [P, P, P, i64, C.POINTER(i64)]
     L.tsdf_extract_mesh.argtypes = [P, P, f, i, P, i64, C.POINTER(i64), i]
     L.tsdf_get_stats.argtypes = [P, C.POINTER(Stats), i]
@@ -163,7 +167,7 @@ def load(path: str | None = None):
     for name in ("tsdf_create", "tsdf_destroy", "tsdf_integrate", "tsdf_raycast", "tsdf_query",
                  "tsdf_integrate_route_begin", "tsdf_integrate_route_end",
                  "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame",
-                 "tsdf_graph_destroy",
+                 "tsdf_graph_destroy", "tsdf_snapshot_bytes", "tsdf_snapshot_save", "tsdf_snapshot_load",
                  "tsdf_extract_mesh",
                  "tsdf_get_stats", "tsdf_synchronize", "tsdf_profile_begin", "tsdf_profile_end",
                  "tsdf_debug_dump", "tsdf_debug_stamps", "tsdf_hash_allocate", "tsdf_hash_delete",

@@ -212,6 +212,15 @@ int tsdf_synchronize(tsdf_engine* e);
 int tsdf_profile_begin(tsdf_engine* e, int mode, int every);
 int tsdf_profile_end(tsdf_engine* e, tsdf_profile* out);
 
+/* Snapshot / restore of the whole volume between frames (checkpoint / resume): hash table,
+ * occupancy, free-block stack, voxel pool and counters, so a restored engine continues a frame
+ * stream bit for bit. Two-call: tsdf_snapshot_bytes, then tsdf_snapshot_save into a host buffer of
+ * that size. tsdf_snapshot_load accepts only a snapshot of an engine with the same voxel size,
+ * truncation and pool size (TSDF_ERR_INVALID_ARG otherwise). */
+int tsdf_snapshot_bytes(tsdf_engine* e, int64_t* bytes);
+int tsdf_snapshot_save(tsdf_engine* e, void* out, int64_t capacity);
+int tsdf_snapshot_load(tsdf_engine* e, const void* in, int64_t size);
+
 /* Test-only full state dump (Query exposes only tsdf): the 2^22-entry hash table as
  * (x, y, z, offset) int16 quadruples + pool idx int32, the free-block heap, the free counter and
  * the SoA voxel pools (tsdf f32, prob f32, rgbw u8x4 per voxel, pool-index major). Host buffers;
