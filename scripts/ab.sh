@@ -7,7 +7,7 @@ OUT=gpurun_out/ab
 mkdir -p $OUT
 for rep in 1 2; do
   for lib in "$@"; do
-    n=$(basename $lib .so)
+    n=$(echo "${lib%.so}" | tr "/" "_")
     TSDF_AMD_LIB=$lib timeout -k 10 120 python3 bench.py --no-cpu --steps $STEPS > $OUT/${n}_$rep.log 2>&1 || { echo "$n failed"; tail -5 $OUT/${n}_$rep.log; exit 1; }
     python3 - "$OUT/${n}_$rep.log" "$n" <<'PY'
 import json, sys
