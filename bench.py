@@ -58,6 +58,9 @@ def parse():
                         "the frame's camera), marching cubes of the whole volume every 30 frames")
     p.add_argument("--graph", action="store_true",
                    help="c3 loop through the graph-captured frame (one hipGraph launch per frame)")
+    p.add_argument("--shard", default=None, metavar="I/G",
+                   help="single-GPU rehearsal of --mode sharded: run shard I of G alone (the G-GPU rate is "
+                        "the slowest shard's; every shard sees the whole frame)")
     p.add_argument("--route-cap", type=int, default=8192,
                    help="routed mode: keys per destination rank per frame (outbox slot size)")
     p.add_argument("--cpu-frames", type=int, default=-1, help="oracle sample size (-1 = auto)")
@@ -107,6 +110,12 @@ def main():
     frames = synth.render_torch(cam, list(range(offset, offset + nframes)), device=dev)
     torch.cuda.synchronize()
     shard_index, shard_count = tdist.shard_of(a.mode, rank, world)
+    if a.shard:
+        if world != 1:
+            raise SystemExit("--shard is a single-process rehearsal; use --mode sharded with N ranks")
+        shard_index, shard_count = (int(v) for v in a.shard.split("/"))
+        if not 0 <= shard_index < shard_count:
+            raise SystemExit("--shard I/G needs 0 <= I < G")
     stream = torch.cuda.current_stream()
     eng = tsdf_amd.Engine(a.voxel, a.trunc, max_width=a.width, max_height=a.height,
                           num_block_bits=a.block_bits, device=torch.cuda.current_device(),
@@ -115,7 +124,7 @@ def main():
     K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])  # ctypes struct cached once
     poses = [tsdf_amd.SE3(frames["q"][i], frames["t"][i]) for i in range(nframes)]
 
-    routed = a.mode == "routed" and shard_count > 1
+    routed = a.mode == "routed" and shard_count > 1 and not a.shard
     if routed:  # one outbox / inbox slot per rank; exchanged by an RCCL all-to-all each frame
         nbytes = tsdf_amd.Engine.route_buffer_bytes(world, a.route_cap)
         outbox = torch.zeros((world, nbytes // world), dtype=torch.uint8, device=dev)
@@ -236,10 +245,13 @@ def main():
             "data": "synthetic (analytic room scene rendered on GPU, resident in HBM)",
             "config": {
                 "workload": workload + f", {a.voxel * 1000:g} mm voxel, {a.trunc * 100:g} cm truncation, "
-                            f"{a.max_depth:g} m max depth, TUM fr1 intrinsics, orbit 1 cm + 0.5 deg/frame",
+                            f"{a.max_depth:g} m max depth, {'TUM fr1' if W <= 640 else 'L515 full-res'} intrinsics, "
+                            "orbit 1 cm + 0.5 deg/frame",
                 "width": W, "height": H, "voxel_m": a.voxel, "truncation_m": a.trunc,
                 "pool_blocks": 1 << a.block_bits,
-                "parallelism": f"{a.mode}{world}" if world > 1 else "single",
+                "parallelism": (f"{a.mode}{world}" if world > 1 else
+                                f"shard {shard_index} of {shard_count} alone (sharded-mode rehearsal)"
+                                if shard_count > 1 else "single"),
             },
             "roofline": {
                 "kernel": "k_integrate",

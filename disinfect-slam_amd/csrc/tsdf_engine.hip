@@ -340,7 +340,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.fresh_vis, kNewKeyCap);
   {  // one resident wave of k_integrate workgroups: no second-round stragglers
     int per_cu = 0, ncu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate_t<false, false>, kIntegrateThreads, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate_t<false>, kIntegrateThreads, 0) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
       return fail(TSDF_ERR_HIP);
     if (const char* v = std::getenv("TSDF_INTEGRATE_WG_PER_CU")) per_cu = std::min(per_cu, std::atoi(v));  // tuning
@@ -505,11 +505,11 @@ int frame_finish(tsdf_engine* e, const FrameParams& P, std::array<hipEvent_t, 5>
   if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
     // the two events are bound to the kernel's own dispatch packet (its begin / end timestamps,
     // the interval rocprofv3's kernel trace reports): no marker packets enter the stream
-    hipExtLaunchKernelGGL(k_integrate_t<false, false>, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
+    hipExtLaunchKernelGGL(k_integrate_t<false>, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
                           (*ev)[2], (*ev)[3], 0, e->D, P, (const FrameArgs*)nullptr);
   } else {
     if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
-    hipLaunchKernelGGL((k_integrate_t<false, false>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
+    hipLaunchKernelGGL((k_integrate_t<false>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
                        e->D, P, (const FrameArgs*)nullptr);
     if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
   }
@@ -656,7 +656,7 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
     else
       hipLaunchKernelGGL(k_ingest_dda_g<2048>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
     hipLaunchKernelGGL(k_resolve_alloc_g, dim3(1), dim3(kResolveThreads), 0, g->cap, e->D, A);
-    hipLaunchKernelGGL((k_integrate_t<true, false>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, g->cap,
+    hipLaunchKernelGGL((k_integrate_t<true>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, g->cap,
                        e->D, FrameParams{}, A);
     hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kResolveThreads), 0, g->cap, e->D, e->D.cand,
                        &e->D.ctr->n_cand, 0);

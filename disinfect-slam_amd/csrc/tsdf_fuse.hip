@@ -31,7 +31,7 @@ __device__ __forceinline__ void setu(uint4& v, int j, uint32_t f) {
 // camera from the FrameArgs block the graph's first node uploads.
 // The visible blocks are the sweep's band lists (blocks that existed before the frame) followed by
 // the blocks k_resolve_alloc created (D.fresh_vis, flagged fresh).
-template <bool Graph, bool Fresh>
+template <bool Graph>
 __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_integrate_t(
     EngineDev D, FrameParams Pv, const FrameArgs* __restrict__ A) {
   const FrameParams P = Graph ? A->P : Pv;
@@ -52,7 +52,6 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
   }
   const int nband = nvis;
   nvis += D.ctr->n_fresh;
-  const int wgb = Fresh ? kIntegrateGrid : 0;  // this launch's per-workgroup slots
   const int g = blockIdx.x & 7, ngrp = gridDim.x >> 3;
   const int rx0 = (lane & 1) * 4, ry = (lane >> 1) & 7, rz = (lane >> 4) + 4 * hf;
   const int off = (hf * 256 + lane * 4) * 4;
@@ -61,7 +60,7 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
   TSDF_STAMP(D, 3, 0);
   // device-clock duration of this launch: start stamp by WG 0 (dispatched first), end stamp per WG;
   // k_resolve_delete takes the max (bench cross-check of the HIP-event timing)
-  if (!Fresh && blockIdx.x == 0 && threadIdx.x == 0) D.wg_end[2 * kIntegrateGrid] = __builtin_amdgcn_s_memrealtime();
+  if (blockIdx.x == 0 && threadIdx.x == 0) D.wg_end[2 * kIntegrateGrid] = __builtin_amdgcn_s_memrealtime();
   // XCD-aware split (workgroups b and b + 8 share an XCD): group g = blockIdx % 8 takes the g-th
   // contiguous eighth of the block pairs in band order, a compact image region whose pixel
   // records stay resident in that XCD's L2.
@@ -242,13 +241,13 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
   if (lane == 0) s_upd[wave] = tot;
   __syncthreads();
   if (threadIdx.x == 0) {
-    D.wg_upd[wgb + blockIdx.x] = s_upd[0] + s_upd[1] + s_upd[2] + s_upd[3];
-    D.wg_end[wgb + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    D.wg_upd[blockIdx.x] = s_upd[0] + s_upd[1] + s_upd[2] + s_upd[3];
+    D.wg_end[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   }
   TSDF_STAMP(D, 3, 1);
 }
-template __global__ void k_integrate_t<false, false>(EngineDev, FrameParams, const FrameArgs*);
-template __global__ void k_integrate_t<true, false>(EngineDev, FrameParams, const FrameArgs*);
+template __global__ void k_integrate_t<false>(EngineDev, FrameParams, const FrameArgs*);
+template __global__ void k_integrate_t<true>(EngineDev, FrameParams, const FrameArgs*);
 
 // ---------------------------------------------------------------------------------------------
 // k_resolve_delete: VoxelHashTable::Delete (voxel_hash.cu:122-171) for every carve candidate in

@@ -87,7 +87,7 @@ template <int TS>  // LDS key-set slots per tile (tsdf_alloc.hip): 1024 for maxs
 __global__ void k_ingest_dda(EngineDev D, FrameParams P, const float* depth, const uint8_t* rgb,
                              const float* ht, const float* lt, int tiles_x, int tiles);
 __global__ void k_resolve_alloc(EngineDev D, FrameParams P, uint32_t range, int frame_mode);
-template <bool Graph, bool Fresh>
+template <bool Graph>
 __global__ void k_integrate_t(EngineDev D, FrameParams P, const FrameArgs* A);
 // graph-captured forms of the frame kernels: identical bodies, arguments from FrameArgs
 template <int TS>

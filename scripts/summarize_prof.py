@@ -35,7 +35,7 @@ def kname(full):
     'k_integrate' (the eager instantiation; the graph one is 'k_integrate_graph')."""
     n = full.split("(")[0].replace("tsdf::", "")
     n = re.sub(r"^void ", "", n)
-    return n.replace("k_integrate_t<false, false>", "k_integrate").replace("k_integrate_t<true, false>", "k_integrate_graph")
+    return re.sub(r"k_integrate_t<true(, false)?>", "k_integrate_graph", re.sub(r"k_integrate_t<false(, false)?>", "k_integrate", n))
 
 
 def main(out):

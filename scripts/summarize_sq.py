@@ -18,7 +18,7 @@ def main(out):
             kn = r.get("Kernel_Name", "")
             if "tsdf::" not in kn:
                 continue
-            name = re.sub(r"^void ", "", kn.split("(")[0].replace("tsdf::", "")).replace("k_integrate_t<false, false>", "k_integrate")
+            name = re.sub(r"^void ", "", kn.split("(")[0].replace("tsdf::", "")).replace("k_integrate_t<false, false>", "k_integrate").replace("k_integrate_t<false>", "k_integrate")
             vals.setdefault(name, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     res = {k: {c: statistics.mean(v) for c, v in cs.items()} for k, cs in vals.items()}
     for k, c in res.items():
