@@ -61,6 +61,9 @@ def parse():
     p.add_argument("--shard", default=None, metavar="I/G",
                    help="single-GPU rehearsal of --mode sharded: run shard I of G alone (the G-GPU rate is "
                         "the slowest shard's; every shard sees the whole frame)")
+    p.add_argument("--streams-per-gpu", type=int, default=1,
+                   help="camera streams per GPU, each its own engine (volume) and HIP stream; their "
+                        "frame chains overlap on the device (multi-camera rig; value counts all streams)")
     p.add_argument("--route-cap", type=int, default=8192,
                    help="routed mode: keys per destination rank per frame (outbox slot size)")
     p.add_argument("--cpu-frames", type=int, default=-1, help="oracle sample size (-1 = auto)")
@@ -125,6 +128,19 @@ def main():
     poses = [tsdf_amd.SE3(frames["q"][i], frames["t"][i]) for i in range(nframes)]
 
     routed = a.mode == "routed" and shard_count > 1 and not a.shard
+    # --streams-per-gpu: further engines, each on its own HIP stream with its own camera stream
+    extra = []
+    for k in range(1, a.streams_per_gpu):
+        if routed or a.loop == "c5" or a.graph or shard_count > 1:
+            raise SystemExit("--streams-per-gpu > 1 takes the eager c3 loop in streams mode")
+        off_k = offset + 97 * k  # a different stretch of the orbit per camera
+        fr_k = synth.render_torch(cam, list(range(off_k, off_k + nframes)), device=dev)
+        s_k = torch.cuda.Stream()
+        e_k = tsdf_amd.Engine(a.voxel, a.trunc, max_width=a.width, max_height=a.height,
+                              num_block_bits=a.block_bits, device=torch.cuda.current_device(),
+                              stream=s_k.cuda_stream)
+        extra.append((e_k, fr_k, [tsdf_amd.SE3(fr_k["q"][i], fr_k["t"][i]) for i in range(nframes)], s_k))
+    torch.cuda.synchronize()
     if routed:  # one outbox / inbox slot per rank; exchanged by an RCCL all-to-all each frame
         nbytes = tsdf_amd.Engine.route_buffer_bytes(world, a.route_cap)
         outbox = torch.zeros((world, nbytes // world), dtype=torch.uint8, device=dev)
@@ -157,6 +173,9 @@ def main():
             eng.integrate_route_end(inbox, a.route_cap)
         else:
             eng.integrate(frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i], a.max_depth)
+        for e_k, fr_k, po_k, _ in extra:
+            e_k.integrate(fr_k["rgb"][i], fr_k["depth"][i], None if a.depth_only else fr_k["ht"][i],
+                          None if a.depth_only else fr_k["lt"][i], K, po_k[i], a.max_depth)
 
     for i in range(a.warmup):
         step(i)
@@ -193,7 +212,10 @@ def main():
     st = eng.stats()
     elapsed = t1 - t0
     elapsed = tdist.max_over_ranks(elapsed, device=dev)
-    value = tdist.units(a.mode, a.steps, world) / elapsed
+    value = tdist.units(a.mode, a.steps, world) * a.streams_per_gpu / elapsed
+    for e_k, _, _, _ in extra:
+        if e_k.stats()["status"] != 0:
+            raise SystemExit("a further stream's engine reported a status")
 
     # ---- roofline of the fused integrate kernel (this rank's launches) ----
     W, H = a.width, a.height
@@ -223,6 +245,8 @@ def main():
         workload = ("C2: 640x480 depth-only" if a.depth_only else "C3: 640x480 depth + ht/lt semantic")
         if (W, H) != (640, 480):
             workload = f"{W}x{H} depth{'' if a.depth_only else ' + ht/lt semantic'}"
+        if a.streams_per_gpu > 1:
+            workload += f", {a.streams_per_gpu} camera streams per GPU (one volume each)"
         metric = "TSDF integrate frames/s (640x480 depth+label, 5mm voxel)"
         if a.loop == "c5":
             metric = ("C5 frame loop frames/s (integrate + raycast every frame, marching cubes every 30 "
@@ -290,6 +314,8 @@ def main():
         print(json.dumps(out), flush=True)
     if graph is not None:
         graph.close()
+    for e_k, _, _, _ in extra:
+        e_k.close()
     eng.close()
     if dist:
         dist.destroy_process_group()
