@@ -12,6 +12,8 @@
 #include <string>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "disinfect_tsdf.h"
 #include "tsdf_kernels.h"
 
@@ -230,6 +232,27 @@ int read_counters(tsdf_engine* e) {
   return TSDF_OK;
 }
 
+}  // namespace
+
+// roctx ranges around the C-ABI calls (SURVEY.md 5 tracing): host-side enqueue intervals that
+// `rocprofv3 --marker-trace` lines up with the kernels they launch. Off unless TSDF_ROCTX=1.
+namespace {
+bool roctx_on() {
+  static const bool on = [] {
+    const char* v = std::getenv("TSDF_ROCTX");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+struct TraceRange {
+  const bool on;
+  explicit TraceRange(const char* name) : on(roctx_on()) {
+    if (on) roctxRangePushA(name);
+  }
+  ~TraceRange() {
+    if (on) roctxRangePop();
+  }
+};
 }  // namespace
 
 extern "C" {
@@ -526,6 +549,7 @@ int frame_finish(tsdf_engine* e, const FrameParams& P, std::array<hipEvent_t, 5>
 
 int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
                    const tsdf_pose* pose, float max_depth) {
+  TraceRange trace_("tsdf_integrate");
   if (e && e->route_pending) {
     set_error("tsdf_integrate: a routed frame is pending (tsdf_integrate_route_end)");
     return TSDF_ERR_INVALID_ARG;
@@ -545,6 +569,7 @@ int64_t tsdf_route_buffer_bytes(int32_t shard_count, int32_t route_cap) {
 int tsdf_integrate_route_begin(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
                                const tsdf_pose* pose, float max_depth, int32_t slice_index,
                                int32_t slice_count, void* outbox, int32_t route_cap) {
+  TraceRange trace_("tsdf_integrate_route_begin");
   if (!e || e->cfg.shard_count < 2 || e->route_pending || !outbox || route_cap < 1) {
     set_error("tsdf_integrate_route_begin: invalid argument");
     return TSDF_ERR_INVALID_ARG;
@@ -563,6 +588,7 @@ int tsdf_integrate_route_begin(tsdf_engine* e, const tsdf_frame* f, const tsdf_i
 }
 
 int tsdf_integrate_route_end(tsdf_engine* e, const void* inbox, int32_t route_cap) {
+  TraceRange trace_("tsdf_integrate_route_end");
   if (!e || !e->route_pending || !inbox || route_cap < 1) {
     set_error("tsdf_integrate_route_end: invalid argument");
     return TSDF_ERR_INVALID_ARG;
@@ -674,6 +700,7 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
 int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* K, const tsdf_pose* pose,
                      float max_depth, const tsdf_intrinsics* render_K, const tsdf_pose* render_pose,
                      uint8_t* rgba, uint8_t* normal) {
+  TraceRange trace_("tsdf_graph_frame");
   if (!g || !f || !K || !pose || f->mem_kind != TSDF_MEM_DEVICE || f->width != g->W || f->height != g->H ||
       !f->depth || !f->rgb || (f->ht == nullptr) != (f->lt == nullptr) ||
       (g->RW && (!render_K || !render_pose))) {
@@ -798,6 +825,7 @@ int tsdf_feed_rgbd_frame(tsdf_engine* e, const uint8_t* rgb, const uint16_t* dep
                          const uint8_t* mask, int width, int height, float depth_factor,
                          const tsdf_intrinsics* K, const tsdf_pose* cam_T_world, float max_depth,
                          int mem_kind) {
+  TraceRange trace_("tsdf_feed_rgbd_frame");
   if (!e || !rgbd_args_ok(rgb, depth, width, height, depth_factor, mem_kind)) {
     set_error("tsdf_feed_rgbd_frame: invalid argument (even width / height, depth_factor > 0)");
     return TSDF_ERR_INVALID_ARG;
@@ -822,6 +850,7 @@ int tsdf_feed_rgbd_frame(tsdf_engine* e, const uint8_t* rgb, const uint16_t* dep
 
 int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const tsdf_pose* pose,
                  float max_depth, uint8_t* rgba, uint8_t* normal, int mem_kind) {
+  TraceRange trace_("tsdf_raycast");
   if (!e || !K || !pose || W <= 0 || H <= 0 || (int64_t)W * H > e->max_pixels ||
       (mem_kind != TSDF_MEM_HOST && mem_kind != TSDF_MEM_DEVICE)) {
     set_error("tsdf_raycast: invalid argument");
@@ -845,6 +874,7 @@ int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const t
 
 int tsdf_query(tsdf_engine* e, const float* bounds, tsdf_voxel* out, int64_t capacity,
                int64_t* count) {
+  TraceRange trace_("tsdf_query");
   if (!e || !count) return TSDF_ERR_INVALID_ARG;
   HIP_OK(hipSetDevice(e->device));
   short4 lo = make_short4(0, 0, 0, 0), hi = make_short4(0, 0, 0, 0);
@@ -886,6 +916,7 @@ int tsdf_query(tsdf_engine* e, const float* bounds, tsdf_voxel* out, int64_t cap
 
 int tsdf_extract_mesh(tsdf_engine* e, const float* bounds, float missing_tsdf, int min_weight,
                       float* triangles, int64_t capacity, int64_t* num_triangles, int mem_kind) {
+  TraceRange trace_("tsdf_extract_mesh");
   if (!e || !num_triangles || (mem_kind != TSDF_MEM_HOST && mem_kind != TSDF_MEM_DEVICE)) {
     set_error("tsdf_extract_mesh: invalid argument");
     return TSDF_ERR_INVALID_ARG;
@@ -1062,6 +1093,7 @@ int tsdf_snapshot_bytes(tsdf_engine* e, int64_t* bytes) {
 }
 
 int tsdf_snapshot_save(tsdf_engine* e, void* out, int64_t capacity) {
+  TraceRange trace_("tsdf_snapshot_save");
   if (!e || !out) return TSDF_ERR_INVALID_ARG;
   if (e->route_pending) {
     set_error("tsdf_snapshot_save: a routed frame is pending");
@@ -1098,6 +1130,7 @@ int tsdf_snapshot_save(tsdf_engine* e, void* out, int64_t capacity) {
 }
 
 int tsdf_snapshot_load(tsdf_engine* e, const void* in, int64_t size) {
+  TraceRange trace_("tsdf_snapshot_load");
   if (!e || !in || size < (int64_t)sizeof(SnapshotHeader)) return TSDF_ERR_INVALID_ARG;
   SnapshotHeader h;
   std::memcpy(&h, in, sizeof(h));

@@ -12,5 +12,5 @@ for f in csrc/tsdf_alloc.hip csrc/tsdf_fuse.hip csrc/tsdf_extract.hip csrc/tsdf_
   /opt/rocm/bin/hipcc $HIPFLAGS -c $f -o $OUT/$(basename $f .hip).o & pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libdisinfect_tsdf.so $OUT/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libdisinfect_tsdf.so $OUT/*.o -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrocprofiler-sdk-roctx
 echo $OUT/libdisinfect_tsdf.so
