@@ -17,8 +17,8 @@ __device__ void keyset_insert(unsigned long long* keys, uint32_t* orders, int32_
                               int32_t* count, uint32_t* status, uint64_t key, uint32_t order) {
   uint32_t h = (uint32_t)mix64(key) & (kNewKeyCap - 1);
   for (int p = 0; p < 256; ++p) {
-    unsigned long long cur = keys[h];
-    if (cur == 0ull) cur = atomicCAS(&keys[h], 0ull, (unsigned long long)key);
+    // the CAS itself reads the slot (measured equal to a plain read first)
+    const unsigned long long cur = atomicCAS(&keys[h], 0ull, (unsigned long long)key);
     if (cur == 0ull) {
       const int s = atomicAdd(count, 1);
       list[s] = (int32_t)h;
@@ -60,6 +60,14 @@ __device__ void rt_insert(const EngineDev& D, uint64_t key, uint32_t order) {
 // workgroups fit a CU and the whole 640x480 grid is resident at once; 2048 up to maxs = 6.
 constexpr int kVisChunk = 1024;   // visibility sweep: 16 occupancy words x 64 entries per wave
 static_assert(kBands == 16, "ResolveLds band arrays");
+
+// LDS key-set slot of a block key: multiplicative hash of the two key words, top log2(TS) bits
+// (a few VALU per DDA sample instead of a 64-bit mixer; placement only, the set is exact)
+template <int TS>
+__device__ __forceinline__ uint32_t tile_slot(uint64_t key) {
+  const uint32_t h = (uint32_t)key * 0x9E3779B1u + (uint32_t)(key >> 32) * 0x85EBCA77u;
+  return h >> (32 - __builtin_ctz(TS));
+}
 
 // the two roles of k_ingest_dda share one LDS allocation
 template <int TS>
@@ -211,12 +219,18 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
     const float range = sqrtf(dot3(pc, pc));  // img_depth_to_range (voxel_tsdf.cu:120)
     const float w_new = (1.0f - quot_const(d, P.max_depth, P.inv_max_depth)) * 4.0f;
     D.pixA[i] = make_float4(d, range, w_new, __uint_as_float(c));
-    D.pixB[i] = log2f(h) - log2f(l);  // base-2 log-odds of the pixel (k_integrate)
+    // base-2 log-odds of the pixel (k_integrate); the hardware log2 (1 ulp) is far inside the
+    // 1e-4 prob tolerance and still gives exactly 0 when ht == lt
+    D.pixB[i] = __log2f(h) - __log2f(l);
     TSDF_STAMP(D, 0, 2);
     if (tile >= P.tile_lo && tile < P.tile_hi && !(d == 0 || d > P.max_depth)) {
       const f3 pcd = {pc.x * d, pc.y * d, pc.z * d};
       const f3 pw = se3_apply(P.wq, P.wt, pcd);
-      const f3 dc = {pc.x / range, pc.y / range, pc.z / range};
+      // pc / range (IEEE quotients; pc.z = 1): the Newton-refined pair division, exact in range
+      const float rr = __builtin_amdgcn_rcpf(range);
+      const v2f dxy = div_pair(v2(pc.x, pc.y), v2(range, range), v2(rr, rr), true, true);
+      const v2f dz1 = div_pair(v2(pc.z, pc.z), v2(range, range), v2(rr, rr), true, false);
+      const f3 dc = {dxy.x, dxy.y, dz1.x};
       const f3 dw = qrot(P.wq, dc);
       const f3 sw = {pw.x - dw.x * P.trunc, pw.y - dw.y * P.trunc, pw.z - dw.z * P.trunc};
       const f3 dg = {quot_const(dw.x, P.voxel, P.inv_voxel), quot_const(dw.y, P.voxel, P.inv_voxel),
@@ -228,7 +242,15 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
       const int step_grid =
           f2i(ceilf(fmaxf(fmaxf(fabsf(rg.x), fabsf(rg.y)), fabsf(rg.z)) / kBlockLen));
       const float div = fmaxf((float)step_grid, 1.0f);
-      const f3 st = {rg.x / div, rg.y / div, rg.z / div};
+      // ray / max(step_grid, 1): step_grid is 1 or 2 at the reference's 6x truncation / voxel
+      // ratio, where the quotient is exact as a product; larger counts take the IEEE divide
+      f3 st;
+      if (__builtin_expect(div <= 2.0f, 1)) {
+        const float m = div == 2.0f ? 0.5f : 1.0f;
+        st = {rg.x * m, rg.y * m, rg.z * m};
+      } else {
+        st = {rg.x / div, rg.y / div, rg.z / div};
+      }
       f3 pos = sg;
       for (int s = 0; s <= step_grid; ++s) {
         if (s >= P.maxs) {
@@ -243,7 +265,7 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
         pos.z += st.z;
         const unsigned long long key = pack_key(kx, ky, kz);
         const uint32_t order = (uint32_t)i * (uint32_t)P.maxs + (uint32_t)s;
-        uint32_t hs = (uint32_t)mix64(key) & (TS - 1);
+        uint32_t hs = tile_slot<TS>(key);
         for (int p = 0; p < TS; ++p) {
           const unsigned long long prev = atomicCAS(&s_key[hs], 0ull, key);
           if (prev == 0ull || prev == key) {
