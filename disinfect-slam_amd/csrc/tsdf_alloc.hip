@@ -425,6 +425,16 @@ __global__ void k_keys_to_newset(EngineDev D, const int16_t* __restrict__ keys, 
   }
 }
 
+// render replica import (tsdf_import_blocks): the records' block keys into the new-key set, in
+// record order, for the resolver; keys already in the table are skipped
+__global__ void k_import_keys(EngineDev D, const uint8_t* __restrict__ recs, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const short4 h = *reinterpret_cast<const short4*>(recs + (size_t)i * kBlockRecBytes);
+    if (find_entry(D.table, h.x, h.y, h.z) >= 0) continue;
+    nk_insert(D, pack_key(h.x, h.y, h.z), (uint32_t)i);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_resolve_alloc: one 1024-thread workgroup replays VoxelHashTable::Allocate in candidate order.
 // Every unique missing key K is evaluated against the current table:

@@ -289,6 +289,39 @@ int32_t tsdf_block_owner(int16_t x, int16_t y, int16_t z, int32_t n) {
 int32_t tsdf_num_entries(void) { return (int32_t)kNumEntry; }
 int32_t tsdf_num_blocks(const tsdf_engine* e) { return e ? e->D.nblocks : 0; }
 
+namespace {
+// empty volume: table, occupancy, free stack, log-odds pool, counters and key sets (tsdf_create,
+// tsdf_reset)
+bool init_state(tsdf_engine* e) {
+  hipStream_t s = e->stream;
+  const EngineDev& D = e->D;
+  const int nb = D.nblocks;
+  bool ok = true;
+  ok &= hipMemsetAsync(D.lock_tag, 0, sizeof(uint32_t) * kNumBucket, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.pool, 0, (size_t)nb * kBlockBytes, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.occ, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.nk_key, 0, sizeof(unsigned long long) * kNewKeyCap, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.nk_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
+  if (D.rt_key) {
+    ok &= hipMemsetAsync(D.rt_key, 0, sizeof(unsigned long long) * kNewKeyCap, s) == hipSuccess;
+    ok &= hipMemsetAsync(D.rt_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
+  }
+  ok &= hipMemsetAsync(D.band, 0, sizeof(int32_t) * kBands * kBandStride, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.visbits, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
+  DevCounters c0{};
+  c0.free_count = nb;
+  ok &= hipMemcpyAsync(D.ctr, &c0, sizeof(c0), hipMemcpyHostToDevice, s) == hipSuccess;
+  hipLaunchKernelGGL(k_init_table, dim3(kNumEntry / 256), dim3(256), 0, s, D.table);
+  hipLaunchKernelGGL(k_init_heap, dim3((nb + 255) / 256), dim3(256), 0, s, D.heap, nb);
+  hipLaunchKernelGGL(k_init_logodds, dim3((unsigned)(((size_t)nb * (kBlockVolume / 4) + 255) / 256)), dim3(256),
+                     0, s, D.pool, nb);
+  ok &= hipGetLastError() == hipSuccess;
+  ok &= hipStreamSynchronize(s) == hipSuccess;
+  return ok;
+}
+
+}  // namespace
+
 int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   if (!out) return TSDF_ERR_INVALID_ARG;
   *out = nullptr;
@@ -398,29 +431,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
       return fail(TSDF_ERR_HIP);
     e->own_stream = true;
   }
-  hipStream_t s = e->stream;
-  bool ok = true;
-  ok &= hipMemsetAsync(D.lock_tag, 0, sizeof(uint32_t) * kNumBucket, s) == hipSuccess;
-  ok &= hipMemsetAsync(D.pool, 0, (size_t)nb * kBlockBytes, s) == hipSuccess;
-  ok &= hipMemsetAsync(D.occ, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
-  ok &= hipMemsetAsync(D.nk_key, 0, sizeof(unsigned long long) * kNewKeyCap, s) == hipSuccess;
-  ok &= hipMemsetAsync(D.nk_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
-  if (D.rt_key) {
-    ok &= hipMemsetAsync(D.rt_key, 0, sizeof(unsigned long long) * kNewKeyCap, s) == hipSuccess;
-    ok &= hipMemsetAsync(D.rt_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
-  }
-  ok &= hipMemsetAsync(D.band, 0, sizeof(int32_t) * kBands * kBandStride, s) == hipSuccess;
-  ok &= hipMemsetAsync(D.visbits, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
-  DevCounters c0{};
-  c0.free_count = nb;
-  ok &= hipMemcpyAsync(D.ctr, &c0, sizeof(c0), hipMemcpyHostToDevice, s) == hipSuccess;
-  hipLaunchKernelGGL(k_init_table, dim3(kNumEntry / 256), dim3(256), 0, s, D.table);
-  hipLaunchKernelGGL(k_init_heap, dim3((nb + 255) / 256), dim3(256), 0, s, D.heap, nb);
-  hipLaunchKernelGGL(k_init_logodds, dim3((unsigned)(((size_t)nb * (kBlockVolume / 4) + 255) / 256)), dim3(256),
-                     0, s, D.pool, nb);
-  ok &= hipGetLastError() == hipSuccess;
-  ok &= hipStreamSynchronize(s) == hipSuccess;
-  if (!ok) {
+  if (!init_state(e)) {
     set_error("tsdf_create: initialisation failed");
     return fail(TSDF_ERR_HIP);
   }
@@ -912,6 +923,161 @@ int tsdf_query(tsdf_engine* e, const float* bounds, tsdf_voxel* out, int64_t cap
   HIP_OK(hipMemcpyAsync(out, e->q_out, (size_t)nvox * sizeof(float4), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
   return TSDF_OK;
+}
+
+static_assert(kBlockRecBytes == TSDF_BLOCK_RECORD_BYTES, "render record layout");
+
+int tsdf_reset(tsdf_engine* e) {
+  TraceRange trace_("tsdf_reset");
+  if (!e) return TSDF_ERR_INVALID_ARG;
+  if (e->route_pending) {
+    set_error("tsdf_reset: a routed frame is pending");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  if (!init_state(e)) {
+    set_error("tsdf_reset: initialisation failed");
+    return TSDF_ERR_HIP;
+  }
+  return TSDF_OK;
+}
+
+int tsdf_render_blocks(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H,
+                       const tsdf_pose* pose, float max_depth, void* out, int64_t capacity,
+                       int64_t* count, int mem_kind) {
+  TraceRange trace_("tsdf_render_blocks");
+  if (!e || !K || !pose || !count || W <= 0 || H <= 0 || !(max_depth > 0) ||
+      (mem_kind != TSDF_MEM_HOST && mem_kind != TSDF_MEM_DEVICE)) {
+    set_error("tsdf_render_blocks: invalid argument");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  const FrameParams P = make_params(e, K, W, H, pose, max_depth);
+  // ray_cast_kernel's march (voxel_tsdf.cu:248-250): max_step samples truncation / 2 apart
+  const double step = (double)(e->cfg.truncation / 2);
+  const double max_step = std::ceil((double)max_depth / step);
+  RenderCull C{};
+  C.a0 = P.icx;
+  C.a1 = (float)(W - 1) * P.ifx + P.icx;
+  C.b0 = P.icy;
+  C.b1 = (float)(H - 1) * P.ify + P.icy;
+  C.na0 = std::sqrt(1.0f + C.a0 * C.a0);
+  C.na1 = std::sqrt(1.0f + C.a1 * C.a1);
+  C.nb0 = std::sqrt(1.0f + C.b0 * C.b0);
+  C.nb1 = std::sqrt(1.0f + C.b1 * C.b1);
+  // bounding sphere of the voxel centres (3.5 sqrt 3 voxels) + nearest-voxel rounding (sqrt 3 / 2)
+  // + the +-1 gradient neighbours = 7.93 voxels; 10 leaves room for float error
+  C.reach = 10.0f * e->cfg.voxel_size;
+  C.len = (float)(max_step * step) + C.reach;
+  hipStream_t s = e->stream;
+  hipLaunchKernelGGL(k_render_count, dim3(kOccWords / 256), dim3(256), 0, s, e->D, P, C);
+  hipLaunchKernelGGL(k_vis_emit, dim3(kOccWords / 256), dim3(256), 0, s, e->D, e->q_sel,
+                     e->q_count);
+  LAUNCH_OK("render select");
+  int32_t nsel = 0;
+  HIP_OK(hipMemcpyAsync(&nsel, e->q_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  *count = nsel;
+  if (!out || nsel == 0) return TSDF_OK;
+  if (capacity < nsel) {
+    set_error("tsdf_render_blocks: capacity too small");
+    return TSDF_ERR_CAPACITY;
+  }
+  const size_t bytes = (size_t)nsel * kBlockRecBytes;
+  uint8_t* dst = reinterpret_cast<uint8_t*>(out);
+  uint8_t* tmp = nullptr;
+  if (mem_kind == TSDF_MEM_HOST) {
+    HIP_OK(dmalloc(&tmp, bytes));
+    dst = tmp;
+  }
+  hipLaunchKernelGGL(k_render_pack, dim3(nsel), dim3(256), 0, s, e->D, e->q_sel, dst);
+  hipError_t err = hipGetLastError();
+  if (err == hipSuccess && tmp) err = hipMemcpyAsync(out, tmp, bytes, hipMemcpyDeviceToHost, s);
+  if (err == hipSuccess) err = hipStreamSynchronize(s);
+  if (tmp) (void)hipFree(tmp);
+  if (err != hipSuccess) {
+    set_error("tsdf_render_blocks", err);
+    return TSDF_ERR_HIP;
+  }
+  return TSDF_OK;
+}
+
+int tsdf_import_blocks(tsdf_engine* e, const void* records, int64_t n, int mem_kind) {
+  TraceRange trace_("tsdf_import_blocks");
+  if (!e || n < 0 || (n > 0 && !records) ||
+      (mem_kind != TSDF_MEM_HOST && mem_kind != TSDF_MEM_DEVICE)) {
+    set_error("tsdf_import_blocks: invalid argument");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  if (e->route_pending) {
+    set_error("tsdf_import_blocks: a routed frame is pending");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  if (n == 0) return TSDF_OK;
+  HIP_OK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  const size_t bytes = (size_t)n * kBlockRecBytes;
+  const uint8_t* recs = reinterpret_cast<const uint8_t*>(records);
+  uint8_t* tmp = nullptr;
+  if (mem_kind == TSDF_MEM_HOST) {
+    HIP_OK(dmalloc(&tmp, bytes));
+    hipError_t err = hipMemcpyAsync(tmp, records, bytes, hipMemcpyHostToDevice, s);
+    if (err != hipSuccess) {
+      (void)hipFree(tmp);
+      set_error("tsdf_import_blocks upload", err);
+      return TSDF_ERR_HIP;
+    }
+    recs = tmp;
+  }
+  auto done = [&](int rc) {
+    if (tmp) {
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(tmp);
+    }
+    return rc;
+  };
+  // VoxelHashTable::Allocate keeps <= 1 structural change per bucket per launch (voxel_hash.cu:
+  // 80-118): resolver launches over the still-missing keys until every record has its block
+  for (int64_t base = 0; base < n; base += kNewKeyCap) {
+    const int m = (int)std::min<int64_t>(kNewKeyCap, n - base);
+    const uint8_t* chunk = recs + (size_t)base * kBlockRecBytes;
+    int32_t missing = m;
+    for (int round = 0; missing > 0; ++round) {
+      if (round == 64) {
+        set_error("tsdf_import_blocks: keys still missing after 64 allocation launches");
+        return done(TSDF_ERR_HIP);
+      }
+      hipLaunchKernelGGL(k_import_keys, dim3((m + 255) / 256), dim3(256), 0, s, e->D, chunk, m);
+      if (hipGetLastError() != hipSuccess) return done(TSDF_ERR_HIP);
+      int rc = launch_resolve_alloc(e, FrameParams{}, (uint32_t)m, 0);
+      if (rc) return done(rc);
+      rc = read_counters(e);
+      if (rc) return done(rc);
+      if (e->h_ctr->status & TSDF_STATUS_POOL_EXHAUSTED) {
+        set_error("tsdf_import_blocks: voxel block pool exhausted");
+        return done(TSDF_ERR_OUT_OF_MEMORY);
+      }
+      if (hipMemsetAsync(e->q_count, 0, sizeof(int32_t), s) != hipSuccess) return done(TSDF_ERR_HIP);
+      hipLaunchKernelGGL(k_import_missing, dim3((m + 255) / 256), dim3(256), 0, s, e->D, chunk, m,
+                         e->q_count);
+      if (hipGetLastError() != hipSuccess ||
+          hipMemcpyAsync(&missing, e->q_count, sizeof(int32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+        return done(TSDF_ERR_HIP);
+    }
+  }
+  int32_t missing = 0;
+  if (hipMemsetAsync(e->q_count, 0, sizeof(int32_t), s) != hipSuccess) return done(TSDF_ERR_HIP);
+  hipLaunchKernelGGL(k_import_payload, dim3((unsigned)n), dim3(256), 0, s, e->D, recs, e->q_count);
+  if (hipGetLastError() != hipSuccess ||
+      hipMemcpyAsync(&missing, e->q_count, sizeof(int32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return done(TSDF_ERR_HIP);
+  if (missing) {
+    set_error("tsdf_import_blocks: a block went missing during import");
+    return done(TSDF_ERR_HIP);
+  }
+  return done(TSDF_OK);
 }
 
 int tsdf_extract_mesh(tsdf_engine* e, const float* bounds, float missing_tsdf, int min_weight,

@@ -228,6 +228,84 @@ __global__ __launch_bounds__(512) void k_query_download(EngineDev D, const VisRe
 }
 
 // ---------------------------------------------------------------------------------------------
+// render replicas of a sharded volume: every shard selects the blocks a raycast of
+// camera P can read, packs them as {key, payload} records, the records are all-gathered, and a
+// scratch engine imports the union and runs the unchanged k_raycast over it. The selection is
+// conservative (a superset): the block's bounding sphere, grown by the reach of one lookup (the
+// nearest voxel of a ray point, its +-1 gradient neighbours), against the half-spaces of the
+// pixel-centre view pyramid and a sphere of the marched ray length around the camera centre.
+// Blocks outside it are never read by ray_cast_kernel (voxel_tsdf.cu:232-307), so the replica
+// renders exactly what the unsharded volume renders.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool render_needs(const FrameParams& P, const RenderCull& C,
+                                             const Ent& en) {
+  const float h = 0.5f * (float)(kBlockLen - 1);
+  const f3 w = {((float)(int16_t)(en.x << kBlockLenBits) + h) * P.voxel,
+                ((float)(int16_t)(en.y << kBlockLenBits) + h) * P.voxel,
+                ((float)(int16_t)(en.z << kBlockLenBits) + h) * P.voxel};
+  const f3 r = qrot(P.cq, w);
+  const f3 c = {r.x + P.ct.x, r.y + P.ct.y, r.z + P.ct.z};
+  return c.z >= -C.reach && c.x - C.a0 * c.z >= -C.reach * C.na0 &&
+         C.a1 * c.z - c.x >= -C.reach * C.na1 && c.y - C.b0 * c.z >= -C.reach * C.nb0 &&
+         C.b1 * c.z - c.y >= -C.reach * C.nb1 && dot3(c, c) <= C.len * C.len;
+}
+// selection into D.visbits + per-workgroup counts; k_vis_emit then lists it in entry order
+__global__ __launch_bounds__(256) void k_render_count(EngineDev D, FrameParams P, RenderCull C) {
+  __shared__ int scratch[4];
+  const int w = blockIdx.x * 256 + threadIdx.x;
+  unsigned long long occ = D.occ[w], sel = 0ull;
+  while (occ) {
+    const int b = __ffsll((long long)occ) - 1;
+    occ &= occ - 1;
+    if (render_needs(P, C, load_ent(D.table, (uint32_t)(w * 64 + b)))) sel |= 1ull << b;
+  }
+  D.visbits[w] = sel;
+  const int s = wave_sum(__popcll(sel));
+  if (lane_id() == 0) scratch[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) D.wgcnt[blockIdx.x] = scratch[0] + scratch[1] + scratch[2] + scratch[3];
+}
+// one workgroup per selected block: 16-B key header + the 6 KiB block record, 16 B per lane
+__global__ __launch_bounds__(256) void k_render_pack(EngineDev D, const VisRec* __restrict__ sel,
+                                                     uint8_t* __restrict__ out) {
+  const VisRec r = sel[blockIdx.x];
+  uint8_t* dst = out + (size_t)blockIdx.x * kBlockRecBytes;
+  const uint4* src = reinterpret_cast<const uint4*>(D.pool + (size_t)r.idx * kBlockBytes);
+  if (threadIdx.x == 0) {
+    const short4 h = make_short4(r.x, r.y, r.z, 0);
+    uint4 head;
+    __builtin_memcpy(&head, &h, 8);
+    head.z = 0u;
+    head.w = 0u;
+    *reinterpret_cast<uint4*>(dst) = head;
+  }
+  for (int i = threadIdx.x; i < kBlockBytes / 16; i += 256)
+    reinterpret_cast<uint4*>(dst + 16)[i] = src[i];
+}
+// import: records whose key is still missing after a resolver launch (bucket-lock losers retry)
+__global__ void k_import_missing(EngineDev D, const uint8_t* __restrict__ recs, int n,
+                                 int32_t* missing) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const short4 h = *reinterpret_cast<const short4*>(recs + (size_t)i * kBlockRecBytes);
+  if (find_entry(D.table, h.x, h.y, h.z) < 0) atomicAdd(missing, 1);
+}
+// import: one workgroup per record writes its payload over the freshly initialised block
+__global__ __launch_bounds__(256) void k_import_payload(EngineDev D, const uint8_t* __restrict__ recs,
+                                                        int32_t* missing) {
+  const uint8_t* src = recs + (size_t)blockIdx.x * kBlockRecBytes;
+  const short4 h = *reinterpret_cast<const short4*>(src);
+  const int32_t e = find_entry(D.table, h.x, h.y, h.z);
+  if (e < 0) {
+    if (threadIdx.x == 0) atomicAdd(missing, 1);
+    return;
+  }
+  uint4* dst = reinterpret_cast<uint4*>(D.pool + (size_t)D.table[e].z * kBlockBytes);
+  for (int i = threadIdx.x; i < kBlockBytes / 16; i += 256)
+    dst[i] = reinterpret_cast<const uint4*>(src + 16)[i];
+}
+
+// ---------------------------------------------------------------------------------------------
 // test-level kernels (VoxelHashTable::Retrieve / assignment, VoxelMemPool acquire / release)
 // ---------------------------------------------------------------------------------------------
 __global__ void k_hash_retrieve(EngineDev D, const int16_t* __restrict__ pts, int n,

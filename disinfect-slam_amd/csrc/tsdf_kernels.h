@@ -119,6 +119,19 @@ __global__ void k_raycast(EngineDev D, FrameParams P, float step_size, uchar4* r
 __global__ void k_query_count(EngineDev D, int use_bounds, short4 lo, short4 hi);
 __global__ void k_vis_emit(EngineDev D, VisRec* out, int32_t* out_count);
 __global__ void k_query_download(EngineDev D, const VisRec* sel, float voxel, float4* out);
+// render replicas of a sharded volume (tsdf_render_blocks / tsdf_import_blocks)
+constexpr int kBlockRecBytes = 16 + kBlockBytes;  // {int16 x, y, z, 0; 8 zero bytes} + payload
+struct RenderCull {
+  float a0, a1, b0, b1;      // x/z and y/z of the pixel-centre pyramid's four side planes
+  float na0, na1, nb0, nb1;  // their normal lengths sqrt(1 + a^2)
+  float reach;               // block bounding radius + lookup reach (m)
+  float len;                 // marched ray length + reach (m)
+};
+__global__ void k_render_count(EngineDev D, FrameParams P, RenderCull C);
+__global__ void k_render_pack(EngineDev D, const VisRec* sel, uint8_t* out);
+__global__ void k_import_keys(EngineDev D, const uint8_t* recs, int n);
+__global__ void k_import_missing(EngineDev D, const uint8_t* recs, int n, int32_t* missing);
+__global__ void k_import_payload(EngineDev D, const uint8_t* recs, int32_t* missing);
 __global__ void k_hash_retrieve(EngineDev D, const int16_t* pts, int n, uint32_t* rgbw,
                                 float* tsdf, float* prob, short4* bpo, int32_t* bidx);
 __global__ void k_hash_assign(EngineDev D, const int16_t* pts, int n, const uint32_t* rgbw,

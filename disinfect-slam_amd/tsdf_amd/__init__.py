@@ -26,6 +26,7 @@ NUM_ENTRY = 1 << 22
 NUM_BUCKET = 1 << 21
 BLOCK_LEN = 8
 BLOCK_VOLUME = 512
+BLOCK_RECORD_BYTES = 16 + 12 * BLOCK_VOLUME  # TSDF_BLOCK_RECORD_BYTES: key header + block
 VOXEL_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("tsdf", "<f4")])
 
 __all__ = [
@@ -393,6 +394,42 @@ class Engine:
                                             C.byref(cam_T_world._c()), max_depth, _ptr(rgba),
                                             _ptr(normal), TSDF_MEM_HOST), "tsdf_raycast")
         return rgba, normal
+
+    def render_blocks(self, K, width, height, cam_T_world: SE3, max_depth: float, device=False):
+        """Records (n, TSDF_BLOCK_RECORD_BYTES) uint8 of the blocks a raycast of this camera can read
+        (tsdf_render_blocks): a numpy array, or a torch tensor on this engine's GPU when device."""
+        L = _lib.load()
+        Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        pc = cam_T_world._c()
+        n = C.c_int64()
+        _lib.check(L.tsdf_render_blocks(self._h, C.byref(Kc), width, height, C.byref(pc), max_depth,
+                                        None, 0, C.byref(n), TSDF_MEM_HOST), "tsdf_render_blocks")
+        if device:
+            import torch
+            out = torch.empty((n.value, BLOCK_RECORD_BYTES), dtype=torch.uint8,
+                              device=f"cuda:{self.device}")
+            kind = TSDF_MEM_DEVICE
+        else:
+            out = np.empty((n.value, BLOCK_RECORD_BYTES), np.uint8)
+            kind = TSDF_MEM_HOST
+        if n.value:
+            _lib.check(L.tsdf_render_blocks(self._h, C.byref(Kc), width, height, C.byref(pc),
+                                            max_depth, _ptr(out), n.value, C.byref(n), kind),
+                       "tsdf_render_blocks")
+        return out
+
+    def import_blocks(self, records):
+        """Allocate and fill the blocks of render records (tsdf_import_blocks); numpy or GPU tensor."""
+        n = int(records.shape[0]) if records.ndim == 2 else int(records.size) // BLOCK_RECORD_BYTES
+        kind = TSDF_MEM_DEVICE if _is_torch_cuda(records) else TSDF_MEM_HOST
+        if kind == TSDF_MEM_HOST:
+            records = np.ascontiguousarray(records, dtype=np.uint8)
+        _lib.check(_lib.load().tsdf_import_blocks(self._h, _ptr(records), n, kind),
+                   "tsdf_import_blocks")
+
+    def reset(self):
+        """Empty the volume (tsdf_reset)."""
+        _lib.check(_lib.load().tsdf_reset(self._h), "tsdf_reset")
 
     def extract_mesh(self, bounds=None, missing_tsdf: float = 0.99, min_weight: int = 0,
                      out=None) -> np.ndarray:

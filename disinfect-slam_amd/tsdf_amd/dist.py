@@ -109,3 +109,42 @@ def gather_query(voxels, device=None):
     dist.all_gather_into_tensor(allrows, mine)
     allrows = allrows.cpu().numpy()
     return np.concatenate([allrows[r * cap:r * cap + counts[r]] for r in range(world)])
+
+
+def gather_rows(rows, device=None):
+    """All-gather-v of a 2-D tensor / array of rows (same row width and dtype on every rank): an
+    all-gather of the counts, then one padded all-gather of the rows, concatenated rank by rank.
+    Returns a tensor on `device` (the rows' own device by default)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    t = rows if isinstance(rows, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(rows))
+    if device is not None:
+        t = t.to(device)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return t
+    world = dist.get_world_size()
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n)
+    counts = [int(c.item()) for c in counts]
+    cap = max(max(counts), 1)
+    mine = torch.zeros((cap,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    mine[:t.shape[0]] = t
+    allrows = torch.empty((world * cap,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(allrows, mine)
+    return torch.cat([allrows[r * cap:r * cap + counts[r]] for r in range(world)])
+
+
+def render_sharded(engine, replica, K, width, height, cam_T_world, max_depth, device=True):
+    """Raycast of a spatially sharded volume (SURVEY.md 8e raycast composite): every
+    rank packs the blocks of its shard that this camera's rays can read (tsdf_render_blocks), the
+    records are all-gathered (RCCL over xGMI on the GPU box), and `replica` -- a scratch engine of
+    the same voxel size / truncation with room for them -- imports the union and renders it with
+    the unchanged raycast kernel. Every rank gets the image the unsharded volume renders.
+    Returns (rgba, normal) as numpy (H, W, 4) uint8."""
+    recs = engine.render_blocks(K, width, height, cam_T_world, max_depth, device=device)
+    allrecs = gather_rows(recs)
+    replica.reset()
+    replica.import_blocks(allrecs if device else allrecs.numpy())
+    return replica.raycast(K, width, height, cam_T_world, max_depth)

@@ -66,6 +66,15 @@ def _worker(rank, world, port):
         inbox = tdist.route_exchange(out, torch.empty_like(out))
         for src in range(world):
             assert bool((inbox[src] == src * world + rank).all()), (rank, src, inbox[src][:4])
+        # render replicas (tsdf_amd.dist.render_sharded): all-gather-v of ragged record rows, rank order
+        rows = np.full((rank + 1, 6160), rank + 1, np.uint8)
+        rows[:, 0] = np.arange(rank + 1)
+        got = tdist.gather_rows(rows).numpy()
+        assert got.shape == (world * (world + 1) // 2, 6160)
+        exp = np.concatenate([np.full((r + 1, 6160), r + 1, np.uint8) for r in range(world)])
+        exp[:, 0] = np.concatenate([np.arange(r + 1) for r in range(world)])
+        np.testing.assert_array_equal(got, exp)
+        assert tdist.gather_rows(np.zeros((0, 6160), np.uint8)).shape == (0, 6160)
         offs = [None] * world
         dist.all_gather_object(offs, tdist.stream_offset("streams", rank, world))
         assert len(set(offs)) == world

@@ -1,0 +1,166 @@
+"""Raycast of a spatially sharded volume (SURVEY.md 8e raycast composite).
+
+Every shard packs the blocks a raycast of the render camera can read (tsdf_render_blocks, a
+conservative view-pyramid selection), the union is imported into a scratch replica engine
+(tsdf_import_blocks) and rendered there with the unchanged raycast kernel. The images must equal the
+unsharded engine's tsdf_raycast bit for bit: ray_cast_kernel (voxel_tsdf.cu:232-307) reads only
+voxels inside the selection, and a missing block reads as the default voxel on both sides.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+W, H, VOXEL, TRUNC = 96, 72, 0.01, 0.04
+
+
+def _engines(G, nb_bits=13, w=W, h=H, voxel=VOXEL, trunc=TRUNC):
+    import tsdf_amd
+    full = tsdf_amd.Engine(voxel, trunc, max_width=w, max_height=h, num_block_bits=nb_bits)
+    shards = [tsdf_amd.Engine(voxel, trunc, max_width=w, max_height=h, num_block_bits=nb_bits,
+                              shard_index=i, shard_count=G) for i in range(G)]
+    replica = tsdf_amd.Engine(voxel, trunc, max_width=w, max_height=h, num_block_bits=nb_bits)
+    return full, shards, replica
+
+
+def _integrate(engines, cam, frames, stride=2):
+    import tsdf_amd
+    from tsdf_amd import synth
+    for f in range(frames):
+        fr = synth.render(cam, stride * f)
+        for e in engines:
+            e.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K,
+                        tsdf_amd.SE3(fr["q"], fr["t"]), 4.0)
+
+
+def _views(cam):
+    """Render cameras: a mapped pose, an in-between pose, and a narrow (4x focal) view."""
+    import tsdf_amd
+    from tsdf_amd import synth
+    out = []
+    for f, zoom in ((8, 1.0), (3, 1.0), (5, 4.0)):
+        fr = synth.render(cam, f)
+        K = np.array(cam.K, np.float32).copy()
+        K[:2] *= zoom
+        out.append((K, tsdf_amd.SE3(fr["q"], fr["t"])))
+    return out
+
+
+def _close(*engines):
+    for e in engines:
+        e.close()
+
+
+def test_replica_of_unsharded_volume_renders_identically():
+    from tsdf_amd import synth
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    full, _, replica = _engines(0)
+    try:
+        _integrate([full], cam, 6)
+        active = full.stats()["active_blocks"]
+        for K, pose in _views(cam):
+            recs = full.render_blocks(K, W, H, pose, 4.0)
+            assert 0 < recs.shape[0] <= active
+            replica.reset()
+            assert replica.stats()["active_blocks"] == 0
+            replica.import_blocks(recs)
+            assert replica.stats()["active_blocks"] == recs.shape[0]
+            exp = full.raycast(K, W, H, pose, 4.0)
+            got = replica.raycast(K, W, H, pose, 4.0)
+            assert (exp[0][..., 3] == 255).sum() > 0.3 * W * H  # the view hits the surface
+            np.testing.assert_array_equal(got[0], exp[0])
+            np.testing.assert_array_equal(got[1], exp[1])
+        # the narrow view selects a strict subset of the volume
+        K, pose = _views(cam)[2]
+        assert full.render_blocks(K, W, H, pose, 4.0).shape[0] < active
+    finally:
+        _close(full, replica)
+
+
+def test_imported_blocks_equal_their_source():
+    """Imported payload = source payload: Query of the replica is a subset of the source's Query
+    (positions and tsdf bit-exact), one whole block per record; keys already present are kept."""
+    from tsdf_amd import synth
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    full, _, replica = _engines(0)
+    try:
+        _integrate([full], cam, 4)
+        K, pose = _views(cam)[0]
+        recs = full.render_blocks(K, W, H, pose, 4.0)
+        replica.import_blocks(recs)
+        replica.import_blocks(recs[: recs.shape[0] // 2])  # re-import: no new blocks
+        assert replica.stats()["active_blocks"] == recs.shape[0]
+        key = lambda a: {bytes(r) for r in a.view(np.uint8).reshape(a.shape[0], -1)}
+        got = replica.query(None)
+        assert got.shape[0] == 512 * recs.shape[0]
+        assert key(got) <= key(full.query(None))
+        hdr = recs[:, :16].view(np.int16)[:, :4]
+        assert (hdr[:, 3] == 0).all() and len({tuple(h) for h in hdr[:, :3]}) == recs.shape[0]
+    finally:
+        _close(full, replica)
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_sharded_render_equals_unsharded(G):
+    import torch
+
+    from tsdf_amd import synth
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    full, shards, replica = _engines(G)
+    try:
+        _integrate([full] + shards, cam, 6)
+        for K, pose in _views(cam):
+            parts = [e.render_blocks(K, W, H, pose, 4.0, device=True) for e in shards]
+            assert sum(p.shape[0] for p in parts) == full.render_blocks(K, W, H, pose, 4.0).shape[0]
+            replica.reset()
+            replica.import_blocks(torch.cat(parts))
+            exp = full.raycast(K, W, H, pose, 4.0)
+            got = replica.raycast(K, W, H, pose, 4.0)
+            np.testing.assert_array_equal(got[0], exp[0])
+            np.testing.assert_array_equal(got[1], exp[1])
+    finally:
+        _close(full, replica, *shards)
+
+
+def test_sharded_render_bench_scale():
+    """C3 geometry (640x480, 5 mm, 3 cm truncation), 8 shards after 12 frames of the orbit."""
+    import torch
+
+    from tsdf_amd import synth
+    w, h, G = 640, 480, 8
+    cam = synth.camera(w, h, synth.TUM_FR1)
+    full, shards, replica = _engines(G, nb_bits=16, w=w, h=h, voxel=0.005, trunc=0.03)
+    try:
+        _integrate([full] + shards, cam, 12, stride=3)
+        fr = synth.render(cam, 20)
+        import tsdf_amd
+        pose = tsdf_amd.SE3(fr["q"], fr["t"])
+        parts = [e.render_blocks(cam.K, w, h, pose, 4.0, device=True) for e in shards]
+        replica.import_blocks(torch.cat(parts))
+        exp = full.raycast(cam.K, w, h, pose, 4.0)
+        got = replica.raycast(cam.K, w, h, pose, 4.0)
+        assert (exp[0][..., 3] == 255).sum() > 0.5 * w * h
+        np.testing.assert_array_equal(got[0], exp[0])
+        np.testing.assert_array_equal(got[1], exp[1])
+    finally:
+        _close(full, replica, *shards)
+
+
+def test_import_errors():
+    import tsdf_amd
+    from tsdf_amd import synth
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    full, _, _ = _engines(0)
+    small = tsdf_amd.Engine(VOXEL, TRUNC, max_width=W, max_height=H, num_block_bits=6)
+    try:
+        _integrate([full], cam, 4)
+        K, pose = _views(cam)[0]
+        recs = full.render_blocks(K, W, H, pose, 4.0)
+        assert recs.shape[0] > 64
+        with pytest.raises(tsdf_amd.TSDFError):
+            small.import_blocks(recs)  # 64-block pool
+        small.reset()
+        small.import_blocks(recs[:10])
+        assert small.stats()["active_blocks"] == 10
+    finally:
+        _close(full, small)
