@@ -291,14 +291,15 @@ int32_t tsdf_num_blocks(const tsdf_engine* e) { return e ? e->D.nblocks : 0; }
 
 namespace {
 // empty volume: table, occupancy, free stack, log-odds pool, counters and key sets (tsdf_create,
-// tsdf_reset)
-bool init_state(tsdf_engine* e) {
+// tsdf_reset); with_pool false leaves the voxel pool as it is (tsdf_import_blocks replace: every
+// block that becomes live is written by the import, free blocks are never read)
+bool init_state(tsdf_engine* e, bool with_pool = true) {
   hipStream_t s = e->stream;
   const EngineDev& D = e->D;
   const int nb = D.nblocks;
   bool ok = true;
   ok &= hipMemsetAsync(D.lock_tag, 0, sizeof(uint32_t) * kNumBucket, s) == hipSuccess;
-  ok &= hipMemsetAsync(D.pool, 0, (size_t)nb * kBlockBytes, s) == hipSuccess;
+  if (with_pool) ok &= hipMemsetAsync(D.pool, 0, (size_t)nb * kBlockBytes, s) == hipSuccess;
   ok &= hipMemsetAsync(D.occ, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
   ok &= hipMemsetAsync(D.nk_key, 0, sizeof(unsigned long long) * kNewKeyCap, s) == hipSuccess;
   ok &= hipMemsetAsync(D.nk_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
@@ -313,8 +314,9 @@ bool init_state(tsdf_engine* e) {
   ok &= hipMemcpyAsync(D.ctr, &c0, sizeof(c0), hipMemcpyHostToDevice, s) == hipSuccess;
   hipLaunchKernelGGL(k_init_table, dim3(kNumEntry / 256), dim3(256), 0, s, D.table);
   hipLaunchKernelGGL(k_init_heap, dim3((nb + 255) / 256), dim3(256), 0, s, D.heap, nb);
-  hipLaunchKernelGGL(k_init_logodds, dim3((unsigned)(((size_t)nb * (kBlockVolume / 4) + 255) / 256)), dim3(256),
-                     0, s, D.pool, nb);
+  if (with_pool)
+    hipLaunchKernelGGL(k_init_logodds, dim3((unsigned)(((size_t)nb * (kBlockVolume / 4) + 255) / 256)),
+                       dim3(256), 0, s, D.pool, nb);
   ok &= hipGetLastError() == hipSuccess;
   ok &= hipStreamSynchronize(s) == hipSuccess;
   return ok;
@@ -1002,7 +1004,7 @@ int tsdf_render_blocks(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H,
   return TSDF_OK;
 }
 
-int tsdf_import_blocks(tsdf_engine* e, const void* records, int64_t n, int mem_kind) {
+int tsdf_import_blocks(tsdf_engine* e, const void* records, int64_t n, int mem_kind, int replace) {
   TraceRange trace_("tsdf_import_blocks");
   if (!e || n < 0 || (n > 0 && !records) ||
       (mem_kind != TSDF_MEM_HOST && mem_kind != TSDF_MEM_DEVICE)) {
@@ -1013,8 +1015,12 @@ int tsdf_import_blocks(tsdf_engine* e, const void* records, int64_t n, int mem_k
     set_error("tsdf_import_blocks: a routed frame is pending");
     return TSDF_ERR_INVALID_ARG;
   }
-  if (n == 0) return TSDF_OK;
   HIP_OK(hipSetDevice(e->device));
+  if (replace && !init_state(e, false)) {
+    set_error("tsdf_import_blocks: clearing the volume failed");
+    return TSDF_ERR_HIP;
+  }
+  if (n == 0) return TSDF_OK;
   hipStream_t s = e->stream;
   const size_t bytes = (size_t)n * kBlockRecBytes;
   const uint8_t* recs = reinterpret_cast<const uint8_t*>(records);

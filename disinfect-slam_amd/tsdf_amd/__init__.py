@@ -418,13 +418,14 @@ class Engine:
                        "tsdf_render_blocks")
         return out
 
-    def import_blocks(self, records):
-        """Allocate and fill the blocks of render records (tsdf_import_blocks); numpy or GPU tensor."""
+    def import_blocks(self, records, replace=False):
+        """Allocate and fill the blocks of render records (tsdf_import_blocks); numpy or GPU tensor.
+        replace: empty the volume first, so it holds exactly these blocks."""
         n = int(records.shape[0]) if records.ndim == 2 else int(records.size) // BLOCK_RECORD_BYTES
         kind = TSDF_MEM_DEVICE if _is_torch_cuda(records) else TSDF_MEM_HOST
         if kind == TSDF_MEM_HOST:
             records = np.ascontiguousarray(records, dtype=np.uint8)
-        _lib.check(_lib.load().tsdf_import_blocks(self._h, _ptr(records), n, kind),
+        _lib.check(_lib.load().tsdf_import_blocks(self._h, _ptr(records), n, kind, int(replace)),
                    "tsdf_import_blocks")
 
     def reset(self):

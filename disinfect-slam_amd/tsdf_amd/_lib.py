@@ -138,7 +138,7 @@ def load(path: str | None = None):
     L.tsdf_snapshot_load.argtypes = [P, P, i64]
     L.tsdf_render_blocks.argtypes = [P, C.POINTER(Intrinsics), i, i, C.POINTER(Pose), f, P, i64,
                                      C.POINTER(i64), i]
-    L.tsdf_import_blocks.argtypes = [P, P, i64, i]
+    L.tsdf_import_blocks.argtypes = [P, P, i64, i, i]
     L.tsdf_reset.argtypes = [P]
     L.tsdf_query.argtypes = [P, P, P, i64, C.POINTER(i64)]
     L.tsdf_extract_mesh.argtypes = [P, P, f, i, P, i64, C.POINTER(i64), i]

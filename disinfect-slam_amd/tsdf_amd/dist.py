@@ -145,6 +145,5 @@ def render_sharded(engine, replica, K, width, height, cam_T_world, max_depth, de
     Returns (rgba, normal) as numpy (H, W, 4) uint8."""
     recs = engine.render_blocks(K, width, height, cam_T_world, max_depth, device=device)
     allrecs = gather_rows(recs)
-    replica.reset()
-    replica.import_blocks(allrecs if device else allrecs.numpy())
+    replica.import_blocks(allrecs if device else allrecs.numpy(), replace=True)
     return replica.raycast(K, width, height, cam_T_world, max_depth)

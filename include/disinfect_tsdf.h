@@ -191,15 +191,18 @@ int tsdf_query(tsdf_engine* e, const float* bounds, tsdf_voxel* out, int64_t cap
  * tsdf f32[512], log-odds f32[512], rgbw u8x4[512]} in entry order. Two-call: out == NULL returns
  * *count only; then out must hold capacity >= *count records (host or device memory per mem_kind).
  * tsdf_import_blocks allocates every record's block in the engine (resolver launches until none is
- * missing) and writes its payload; a scratch engine that imported every shard's records renders
+ * missing) and writes its payload; replace != 0 first empties the volume (table, occupancy, free
+ * stack, counters; free pool blocks keep stale contents, which nothing reads), so the engine then
+ * holds exactly the records' blocks. A scratch engine that imported every shard's records renders
  * with tsdf_raycast exactly what the unsharded volume renders (ray_cast_kernel,
- * voxel_tsdf.cu:232-307). tsdf_reset empties an engine (as created). No reference counterpart:
- * TSDFGrid is single-GPU. */
+ * voxel_tsdf.cu:232-307). tsdf_reset empties an engine to its state as created (pool included).
+ * No reference counterpart: TSDFGrid is single-GPU. */
 #define TSDF_BLOCK_RECORD_BYTES 6160
 int tsdf_render_blocks(tsdf_engine* e, const tsdf_intrinsics* K, int width, int height,
                        const tsdf_pose* cam_T_world, float max_depth, void* out, int64_t capacity,
                        int64_t* count, int mem_kind);
-int tsdf_import_blocks(tsdf_engine* e, const void* records, int64_t n, int mem_kind);
+int tsdf_import_blocks(tsdf_engine* e, const void* records, int64_t n, int mem_kind,
+                       int replace);
 int tsdf_reset(tsdf_engine* e);
 
 /* Marching-cubes mesh of the volume (GPU; replaces Query + KrisLibrary

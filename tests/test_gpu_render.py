@@ -112,8 +112,8 @@ def test_sharded_render_equals_unsharded(G):
         for K, pose in _views(cam):
             parts = [e.render_blocks(K, W, H, pose, 4.0, device=True) for e in shards]
             assert sum(p.shape[0] for p in parts) == full.render_blocks(K, W, H, pose, 4.0).shape[0]
-            replica.reset()
-            replica.import_blocks(torch.cat(parts))
+            replica.import_blocks(torch.cat(parts), replace=True)  # drops the previous view's blocks
+            assert replica.stats()["active_blocks"] == sum(p.shape[0] for p in parts)
             exp = full.raycast(K, W, H, pose, 4.0)
             got = replica.raycast(K, W, H, pose, 4.0)
             np.testing.assert_array_equal(got[0], exp[0])
@@ -164,3 +164,61 @@ def test_import_errors():
         assert small.stats()["active_blocks"] == 10
     finally:
         _close(full, small)
+
+
+def _render_worker(rank, world, port, q):
+    import os
+    import sys
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "disinfect-slam_amd"))
+    import torch
+    import torch.distributed as dist
+
+    import tsdf_amd
+    from tsdf_amd import dist as tdist
+    from tsdf_amd import synth
+    torch.cuda.init()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cam = synth.camera(W, H, synth.TUM_FR1)
+        shard = tsdf_amd.Engine(VOXEL, TRUNC, max_width=W, max_height=H, num_block_bits=13,
+                                shard_index=rank, shard_count=world)
+        replica = tsdf_amd.Engine(VOXEL, TRUNC, max_width=W, max_height=H, num_block_bits=13)
+        engines = [shard]
+        if rank == 0:
+            full = tsdf_amd.Engine(VOXEL, TRUNC, max_width=W, max_height=H, num_block_bits=13)
+            engines.append(full)
+        _integrate(engines, cam, 6)
+        for K, pose in _views(cam):
+            got = tdist.render_sharded(shard, replica, K, W, H, pose, 4.0, device=False)
+            if rank == 0:
+                exp = full.raycast(K, W, H, pose, 4.0)
+                assert np.array_equal(got[0], exp[0]) and np.array_equal(got[1], exp[1])
+        dist.barrier()
+        for e in engines + [replica]:
+            e.close()
+        q.put((rank, "ok"))
+    except BaseException as ex:  # report to the parent instead of hanging the spawn
+        q.put((rank, repr(ex)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_render_sharded_two_ranks():
+    """tsdf_amd.dist.render_sharded across 2 processes (gloo all-gather of host records, both ranks
+    on this GPU): rank 0's image equals its unsharded engine's raycast bit for bit."""
+    import socket
+
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_render_worker, args=(2, port, q), nprocs=2, join=True, start_method="spawn")
+    res = dict(q.get(timeout=5) for _ in range(2))
+    assert res == {0: "ok", 1: "ok"}, res
