@@ -151,11 +151,22 @@ def main():
         raise SystemExit("--graph / --loop c5 take streams or sharded mode")
     graph = None
     mesh_tris = []
+    # C5 over a sharded volume: the graph frame integrates only; every frame's render is the raycast
+    # composite (tsdf_amd.dist.render_sharded: view-selected block records all-gathered over RCCL
+    # into a replica engine, raycast there), since one shard's own raycast sees only its blocks
+    composite = a.loop == "c5" and shard_count > 1
+    replica = None
     if use_graph:
-        rw, rh = (a.width, a.height) if a.loop == "c5" else (0, 0)
+        rw, rh = (a.width, a.height) if (a.loop == "c5" and not composite) else (0, 0)
         graph = eng.frame_graph(a.width, a.height, rw, rh)
         rgba = torch.zeros((a.height, a.width, 4), dtype=torch.uint8, device=dev) if rw else None
         normal = torch.zeros_like(rgba) if rw else None
+        if composite:
+            replica = tsdf_amd.Engine(a.voxel, a.trunc, max_width=a.width, max_height=a.height,
+                                      num_block_bits=a.block_bits, device=torch.cuda.current_device(),
+                                      stream=stream.cuda_stream)
+            c_rgba = torch.zeros((a.height, a.width, 4), dtype=torch.uint8, device=dev)
+            c_normal = torch.zeros_like(c_rgba)
         mesh_buf = torch.empty(9 * (8 << 20), dtype=torch.float32, device=dev) if a.loop == "c5" else None
 
     def step(i):
@@ -164,6 +175,9 @@ def main():
         if graph is not None:
             graph.frame(frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i], a.max_depth,
                         K if rgba is not None else None, poses[i] if rgba is not None else None, rgba, normal)
+            if replica is not None:
+                tdist.render_sharded(eng, replica, K, a.width, a.height, poses[i], a.max_depth,
+                                     rgba=c_rgba, normal=c_normal)
             if a.loop == "c5" and (i + 1) % 30 == 0:  # marching cubes of the whole volume (on device)
                 mesh_tris.append(int(eng.extract_mesh(None, 0.99, 0, out=mesh_buf).shape[0]))
         elif routed:
@@ -252,6 +266,9 @@ def main():
             metric = ("C5 frame loop frames/s (integrate + raycast every frame, marching cubes every 30 "
                       "frames, one hipGraph launch per frame)")
             workload = "C5: " + workload
+            if replica is not None:
+                workload += (", sharded volume: per-frame raycast composite (view-selected block records "
+                             "all-gathered into a replica engine)")
         elif graph is not None:
             workload += " (hipGraph frame)"
         out = {
@@ -316,6 +333,8 @@ def main():
         graph.close()
     for e_k, _, _, _ in extra:
         e_k.close()
+    if replica is not None:
+        replica.close()
     eng.close()
     if dist:
         dist.destroy_process_group()

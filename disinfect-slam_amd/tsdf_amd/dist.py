@@ -136,14 +136,15 @@ def gather_rows(rows, device=None):
     return torch.cat([allrows[r * cap:r * cap + counts[r]] for r in range(world)])
 
 
-def render_sharded(engine, replica, K, width, height, cam_T_world, max_depth, device=True):
+def render_sharded(engine, replica, K, width, height, cam_T_world, max_depth, device=True,
+                   rgba=None, normal=None):
     """Raycast of a spatially sharded volume (SURVEY.md 8e raycast composite): every
     rank packs the blocks of its shard that this camera's rays can read (tsdf_render_blocks), the
     records are all-gathered (RCCL over xGMI on the GPU box), and `replica` -- a scratch engine of
     the same voxel size / truncation with room for them -- imports the union and renders it with
     the unchanged raycast kernel. Every rank gets the image the unsharded volume renders.
-    Returns (rgba, normal) as numpy (H, W, 4) uint8."""
+    Returns (rgba, normal) as numpy (H, W, 4) uint8, or the given device tensors rgba / normal."""
     recs = engine.render_blocks(K, width, height, cam_T_world, max_depth, device=device)
     allrecs = gather_rows(recs)
     replica.import_blocks(allrecs if device else allrecs.numpy(), replace=True)
-    return replica.raycast(K, width, height, cam_T_world, max_depth)
+    return replica.raycast(K, width, height, cam_T_world, max_depth, rgba=rgba, normal=normal)
