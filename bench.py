@@ -179,7 +179,11 @@ def main():
                 tdist.render_sharded(eng, replica, K, a.width, a.height, poses[i], a.max_depth,
                                      rgba=c_rgba, normal=c_normal)
             if a.loop == "c5" and (i + 1) % 30 == 0:  # marching cubes of the whole volume (on device)
-                mesh_tris.append(int(eng.extract_mesh(None, 0.99, 0, out=mesh_buf).shape[0]))
+                if replica is not None:  # sharded: all blocks gathered into the replica first
+                    mesh_tris.append(int(tdist.mesh_sharded(eng, replica, None, 0.99, 0,
+                                                            out=mesh_buf).shape[0]))
+                else:
+                    mesh_tris.append(int(eng.extract_mesh(None, 0.99, 0, out=mesh_buf).shape[0]))
         elif routed:
             eng.integrate_route_begin(frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i],
                                       a.max_depth, rank, world, outbox, a.route_cap)
@@ -268,7 +272,7 @@ def main():
             workload = "C5: " + workload
             if replica is not None:
                 workload += (", sharded volume: per-frame raycast composite (view-selected block records "
-                             "all-gathered into a replica engine)")
+                             "all-gathered into a replica engine), marching cubes of the gathered volume")
         elif graph is not None:
             workload += " (hipGraph frame)"
         out = {

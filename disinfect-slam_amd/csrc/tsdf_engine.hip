@@ -927,6 +927,30 @@ int tsdf_query(tsdf_engine* e, const float* bounds, tsdf_voxel* out, int64_t cap
   return TSDF_OK;
 }
 
+namespace {
+// the nsel blocks listed in q_sel as TSDF_BLOCK_RECORD_BYTES records into out (host or device)
+int pack_selected(tsdf_engine* e, int32_t nsel, void* out, int mem_kind, const char* what) {
+  hipStream_t s = e->stream;
+  const size_t bytes = (size_t)nsel * kBlockRecBytes;
+  uint8_t* dst = reinterpret_cast<uint8_t*>(out);
+  uint8_t* tmp = nullptr;
+  if (mem_kind == TSDF_MEM_HOST) {
+    HIP_OK(dmalloc(&tmp, bytes));
+    dst = tmp;
+  }
+  hipLaunchKernelGGL(k_render_pack, dim3(nsel), dim3(256), 0, s, e->D, e->q_sel, dst);
+  hipError_t err = hipGetLastError();
+  if (err == hipSuccess && tmp) err = hipMemcpyAsync(out, tmp, bytes, hipMemcpyDeviceToHost, s);
+  if (err == hipSuccess) err = hipStreamSynchronize(s);
+  if (tmp) (void)hipFree(tmp);
+  if (err != hipSuccess) {
+    set_error(what, err);
+    return TSDF_ERR_HIP;
+  }
+  return TSDF_OK;
+}
+}  // namespace
+
 static_assert(kBlockRecBytes == TSDF_BLOCK_RECORD_BYTES, "render record layout");
 
 int tsdf_reset(tsdf_engine* e) {
@@ -985,23 +1009,39 @@ int tsdf_render_blocks(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H,
     set_error("tsdf_render_blocks: capacity too small");
     return TSDF_ERR_CAPACITY;
   }
-  const size_t bytes = (size_t)nsel * kBlockRecBytes;
-  uint8_t* dst = reinterpret_cast<uint8_t*>(out);
-  uint8_t* tmp = nullptr;
-  if (mem_kind == TSDF_MEM_HOST) {
-    HIP_OK(dmalloc(&tmp, bytes));
-    dst = tmp;
+  return pack_selected(e, nsel, out, mem_kind, "tsdf_render_blocks");
+}
+
+int tsdf_pack_blocks(tsdf_engine* e, const float* bounds, void* out, int64_t capacity,
+                     int64_t* count, int mem_kind) {
+  TraceRange trace_("tsdf_pack_blocks");
+  if (!e || !count || (mem_kind != TSDF_MEM_HOST && mem_kind != TSDF_MEM_DEVICE)) {
+    set_error("tsdf_pack_blocks: invalid argument");
+    return TSDF_ERR_INVALID_ARG;
   }
-  hipLaunchKernelGGL(k_render_pack, dim3(nsel), dim3(256), 0, s, e->D, e->q_sel, dst);
-  hipError_t err = hipGetLastError();
-  if (err == hipSuccess && tmp) err = hipMemcpyAsync(out, tmp, bytes, hipMemcpyDeviceToHost, s);
-  if (err == hipSuccess) err = hipStreamSynchronize(s);
-  if (tmp) (void)hipFree(tmp);
-  if (err != hipSuccess) {
-    set_error("tsdf_render_blocks", err);
-    return TSDF_ERR_HIP;
+  HIP_OK(hipSetDevice(e->device));
+  short4 lo = make_short4(0, 0, 0, 0), hi = make_short4(0, 0, 0, 0);
+  if (bounds) {  // the Query block selection (voxel_tsdf.cuh:21-26, voxel_tsdf.cu:429)
+    const float scale = (float)(1. / (double)e->cfg.voxel_size);
+    lo = make_short4(h_f2s(bounds[0] * scale), h_f2s(bounds[2] * scale), h_f2s(bounds[4] * scale), 0);
+    hi = make_short4(h_f2s(bounds[1] * scale), h_f2s(bounds[3] * scale), h_f2s(bounds[5] * scale), 0);
   }
-  return TSDF_OK;
+  hipStream_t s = e->stream;
+  hipLaunchKernelGGL(k_query_count, dim3(kOccWords / 256), dim3(256), 0, s, e->D, bounds ? 1 : 0,
+                     lo, hi);
+  hipLaunchKernelGGL(k_vis_emit, dim3(kOccWords / 256), dim3(256), 0, s, e->D, e->q_sel,
+                     e->q_count);
+  LAUNCH_OK("pack select");
+  int32_t nsel = 0;
+  HIP_OK(hipMemcpyAsync(&nsel, e->q_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  *count = nsel;
+  if (!out || nsel == 0) return TSDF_OK;
+  if (capacity < nsel) {
+    set_error("tsdf_pack_blocks: capacity too small");
+    return TSDF_ERR_CAPACITY;
+  }
+  return pack_selected(e, nsel, out, mem_kind, "tsdf_pack_blocks");
 }
 
 int tsdf_import_blocks(tsdf_engine* e, const void* records, int64_t n, int mem_kind, int replace) {

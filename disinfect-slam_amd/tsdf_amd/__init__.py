@@ -418,6 +418,27 @@ class Engine:
                        "tsdf_render_blocks")
         return out
 
+    def pack_blocks(self, bounds=None, device=False):
+        """Records (n, TSDF_BLOCK_RECORD_BYTES) of the Query block selection (tsdf_pack_blocks;
+        bounds None = every live block): numpy, or a torch tensor on this engine's GPU."""
+        L = _lib.load()
+        b = None if bounds is None else np.ascontiguousarray(
+            bounds.as_array() if isinstance(bounds, BoundingCube) else bounds, dtype=np.float32)
+        n = C.c_int64()
+        _lib.check(L.tsdf_pack_blocks(self._h, _ptr(b), None, 0, C.byref(n), TSDF_MEM_HOST),
+                   "tsdf_pack_blocks")
+        if device:
+            import torch
+            out = torch.empty((n.value, BLOCK_RECORD_BYTES), dtype=torch.uint8,
+                              device=f"cuda:{self.device}")
+        else:
+            out = np.empty((n.value, BLOCK_RECORD_BYTES), np.uint8)
+        if n.value:
+            _lib.check(L.tsdf_pack_blocks(self._h, _ptr(b), _ptr(out), n.value, C.byref(n),
+                                          TSDF_MEM_DEVICE if device else TSDF_MEM_HOST),
+                       "tsdf_pack_blocks")
+        return out
+
     def import_blocks(self, records, replace=False):
         """Allocate and fill the blocks of render records (tsdf_import_blocks); numpy or GPU tensor.
         replace: empty the volume first, so it holds exactly these blocks."""

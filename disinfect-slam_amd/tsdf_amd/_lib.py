@@ -99,7 +99,7 @@ EXPORTS = [
     "tsdf_route_buffer_bytes", "tsdf_integrate_route_begin", "tsdf_integrate_route_end",
     "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame", "tsdf_graph_destroy",
     "tsdf_snapshot_bytes", "tsdf_snapshot_save", "tsdf_snapshot_load",
-    "tsdf_render_blocks", "tsdf_import_blocks", "tsdf_reset",
+    "tsdf_render_blocks", "tsdf_import_blocks", "tsdf_reset", "tsdf_pack_blocks",
 ]
 
 _lib = None
@@ -140,6 +140,7 @@ def load(path: str | None = None):
                                      C.POINTER(i64), i]
     L.tsdf_import_blocks.argtypes = [P, P, i64, i, i]
     L.tsdf_reset.argtypes = [P]
+    L.tsdf_pack_blocks.argtypes = [P, P, P, i64, C.POINTER(i64), i]
     L.tsdf_query.argtypes = [P, P, P, i64, C.POINTER(i64)]
     L.tsdf_extract_mesh.argtypes = [P, P, f, i, P, i64, C.POINTER(i64), i]
     L.tsdf_get_stats.argtypes = [P, C.POINTER(Stats), i]

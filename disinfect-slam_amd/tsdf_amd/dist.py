@@ -148,3 +148,16 @@ def render_sharded(engine, replica, K, width, height, cam_T_world, max_depth, de
     allrecs = gather_rows(recs)
     replica.import_blocks(allrecs if device else allrecs.numpy(), replace=True)
     return replica.raycast(K, width, height, cam_T_world, max_depth, rgba=rgba, normal=normal)
+
+
+def mesh_sharded(engine, replica, bounds=None, missing_tsdf=0.99, min_weight=0, device=True,
+                 out=None):
+    """Marching cubes of a spatially sharded volume: a shard's own extraction misses the cells that
+    straddle another owner's blocks, so every rank packs all its live blocks (tsdf_pack_blocks),
+    the records are all-gathered, `replica` imports the union -- the whole unsharded volume -- and
+    extracts there (tsdf_extract_mesh with bounds). Same triangles as the unsharded mesh, in the
+    replica's entry order."""
+    recs = engine.pack_blocks(None, device=device)
+    allrecs = gather_rows(recs)
+    replica.import_blocks(allrecs if device else allrecs.numpy(), replace=True)
+    return replica.extract_mesh(bounds, missing_tsdf, min_weight, out=out)

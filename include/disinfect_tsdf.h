@@ -204,6 +204,11 @@ int tsdf_render_blocks(tsdf_engine* e, const tsdf_intrinsics* K, int width, int 
 int tsdf_import_blocks(tsdf_engine* e, const void* records, int64_t n, int mem_kind,
                        int replace);
 int tsdf_reset(tsdf_engine* e);
+/* The same records for the Query block selection (bounds as tsdf_query, NULL = every live block):
+ * a replica that imports every shard's records with bounds NULL is the whole unsharded volume, so
+ * its tsdf_extract_mesh equals the unsharded mesh (as a set of triangles). */
+int tsdf_pack_blocks(tsdf_engine* e, const float* bounds, void* out, int64_t capacity,
+                     int64_t* count, int mem_kind);
 
 /* Marching-cubes mesh of the volume (GPU; replaces Query + KrisLibrary
  * SparseTSDFReconstruction::ExtractMesh in examples/ros_camera_driver/ros_offline.cc:258-318).

@@ -146,6 +146,44 @@ def test_sharded_render_bench_scale():
         _close(full, replica, *shards)
 
 
+def _tri_set(t):
+    t = np.ascontiguousarray(t, dtype=np.float32).reshape(-1, 9)
+    return t[np.lexsort(t.view(np.uint32).T[::-1])].view(np.uint32)
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_sharded_mesh_equals_unsharded(G):
+    """tsdf_pack_blocks (all live blocks) -> replica -> tsdf_extract_mesh = the unsharded mesh as a
+    set of triangles; the union of the shards' own meshes is not (cells across owners are lost)."""
+    import torch
+
+    from tsdf_amd import synth
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    full, shards, replica = _engines(G)
+    try:
+        _integrate([full] + shards, cam, 6)
+        xyz = full.query(None).view(np.float32).reshape(-1, 4)[:, :3]
+        lo, hi = np.percentile(xyz, 20, axis=0), np.percentile(xyz, 80, axis=0)
+        box = np.array([lo[0], hi[0], lo[1], hi[1], lo[2], hi[2]], np.float32)
+        parts = [e.pack_blocks(None, device=True) for e in shards]
+        assert sum(p.shape[0] for p in parts) == full.stats()["active_blocks"]
+        replica.import_blocks(torch.cat(parts), replace=True)
+        for bounds in (None, box):
+            exp = full.extract_mesh(bounds)
+            got = replica.extract_mesh(bounds)
+            assert exp.shape[0] > 100
+            np.testing.assert_array_equal(_tri_set(got), _tri_set(exp))
+        own = _tri_set(np.concatenate([e.extract_mesh(None) for e in shards]))
+        ref = _tri_set(full.extract_mesh(None))
+        assert own.shape != ref.shape or not np.array_equal(own, ref)
+        # bounded packing selects the Query blocks of the box
+        sel = full.pack_blocks(box)
+        assert 0 < sel.shape[0] < full.stats()["active_blocks"]
+        assert sel.shape[0] * 512 == full.query(box).shape[0]
+    finally:
+        _close(full, replica, *shards)
+
+
 def test_import_errors():
     import tsdf_amd
     from tsdf_amd import synth
@@ -196,6 +234,9 @@ def _render_worker(rank, world, port, q):
             if rank == 0:
                 exp = full.raycast(K, W, H, pose, 4.0)
                 assert np.array_equal(got[0], exp[0]) and np.array_equal(got[1], exp[1])
+        tris = tdist.mesh_sharded(shard, replica, device=False)
+        if rank == 0:
+            assert np.array_equal(_tri_set(tris), _tri_set(full.extract_mesh(None)))
         dist.barrier()
         for e in engines + [replica]:
             e.close()
