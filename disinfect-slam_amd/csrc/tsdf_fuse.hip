@@ -91,19 +91,26 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
       float4 ts = make_float4(0.5f, 0.5f, 0.5f, 0.5f), pr = ts;
       uint4 cw = make_uint4(0x05808080u, 0x05808080u, 0x05808080u, 0x05808080u);
 #else
-      float4 ts = pool_ld(blk + off);
-      float4 pr = pool_ld(blk + kProbOffset + off);
-      uint4 cw = pool_ldu(blk + kRgbwOffset + off);
-#endif
+      float4 ts, pr;
+      uint4 cw;
       fresh = r.pad != 0;
-      if (fresh) {
+      if (fresh) {  // wave-uniform: a block created this frame loads only its colour bytes
         ts = make_float4(-1.f, -1.f, -1.f, -1.f);
         pr = make_float4(0.f, 0.f, 0.f, 0.f);  // log-odds of AquireBlock's p = 0.5
+        cw = pool_ldu(blk + kRgbwOffset + off);
         cw.x &= 0x00FFFFFFu;
         cw.y &= 0x00FFFFFFu;
         cw.z &= 0x00FFFFFFu;
         cw.w &= 0x00FFFFFFu;
+      } else {
+        ts = pool_ld(blk + off);
+        pr = pool_ld(blk + kProbOffset + off);
+        cw = pool_ldu(blk + kRgbwOffset + off);
       }
+#endif
+#if defined(TSDF_EXP) && (TSDF_EXP & 2)
+      fresh = r.pad != 0;
+#endif
       const int16_t ax0 = (int16_t)(r.x << kBlockLenBits), ay = (int16_t)((r.y << kBlockLenBits) + ry),
                     az = (int16_t)((r.z << kBlockLenBits) + rz);
       const float fy = (float)ay * P.voxel, fz = (float)az * P.voxel;
