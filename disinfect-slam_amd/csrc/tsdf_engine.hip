@@ -1097,31 +1097,20 @@ int tsdf_import_blocks(tsdf_engine* e, const void* records, int64_t n, int mem_k
       if (hipGetLastError() != hipSuccess) return done(TSDF_ERR_HIP);
       int rc = launch_resolve_alloc(e, FrameParams{}, (uint32_t)m, 0);
       if (rc) return done(rc);
-      rc = read_counters(e);
-      if (rc) return done(rc);
-      if (e->h_ctr->status & TSDF_STATUS_POOL_EXHAUSTED) {
-        set_error("tsdf_import_blocks: voxel block pool exhausted");
-        return done(TSDF_ERR_OUT_OF_MEMORY);
-      }
+      // every record whose block exists gets its payload; the rest are counted (one round trip
+      // for that count and the status word)
       if (hipMemsetAsync(e->q_count, 0, sizeof(int32_t), s) != hipSuccess) return done(TSDF_ERR_HIP);
-      hipLaunchKernelGGL(k_import_missing, dim3((m + 255) / 256), dim3(256), 0, s, e->D, chunk, m,
-                         e->q_count);
+      hipLaunchKernelGGL(k_import_payload, dim3((unsigned)m), dim3(256), 0, s, e->D, chunk, e->q_count);
       if (hipGetLastError() != hipSuccess ||
+          hipMemcpyAsync(e->h_ctr, e->D.ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s) != hipSuccess ||
           hipMemcpyAsync(&missing, e->q_count, sizeof(int32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
           hipStreamSynchronize(s) != hipSuccess)
         return done(TSDF_ERR_HIP);
+      if (missing > 0 && (e->h_ctr->status & TSDF_STATUS_POOL_EXHAUSTED)) {
+        set_error("tsdf_import_blocks: voxel block pool exhausted");
+        return done(TSDF_ERR_OUT_OF_MEMORY);
+      }
     }
-  }
-  int32_t missing = 0;
-  if (hipMemsetAsync(e->q_count, 0, sizeof(int32_t), s) != hipSuccess) return done(TSDF_ERR_HIP);
-  hipLaunchKernelGGL(k_import_payload, dim3((unsigned)n), dim3(256), 0, s, e->D, recs, e->q_count);
-  if (hipGetLastError() != hipSuccess ||
-      hipMemcpyAsync(&missing, e->q_count, sizeof(int32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
-    return done(TSDF_ERR_HIP);
-  if (missing) {
-    set_error("tsdf_import_blocks: a block went missing during import");
-    return done(TSDF_ERR_HIP);
   }
   return done(TSDF_OK);
 }

@@ -282,15 +282,8 @@ __global__ __launch_bounds__(256) void k_render_pack(EngineDev D, const VisRec* 
   for (int i = threadIdx.x; i < kBlockBytes / 16; i += 256)
     reinterpret_cast<uint4*>(dst + 16)[i] = src[i];
 }
-// import: records whose key is still missing after a resolver launch (bucket-lock losers retry)
-__global__ void k_import_missing(EngineDev D, const uint8_t* __restrict__ recs, int n,
-                                 int32_t* missing) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const short4 h = *reinterpret_cast<const short4*>(recs + (size_t)i * kBlockRecBytes);
-  if (find_entry(D.table, h.x, h.y, h.z) < 0) atomicAdd(missing, 1);
-}
-// import: one workgroup per record writes its payload over the freshly initialised block
+// import: one workgroup per record writes its payload over its block; records whose key is still
+// missing after a resolver launch (bucket-lock losers, retried) are counted
 __global__ __launch_bounds__(256) void k_import_payload(EngineDev D, const uint8_t* __restrict__ recs,
                                                         int32_t* missing) {
   const uint8_t* src = recs + (size_t)blockIdx.x * kBlockRecBytes;

@@ -130,7 +130,6 @@ struct RenderCull {
 __global__ void k_render_count(EngineDev D, FrameParams P, RenderCull C);
 __global__ void k_render_pack(EngineDev D, const VisRec* sel, uint8_t* out);
 __global__ void k_import_keys(EngineDev D, const uint8_t* recs, int n);
-__global__ void k_import_missing(EngineDev D, const uint8_t* recs, int n, int32_t* missing);
 __global__ void k_import_payload(EngineDev D, const uint8_t* recs, int32_t* missing);
 __global__ void k_hash_retrieve(EngineDev D, const int16_t* pts, int n, uint32_t* rgbw,
                                 float* tsdf, float* prob, short4* bpo, int32_t* bidx);
