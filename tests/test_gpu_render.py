@@ -146,6 +146,43 @@ def test_sharded_render_bench_scale():
         _close(full, replica, *shards)
 
 
+def test_replica_random_views():
+    """Selection superset property under arbitrary cameras: random positions in the room, random
+    orientations (including views of unmapped space and of the room from outside it), random focal
+    lengths and image sizes -- the replica always renders what the volume renders."""
+    import tsdf_amd
+    from tsdf_amd import synth
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    full, _, replica = _engines(0)
+    rng = np.random.default_rng(0x5EED)
+    try:
+        _integrate([full], cam, 8)
+        hits = 0
+        for _ in range(24):
+            q = rng.normal(size=4).astype(np.float32)
+            q /= np.linalg.norm(q)
+            x, y, z, qw = (float(v) for v in q)
+            R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * qw), 2 * (x * z + y * qw)],
+                          [2 * (x * y + z * qw), 1 - 2 * (x * x + z * z), 2 * (y * z - x * qw)],
+                          [2 * (x * z - y * qw), 2 * (y * z + x * qw), 1 - 2 * (x * x + y * y)]])
+            centre = rng.uniform([-1.0, -1.0, -0.5], [7.0, 6.0, 3.5])  # camera centre in the world
+            t = (-R @ centre).astype(np.float32)  # cam_T_world translation
+            w, h = int(rng.integers(16, W + 1)), int(rng.integers(12, H + 1))
+            f = float(rng.uniform(20.0, 400.0))
+            K = np.array([f, f * float(rng.uniform(0.8, 1.2)), w / 2 - 0.5, h / 2 - 0.5], np.float32)
+            pose = tsdf_amd.SE3(q, t)
+            recs = full.render_blocks(K, w, h, pose, 4.0)
+            replica.import_blocks(recs, replace=True)
+            exp = full.raycast(K, w, h, pose, 4.0)
+            got = replica.raycast(K, w, h, pose, 4.0)
+            hits += int((exp[0][..., 3] == 255).sum())
+            np.testing.assert_array_equal(got[0], exp[0])
+            np.testing.assert_array_equal(got[1], exp[1])
+        assert hits > 0
+    finally:
+        _close(full, replica)
+
+
 def _tri_set(t):
     t = np.ascontiguousarray(t, dtype=np.float32).reshape(-1, 9)
     return t[np.lexsort(t.view(np.uint32).T[::-1])].view(np.uint32)
