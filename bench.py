@@ -64,8 +64,10 @@ def parse():
     p.add_argument("--streams-per-gpu", type=int, default=1,
                    help="camera streams per GPU, each its own engine (volume) and HIP stream; their "
                         "frame chains overlap on the device (multi-camera rig; value counts all streams)")
-    p.add_argument("--route-cap", type=int, default=8192,
-                   help="routed mode: keys per destination rank per frame (outbox slot size)")
+    p.add_argument("--key-cap", type=int, default=16384,
+                   help="sharded modes: key records per rank per frame (exchange slot size)")
+    p.add_argument("--cand-cap", type=int, default=8192,
+                   help="sharded modes: carve-candidate records per rank per frame")
     p.add_argument("--cpu-frames", type=int, default=-1, help="oracle sample size (-1 = auto)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--block-bits", type=int, default=18)
@@ -141,10 +143,8 @@ def main():
                               stream=s_k.cuda_stream)
         extra.append((e_k, fr_k, [tsdf_amd.SE3(fr_k["q"][i], fr_k["t"][i]) for i in range(nframes)], s_k))
     torch.cuda.synchronize()
-    if routed:  # one outbox / inbox slot per rank; exchanged by an RCCL all-to-all each frame
-        nbytes = tsdf_amd.Engine.route_buffer_bytes(world, a.route_cap)
-        outbox = torch.zeros((world, nbytes // world), dtype=torch.uint8, device=dev)
-        inbox = torch.zeros_like(outbox)
+    if shard_count > 1:  # exchange slots of the sharded frame (RCCL all-gathers on this stream)
+        bufs = tdist.ShardBuffers(eng, shard_count, a.key_cap, a.cand_cap, device=dev)
 
     use_graph = a.loop == "c5" or a.graph
     if use_graph and routed:
@@ -184,11 +184,9 @@ def main():
                                                             out=mesh_buf).shape[0]))
                 else:
                     mesh_tris.append(int(eng.extract_mesh(None, 0.99, 0, out=mesh_buf).shape[0]))
-        elif routed:
-            eng.integrate_route_begin(frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i],
-                                      a.max_depth, rank, world, outbox, a.route_cap)
-            tdist.route_exchange(outbox, inbox)
-            eng.integrate_route_end(inbox, a.route_cap)
+        elif shard_count > 1:
+            tdist.integrate_sharded(eng, bufs, frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i],
+                                    a.max_depth, split=a.mode == "routed")
         else:
             eng.integrate(frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i], a.max_depth)
         for e_k, fr_k, po_k, _ in extra:

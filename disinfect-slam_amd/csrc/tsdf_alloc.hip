@@ -36,10 +36,6 @@ __device__ void keyset_insert(unsigned long long* keys, uint32_t* orders, int32_
 __device__ void nk_insert(const EngineDev& D, uint64_t key, uint32_t order) {
   keyset_insert(D.nk_key, D.nk_order, D.nk_list, &D.ctr->nk_count, &D.ctr->status, key, order);
 }
-// routed frames: a visible key another shard owns, kept once with its smallest candidate order
-__device__ void rt_insert(const EngineDev& D, uint64_t key, uint32_t order) {
-  keyset_insert(D.rt_key, D.rt_order, D.rt_list, &D.ctr->rt_count, &D.ctr->status, key, order);
-}
 
 // ---------------------------------------------------------------------------------------------
 // k_ingest_dda: 16x16 pixel tile per workgroup.
@@ -49,11 +45,11 @@ __device__ void rt_insert(const EngineDev& D, uint64_t key, uint32_t order) {
 //     (exactly the values tsdf_integrate_kernel recomputes per voxel, voxel_tsdf.cu:174-201)
 //  2. DDA of [p - trunc dir, p + trunc dir] (voxel_tsdf.cu:116-146); block keys deduplicated in
 //     an LDS hash set with their smallest candidate order (y*W + x)*maxs + i
-//  3. each unique key once: all-8-corners visibility (is_block_visible<true>), shard ownership,
-//     table probe; missing keys go to the global new-key set.
-// Steps 2-3 run only for tiles in [P.tile_lo, P.tile_hi) (a routed frame's pixel slice; every
-// tile otherwise). In a routed frame visible keys owned by another shard go to the route set
-// (k_route_pack sends them to their owner) instead of being dropped.
+//  3. each unique key once: all-8-corners visibility (is_block_visible<true>), table probe;
+//     missing keys go to the global new-key set.
+// Steps 2-3 run only for tiles in [P.tile_lo, P.tile_hi) (a sharded frame's pixel slice; every
+// tile otherwise). A shard probes its copy of the whole hash index, so its keys are exactly the
+// ones one volume's DDA finds in those tiles, whichever shard owns them.
 // ---------------------------------------------------------------------------------------------
 // LDS key-set slots per 16x16 tile: TS > 256 pixels x maxs. 1024 for maxs <= 3 (the reference's
 // 6x truncation / voxel ratio: 2-3 samples per pixel) keeps the workgroup at 16.5 KiB of LDS, so 9
@@ -320,11 +316,6 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
     const unsigned long long key = s_key[slot];
     int16_t kx, ky, kz;
     unpack_key(key, kx, ky, kz);
-    if (P.shard_count > 1 &&
-        brick_owner(kx, ky, kz, (uint32_t)P.shard_count) != (uint32_t)P.shard_index) {
-      if (P.route) rt_insert(D, key, s_ord[slot]);
-      continue;
-    }
     if (find_entry(D.table, kx, ky, kz) >= 0) continue;
     nk_insert(D, key, s_ord[slot]);
   }
@@ -352,68 +343,47 @@ template __global__ void k_ingest_dda_g<1024>(EngineDev, const FrameArgs*);
 template __global__ void k_ingest_dda_g<2048>(EngineDev, const FrameArgs*);
 
 // ---------------------------------------------------------------------------------------------
-// Routed frames (SURVEY.md 8e option 2). k_route_pack drains the route set into the outbox, one
-// slot of `cap` records per destination shard (record order within a slot is irrelevant: the
-// owner keeps the smallest candidate order per key); k_route_ingest merges an inbox -- slot s
-// holding what shard s sent here -- into this shard's new-key set after the same table probe
-// the local keys get. Keys, visibility and candidate orders are those of the unsharded DDA, so
-// a routed frame allocates exactly what the replicated-frame (option 1) shard would.
+// Sharded frames: the key exchange. k_key_pack drains this shard's new-key set
+// (its DDA slice's keys) into its outbox slot; after the all-gather, k_key_merge inserts every
+// shard's slot into the set with the smallest candidate order per key -- the set one volume's DDA
+// over the whole frame builds -- so every shard's allocation resolver makes the same decisions.
+// The senders probed the same index, so no probe is repeated here.
 // ---------------------------------------------------------------------------------------------
-constexpr int kMaxShards = 64;
-__global__ __launch_bounds__(1024) void k_route_pack(EngineDev D, RouteRec* __restrict__ out, int cap,
-                                                     int nshard) {
-  __shared__ int s_cnt[kMaxShards];
-  const int t = threadIdx.x;
-  if (t < nshard) s_cnt[t] = 0;
-  __syncthreads();
-  const int n = D.ctr->rt_count;
-  for (int i = t; i < n; i += blockDim.x) {
-    const int h = D.rt_list[i];
-    const unsigned long long key = D.rt_key[h];
-    const uint32_t ord = D.rt_order[h];
-    D.rt_key[h] = 0ull;  // the set starts empty next frame
-    D.rt_order[h] = 0xFFFFFFFFu;
-    int16_t x, y, z;
-    unpack_key(key, x, y, z);
-    const int o = (int)brick_owner(x, y, z, (uint32_t)nshard);
-    const int s = atomicAdd(&s_cnt[o], 1);
-    if (s < cap) {
-      RouteRec r;
-      r.x = x;
-      r.y = y;
-      r.z = z;
+__global__ __launch_bounds__(1024) void k_key_pack(EngineDev D, ShardRec* __restrict__ out, int cap) {
+  const int n = D.ctr->nk_count;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int h = D.nk_list[i];
+    const unsigned long long key = D.nk_key[h];
+    const uint32_t ord = D.nk_order[h];
+    D.nk_key[h] = 0ull;  // the set is rebuilt from the exchanged slots
+    D.nk_order[h] = 0xFFFFFFFFu;
+    if (i < cap) {
+      ShardRec r;
+      unpack_key(key, r.x, r.y, r.z);
       r.pad = 0;
-      r.order = ord;
+      r.val = ord;
       r.zero = 0u;
-      out[(size_t)o * (cap + 1) + 1 + s] = r;
+      out[1 + i] = r;
     }
   }
-  __syncthreads();
-  if (t < nshard) {
-    const int c = s_cnt[t];
-    RouteRec h{};
-    h.order = (uint32_t)min(c, cap);
-    out[(size_t)t * (cap + 1)] = h;
-    if (c > cap) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_ROUTE_OVERFLOW
+  __syncthreads();  // every wave has read nk_count before it is reset
+  if (threadIdx.x == 0) {
+    ShardRec h{};
+    h.val = (uint32_t)min(n, cap);
+    out[0] = h;
+    if (n > cap) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_SHARD_OVERFLOW
+    D.ctr->nk_count = 0;
   }
-  if (t == 0) D.ctr->rt_count = 0;
 }
 
-// grid (ceil(cap / 256), nshard): workgroup row s reads the slot shard s sent
-__global__ __launch_bounds__(256) void k_route_ingest(EngineDev D, FrameParams P,
-                                                      const RouteRec* __restrict__ in, int cap) {
-  const int src = blockIdx.y;
-  const RouteRec* slot = in + (size_t)src * (cap + 1);
-  const int n = min((int)slot[0].order, cap);
+// grid (ceil(cap / 256), nshard): workgroup row s merges the slot shard s wrote
+__global__ __launch_bounds__(256) void k_key_merge(EngineDev D, const ShardRec* __restrict__ in, int cap) {
+  const ShardRec* slot = in + (size_t)blockIdx.y * (cap + 1);
+  const int n = min((int)slot[0].val, cap);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const RouteRec r = slot[1 + i];
-  if (brick_owner(r.x, r.y, r.z, (uint32_t)P.shard_count) != (uint32_t)P.shard_index) {
-    atomicOr(&D.ctr->status, 32u);  // TSDF_STATUS_ROUTE_MISROUTED: inbox not from this layout
-    return;
-  }
-  if (find_entry(D.table, r.x, r.y, r.z) >= 0) return;
-  nk_insert(D, pack_key(r.x, r.y, r.z), r.order);
+  const ShardRec r = slot[1 + i];
+  nk_insert(D, pack_key(r.x, r.y, r.z), r.val);
 }
 
 // test path: keys[n] in list order (one VoxelHashTable::Allocate launch, voxel_hash_test.cu)
@@ -592,16 +562,29 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
           }
         }
       }
+      // Sharded volume: every shard commits every key's table change (the replicated index), and
+      // only the key's owner pops a pool block; the others store kForeignIdx.
+      const bool mine = ok && (P.shard_count <= 1 ||
+                               brick_owner(kx, ky, kz, (uint32_t)P.shard_count) == (uint32_t)P.shard_index);
       int nok;
-      const int rank = block_excl_scan(ok ? 1 : 0, L.scan, &nok);
+      const int rank = block_excl_scan(mine ? 1 : 0, L.scan, &nok);
       const int free_now = L.sfree;
       if (ok) {
-        const int hi = free_now - 1 - rank;
-        if (hi < 0) {
-          atomicOr(&D.ctr->status, 1u);  // TSDF_STATUS_POOL_EXHAUSTED: insert dropped
-        } else {
-          const int top = free0 - 1 - hi;  // pops so far this launch + rank
-          const int32_t idx = single ? L.heap_top[top] : D.heap[hi];
+        int32_t idx = kForeignIdx;
+        bool insert = true;
+        if (mine) {
+          const int hi = free_now - 1 - rank;
+          if (hi < 0) {
+            atomicOr(&D.ctr->status, 1u);  // TSDF_STATUS_POOL_EXHAUSTED
+            // one volume drops the insert; a shard keeps a voxel-less entry so that every
+            // shard's index stays the same
+            insert = P.shard_count > 1;
+          } else {
+            const int top = free0 - 1 - hi;  // pops so far this launch + rank
+            idx = single ? L.heap_top[top] : D.heap[hi];
+          }
+        }
+        if (insert) {
           uint32_t e;
           if (kind == 1) {
             e = 2 * B + (uint32_t)slot;
@@ -611,21 +594,23 @@ __device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32
             e = E;
           }
           store_ent(D.table, e, kx, ky, kz, 0, idx);
-          atomicOr(&D.occ[e >> 6], 1ull << (e & 63));
-          if (frame_mode) {
-            // a new block has all 8 corners in view, so it is visible this frame: listed for the
-            // fresh-block integrate launch (the sweep in k_ingest_dda listed only the blocks that
-            // existed before), flagged fresh so it starts from AquireBlock's state
-            VisRec vr;
-            vr.x = kx;
-            vr.y = ky;
-            vr.z = kz;
-            vr.pad = 1;
-            vr.idx = idx;
-            vr.entry = (int32_t)e;
-            D.fresh_vis[L.nfresh + rank] = vr;
-          } else {
-            D.fresh[L.nfresh + rank] = idx;
+          if (local_idx(idx)) {  // the occupancy bitmap lists the blocks this engine holds
+            atomicOr(&D.occ[e >> 6], 1ull << (e & 63));
+            if (frame_mode) {
+              // a new block has all 8 corners in view, so it is visible this frame: listed for
+              // the fresh-block integrate launch (the sweep in k_ingest_dda listed only the
+              // blocks that existed before), flagged fresh so it starts from AquireBlock's state
+              VisRec vr;
+              vr.x = kx;
+              vr.y = ky;
+              vr.z = kz;
+              vr.pad = 1;
+              vr.idx = idx;
+              vr.entry = (int32_t)e;
+              D.fresh_vis[L.nfresh + rank] = vr;
+            } else {
+              D.fresh[L.nfresh + rank] = idx;
+            }
           }
         }
       }
@@ -679,13 +664,8 @@ __global__ __launch_bounds__(256) void k_fresh_init(EngineDev D) {
     uint8_t* blk = D.pool + (size_t)D.fresh[b] * kBlockBytes;
     *reinterpret_cast<float4*>(blk + v * 4) = make_float4(-1.f, -1.f, -1.f, -1.f);
     *reinterpret_cast<float4*>(blk + kProbOffset + v * 4) = make_float4(0.f, 0.f, 0.f, 0.f);  // p = 0.5
-    uint4* cw = reinterpret_cast<uint4*>(blk + kRgbwOffset + v * 4);
-    uint4 c = *cw;
-    c.x &= 0x00FFFFFFu;
-    c.y &= 0x00FFFFFFu;
-    c.z &= 0x00FFFFFFu;
-    c.w &= 0x00FFFFFFu;
-    *cw = c;
+    // weight 0; the colour of a weight-0 voxel is defined as 0 (see k_integrate / the oracle)
+    *reinterpret_cast<uint4*>(blk + kRgbwOffset + v * 4) = make_uint4(0u, 0u, 0u, 0u);
   }
 }
 

@@ -68,15 +68,22 @@ struct FrameParams {
   int W, H;
   int maxs;                  // DDA samples reserved per pixel in the candidate order space
   int shard_index, shard_count;
-  int tile_lo, tile_hi;      // pixel tiles whose DDA this engine runs (all of them unless routed)
-  int route;                 // 1: keys owned by other shards go to the route set (SURVEY 8e opt. 2)
+  int tile_lo, tile_hi;      // pixel tiles whose DDA this engine runs (a shard's slice, else all)
 };
 
-// one routed candidate key (16 B); record 0 of each destination slot is a header whose `order`
-// holds the record count. Route buffer = shard_count slots x (cap + 1) records.
-struct alignas(16) RouteRec {
+// Sharded volume: every shard keeps the whole hash index, so bucket locks and table
+// layout evolve exactly as in one volume; a block's voxels live only on its owner. The other
+// shards' entry of it carries kForeignIdx: occupied for Allocate / Delete (idx >= 0), missing for
+// every reader (local_idx false).
+constexpr int32_t kForeignIdx = 0x7FFFFFFF;
+__device__ __host__ __forceinline__ bool local_idx(int32_t idx) { return idx >= 0 && idx != kForeignIdx; }
+
+// one exchanged record of a sharded frame (16 B): a new block key with its candidate order, or a
+// carve candidate with its hash entry. A slot is (cap + 1) records, record 0 a header whose `val`
+// holds the count; an inbox is shard_count slots, slot s written by shard s.
+struct alignas(16) ShardRec {
   int16_t x, y, z, pad;
-  uint32_t order;
+  uint32_t val;   // candidate order (keys) / hash entry (carve candidates) / count (header)
   uint32_t zero;
 };
 
@@ -105,8 +112,8 @@ struct DevCounters {
   unsigned long long total_deleted;
   unsigned long long frames;
   unsigned long long integrate_ticks;  // sum of k_integrate device durations (100 MHz clock)
-  int32_t rt_count;       // unique keys in the route set (routed frames)
-  int32_t rt_pad;
+  int32_t n_keys_in;      // sharded frames: key records merged from the exchange (last frame)
+  int32_t pad0;
 };
 
 // ------------------------------------------------------------------------------------------
@@ -409,6 +416,13 @@ __device__ __forceinline__ int32_t find_entry(const int4* __restrict__ table, in
     if (b.x == x && b.y == y && b.z == z && b.idx >= 0) return (int32_t)last;
   }
   return -1;
+}
+
+// the entry of a block this engine holds voxels for, or -1 (missing, or another shard's block)
+__device__ __forceinline__ int32_t find_local(const int4* __restrict__ table, int16_t x, int16_t y,
+                                              int16_t z) {
+  const int32_t e = find_entry(table, x, y, z);
+  return (e >= 0 && local_idx(table[e].z)) ? e : -1;
 }
 
 // camera.cuh:47-51 and voxel_tsdf.cu:48-57 is_voxel_visible

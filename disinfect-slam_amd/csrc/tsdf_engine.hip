@@ -128,10 +128,12 @@ struct tsdf_engine {
   std::vector<std::array<hipEvent_t, 5>> events;
   size_t ev_used = 0;
   unsigned long long prof_vis0 = 0, prof_upd0 = 0, prof_ticks0 = 0;
-  // routed frame between tsdf_integrate_route_begin and _end
-  bool route_pending = false;
-  FrameParams route_P{};
-  std::array<hipEvent_t, 5>* route_ev = nullptr;
+  // sharded frame (tsdf_integrate_shard_*): 0 idle, 1 after _begin, 2 after _update
+  hipEvent_t order_ev = nullptr;  // tsdf_stream_wait / _signal
+  int shard_phase = 0;
+  bool shard_keys_packed = false;  // _begin wrote a key slot (split DDA): _update merges an inbox
+  FrameParams shard_P{};
+  std::array<hipEvent_t, 5>* shard_ev = nullptr;
   // feed_rgbd_frame staging: raw full-size inputs (host frames) and the half-size outputs
   uint8_t* fe_rgb = nullptr;
   uint16_t* fe_depth = nullptr;
@@ -148,7 +150,6 @@ void free_all(tsdf_engine* e) {
   EngineDev& D = e->D;
   void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.occ,
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs, D.pkey,      D.fresh,
-                  D.rt_key,  D.rt_order, D.rt_list,
                   e->fe_rgb, e->fe_depth, e->fe_mask, e->fe_out_rgb, e->fe_out_depth,
                   D.vis,     D.band,    D.cand,     D.wg_upd, D.wg_end, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
@@ -159,6 +160,7 @@ void free_all(tsdf_engine* e) {
   if (e->h_ctr) (void)hipHostFree(e->h_ctr);
   for (auto& ev : e->events)
     for (hipEvent_t x : ev) (void)hipEventDestroy(x);
+  if (e->order_ev) (void)hipEventDestroy(e->order_ev);
   if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
 }
 
@@ -196,15 +198,27 @@ FrameParams make_params(const tsdf_engine* e, const tsdf_intrinsics* K, int W, i
   P.shard_count = e->cfg.shard_count;
   P.tile_lo = 0;
   P.tile_hi = 1 << 30;
-  P.route = 0;
   return P;
 }
 
 int ensure_test_cap(tsdf_engine* e, int n) {
   if (n <= e->t_cap) return TSDF_OK;
-  void* ptrs[] = {e->t_keys, e->t_recs, e->t_i32, e->t_u32, e->t_f0, e->t_f1, e->t_s4};
-  for (void* p : ptrs)
-    if (p) (void)hipFree(p);
+  (void)hipFree(e->t_keys);
+  (void)hipFree(e->t_recs);
+  (void)hipFree(e->t_i32);
+  (void)hipFree(e->t_u32);
+  (void)hipFree(e->t_f0);
+  (void)hipFree(e->t_f1);
+  (void)hipFree(e->t_s4);
+  // nothing dangles if an allocation below fails: tsdf_destroy frees what was allocated
+  e->t_keys = nullptr;
+  e->t_recs = nullptr;
+  e->t_i32 = nullptr;
+  e->t_u32 = nullptr;
+  e->t_f0 = nullptr;
+  e->t_f1 = nullptr;
+  e->t_s4 = nullptr;
+  e->t_cap = 0;
   const int cap = std::max(n, 1024);
   HIP_OK(dmalloc(&e->t_keys, (size_t)cap * 3));
   HIP_OK(dmalloc(&e->t_recs, (size_t)cap));
@@ -267,6 +281,7 @@ void tsdf_config_default(tsdf_config* c) {
   c->shard_index = 0;
   c->shard_count = 1;
   c->stream = nullptr;
+  c->use_stream = 0;
 }
 
 const char* tsdf_error_string(int code) {
@@ -303,10 +318,6 @@ bool init_state(tsdf_engine* e, bool with_pool = true) {
   ok &= hipMemsetAsync(D.occ, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
   ok &= hipMemsetAsync(D.nk_key, 0, sizeof(unsigned long long) * kNewKeyCap, s) == hipSuccess;
   ok &= hipMemsetAsync(D.nk_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
-  if (D.rt_key) {
-    ok &= hipMemsetAsync(D.rt_key, 0, sizeof(unsigned long long) * kNewKeyCap, s) == hipSuccess;
-    ok &= hipMemsetAsync(D.rt_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
-  }
   ok &= hipMemsetAsync(D.band, 0, sizeof(int32_t) * kBands * kBandStride, s) == hipSuccess;
   ok &= hipMemsetAsync(D.visbits, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
   DevCounters c0{};
@@ -334,7 +345,8 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
     tsdf_config_default(&cfg);
   if (!(cfg.voxel_size > 0) || !(cfg.truncation > 0) || cfg.max_width <= 0 ||
       cfg.max_height <= 0 || cfg.num_block_bits < 1 || cfg.num_block_bits > 22 ||
-      cfg.shard_count < 1 || cfg.shard_index < 0 || cfg.shard_index >= cfg.shard_count) {
+      cfg.shard_count < 1 || cfg.shard_count > kMaxShards || cfg.shard_index < 0 ||
+      cfg.shard_index >= cfg.shard_count) {
     set_error("tsdf_create: invalid config");
     return TSDF_ERR_INVALID_ARG;
   }
@@ -383,11 +395,6 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.nk_order, kNewKeyCap);
   ALLOC(D.nk_list, kNewKeyCap);
   ALLOC(D.pairs, kNewKeyCap);
-  if (cfg.shard_count > 1) {  // route set of routed frames
-    ALLOC(D.rt_key, kNewKeyCap);
-    ALLOC(D.rt_order, kNewKeyCap);
-    ALLOC(D.rt_list, kNewKeyCap);
-  }
   ALLOC(D.pkey, kNewKeyCap);
   ALLOC(D.fresh, kNewKeyCap);
   ALLOC(D.vis, (size_t)kBands * nb);
@@ -426,7 +433,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
 #undef ALLOC
   if (hipHostMalloc(reinterpret_cast<void**>(&e->h_ctr), sizeof(DevCounters)) != hipSuccess)
     return fail(TSDF_ERR_OUT_OF_MEMORY);
-  if (cfg.stream) {
+  if (cfg.use_stream) {  // the caller's stream; NULL is the legacy default stream (torch's default)
     e->stream = reinterpret_cast<hipStream_t>(cfg.stream);
   } else {
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
@@ -459,10 +466,10 @@ int tsdf_synchronize(tsdf_engine* e) {
 namespace {
 
 // Phase 1 of a frame: stage host inputs, then k_ingest_dda (pixel records for the whole frame, the
-// DDA over tiles [tile_lo, tile_hi), visibility of the existing blocks). *P / *ev carry the frame
-// to frame_finish.
+// DDA over tiles of slice `slice_index` of `slice_count` -- contiguous bands of tile rows --, the
+// visibility of the existing blocks). *P / *ev carry the frame to the later phases.
 int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, const tsdf_pose* pose,
-                 float max_depth, int slice_index, int slice_count, int route, FrameParams* P,
+                 float max_depth, int slice_index, int slice_count, FrameParams* P,
                  std::array<hipEvent_t, 5>** ev_out) {
   if (!e || !f || !K || !pose || !f->depth || !f->rgb || f->width <= 0 || f->height <= 0 ||
       (int64_t)f->width * f->height > e->max_pixels || f->width > e->cfg.max_width ||
@@ -501,7 +508,6 @@ int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, 
     P->tile_lo = std::min(tiles_y, slice_index * rows) * tiles_x;
     P->tile_hi = std::min(tiles_y, (slice_index + 1) * rows) * tiles_x;
   }
-  P->route = route;
   std::array<hipEvent_t, 5>* ev = nullptr;
   if (e->profiling && (e->prof_calls++ % e->prof_every) == 0) {
     if (e->ev_used == e->events.size()) {
@@ -526,12 +532,12 @@ int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, 
   return TSDF_OK;
 }
 
-// Phase 2: ordered allocation of the new keys -> fused update -> space carving.
+// Phase 2: ordered allocation of the new keys -> fused update (+ carve minimum).
 // (Measured and not kept: running the update of the existing blocks beside k_resolve_alloc, on a
 // second stream or as a dispatch without the AQL barrier bit that waits on a release flag for the
 // new blocks. The resolver's chain of dependent HBM round trips slows ~2.5x under the update's
 // memory load, and the stream fork / join costs more than it hides: 15-16k frames/s against 18k.)
-int frame_finish(tsdf_engine* e, const FrameParams& P, std::array<hipEvent_t, 5>* ev) {
+int frame_update(tsdf_engine* e, const FrameParams& P, std::array<hipEvent_t, 5>* ev) {
   hipStream_t s = e->stream;
   const bool all_ev = ev && e->prof_mode == TSDF_PROFILE_PHASES;
   int rc = launch_resolve_alloc(e, P, (uint32_t)((size_t)P.W * P.H * e->maxs), 1);
@@ -550,68 +556,140 @@ int frame_finish(tsdf_engine* e, const FrameParams& P, std::array<hipEvent_t, 5>
     if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
   }
   LAUNCH_OK("k_integrate");
-  // ---- space carving (voxel_tsdf.cu:483-488) ----
+  return TSDF_OK;
+}
+
+// Phase 3: space carving (voxel_tsdf.cu:483-488) of the candidates in D.cand.
+int frame_carve(tsdf_engine* e, std::array<hipEvent_t, 5>* ev) {
+  hipStream_t s = e->stream;
   hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kResolveThreads), 0, s, e->D, e->D.cand,
                      &e->D.ctr->n_cand, 0);
   LAUNCH_OK("k_resolve_delete");
-  if (all_ev) HIP_OK(hipEventRecord((*ev)[4], s));
+  if (ev && e->prof_mode == TSDF_PROFILE_PHASES) HIP_OK(hipEventRecord((*ev)[4], s));
   return TSDF_OK;
 }
+
+bool sharded(const tsdf_engine* e) { return e->cfg.shard_count > 1; }
 
 }  // namespace
 
 int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
                    const tsdf_pose* pose, float max_depth) {
   TraceRange trace_("tsdf_integrate");
-  if (e && e->route_pending) {
-    set_error("tsdf_integrate: a routed frame is pending (tsdf_integrate_route_end)");
+  if (e && sharded(e)) {
+    set_error("tsdf_integrate: a shard of a sharded volume integrates through tsdf_integrate_shard_*");
     return TSDF_ERR_INVALID_ARG;
   }
   FrameParams P;
   std::array<hipEvent_t, 5>* ev = nullptr;
-  int rc = frame_ingest(e, f, K, pose, max_depth, 0, 1, 0, &P, &ev);
+  int rc = frame_ingest(e, f, K, pose, max_depth, 0, 1, &P, &ev);
   if (rc) return rc;
-  return frame_finish(e, P, ev);
+  rc = frame_update(e, P, ev);
+  if (rc) return rc;
+  return frame_carve(e, ev);
 }
 
-int64_t tsdf_route_buffer_bytes(int32_t shard_count, int32_t route_cap) {
-  if (shard_count < 1 || route_cap < 1) return 0;
-  return (int64_t)shard_count * (route_cap + 1) * (int64_t)sizeof(RouteRec);
+// ---------------------------------------------------------------------------------------------
+// Sharded frames. Every shard keeps the whole hash index and holds the voxels of its
+// own blocks; one frame is three calls around two all-gathers (include/disinfect_tsdf.h).
+// ---------------------------------------------------------------------------------------------
+int64_t tsdf_shard_slot_bytes(int32_t cap) {
+  if (cap < 1) return 0;
+  return (int64_t)(cap + 1) * (int64_t)sizeof(ShardRec);
 }
 
-int tsdf_integrate_route_begin(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
+int tsdf_integrate_shard_begin(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
                                const tsdf_pose* pose, float max_depth, int32_t slice_index,
-                               int32_t slice_count, void* outbox, int32_t route_cap) {
-  TraceRange trace_("tsdf_integrate_route_begin");
-  if (!e || e->cfg.shard_count < 2 || e->route_pending || !outbox || route_cap < 1) {
-    set_error("tsdf_integrate_route_begin: invalid argument");
+                               int32_t slice_count, void* keys_out, int32_t key_cap) {
+  TraceRange trace_("tsdf_integrate_shard_begin");
+  if (!e || !sharded(e) || e->shard_phase != 0 || (keys_out && key_cap < 1) ||
+      (!keys_out && slice_count != 1)) {
+    set_error("tsdf_integrate_shard_begin: invalid argument (a shard engine between frames; a key "
+              "slot unless slice_count == 1)");
     return TSDF_ERR_INVALID_ARG;
   }
   FrameParams P;
   std::array<hipEvent_t, 5>* ev = nullptr;
-  int rc = frame_ingest(e, f, K, pose, max_depth, slice_index, slice_count, 1, &P, &ev);
+  int rc = frame_ingest(e, f, K, pose, max_depth, slice_index, slice_count, &P, &ev);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_route_pack, dim3(1), dim3(1024), 0, e->stream, e->D,
-                     reinterpret_cast<RouteRec*>(outbox), route_cap, e->cfg.shard_count);
-  LAUNCH_OK("k_route_pack");
-  e->route_P = P;
-  e->route_ev = ev;
-  e->route_pending = true;
+  if (keys_out) {
+    hipLaunchKernelGGL(k_key_pack, dim3(1), dim3(1024), 0, e->stream, e->D,
+                       reinterpret_cast<ShardRec*>(keys_out), key_cap);
+    LAUNCH_OK("k_key_pack");
+  }
+  e->shard_P = P;
+  e->shard_ev = ev;
+  e->shard_keys_packed = keys_out != nullptr;
+  e->shard_phase = 1;
   return TSDF_OK;
 }
 
-int tsdf_integrate_route_end(tsdf_engine* e, const void* inbox, int32_t route_cap) {
-  TraceRange trace_("tsdf_integrate_route_end");
-  if (!e || !e->route_pending || !inbox || route_cap < 1) {
-    set_error("tsdf_integrate_route_end: invalid argument");
+int tsdf_integrate_shard_update(tsdf_engine* e, const void* keys_in, int32_t key_cap, void* cands_out,
+                                int32_t cand_cap) {
+  TraceRange trace_("tsdf_integrate_shard_update");
+  if (!e || e->shard_phase != 1 || (keys_in != nullptr) != e->shard_keys_packed ||
+      (keys_in && key_cap < 1) || !cands_out || cand_cap < 1) {
+    set_error("tsdf_integrate_shard_update: invalid argument (after tsdf_integrate_shard_begin; the "
+              "key inbox iff _begin packed keys; a candidate slot)");
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  e->route_pending = false;
-  hipLaunchKernelGGL(k_route_ingest, dim3((route_cap + 255) / 256, e->cfg.shard_count), dim3(256), 0,
-                     e->stream, e->D, e->route_P, reinterpret_cast<const RouteRec*>(inbox), route_cap);
-  LAUNCH_OK("k_route_ingest");
-  return frame_finish(e, e->route_P, e->route_ev);
+  hipStream_t s = e->stream;
+  if (keys_in) {
+    hipLaunchKernelGGL(k_key_merge, dim3((key_cap + 255) / 256, e->cfg.shard_count), dim3(256), 0, s, e->D,
+                       reinterpret_cast<const ShardRec*>(keys_in), key_cap);
+    LAUNCH_OK("k_key_merge");
+  }
+  int rc = frame_update(e, e->shard_P, e->shard_ev);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_cand_pack, dim3(1), dim3(1024), 0, s, e->D, reinterpret_cast<ShardRec*>(cands_out),
+                     cand_cap);
+  LAUNCH_OK("k_cand_pack");
+  e->shard_phase = 2;
+  return TSDF_OK;
+}
+
+int tsdf_integrate_shard_end(tsdf_engine* e, const void* cands_in, int32_t cand_cap) {
+  TraceRange trace_("tsdf_integrate_shard_end");
+  if (!e || e->shard_phase != 2 || !cands_in || cand_cap < 1) {
+    set_error("tsdf_integrate_shard_end: invalid argument (after tsdf_integrate_shard_update; the "
+              "candidate inbox)");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  hipLaunchKernelGGL(k_cand_gather, dim3(1), dim3(1024), 0, e->stream, e->D,
+                     reinterpret_cast<const ShardRec*>(cands_in), cand_cap, e->cfg.shard_count);
+  LAUNCH_OK("k_cand_gather");
+  e->shard_phase = 0;
+  return frame_carve(e, e->shard_ev);
+}
+
+int tsdf_stream_wait(tsdf_engine* e, void* stream) {
+  if (!e) return TSDF_ERR_INVALID_ARG;
+  hipStream_t other = reinterpret_cast<hipStream_t>(stream);
+  if (other == e->stream) return TSDF_OK;
+  HIP_OK(hipSetDevice(e->device));
+  if (!e->order_ev) HIP_OK(hipEventCreateWithFlags(&e->order_ev, hipEventDisableTiming));
+  HIP_OK(hipEventRecord(e->order_ev, other));
+  HIP_OK(hipStreamWaitEvent(e->stream, e->order_ev, 0));
+  return TSDF_OK;
+}
+
+int tsdf_stream_signal(tsdf_engine* e, void* stream) {
+  if (!e) return TSDF_ERR_INVALID_ARG;
+  hipStream_t other = reinterpret_cast<hipStream_t>(stream);
+  if (other == e->stream) return TSDF_OK;
+  HIP_OK(hipSetDevice(e->device));
+  if (!e->order_ev) HIP_OK(hipEventCreateWithFlags(&e->order_ev, hipEventDisableTiming));
+  HIP_OK(hipEventRecord(e->order_ev, e->stream));
+  HIP_OK(hipStreamWaitEvent(other, e->order_ev, 0));
+  return TSDF_OK;
+}
+
+int tsdf_get_stream(tsdf_engine* e, void** stream) {
+  if (!e || !stream) return TSDF_ERR_INVALID_ARG;
+  *stream = reinterpret_cast<void*>(e->stream);
+  return TSDF_OK;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -653,6 +731,11 @@ void graph_free(tsdf_graph* g) {
 
 int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, int render_height,
                       tsdf_graph** out) {
+  if (e && e->cfg.shard_count > 1) {
+    set_error("tsdf_graph_create: graph frames are for a whole volume (a shard integrates through "
+              "tsdf_integrate_shard_*)");
+    return TSDF_ERR_INVALID_ARG;
+  }
   if (!e || !out || width <= 0 || height <= 0 || width > e->cfg.max_width || height > e->cfg.max_height ||
       render_width < 0 || render_height < 0 || (int64_t)render_width * render_height > e->max_pixels ||
       (render_width == 0) != (render_height == 0)) {
@@ -721,8 +804,8 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
     return TSDF_ERR_INVALID_ARG;
   }
   tsdf_engine* e = g->e;
-  if (e->route_pending) {
-    set_error("tsdf_graph_frame: a routed frame is pending");
+  if (e->shard_phase != 0) {
+    set_error("tsdf_graph_frame: a sharded frame is pending");
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
@@ -956,8 +1039,8 @@ static_assert(kBlockRecBytes == TSDF_BLOCK_RECORD_BYTES, "render record layout")
 int tsdf_reset(tsdf_engine* e) {
   TraceRange trace_("tsdf_reset");
   if (!e) return TSDF_ERR_INVALID_ARG;
-  if (e->route_pending) {
-    set_error("tsdf_reset: a routed frame is pending");
+  if (e->shard_phase != 0) {
+    set_error("tsdf_reset: a sharded frame is pending");
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
@@ -1051,8 +1134,8 @@ int tsdf_import_blocks(tsdf_engine* e, const void* records, int64_t n, int mem_k
     set_error("tsdf_import_blocks: invalid argument");
     return TSDF_ERR_INVALID_ARG;
   }
-  if (e->route_pending) {
-    set_error("tsdf_import_blocks: a routed frame is pending");
+  if (e->shard_phase != 0) {
+    set_error("tsdf_import_blocks: a sharded frame is pending");
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
@@ -1278,8 +1361,61 @@ struct SnapshotHeader {
   int32_t nblocks;
   float voxel, truncation;
   int64_t bytes;
+  int32_t shard_index, shard_count;
 };
-constexpr uint32_t kSnapshotVersion = 1;
+constexpr uint32_t kSnapshotVersion = 2;
+
+// A snapshot is accepted only if the state it describes is one the engine could have reached: the
+// free stack and the table's pool indices partition the pool, foreign entries only on a shard,
+// the occupancy bits are exactly the entries with voxels here, and every bucket's list ends. A
+// corrupt or hand-edited one would otherwise send the next frame's kernels out of bounds.
+bool snapshot_consistent(const tsdf_engine* e, const uint8_t* p) {
+  const int nb = e->D.nblocks;
+  DevCounters c;
+  std::memcpy(&c, p, sizeof(c));
+  p += sizeof(DevCounters);
+  const int4* table = reinterpret_cast<const int4*>(p);
+  p += (size_t)kNumEntry * 16;
+  const uint64_t* occ = reinterpret_cast<const uint64_t*>(p);
+  p += (size_t)kOccWords * 8;
+  const int32_t* heap = reinterpret_cast<const int32_t*>(p);
+  if (c.free_count < 0 || c.free_count > nb) return false;
+  std::vector<uint8_t> seen((size_t)nb, 0);
+  for (int i = 0; i < c.free_count; ++i) {
+    const int32_t b = heap[i];
+    if (b < 0 || b >= nb || seen[b]) return false;
+    seen[b] = 1;
+  }
+  int64_t occupied = 0, held = 0;
+  for (uint32_t en = 0; en < kNumEntry; ++en) {
+    const int32_t idx = table[en].z;
+    const bool bit = (occ[en >> 6] >> (en & 63)) & 1ull;
+    if (idx == -1) {
+      if (bit) return false;
+      continue;
+    }
+    ++occupied;
+    if (idx == kForeignIdx) {
+      if (e->cfg.shard_count <= 1 || bit) return false;
+      continue;
+    }
+    if (idx < 0 || idx >= nb || seen[idx] || !bit) return false;
+    seen[idx] = 1;
+    ++held;
+  }
+  if (held + c.free_count != nb) return false;
+  // bucket lists (slot 1's offset chain) end within the occupied entries
+  for (uint32_t b = 0; b < kNumBucket; ++b) {
+    uint32_t last = 2 * b + 1;
+    int16_t off = (int16_t)((uint32_t)table[last].y >> 16);
+    for (int64_t steps = 0; off; ++steps) {
+      if (steps > occupied) return false;
+      last = (uint32_t)(last + (int32_t)off) & kEntryMask;
+      off = (int16_t)((uint32_t)table[last].y >> 16);
+    }
+  }
+  return true;
+}
 
 int64_t snapshot_bytes(const tsdf_engine* e) {
   return (int64_t)sizeof(SnapshotHeader) + (int64_t)sizeof(DevCounters) + (int64_t)kNumEntry * 16 +
@@ -1296,8 +1432,8 @@ int tsdf_snapshot_bytes(tsdf_engine* e, int64_t* bytes) {
 int tsdf_snapshot_save(tsdf_engine* e, void* out, int64_t capacity) {
   TraceRange trace_("tsdf_snapshot_save");
   if (!e || !out) return TSDF_ERR_INVALID_ARG;
-  if (e->route_pending) {
-    set_error("tsdf_snapshot_save: a routed frame is pending");
+  if (e->shard_phase != 0) {
+    set_error("tsdf_snapshot_save: a sharded frame is pending");
     return TSDF_ERR_INVALID_ARG;
   }
   const int64_t need = snapshot_bytes(e);
@@ -1315,6 +1451,8 @@ int tsdf_snapshot_save(tsdf_engine* e, void* out, int64_t capacity) {
   h.voxel = e->cfg.voxel_size;
   h.truncation = e->cfg.truncation;
   h.bytes = need;
+  h.shard_index = e->cfg.shard_index;
+  h.shard_count = e->cfg.shard_count;
   std::memcpy(p, &h, sizeof(h));
   p += sizeof(h);
   HIP_OK(hipMemcpyAsync(p, e->D.ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
@@ -1337,8 +1475,14 @@ int tsdf_snapshot_load(tsdf_engine* e, const void* in, int64_t size) {
   std::memcpy(&h, in, sizeof(h));
   if (std::memcmp(h.magic, "TSDFSNAP", 8) != 0 || h.version != kSnapshotVersion || h.nblocks != e->D.nblocks ||
       h.voxel != e->cfg.voxel_size || h.truncation != e->cfg.truncation || h.bytes != snapshot_bytes(e) ||
-      size < h.bytes || e->route_pending) {
+      size < h.bytes || h.shard_index != e->cfg.shard_index || h.shard_count != e->cfg.shard_count ||
+      e->shard_phase != 0) {
     set_error("tsdf_snapshot_load: not a snapshot of an engine with this configuration");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  if (!snapshot_consistent(e, static_cast<const uint8_t*>(in) + sizeof(h))) {
+    set_error("tsdf_snapshot_load: inconsistent snapshot (pool indices, free stack, occupancy or "
+              "bucket lists)");
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));

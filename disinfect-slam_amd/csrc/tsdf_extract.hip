@@ -119,7 +119,7 @@ __device__ __forceinline__ bool voxel_ref(const EngineDev& D, int16_t px, int16_
                                           VoxRef& ref) {
   const int16_t bx = (int16_t)(px >> kBlockLenBits), by = (int16_t)(py >> kBlockLenBits),
                 bz = (int16_t)(pz >> kBlockLenBits);
-  const int32_t e = find_entry(D.table, bx, by, bz);
+  const int32_t e = find_local(D.table, bx, by, bz);
   if (e < 0) return false;
   const int32_t idx = D.table[e].z;
   ref.blk = D.pool + (size_t)idx * kBlockBytes;
@@ -288,7 +288,7 @@ __global__ __launch_bounds__(256) void k_import_payload(EngineDev D, const uint8
                                                         int32_t* missing) {
   const uint8_t* src = recs + (size_t)blockIdx.x * kBlockRecBytes;
   const short4 h = *reinterpret_cast<const short4*>(src);
-  const int32_t e = find_entry(D.table, h.x, h.y, h.z);
+  const int32_t e = find_local(D.table, h.x, h.y, h.z);
   if (e < 0) {
     if (threadIdx.x == 0) atomicAdd(missing, 1);
     return;
@@ -308,7 +308,7 @@ __global__ void k_hash_retrieve(EngineDev D, const int16_t* __restrict__ pts, in
   if (i >= n) return;
   const int16_t x = pts[3 * i], y = pts[3 * i + 1], z = pts[3 * i + 2];
   const int16_t bx = (int16_t)(x >> 3), by = (int16_t)(y >> 3), bz = (int16_t)(z >> 3);
-  const int32_t e = find_entry(D.table, bx, by, bz);
+  const int32_t e = find_local(D.table, bx, by, bz);
   const int o = (x & 7) + (y & 7) * 8 + (z & 7) * 64;
   if (e < 0) {
     rgbw[i] = 0;
@@ -331,7 +331,7 @@ __global__ void k_hash_assign(EngineDev D, const int16_t* __restrict__ pts, int 
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int16_t x = pts[3 * i], y = pts[3 * i + 1], z = pts[3 * i + 2];
-  const int32_t e = find_entry(D.table, (int16_t)(x >> 3), (int16_t)(y >> 3), (int16_t)(z >> 3));
+  const int32_t e = find_local(D.table, (int16_t)(x >> 3), (int16_t)(y >> 3), (int16_t)(z >> 3));
   if (e < 0) {
     atomicAdd(missing, 1);
     return;
@@ -355,7 +355,7 @@ __global__ void k_pool_acquire(EngineDev D, int n, int32_t* out) {
     for (int v = 0; v < kBlockVolume; ++v) {
       reinterpret_cast<float*>(blk)[v] = -1.0f;
       reinterpret_cast<float*>(blk + kProbOffset)[v] = 0.0f;  // p = 0.5
-      blk[kRgbwOffset + 4 * v + 3] = 0;
+      reinterpret_cast<uint32_t*>(blk + kRgbwOffset)[v] = 0u;  // weight 0 (rgb defined as 0)
     }
     out[k] = idx;
   }

@@ -94,14 +94,13 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
       float4 ts, pr;
       uint4 cw;
       fresh = r.pad != 0;
-      if (fresh) {  // wave-uniform: a block created this frame loads only its colour bytes
+      if (fresh) {  // wave-uniform: a block created this frame loads nothing
         ts = make_float4(-1.f, -1.f, -1.f, -1.f);
         pr = make_float4(0.f, 0.f, 0.f, 0.f);  // log-odds of AquireBlock's p = 0.5
-        cw = pool_ldu(blk + kRgbwOffset + off);
-        cw.x &= 0x00FFFFFFu;
-        cw.y &= 0x00FFFFFFu;
-        cw.z &= 0x00FFFFFFu;
-        cw.w &= 0x00FFFFFFu;
+        // weight 0; AquireBlock leaves rgb as it was (voxel_mem.cu:43-51): uninitialised memory
+        // or a previous block's colour, i.e. unspecified, visible only on weight-0 voxels. It is
+        // defined as 0 here and in the oracle (a sharded volume's pool indices differ).
+        cw = make_uint4(0u, 0u, 0u, 0u);
       } else {
         ts = pool_ld(blk + off);
         pr = pool_ld(blk + kProbOffset + off);
@@ -392,6 +391,14 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
           const int16_t noff = ecur.off ? (int16_t)(eprev.off + ecur.off) : (int16_t)0;
           store_ent(D.table, prev, ecur.x, ecur.y, ecur.z, noff, ecur.idx);
           store_off_idx(D.table, cur, 0, -1);
+          // the next list element moved into the head entry: its occupancy bit moves with it
+          // (a shard lists only its own blocks; one volume's head bit simply stays set)
+          if (prev != cur) {
+            if (local_idx(ecur.idx))
+              atomicOr(&D.occ[prev >> 6], 1ull << (prev & 63));
+            else
+              atomicAnd(&D.occ[prev >> 6], ~(1ull << (prev & 63)));
+          }
         } else {  // :154-170
           released = ecur.idx;
           const int16_t noff = ecur.off ? (int16_t)(eprev.off + ecur.off) : (int16_t)0;
@@ -400,9 +407,12 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
         }
         atomicAnd(&D.occ[cur >> 6], ~(1ull << (cur & 63)));
       }
+      // ReleaseBlock (voxel_mem.cu:54-59) of the blocks this engine holds (a shard deletes every
+      // shard's candidates from its index, and releases only its own pool blocks)
+      const bool rel = ok && local_idx(released);
       int nok;
-      const int rank = block_excl_scan(ok ? 1 : 0, L.scan, &nok);
-      if (ok) D.heap[L.sfree + rank] = released;  // ReleaseBlock (voxel_mem.cu:54-59)
+      const int rank = block_excl_scan(rel ? 1 : 0, L.scan, &nok);
+      if (rel) D.heap[L.sfree + rank] = released;
       claims_clear(L);
       __syncthreads();
       if (t == 0) {
@@ -425,6 +435,64 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
     }
   }
   if (!direct && t < kBands) D.band[t * kBandStride] = 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sharded frames: the carve-candidate exchange. k_cand_pack writes this shard's
+// candidates (its own blocks) into its outbox slot; after the all-gather, k_cand_gather lists every
+// shard's slot as the delete resolver's input -- the candidate set of one volume -- so every
+// shard's index takes the same deletes (the resolver sorts by hash entry, the reference's order).
+// One workgroup each (a few hundred candidates per frame).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_cand_pack(EngineDev D, ShardRec* __restrict__ out, int cap) {
+  const int n = D.ctr->n_cand;
+  for (int i = threadIdx.x; i < min(n, cap); i += blockDim.x) {
+    const VisRec c = D.cand[i];
+    ShardRec r;
+    r.x = c.x;
+    r.y = c.y;
+    r.z = c.z;
+    r.pad = 0;
+    r.val = (uint32_t)c.entry;
+    r.zero = 0u;
+    out[1 + i] = r;
+  }
+  if (threadIdx.x == 0) {
+    ShardRec h{};
+    h.val = (uint32_t)min(n, cap);
+    out[0] = h;
+    if (n > cap) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_SHARD_OVERFLOW
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_cand_gather(EngineDev D, const ShardRec* __restrict__ in, int cap,
+                                                      int nshard) {
+  __shared__ int s_base[kMaxShards + 1];
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int s = 0; s < nshard; ++s) {
+      s_base[s] = run;
+      run += min((int)in[(size_t)s * (cap + 1)].val, cap);
+    }
+    s_base[nshard] = run;
+    D.ctr->n_cand = run;
+  }
+  __syncthreads();
+  for (int s = 0; s < nshard; ++s) {
+    const ShardRec* slot = in + (size_t)s * (cap + 1) + 1;
+    const int n = s_base[s + 1] - s_base[s];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const ShardRec r = slot[i];
+      VisRec c;
+      c.x = r.x;
+      c.y = r.y;
+      c.z = r.z;
+      c.pad = 0;
+      c.idx = -1;
+      c.entry = (int32_t)r.val;
+      D.cand[s_base[s] + i] = c;
+    }
+  }
 }
 
 }  // namespace tsdf

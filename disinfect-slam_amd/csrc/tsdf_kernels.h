@@ -41,10 +41,6 @@ struct EngineDev {
   unsigned long long* pairs;    // kNewKeyCap (order << 32 | slot) resolver scratch
   unsigned long long* pkey;     // kNewKeyCap packed key of pairs[i] (one load in the rounds)
   int32_t* fresh;               // pool indices acquired by the hash-level test path
-  // routed frames (shard_count > 1): visible keys other shards own, min candidate order per key
-  unsigned long long* rt_key;   // kNewKeyCap
-  uint32_t* rt_order;           // kNewKeyCap
-  int32_t* rt_list;             // kNewKeyCap
   // visibility / carving
   VisRec* vis;                  // kBands x nblocks visible blocks (band-major, any order within)
   int32_t* band;                // kBands x kBandStride: record count of each band list
@@ -98,9 +94,12 @@ __global__ void k_resolve_delete(EngineDev D, const VisRec* recs, const int32_t*
                                  int direct);
 // hash-level test path
 __global__ void k_keys_to_newset(EngineDev D, const int16_t* keys, int n);
-// routed frames (SURVEY 8e option 2)
-__global__ void k_route_pack(EngineDev D, RouteRec* out, int cap, int nshard);
-__global__ void k_route_ingest(EngineDev D, FrameParams P, const RouteRec* in, int cap);
+// sharded frames: key exchange and carve-candidate exchange
+constexpr int kMaxShards = 64;
+__global__ void k_key_pack(EngineDev D, ShardRec* out, int cap);
+__global__ void k_key_merge(EngineDev D, const ShardRec* in, int cap);
+__global__ void k_cand_pack(EngineDev D, ShardRec* out, int cap);
+__global__ void k_cand_gather(EngineDev D, const ShardRec* in, int cap, int nshard);
 // DISINFSystem::feed_rgbd_frame preprocessing (tsdf_frontend.hip); grid (ceil(w / 64), ceil(h / 4))
 __global__ void k_rgbd_half(const uint8_t* rgb, const uint16_t* depth, const uint8_t* mask, int W,
                             int H, float alpha, uint8_t* rgb_out, float* depth_out);

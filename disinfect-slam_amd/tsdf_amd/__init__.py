@@ -18,8 +18,8 @@ import dataclasses
 import numpy as np
 
 from . import _lib
-from ._lib import (STATUS_DDA_OVERFLOW, STATUS_NEWKEY_OVERFLOW, STATUS_POOL_EXHAUSTED,
-                   STATUS_ROUTE_MISROUTED, STATUS_ROUTE_OVERFLOW, TSDF_MEM_DEVICE, TSDF_MEM_HOST,
+from ._lib import (SHARD_RECORD_BYTES, STATUS_DDA_OVERFLOW, STATUS_NEWKEY_OVERFLOW,
+                   STATUS_POOL_EXHAUSTED, STATUS_SHARD_OVERFLOW, TSDF_MEM_DEVICE, TSDF_MEM_HOST,
                    TSDFError)
 
 NUM_ENTRY = 1 << 22
@@ -30,9 +30,10 @@ BLOCK_RECORD_BYTES = 16 + 12 * BLOCK_VOLUME  # TSDF_BLOCK_RECORD_BYTES: key head
 VOXEL_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("tsdf", "<f4")])
 
 __all__ = [
-    "CameraIntrinsics", "CameraParams", "SE3", "BoundingCube", "TSDFGrid", "Engine",
-    "VOXEL_DTYPE", "TSDFError", "hash_block", "block_owner", "load_library",
+    "CameraIntrinsics", "CameraParams", "SE3", "BoundingCube", "TSDFGrid", "Engine", "ShardGroup",
+    "VOXEL_DTYPE", "TSDFError", "hash_block", "block_owner", "load_library", "FOREIGN_IDX",
 ]
+FOREIGN_IDX = 0x7FFFFFFF  # a shard's index entry of a block another shard holds (kForeignIdx)
 
 
 def load_library():
@@ -200,11 +201,13 @@ class FrameGraph:
         if render_K is not None:
             Rk = render_K._c() if isinstance(render_K, CameraIntrinsics) else \
                 _lib.Intrinsics(*[float(v) for v in render_K])
+        self._eng._wait_torch(depth)
         _lib.check(_lib.load().tsdf_graph_frame(
             self._g, C.byref(fr), C.byref(Kc), C.byref(cam_T_world._c()), max_depth,
             C.byref(Rk) if Rk is not None else None,
             C.byref(render_cam_T_world._c()) if render_cam_T_world is not None else None,
             _ptr(rgba), _ptr(normal)), "tsdf_graph_frame")
+        self._eng._signal_torch(depth)
 
     def close(self):
         if getattr(self, "_g", None):
@@ -232,10 +235,15 @@ class Engine:
         cfg.num_block_bits = num_block_bits
         cfg.shard_index = shard_index
         cfg.shard_count = shard_count
-        cfg.stream = stream
+        if stream is not None:  # a torch.cuda.Stream or a raw hipStream_t (0 = the legacy default stream)
+            cfg.stream = C.c_void_p(int(getattr(stream, "cuda_stream", getattr(stream, "value", stream)) or 0))
+            cfg.use_stream = 1
         h = C.c_void_p()
         _lib.check(L.tsdf_create(C.byref(cfg), device, C.byref(h)), "tsdf_create")
         self._h = h
+        # an engine on its own stream orders itself after / before torch's current stream around
+        # every call that reads / writes a torch device tensor (tsdf_stream_wait / _signal)
+        self._own_stream = stream is None
         self.voxel_size = voxel_size
         self.truncation = truncation
         self.num_blocks = int(L.tsdf_num_blocks(h))
@@ -306,9 +314,11 @@ class Engine:
         else:
             ro = np.zeros((H // 2, W // 2, 3), np.uint8)
             do = np.zeros((H // 2, W // 2), np.float32)
+        self._wait_torch(depth_u16, ro)
         _lib.check(_lib.load().tsdf_rgbd_half(self._h, _ptr(rgb), _ptr(depth_u16), _ptr(mask), W, H,
                                               depth_factor, _ptr(ro), _ptr(do),
                                               TSDF_MEM_DEVICE if dev else TSDF_MEM_HOST), "tsdf_rgbd_half")
+        self._signal_torch(depth_u16, ro)
         return ro, do
 
     def feed_rgbd_frame(self, rgb, depth_u16, mask, depth_factor: float, K, cam_T_world: SE3,
@@ -317,43 +327,81 @@ class Engine:
         (K = intrinsics of the half-size image)."""
         dev, rgb, depth_u16, mask, W, H = self._rgbd_inputs(rgb, depth_u16, mask)
         Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        self._wait_torch(depth_u16)
         _lib.check(_lib.load().tsdf_feed_rgbd_frame(self._h, _ptr(rgb), _ptr(depth_u16), _ptr(mask), W, H,
                                                     depth_factor, C.byref(Kc), C.byref(cam_T_world._c()),
                                                     max_depth, TSDF_MEM_DEVICE if dev else TSDF_MEM_HOST),
                    "tsdf_feed_rgbd_frame")
+        self._signal_torch(depth_u16)
 
     def frame_graph(self, width: int, height: int, render_width: int = 0, render_height: int = 0):
         """Graph-captured frame loop (tsdf_graph_*, BASELINE config C5): integrate (+ raycast of
         a render camera) as one hipGraph launch per frame."""
         return FrameGraph(self, width, height, render_width, render_height)
 
-    @staticmethod
-    def route_buffer_bytes(shard_count: int, route_cap: int) -> int:
-        """Bytes of one routed-frame outbox / inbox (shard_count slots of route_cap + 1 records)."""
-        return int(_lib.load().tsdf_route_buffer_bytes(shard_count, route_cap))
+    # ---- stream ordering with torch (ADVICE r1: device tensors on torch's current stream) ----
+    def _wait_torch(self, *tensors):
+        """Engine stream waits for torch's current stream when a device tensor goes in."""
+        if self._own_stream and any(_is_torch_cuda(t) for t in tensors if t is not None):
+            import torch
+            _lib.check(_lib.load().tsdf_stream_wait(self._h, C.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                       "tsdf_stream_wait")
 
-    def integrate_route_begin(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float,
-                              slice_index: int, slice_count: int, outbox, route_cap: int):
-        """Routed frame, phase 1 (SURVEY 8e option 2): DDA over this slice of pixel-tile rows; keys
-        other shards own are written to `outbox` (device tensor of route_buffer_bytes)."""
-        if not _is_torch_cuda(outbox) or outbox.numel() * outbox.element_size() < \
-                self.route_buffer_bytes(self.shard_count, route_cap):
-            raise ValueError("outbox must be a device tensor of route_buffer_bytes(shard_count, route_cap)")
+    def _signal_torch(self, *tensors):
+        """Torch's current stream waits for the engine when a device tensor it wrote / reads is
+        handed back (or may be freed by the caller)."""
+        if self._own_stream and any(_is_torch_cuda(t) for t in tensors if t is not None):
+            import torch
+            _lib.check(_lib.load().tsdf_stream_signal(self._h, C.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                       "tsdf_stream_signal")
+
+    # ---- sharded frames (SURVEY 8e; tsdf_integrate_shard_*) ----
+    @staticmethod
+    def shard_slot_bytes(cap: int) -> int:
+        """Bytes of one exchange slot: cap records + the count header (tsdf_shard_slot_bytes)."""
+        return int(_lib.load().tsdf_shard_slot_bytes(cap))
+
+    def _check_slot(self, buf, cap, slots, what):
+        if not _is_torch_cuda(buf) or not buf.is_contiguous() or \
+                buf.numel() * buf.element_size() < slots * self.shard_slot_bytes(cap):
+            raise ValueError(f"{what} must be a contiguous device tensor of {slots} x shard_slot_bytes({cap})")
+
+    def integrate_shard_begin(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float,
+                              slice_index: int = 0, slice_count: int = 1, keys_out=None, key_cap: int = 0):
+        """Sharded frame, phase 1: pixel records, visibility of this shard's blocks, and the DDA over
+        slice `slice_index` of `slice_count` (tile-row bands); the keys it finds go to keys_out (one
+        slot), or stay here when slice_count == 1 and keys_out is None (every shard runs the whole
+        DDA)."""
+        if keys_out is not None:
+            self._check_slot(keys_out, key_cap, 1, "keys_out")
         fr, keep = self._frame(rgb, depth, ht, lt)
+        self._wait_torch(depth, keys_out)
         Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
-        _lib.check(_lib.load().tsdf_integrate_route_begin(self._h, C.byref(fr), C.byref(Kc),
+        _lib.check(_lib.load().tsdf_integrate_shard_begin(self._h, C.byref(fr), C.byref(Kc),
                                                           C.byref(cam_T_world._c()), max_depth,
-                                                          slice_index, slice_count, _ptr(outbox),
-                                                          route_cap), "tsdf_integrate_route_begin")
+                                                          slice_index, slice_count, _ptr(keys_out),
+                                                          key_cap), "tsdf_integrate_shard_begin")
+        self._signal_torch(depth, keys_out)
         del keep
 
-    def integrate_route_end(self, inbox, route_cap: int):
-        """Routed frame, phase 2: merge the exchanged keys and finish the frame."""
-        if not _is_torch_cuda(inbox) or inbox.numel() * inbox.element_size() < \
-                self.route_buffer_bytes(self.shard_count, route_cap):
-            raise ValueError("inbox must be a device tensor of route_buffer_bytes(shard_count, route_cap)")
-        _lib.check(_lib.load().tsdf_integrate_route_end(self._h, _ptr(inbox), route_cap),
-                   "tsdf_integrate_route_end")
+    def integrate_shard_update(self, keys_in, key_cap: int, cands_out, cand_cap: int):
+        """Sharded frame, phase 2: merge the all-gathered key slots (None after a whole-frame DDA),
+        allocate, update this shard's blocks, write its carve candidates to cands_out (one slot)."""
+        if keys_in is not None:
+            self._check_slot(keys_in, key_cap, self.shard_count, "keys_in")
+        self._check_slot(cands_out, cand_cap, 1, "cands_out")
+        self._wait_torch(keys_in, cands_out)
+        _lib.check(_lib.load().tsdf_integrate_shard_update(self._h, _ptr(keys_in), key_cap, _ptr(cands_out),
+                                                           cand_cap), "tsdf_integrate_shard_update")
+        self._signal_torch(keys_in, cands_out)
+
+    def integrate_shard_end(self, cands_in, cand_cap: int):
+        """Sharded frame, phase 3: delete the all-gathered carve candidates (every shard's)."""
+        self._check_slot(cands_in, cand_cap, self.shard_count, "cands_in")
+        self._wait_torch(cands_in)
+        _lib.check(_lib.load().tsdf_integrate_shard_end(self._h, _ptr(cands_in), cand_cap),
+                   "tsdf_integrate_shard_end")
+        self._signal_torch(cands_in)
 
     def integrate(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float):
         dev = _is_torch_cuda(depth)
@@ -373,9 +421,11 @@ class Engine:
         fr = _lib.Frame(W, H, _ptr(rgb), _ptr(depth), _ptr(ht), _ptr(lt),
                         TSDF_MEM_DEVICE if dev else TSDF_MEM_HOST)
         Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        self._wait_torch(depth)
         _lib.check(_lib.load().tsdf_integrate(self._h, C.byref(fr), C.byref(Kc),
                                               C.byref(cam_T_world._c()), max_depth),
                    "tsdf_integrate")
+        self._signal_torch(depth)  # the caller may overwrite / free the frame after this
 
     def synchronize(self):
         _lib.check(_lib.load().tsdf_synchronize(self._h), "tsdf_synchronize")
@@ -384,9 +434,11 @@ class Engine:
     def raycast(self, K, width, height, cam_T_world: SE3, max_depth: float, rgba=None, normal=None):
         Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
         if rgba is not None and _is_torch_cuda(rgba):
+            self._wait_torch(rgba, normal)
             _lib.check(_lib.load().tsdf_raycast(self._h, C.byref(Kc), width, height,
                                                 C.byref(cam_T_world._c()), max_depth, _ptr(rgba),
                                                 _ptr(normal), TSDF_MEM_DEVICE), "tsdf_raycast")
+            self._signal_torch(rgba, normal)
             return rgba, normal
         rgba = np.zeros((height, width, 4), np.uint8)
         normal = np.zeros((height, width, 4), np.uint8)
@@ -413,9 +465,11 @@ class Engine:
             out = np.empty((n.value, BLOCK_RECORD_BYTES), np.uint8)
             kind = TSDF_MEM_HOST
         if n.value:
+            self._wait_torch(out)
             _lib.check(L.tsdf_render_blocks(self._h, C.byref(Kc), width, height, C.byref(pc),
                                             max_depth, _ptr(out), n.value, C.byref(n), kind),
                        "tsdf_render_blocks")
+            self._signal_torch(out)
         return out
 
     def pack_blocks(self, bounds=None, device=False):
@@ -434,9 +488,11 @@ class Engine:
         else:
             out = np.empty((n.value, BLOCK_RECORD_BYTES), np.uint8)
         if n.value:
+            self._wait_torch(out)
             _lib.check(L.tsdf_pack_blocks(self._h, _ptr(b), _ptr(out), n.value, C.byref(n),
                                           TSDF_MEM_DEVICE if device else TSDF_MEM_HOST),
                        "tsdf_pack_blocks")
+            self._signal_torch(out)
         return out
 
     def import_blocks(self, records, replace=False):
@@ -446,8 +502,10 @@ class Engine:
         kind = TSDF_MEM_DEVICE if _is_torch_cuda(records) else TSDF_MEM_HOST
         if kind == TSDF_MEM_HOST:
             records = np.ascontiguousarray(records, dtype=np.uint8)
+        self._wait_torch(records)  # e.g. an all-gather / torch.cat still queued on torch's stream
         _lib.check(_lib.load().tsdf_import_blocks(self._h, _ptr(records), n, kind, int(replace)),
                    "tsdf_import_blocks")
+        self._signal_torch(records)
 
     def reset(self):
         """Empty the volume (tsdf_reset)."""
@@ -464,9 +522,11 @@ class Engine:
         _lib.check(L.tsdf_extract_mesh(self._h, _ptr(b), missing_tsdf, min_weight, None, 0,
                                        C.byref(n), TSDF_MEM_HOST), "tsdf_extract_mesh")
         if out is not None:
+            self._wait_torch(out)
             _lib.check(L.tsdf_extract_mesh(self._h, _ptr(b), missing_tsdf, min_weight, _ptr(out),
                                            out.numel() // 9, C.byref(n), TSDF_MEM_DEVICE),
                        "tsdf_extract_mesh")
+            self._signal_torch(out)
             return out[:9 * n.value].view(-1, 3, 3)
         tris = np.zeros((n.value, 3, 3), np.float32)
         if n.value:
@@ -585,6 +645,65 @@ class Engine:
         out = np.zeros(BLOCK_VOLUME, np.uint8)
         _lib.check(_lib.load().tsdf_pool_get_weights(self._h, int(block), _ptr(out)), "tsdf_pool_get_weights")
         return out
+
+
+class ShardGroup:
+    """G shard engines of one spatially sharded volume on ONE GPU, exchanging their key
+    and carve-candidate slots with device copies where a multi-GPU job all-gathers them
+    (tsdf_amd.dist.integrate_sharded). The engines run on torch's current stream, so the copies are
+    ordered between the phases. For tests and single-GPU rehearsals of the sharded path.
+    split: True -- shard i runs the DDA over tile-row band i of G and the keys are exchanged;
+    False -- every shard runs the whole frame's DDA, only carve candidates are exchanged."""
+
+    def __init__(self, shard_count: int, voxel_size=0.005, truncation=0.03, max_width=1920,
+                 max_height=1080, num_block_bits=18, device=0, key_cap=16384, cand_cap=16384,
+                 split=True, stream=None):
+        import torch
+        self.G = shard_count
+        self.split = split
+        self.key_cap, self.cand_cap = key_cap, cand_cap
+        # all shards on ONE stream (torch's current one unless given), so the phases and the slot
+        # reads / writes between them are ordered
+        stream = torch.cuda.current_stream(device) if stream is None else stream
+        self.engines = [Engine(voxel_size, truncation, max_width, max_height, num_block_bits, device,
+                               shard_index=i, shard_count=shard_count, stream=stream)
+                        for i in range(shard_count)]
+        dev = f"cuda:{device}"
+        self._keys = torch.zeros((shard_count, Engine.shard_slot_bytes(key_cap)), dtype=torch.uint8, device=dev)
+        self._cands = torch.zeros((shard_count, Engine.shard_slot_bytes(cand_cap)), dtype=torch.uint8, device=dev)
+        self.keys_exchanged = 0   # key records that went through the exchange (all frames)
+        self.cands_exchanged = 0  # carve-candidate records likewise
+
+    def integrate(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float, count=False):
+        G = self.G
+        for i, e in enumerate(self.engines):
+            if self.split:
+                e.integrate_shard_begin(rgb, depth, ht, lt, K, cam_T_world, max_depth, i, G, self._keys[i],
+                                        self.key_cap)
+            else:
+                e.integrate_shard_begin(rgb, depth, ht, lt, K, cam_T_world, max_depth)
+        keys_in = self._keys if self.split else None  # the all-gathered key slots
+        for i, e in enumerate(self.engines):
+            e.integrate_shard_update(keys_in, self.key_cap, self._cands[i], self.cand_cap)
+        for e in self.engines:
+            e.integrate_shard_end(self._cands, self.cand_cap)
+        if count:  # slot headers (record 0's count word), a host sync
+            import torch
+            hdr = lambda t: int(t[:, 8:12].contiguous().view(torch.int32).sum())
+            if self.split:
+                self.keys_exchanged += hdr(self._keys)
+            self.cands_exchanged += hdr(self._cands)
+
+    def synchronize(self):
+        for e in self.engines:
+            e.synchronize()
+
+    def stats(self):
+        return [e.stats() for e in self.engines]
+
+    def close(self):
+        for e in self.engines:
+            e.close()
 
 
 class TSDFGrid:

@@ -19,8 +19,8 @@ STATUS_POOL_EXHAUSTED = 1
 STATUS_NEWKEY_OVERFLOW = 2
 STATUS_DDA_OVERFLOW = 4
 STATUS_RESOLVE_ABORT = 8
-STATUS_ROUTE_OVERFLOW = 16
-STATUS_ROUTE_MISROUTED = 32
+STATUS_SHARD_OVERFLOW = 16
+SHARD_RECORD_BYTES = 16
 
 
 class Config(C.Structure):
@@ -33,6 +33,7 @@ class Config(C.Structure):
         ("shard_index", C.c_int),
         ("shard_count", C.c_int),
         ("stream", C.c_void_p),
+        ("use_stream", C.c_int),
     ]
 
 
@@ -96,7 +97,8 @@ EXPORTS = [
     "tsdf_hash_delete", "tsdf_hash_retrieve", "tsdf_hash_assign", "tsdf_num_active_blocks",
     "tsdf_pool_acquire", "tsdf_pool_release", "tsdf_pool_set_weight", "tsdf_pool_get_weights",
     "tsdf_hash_block", "tsdf_block_owner", "tsdf_error_string", "tsdf_last_error",
-    "tsdf_route_buffer_bytes", "tsdf_integrate_route_begin", "tsdf_integrate_route_end",
+    "tsdf_shard_slot_bytes", "tsdf_integrate_shard_begin", "tsdf_integrate_shard_update",
+    "tsdf_integrate_shard_end", "tsdf_stream_wait", "tsdf_stream_signal", "tsdf_get_stream",
     "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame", "tsdf_graph_destroy",
     "tsdf_snapshot_bytes", "tsdf_snapshot_save", "tsdf_snapshot_load",
     "tsdf_render_blocks", "tsdf_import_blocks", "tsdf_reset", "tsdf_pack_blocks",
@@ -122,11 +124,15 @@ def load(path: str | None = None):
     L.tsdf_destroy.argtypes = [P]
     L.tsdf_integrate.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f]
     L.tsdf_raycast.argtypes = [P, C.POINTER(Intrinsics), i, i, C.POINTER(Pose), f, P, P, i]
-    L.tsdf_route_buffer_bytes.restype = C.c_int64
-    L.tsdf_route_buffer_bytes.argtypes = [C.c_int32, C.c_int32]
-    L.tsdf_integrate_route_begin.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f,
+    L.tsdf_shard_slot_bytes.restype = C.c_int64
+    L.tsdf_shard_slot_bytes.argtypes = [C.c_int32]
+    L.tsdf_integrate_shard_begin.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f,
                                              C.c_int32, C.c_int32, P, C.c_int32]
-    L.tsdf_integrate_route_end.argtypes = [P, P, C.c_int32]
+    L.tsdf_integrate_shard_update.argtypes = [P, P, C.c_int32, P, C.c_int32]
+    L.tsdf_integrate_shard_end.argtypes = [P, P, C.c_int32]
+    L.tsdf_stream_wait.argtypes = [P, P]
+    L.tsdf_stream_signal.argtypes = [P, P]
+    L.tsdf_get_stream.argtypes = [P, C.POINTER(P)]
     L.tsdf_feed_rgbd_frame.argtypes = [P, P, P, P, i, i, f, C.POINTER(Intrinsics), C.POINTER(Pose), f, i]
     L.tsdf_rgbd_half.argtypes = [P, P, P, P, i, i, f, P, P, i]
     L.tsdf_graph_create.argtypes = [P, i, i, i, i, C.POINTER(P)]
@@ -171,7 +177,8 @@ def load(path: str | None = None):
     L.tsdf_last_error.restype = C.c_char_p
     L.tsdf_last_error.argtypes = []
     for name in ("tsdf_create", "tsdf_destroy", "tsdf_integrate", "tsdf_raycast", "tsdf_query",
-                 "tsdf_integrate_route_begin", "tsdf_integrate_route_end",
+                 "tsdf_integrate_shard_begin", "tsdf_integrate_shard_update", "tsdf_integrate_shard_end",
+                 "tsdf_stream_wait", "tsdf_stream_signal", "tsdf_get_stream",
                  "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame",
                  "tsdf_graph_destroy", "tsdf_snapshot_bytes", "tsdf_snapshot_save", "tsdf_snapshot_load",
                  "tsdf_extract_mesh",

@@ -2,12 +2,13 @@
 
  - streams mode (weak scaling): rank r integrates its own camera stream into its own volume; no
    data-path collective;
- - sharded mode (strong scaling, SURVEY 8e option 1): every rank sees the same frames, runs the
-   whole DDA and owns the blocks whose 4^3 brick hashes to it (tsdf_block_owner); no data-path
-   collective; a whole-volume Query is the union of the shards;
- - routed mode (strong scaling, SURVEY 8e option 2): same ownership, but rank r runs the DDA only
-   over its slice of pixel-tile rows and routes the keys other ranks own with one all-to-all per
-   frame (route_exchange: RCCL over xGMI on the GPU box).
+ - sharded modes (strong scaling): ONE stream into ONE volume spatially sharded over
+   the ranks by 4^3-block bricks. Every rank keeps the whole hash index and the voxels of its own
+   bricks, and a frame is three engine calls around two all-gathers (integrate_sharded): the new
+   block keys (each rank runs the DDA over its band of pixel-tile rows; "routed") and the
+   space-carving candidates. With split=False ("sharded") every rank runs the whole DDA and only
+   the candidates are exchanged. Either way the union of the ranks is the unsharded volume, block
+   for block and voxel for voxel.
 
 The functions here are backend-agnostic (RCCL "nccl" on the GPU box, "gloo" in the CPU tests).
 """
@@ -27,18 +28,57 @@ def shard_of(mode: str, rank: int, world: int):
     return (rank, world) if (mode in ("sharded", "routed") and world > 1) else (0, 1)
 
 
-def route_exchange(outbox, inbox):
-    """Routed frames: inbox slot s <- rank s's outbox slot <this rank> (all-to-all, equal splits).
-
-    outbox / inbox: contiguous (world, slot_bytes) tensors (tsdf_route_buffer_bytes in all). On the
-    GPU box this is one RCCL all-to-all ordered on the current stream (the engine's stream), so the
-    frame stays asynchronous; without a process group it is the identity (one shard)."""
+def all_gather_slots(slot, out):
+    """out (world, slot_bytes) <- every rank's slot (world x slot_bytes u8), rank order: one
+    all-gather, RCCL over xGMI on the GPU box, ordered on the current stream (no host sync).
+    Without a process group (one rank) it is a copy."""
+    import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-        inbox.copy_(outbox)
-        return inbox
-    dist.all_to_all_single(inbox, outbox)
-    return inbox
+        out.view(-1)[:slot.numel()].copy_(slot.view(-1))
+        return out
+    if slot.is_cuda and dist.get_backend() == "gloo":  # CPU-backend tests: stage through the host
+        host = torch.empty(out.numel(), dtype=out.dtype)
+        dist.all_gather_into_tensor(host, slot.view(-1).cpu())
+        out.view(-1).copy_(host)
+        return out
+    dist.all_gather_into_tensor(out.view(-1), slot.view(-1))
+    return out
+
+
+class ShardBuffers:
+    """Exchange slots of one rank's sharded engine (tsdf_shard_slot_bytes each)."""
+
+    def __init__(self, engine, world, key_cap=16384, cand_cap=16384, device=None):
+        import torch
+        dev = device if device is not None else f"cuda:{engine.device}"
+        self.key_cap, self.cand_cap = key_cap, cand_cap
+        kb, cb = engine.shard_slot_bytes(key_cap), engine.shard_slot_bytes(cand_cap)
+        self.keys_out = torch.zeros(kb, dtype=torch.uint8, device=dev)
+        self.keys_in = torch.zeros((world, kb), dtype=torch.uint8, device=dev)
+        self.cands_out = torch.zeros(cb, dtype=torch.uint8, device=dev)
+        self.cands_in = torch.zeros((world, cb), dtype=torch.uint8, device=dev)
+
+
+def integrate_sharded(engine, bufs, rgb, depth, ht, lt, K, cam_T_world, max_depth, split=True):
+    """One frame of a spatially sharded volume on this rank (tsdf_integrate_shard_*):
+    begin (DDA over this rank's band of tile rows when split) -> all-gather of the key slots ->
+    update -> all-gather of the carve-candidate slots -> end. Asynchronous on the current stream."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        rank, world = dist.get_rank(), dist.get_world_size()
+    else:
+        rank, world = 0, 1
+    if split:
+        engine.integrate_shard_begin(rgb, depth, ht, lt, K, cam_T_world, max_depth, rank, world,
+                                     bufs.keys_out, bufs.key_cap)
+        all_gather_slots(bufs.keys_out, bufs.keys_in)
+        engine.integrate_shard_update(bufs.keys_in, bufs.key_cap, bufs.cands_out, bufs.cand_cap)
+    else:
+        engine.integrate_shard_begin(rgb, depth, ht, lt, K, cam_T_world, max_depth)
+        engine.integrate_shard_update(None, bufs.key_cap, bufs.cands_out, bufs.cand_cap)
+    all_gather_slots(bufs.cands_out, bufs.cands_in)
+    engine.integrate_shard_end(bufs.cands_in, bufs.cand_cap)
 
 
 def stream_offset(mode: str, rank: int, world: int, stride: int = 240) -> int:

@@ -36,8 +36,7 @@ extern "C" {
 #define TSDF_STATUS_NEWKEY_OVERFLOW 2u /* more new blocks in one frame than the key set holds */
 #define TSDF_STATUS_DDA_OVERFLOW 4u    /* a DDA ray took more samples than sized for */
 #define TSDF_STATUS_RESOLVE_ABORT 8u   /* allocation resolver made no progress (internal error) */
-#define TSDF_STATUS_ROUTE_OVERFLOW 16u /* a routed frame had more keys for one shard than route_cap */
-#define TSDF_STATUS_ROUTE_MISROUTED 32u /* an inbox record belongs to another shard */
+#define TSDF_STATUS_SHARD_OVERFLOW 16u /* a sharded frame had more keys / candidates than a slot holds */
 
 typedef struct tsdf_engine tsdf_engine;
 typedef struct tsdf_graph tsdf_graph;
@@ -48,9 +47,10 @@ typedef struct tsdf_config {
   int max_width;      /* largest integrate / raycast image; reference MAX_IMG_* = 1920x1080 */
   int max_height;     /*   (voxel_tsdf.cu:10-12) */
   int num_block_bits; /* voxel-block pool = 2^bits blocks; reference NUM_BLOCK_BITS 18 */
-  int shard_index;    /* spatial sharding: this engine owns blocks b with owner(b) == index */
-  int shard_count;    /*   owner(b) = hash(b >> 2) mod count; 1 = unsharded */
-  void* stream;       /* optional hipStream_t to run on; NULL = engine-owned stream */
+  int shard_index;    /* spatial sharding: this engine holds the voxels of blocks b with */
+  int shard_count;    /*   owner(b) = hash(b >> 2) mod count == index; 1 = unsharded (<= 64) */
+  void* stream;       /* hipStream_t to run on when use_stream != 0 (NULL then means the legacy */
+  int use_stream;     /*   default stream); use_stream == 0: an engine-owned stream */
 } tsdf_config;
 
 /* Fill reference defaults: 5 mm / 3 cm, 1920x1080, 2^18 blocks, unsharded. */
@@ -121,26 +121,49 @@ int tsdf_destroy(tsdf_engine* e);
 int tsdf_integrate(tsdf_engine* e, const tsdf_frame* frame, const tsdf_intrinsics* K,
                    const tsdf_pose* cam_T_world, float max_depth);
 
-/* Routed frames (SURVEY.md 8e option 2, shard_count > 1): TSDFGrid::Integrate split across the
- * shards of one volume. Every shard gets the whole frame (its pixel records feed the update) but
- * runs the block-allocation DDA (block_allocate_kernel, voxel_tsdf.cu:104-147) only over its slice
- * of pixel-tile rows; visible keys another shard owns are routed to it:
- *   1. tsdf_integrate_route_begin: DDA over slice `slice_index` of `slice_count`, then writes the
- *      outbox -- device memory of tsdf_route_buffer_bytes(shard_count, route_cap) bytes: one slot
- *      of (route_cap + 1) 16-B records per destination shard (record 0 = count header).
- *   2. the caller exchanges the buffers (an all-to-all with equal splits, e.g. RCCL over xGMI):
- *      inbox slot s = what shard s's outbox holds in slot <this shard>. The exchange must be
- *      ordered after begin and before end on the engine stream (or synchronised around).
- *   3. tsdf_integrate_route_end: merges the inbox and finishes the frame (ordered allocation,
- *      update, carving).
- * Keys, candidate orders and allocation outcomes equal the replicated-frame sharded integrate
- * (tsdf_integrate on the same shard engine). More than route_cap keys for one destination sets
- * TSDF_STATUS_ROUTE_OVERFLOW (the excess is dropped). No other engine call may come between. */
-int64_t tsdf_route_buffer_bytes(int32_t shard_count, int32_t route_cap);
-int tsdf_integrate_route_begin(tsdf_engine* e, const tsdf_frame* frame, const tsdf_intrinsics* K,
+/* Sharded volume (no reference counterpart: TSDFGrid is single-GPU). An engine
+ * created with shard_count > 1 is shard `shard_index` of one volume: it keeps the whole hash index
+ * (VoxelHashTable, voxel_hash.cuh:47-183) and holds the voxels of the blocks whose 4^3-block brick
+ * hashes to it (tsdf_block_owner). Every shard applies every Allocate / Delete to its index --
+ * another shard's block is an occupied entry without voxels here -- so the bucket-lock outcomes
+ * (one structural change per bucket per launch, voxel_hash.cu:80-118,137-170) are those of ONE
+ * volume, and the union of the shards equals the unsharded volume block for block and voxel for
+ * voxel. TSDFGrid::Integrate (voxel_tsdf.cu:347-375) of a shard is three calls around two
+ * exchanges, all asynchronous on the engine stream:
+ *   1. tsdf_integrate_shard_begin: the frame's pixel records (every shard's blocks may project
+ *      anywhere), the visibility of this shard's blocks, and the block_allocate_kernel DDA
+ *      (voxel_tsdf.cu:104-147) over slice `slice_index` of `slice_count` (bands of 16-pixel tile
+ *      rows). The keys it finds missing from the index go to keys_out: one slot of
+ *      tsdf_shard_slot_bytes(key_cap) bytes (record 0 = count header, then 16-B records).
+ *      slice_count == 1 with keys_out == NULL: every shard runs the whole DDA and finds the same
+ *      keys itself, so no key exchange is needed (keys_in NULL below).
+ *   2. the caller all-gathers the key slots (e.g. RCCL all-gather over xGMI): keys_in = shard_count
+ *      slots, slot s from shard s. tsdf_integrate_shard_update merges them (smallest candidate
+ *      order per key = the whole frame's DDA), runs the ordered allocation (pool blocks only for
+ *      owned keys), the fused update of this shard's visible blocks, and writes its space-carving
+ *      candidates (space_carving_kernel, voxel_tsdf.cu:207-230) to cands_out (one slot).
+ *   3. the caller all-gathers the candidate slots; tsdf_integrate_shard_end deletes the union in
+ *      hash-entry order (every shard's index) and releases this shard's pool blocks.
+ * Exchanges must be ordered between the calls on the engine stream (same stream, or
+ * tsdf_stream_wait / tsdf_stream_signal). No other engine call may come between _begin and _end;
+ * tsdf_integrate / feed / graph frames refuse a shard. More records than a slot holds set
+ * TSDF_STATUS_SHARD_OVERFLOW (the shards then diverge: size the caps for the first frame). */
+int64_t tsdf_shard_slot_bytes(int32_t cap);
+int tsdf_integrate_shard_begin(tsdf_engine* e, const tsdf_frame* frame, const tsdf_intrinsics* K,
                                const tsdf_pose* cam_T_world, float max_depth, int32_t slice_index,
-                               int32_t slice_count, void* outbox, int32_t route_cap);
-int tsdf_integrate_route_end(tsdf_engine* e, const void* inbox, int32_t route_cap);
+                               int32_t slice_count, void* keys_out, int32_t key_cap);
+int tsdf_integrate_shard_update(tsdf_engine* e, const void* keys_in, int32_t key_cap, void* cands_out,
+                                int32_t cand_cap);
+int tsdf_integrate_shard_end(tsdf_engine* e, const void* cands_in, int32_t cand_cap);
+
+/* Stream ordering with a caller's HIP stream (e.g. torch's current stream) for device buffers
+ * passed to an engine that runs on its own stream: tsdf_stream_wait makes the engine stream wait
+ * for the work queued on `stream` so far (before the engine reads a buffer the caller wrote);
+ * tsdf_stream_signal makes `stream` wait for the engine's queued work (before the caller reads a
+ * buffer the engine wrote, or frees one it reads). tsdf_get_stream returns the engine stream. */
+int tsdf_stream_wait(tsdf_engine* e, void* stream);
+int tsdf_stream_signal(tsdf_engine* e, void* stream);
+int tsdf_get_stream(tsdf_engine* e, void** stream);
 
 /* DISINFSystem::feed_rgbd_frame (disinfect_slam/disinfect_slam.cc:31-67) after the pose lookup:
  * cv::resize(x0.5) of rgb (height x width x 3 u8), depth (height x width u16 raw sensor units) and
@@ -241,7 +264,9 @@ int tsdf_profile_end(tsdf_engine* e, tsdf_profile* out);
  * occupancy, free-block stack, voxel pool and counters, so a restored engine continues a frame
  * stream bit for bit. Two-call: tsdf_snapshot_bytes, then tsdf_snapshot_save into a host buffer of
  * that size. tsdf_snapshot_load accepts only a snapshot of an engine with the same voxel size,
- * truncation and pool size (TSDF_ERR_INVALID_ARG otherwise). */
+ * truncation, pool size and shard layout whose counters, free stack and entries are consistent
+ * (every pool index in range, each block exactly once on the stack or in the table);
+ * TSDF_ERR_INVALID_ARG otherwise, the engine unchanged. */
 int tsdf_snapshot_bytes(tsdf_engine* e, int64_t* bytes);
 int tsdf_snapshot_save(tsdf_engine* e, void* out, int64_t capacity);
 int tsdf_snapshot_load(tsdf_engine* e, const void* in, int64_t size);

@@ -158,7 +158,12 @@ static s3 block_to_point(s3 b) { /* voxel_mem.cuh:41-44 */
 }
 static int offset_to_index(int ox, int oy, int oz) { return ox + oy * BLOCK_LEN + oz * BLOCK_AREA; }
 
-/* voxel_mem.cu:37-52 AquireBlock (weight 0, tsdf -1, prob 0.5; rgb left as is) */
+/* voxel_mem.cu:37-52 AquireBlock (weight 0, tsdf -1, prob 0.5). The reference leaves rgb as it
+ * is: uninitialised cudaMalloc memory for a never-used block, the previous occupant's colour for a
+ * re-used one -- which occupant depends on the racy pool order. That colour is
+ * only observable on weight-0 voxels (an update multiplies it by w_old = 0), so it is unspecified
+ * in the reference; here and in the engine it is defined as 0, which keeps a sharded volume (other
+ * pool indices) voxel-identical to one volume. */
 static int32_t pool_acquire(ora_grid* g) {
   const int32_t i = g->free_count;
   if (i < 1) return -1; /* reference: assert(idx >= 1), undefined in release; defined here as a
@@ -167,7 +172,7 @@ static int32_t pool_acquire(ora_grid* g) {
   const int32_t idx = g->heap[i - 1];
   const int64_t base = (int64_t)idx << BLOCK_VOLUME_BITS;
   for (int v = 0; v < BLOCK_VOLUME; ++v) {
-    g->rgbw[(base + v) * 4 + 3] = 0;
+    memset(&g->rgbw[(base + v) * 4], 0, 4);
     g->tsdf[base + v] = -1.0f;
     g->prob[base + v] = 0.5f;
   }
@@ -180,10 +185,51 @@ static void pool_release(ora_grid* g, int32_t idx) {
   g->heap[i] = idx;
 }
 
+/* Sharded volume (not in the reference): every shard holds the whole hash index, so
+ * the bucket locks and the table layout evolve exactly as in one volume; a block's voxels live only
+ * on its owner. Other shards mark its entry ORA_FOREIGN: occupied for Allocate / Delete, missing
+ * for every reader. local_idx: the entry has voxels in this grid. */
+#define ORA_FOREIGN 0x7FFFFFFF
+static int local_idx(int32_t idx) { return idx >= 0 && idx != ORA_FOREIGN; }
+static int owns(const ora_grid* g, s3 key) {
+  return g->shard_count <= 1 ||
+         ora_block_owner(key.x, key.y, key.z, (uint32_t)g->shard_count) == (uint32_t)g->shard_index;
+}
+/* atomicExch(&bucket_locks_[b], LOCKED) == FREE; the lock word remembers the owner shard + 1 of
+ * the key that took it, so a sharded grid can count the losses to another shard's key */
+static int lock_take(ora_grid* g, uint32_t b, uint8_t tag, int* cross) {
+  if (g->locks[b] == 0) {
+    g->locks[b] = tag;
+    return 1;
+  }
+  if (g->locks[b] != tag) *cross = 1;
+  return 0;
+}
+/* the pool block of a new entry of `key`: AquireBlock on its owner, ORA_FOREIGN elsewhere.
+ * An exhausted pool drops the insert (returns 0; the lock stays taken) in one volume; a shard
+ * keeps the entry (ORA_FOREIGN, no voxels) so every shard's index stays the same. */
+static int new_block(ora_grid* g, s3 key, int32_t* idx) {
+  if (!owns(g, key)) {
+    *idx = ORA_FOREIGN;
+    return 1;
+  }
+  if (g->free_count < 1) {
+    g->st.pool_exhausted = 1;
+    *idx = ORA_FOREIGN;
+    return g->shard_count > 1;
+  }
+  *idx = pool_acquire(g);
+  return 1;
+}
+
 /* voxel_hash.cu:58-120 VoxelHashTable::Allocate, executed as one step of a sequential launch. */
 static int hash_allocate(ora_grid* g, s3 key) {
   const uint32_t bucket = ora_hash(key.x, key.y, key.z);
   const uint32_t e0 = bucket << 1;
+  const uint8_t tag = (uint8_t)(1 + (g->shard_count > 1
+                                         ? ora_block_owner(key.x, key.y, key.z, (uint32_t)g->shard_count)
+                                         : 0u));
+  int cross = 0;
   for (int i = 0; i < NUM_ENTRY_PER_BUCKET; ++i) { /* existence :62-68 */
     const entry* b = &g->table[e0 + i];
     if (s3_eq(b->pos, key) && b->idx >= 0) return 0;
@@ -197,14 +243,15 @@ static int hash_allocate(ora_grid* g, s3 key) {
   for (int i = 0; i < NUM_ENTRY_PER_BUCKET; ++i) { /* current bucket :79-91 */
     entry* b = &g->table[e0 + i];
     if (b->idx < 0) {
-      if (g->locks[bucket] == 0) {
-        g->locks[bucket] = 1;
-        if (g->free_count < 1) return -2; /* pool exhausted: insert dropped, lock stays taken */
+      if (lock_take(g, bucket, tag, &cross)) {
+        int32_t idx;
+        if (!new_block(g, key, &idx)) return -2; /* pool exhausted: insert dropped, lock stays taken */
         b->pos = key;
         b->offset = 0;
-        b->idx = pool_acquire(g);
+        b->idx = idx;
         return 1;
       }
+      g->st.last_cross_losses += cross;
       return -1;
     }
   }
@@ -217,25 +264,21 @@ static int hash_allocate(ora_grid* g, s3 key) {
     next = (next + 1) & ENTRY_MASK;
     if ((next & ENTRY_PER_BUCKET_MASK) != ENTRY_PER_BUCKET_MASK && g->table[next].idx < 0) {
       const uint32_t bucket_next = next >> 1;
-      int ok = 0;
-      if (g->locks[bucket_last] == 0) {          /* atomicExch(last) == FREE */
-        g->locks[bucket_last] = 1;
-        if (g->locks[bucket_next] == 0) {        /* && atomicExch(next) == FREE */
-          g->locks[bucket_next] = 1;
-          ok = 1;
-        }
-      }
-      if (ok && g->free_count < 1) return -2; /* pool exhausted (see pool_acquire) */
+      /* atomicExch(last) == FREE && atomicExch(next) == FREE */
+      const int ok = lock_take(g, bucket_last, tag, &cross) && lock_take(g, bucket_next, tag, &cross);
       if (ok) {
+        int32_t idx;
+        if (!new_block(g, key, &idx)) return -2; /* pool exhausted (see new_block) */
         entry* bl = &g->table[last];
         entry* bn = &g->table[next];
         const uint32_t wrap = next > last ? 0u : (uint32_t)NUM_ENTRY;
         bl->offset = (int16_t)(next + wrap - last);
         bn->pos = key;
         bn->offset = 0;
-        bn->idx = pool_acquire(g);
+        bn->idx = idx;
         return 1;
       }
+      g->st.last_cross_losses += cross;
       return -1;
     }
   }
@@ -246,10 +289,11 @@ static int hash_allocate(ora_grid* g, s3 key) {
 static int hash_delete(ora_grid* g, s3 key) {
   const uint32_t bucket = ora_hash(key.x, key.y, key.z);
   const uint32_t e0 = bucket << 1;
+  int cross = 0; /* (delete locks: the owner tag is irrelevant) */
   { /* slot 0, lock free :126-135 */
     entry* b = &g->table[e0];
     if (s3_eq(b->pos, key) && b->idx >= 0) {
-      pool_release(g, b->idx);
+      if (local_idx(b->idx)) pool_release(g, b->idx); /* a shard releases only its own blocks */
       b->offset = 0;
       b->idx = -1;
       return 1;
@@ -258,11 +302,10 @@ static int hash_delete(ora_grid* g, s3 key) {
   uint32_t last = e0 + NUM_ENTRY_PER_BUCKET - 1;
   entry* head = &g->table[last];
   if (s3_eq(head->pos, key) && head->idx >= 0) { /* list head :137-152 */
-    if (g->locks[bucket] == 0) {
-      g->locks[bucket] = 1;
+    if (lock_take(g, bucket, 1, &cross)) {
       const uint32_t nidx = (uint32_t)(last + (int32_t)head->offset) & ENTRY_MASK;
       entry* nx = &g->table[nidx];
-      pool_release(g, head->idx);
+      if (local_idx(head->idx)) pool_release(g, head->idx);
       head->pos = nx->pos;
       head->offset = nx->offset ? (int16_t)(head->offset + nx->offset) : 0;
       head->idx = nx->idx;
@@ -277,10 +320,9 @@ static int hash_delete(ora_grid* g, s3 key) {
     const uint32_t cur = (uint32_t)(last + (int32_t)bl->offset) & ENTRY_MASK;
     entry* bc = &g->table[cur];
     if (s3_eq(bc->pos, key) && bc->idx >= 0) {
-      if (g->locks[bucket] == 0) {
-        g->locks[bucket] = 1;
+      if (lock_take(g, bucket, 1, &cross)) {
         bl->offset = bc->offset ? (int16_t)(bl->offset + bc->offset) : 0;
-        pool_release(g, bc->idx);
+        if (local_idx(bc->idx)) pool_release(g, bc->idx);
         bc->offset = 0;
         bc->idx = -1;
         return 1;
@@ -313,7 +355,7 @@ static int64_t voxel_addr(const ora_grid* g, s3 point, int64_t* entry_out) {
   const s3 block = point_to_block(point);
   const int64_t e = hash_find(g, block);
   if (entry_out) *entry_out = e;
-  if (e < 0) return -1;
+  if (e < 0 || !local_idx(g->table[e].idx)) return -1;
   const int off = offset_to_index(point.x & 7, point.y & 7, point.z & 7);
   return ((int64_t)g->table[e].idx << BLOCK_VOLUME_BITS) + off;
 }
@@ -395,7 +437,6 @@ static void make_params(const ora_grid* g, frame_params* P, const float K[4], in
   P->voxel = g->voxel; P->trunc = g->trunc; P->max_depth = max_depth;
 }
 
-/* voxel_tsdf.cu:104-147 block_allocate_kernel (one pixel); allocations sequential. */
 /* owner of block b among shard_count GPUs: hash of the 4^3-block brick; must match
  * tsdf_block_owner / brick_owner in the engine */
 uint32_t ora_block_owner(int16_t x, int16_t y, int16_t z, uint32_t shards) {
@@ -412,7 +453,21 @@ void ora_set_shard(ora_grid* g, int index, int count) {
   g->shard_count = count;
 }
 
-static void allocate_pixel(ora_grid* g, const frame_params* P, const float* depth, int x, int y) {
+static void ensure_range(ora_grid* g, int W, int H) {
+  if (g->range_cap < W * H) {
+    free(g->range);
+    g->range = (float*)malloc(sizeof(float) * (size_t)W * H);
+    g->range_cap = W * H;
+  }
+}
+
+/* voxel_tsdf.cu:104-147 block_allocate_kernel for one pixel: writes img_depth_to_range_ and hands
+ * every DDA sample's block whose 8 corners are all in view (is_block_visible<true>) to `visit`,
+ * with its candidate order (pixel raster index, then DDA step): Allocate in one volume, key
+ * collection in a sharded frame. */
+typedef void (*key_visit)(ora_grid* g, void* ctx, s3 key, uint64_t order);
+static void dda_pixel(ora_grid* g, const frame_params* P, const float* depth, int x, int y,
+                      key_visit visit, void* ctx) {
   const int idx = y * P->W + x;
   const float d = depth[idx];
   v3 ph = {(float)x, (float)y, 1.0f};
@@ -436,48 +491,35 @@ static void allocate_pixel(ora_grid* g, const frame_params* P, const float* dept
   for (int i = 0; i <= step_grid; ++i) {
     s3 p = {f2s(roundf(pos.x)), f2s(roundf(pos.y)), f2s(roundf(pos.z))};
     s3 b = point_to_block(p);
-    if (block_visible(P, b, 1) &&
-        (g->shard_count <= 1 ||
-         ora_block_owner(b.x, b.y, b.z, (uint32_t)g->shard_count) == (uint32_t)g->shard_index)) {
-      const int r2 = hash_allocate(g, b);
-      if (r2 != 0) g->st.last_num_candidates++;
-      if (r2 > 0) g->st.last_num_alloc++;
-    }
+    if (block_visible(P, b, 1)) visit(g, ctx, b, ((uint64_t)idx << 8) | (uint64_t)(i & 0xFF));
     pos.x += st.x; pos.y += st.y; pos.z += st.z;
   }
 }
+static void visit_allocate(ora_grid* g, void* ctx, s3 key, uint64_t order) {
+  const int r2 = hash_allocate(g, key);
+  if (r2 != 0) g->st.last_num_candidates++;
+  if (r2 > 0) g->st.last_num_alloc++;
+}
 
-int ora_integrate(ora_grid* g, const uint8_t* rgb, const float* depth, const float* ht,
-                  const float* lt, int W, int H, const float K[4], const float q[4],
-                  const float t[3], float max_depth) {
-  if (W <= 0 || H <= 0) return -1;
-  if (g->range_cap < W * H) {
-    free(g->range);
-    g->range = (float*)malloc(sizeof(float) * (size_t)W * H);
-    g->range_cap = W * H;
-  }
-  frame_params P;
-  make_params(g, &P, K, W, H, q, t, max_depth);
-  g->st.last_num_alloc = 0;
-  g->st.last_num_candidates = 0;
-  g->st.last_num_deleted = 0;
-  g->st.last_num_updated = 0;
-
-  /* ---- Allocate (voxel_tsdf.cu:377-386): sequential raster order, then ResetLocks ---- */
-  for (int y = 0; y < H; ++y)
-    for (int x = 0; x < W; ++x) allocate_pixel(g, &P, depth, x, y);
-  memset(g->locks, 0, NUM_BUCKET);
-
-  /* ---- GatherVisible (voxel_tsdf.cu:388-397, 82-102, 456-472): full-table scan ---- */
+/* GatherVisible (voxel_tsdf.cu:388-397, 82-102, 456-472: full-table scan, entry order) +
+ * UpdateTSDF (:149-205) + the min |tsdf| >= 0.9 test of space_carving_kernel (:207-230), over the
+ * blocks this grid holds voxels for. The carve candidates are returned in visible-list (= entry)
+ * order as the snapshot gather_visible_blocks_kernel took: positions in *cpos, entries in *cent
+ * (malloc'ed, caller frees). */
+static int update_and_carve_test(ora_grid* g, const frame_params* Pp, const uint8_t* rgb,
+                                 const float* depth, const float* ht, const float* lt, s3** cpos,
+                                 int32_t** cent) {
+  const frame_params P = *Pp;
+  const int W = P.W, H = P.H;
+  const float max_depth = P.max_depth;
   int nvis = 0;
   for (int e = 0; e < NUM_ENTRY; ++e) {
     const entry* b = &g->table[e];
-    if (b->idx < 0) continue;
+    if (!local_idx(b->idx)) continue;
     if (block_visible(&P, b->pos, 0)) g->vis[nvis++] = e;
   }
   g->st.last_num_visible = nvis;
 
-  /* ---- UpdateTSDF (voxel_tsdf.cu:149-205) ---- */
   s3* snap_pos = (s3*)malloc(sizeof(s3) * (nvis ? nvis : 1));
   int32_t* snap_idx = (int32_t*)malloc(sizeof(int32_t) * (nvis ? nvis : 1));
   for (int i = 0; i < nvis; ++i) { /* gather_visible_blocks_kernel copies the entries */
@@ -529,20 +571,190 @@ int ora_integrate(ora_grid* g, const uint8_t* rgb, const float* depth, const flo
   }
   g->st.last_num_updated = nupd;
 
-  /* ---- SpaceCarving (voxel_tsdf.cu:207-230, 483-488): deletes in entry order ---- */
+  /* space_carving_kernel's block minimum (deletes do not touch voxel values, so all minima can be
+   * taken before the first Delete) */
+  int nc = 0;
   for (int i = 0; i < nvis; ++i) {
     const int64_t base = (int64_t)snap_idx[i] << BLOCK_VOLUME_BITS;
     float mn = fabsf(g->tsdf[base]);
     for (int v = 1; v < BLOCK_VOLUME; ++v) mn = fminf(mn, fabsf(g->tsdf[base + v]));
     if (mn >= 0.9f) {
-      if (hash_delete(g, snap_pos[i]) > 0) g->st.last_num_deleted++;
+      snap_pos[nc] = snap_pos[i];
+      snap_idx[nc] = g->vis[i];
+      ++nc;
     }
   }
+  *cpos = snap_pos;
+  *cent = snap_idx;
+  return nc;
+}
+
+int ora_integrate(ora_grid* g, const uint8_t* rgb, const float* depth, const float* ht,
+                  const float* lt, int W, int H, const float K[4], const float q[4],
+                  const float t[3], float max_depth) {
+  if (W <= 0 || H <= 0) return -1;
+  if (g->shard_count > 1) return -2; /* a shard integrates through ora_shard_keys/_update/_delete */
+  ensure_range(g, W, H);
+  frame_params P;
+  make_params(g, &P, K, W, H, q, t, max_depth);
+  g->st.last_num_alloc = 0;
+  g->st.last_num_candidates = 0;
+  g->st.last_num_deleted = 0;
+  g->st.last_num_updated = 0;
+  g->st.last_cross_losses = 0;
+
+  /* ---- Allocate (voxel_tsdf.cu:377-386): sequential raster order, then ResetLocks ---- */
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x) dda_pixel(g, &P, depth, x, y, visit_allocate, NULL);
   memset(g->locks, 0, NUM_BUCKET);
-  free(snap_pos);
-  free(snap_idx);
+
+  /* ---- GatherVisible + UpdateTSDF + SpaceCarving (voxel_tsdf.cu:388-397, 474-488) ---- */
+  s3* cpos;
+  int32_t* cent;
+  const int nc = update_and_carve_test(g, &P, rgb, depth, ht, lt, &cpos, &cent);
+  for (int i = 0; i < nc; ++i) /* deletes in entry order, then ResetLocks */
+    if (hash_delete(g, cpos[i]) > 0) g->st.last_num_deleted++;
+  memset(g->locks, 0, NUM_BUCKET);
+  free(cpos);
+  free(cent);
   g->st.frames++;
   return 0;
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Sharded frame (not in the reference), the engine's tsdf_integrate_shard_* in three
+ * phases around the two exchanges. Every shard keeps the whole hash index, so the union of the
+ * shards is the one-volume TSDFGrid::Integrate above, block for block and voxel for voxel:
+ *   ora_shard_keys   : the DDA over pixel rows [row_lo, row_hi) -> the fully visible keys missing
+ *                      from the index, each once with its smallest candidate order;
+ *   ora_shard_update : Allocate of the union of every shard's keys in candidate order (a key's
+ *                      first attempt decides it: a lock it lost stays taken for the launch), pool
+ *                      blocks only for owned keys; then visibility, update and the carve test of
+ *                      the owned blocks -> carve candidates;
+ *   ora_shard_delete : Delete of the union of every shard's candidates in entry order.
+ * --------------------------------------------------------------------------------------------- */
+typedef struct {
+  uint64_t* key;   /* packed (x, y, z) | 1 << 48 */
+  uint64_t* order;
+  int64_t n, cap;
+} keylist;
+static uint64_t pack_s3(s3 k) {
+  return (uint64_t)(uint16_t)k.x | ((uint64_t)(uint16_t)k.y << 16) | ((uint64_t)(uint16_t)k.z << 32) |
+         (1ull << 48);
+}
+static void visit_collect(ora_grid* g, void* ctx, s3 key, uint64_t order) {
+  keylist* L = (keylist*)ctx;
+  if (hash_find(g, key) >= 0) return; /* already in the index (any shard's) */
+  if (L->n == L->cap) {
+    L->cap = L->cap ? 2 * L->cap : 4096;
+    L->key = (uint64_t*)realloc(L->key, sizeof(uint64_t) * (size_t)L->cap);
+    L->order = (uint64_t*)realloc(L->order, sizeof(uint64_t) * (size_t)L->cap);
+  }
+  L->key[L->n] = pack_s3(key);
+  L->order[L->n] = order;
+  L->n++;
+}
+typedef struct { uint64_t a, b; int64_t i; } triple;
+static int cmp_triple(const void* x, const void* y) {
+  const triple* p = (const triple*)x;
+  const triple* q = (const triple*)y;
+  if (p->a != q->a) return p->a < q->a ? -1 : 1;
+  if (p->b != q->b) return p->b < q->b ? -1 : 1;
+  return 0;
+}
+
+int64_t ora_shard_keys(ora_grid* g, const float* depth, int W, int H, const float K[4],
+                       const float q[4], const float t[3], float max_depth, int row_lo, int row_hi,
+                       int16_t* keys_out, uint64_t* orders_out, int64_t capacity) {
+  if (W <= 0 || H <= 0) return -1;
+  ensure_range(g, W, H);
+  frame_params P;
+  make_params(g, &P, K, W, H, q, t, max_depth);
+  keylist L = {NULL, NULL, 0, 0};
+  if (row_lo < 0) row_lo = 0;
+  if (row_hi > H) row_hi = H;
+  for (int y = row_lo; y < row_hi; ++y)
+    for (int x = 0; x < W; ++x) dda_pixel(g, &P, depth, x, y, visit_collect, &L);
+  /* unique keys, smallest order each */
+  triple* s = (triple*)malloc(sizeof(triple) * (size_t)(L.n ? L.n : 1));
+  for (int64_t i = 0; i < L.n; ++i) s[i] = (triple){L.key[i], L.order[i], i};
+  qsort(s, (size_t)L.n, sizeof(triple), cmp_triple);
+  int64_t n = 0;
+  for (int64_t i = 0; i < L.n; ++i) {
+    if (i > 0 && s[i].a == s[i - 1].a) continue;
+    if (n < capacity) {
+      keys_out[3 * n + 0] = (int16_t)(s[i].a & 0xFFFF);
+      keys_out[3 * n + 1] = (int16_t)((s[i].a >> 16) & 0xFFFF);
+      keys_out[3 * n + 2] = (int16_t)((s[i].a >> 32) & 0xFFFF);
+      orders_out[n] = s[i].b;
+    }
+    ++n;
+  }
+  free(s);
+  free(L.key);
+  free(L.order);
+  return n;
+}
+
+int64_t ora_shard_update(ora_grid* g, const int16_t* keys, const uint64_t* orders, int64_t n,
+                         const uint8_t* rgb, const float* depth, const float* ht, const float* lt,
+                         int W, int H, const float K[4], const float q[4], const float t[3],
+                         float max_depth, int16_t* cand_pos, int32_t* cand_entry, int64_t cand_cap) {
+  if (W <= 0 || H <= 0 || n < 0) return -1;
+  ensure_range(g, W, H);
+  frame_params P;
+  make_params(g, &P, K, W, H, q, t, max_depth);
+  for (int y = 0; y < H; ++y) /* img_depth_to_range_ of every pixel (block_allocate_kernel :120) */
+    for (int x = 0; x < W; ++x) {
+      v3 ph = {(float)x, (float)y, 1.0f};
+      g->range[y * W + x] = v3_norm(intr_mul(P.Kinv, ph));
+    }
+  g->st.last_num_alloc = 0;
+  g->st.last_num_candidates = 0;
+  g->st.last_num_deleted = 0;
+  g->st.last_num_updated = 0;
+  g->st.last_cross_losses = 0;
+  /* ---- Allocate of the union in candidate order, then ResetLocks ---- */
+  triple* s = (triple*)malloc(sizeof(triple) * (size_t)(n ? n : 1));
+  for (int64_t i = 0; i < n; ++i) s[i] = (triple){orders[i], (uint64_t)i, i};
+  qsort(s, (size_t)n, sizeof(triple), cmp_triple);
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t k = s[i].i;
+    const s3 key = {keys[3 * k], keys[3 * k + 1], keys[3 * k + 2]};
+    visit_allocate(g, NULL, key, orders[k]);
+  }
+  free(s);
+  memset(g->locks, 0, NUM_BUCKET);
+  /* ---- visibility, update, carve test of the owned blocks ---- */
+  s3* cpos;
+  int32_t* cent;
+  const int nc = update_and_carve_test(g, &P, rgb, depth, ht, lt, &cpos, &cent);
+  for (int i = 0; i < nc && i < cand_cap; ++i) {
+    cand_pos[3 * i + 0] = cpos[i].x;
+    cand_pos[3 * i + 1] = cpos[i].y;
+    cand_pos[3 * i + 2] = cpos[i].z;
+    cand_entry[i] = cent[i];
+  }
+  free(cpos);
+  free(cent);
+  return nc;
+}
+
+void ora_shard_delete(ora_grid* g, const int16_t* cand_pos, const int32_t* cand_entry, int64_t n) {
+  triple* s = (triple*)malloc(sizeof(triple) * (size_t)(n ? n : 1));
+  for (int64_t i = 0; i < n; ++i) s[i] = (triple){(uint64_t)(uint32_t)cand_entry[i], 0, i};
+  qsort(s, (size_t)n, sizeof(triple), cmp_triple);
+  int deleted = 0;
+  for (int64_t i = 0; i < n; ++i) { /* Delete in entry order (the union of the visible lists) */
+    const int64_t k = s[i].i;
+    const s3 key = {cand_pos[3 * k], cand_pos[3 * k + 1], cand_pos[3 * k + 2]};
+    const int32_t f0 = g->free_count;
+    if (hash_delete(g, key) > 0 && g->free_count > f0) ++deleted; /* owned blocks released */
+  }
+  memset(g->locks, 0, NUM_BUCKET);
+  free(s);
+  g->st.last_num_deleted = deleted;
+  g->st.frames++;
 }
 
 /* voxel_tsdf.cu:232-307 ray_cast_kernel */
@@ -635,7 +847,7 @@ int64_t ora_query(const ora_grid* g, const float* bounds, float* out, int64_t ca
     int64_t k = 0;
     for (int e = 0; e < NUM_ENTRY; ++e) {
       const entry* b = &g->table[e];
-      if (b->idx < 0) continue;
+      if (!local_idx(b->idx)) continue;
       const s3 vg = block_to_point(b->pos);
       if (bounds) {
         const int inside = vg.x >= bb[0] && vg.y >= bb[2] && vg.z >= bb[4] &&
@@ -779,7 +991,7 @@ static const int8_t kOraMcTri[256][3 * TSDF_MC_MAX_TRI] = TSDF_MC_TRI_INIT;
 static int block_selected(const ora_grid* g, s3 blk, const int16_t* bb, int64_t* e_out) {
   const int64_t e = hash_find(g, blk);
   if (e_out) *e_out = e;
-  if (e < 0) return 0;
+  if (e < 0 || !local_idx(g->table[e].idx)) return 0;
   if (!bb) return 1;
   const s3 vg = block_to_point(blk);
   return vg.x >= bb[0] && vg.y >= bb[2] && vg.z >= bb[4] && vg.x + BLOCK_LEN - 1 <= bb[1] &&
@@ -799,7 +1011,7 @@ int64_t ora_extract_mesh(const ora_grid* g, const float* bounds, float missing, 
   int64_t n = 0;
   for (int e = 0; e < NUM_ENTRY; ++e) {
     const entry* b = &g->table[e];
-    if (b->idx < 0 || !block_selected(g, b->pos, bb, NULL)) continue;
+    if (!local_idx(b->idx) || !block_selected(g, b->pos, bb, NULL)) continue;
     const s3 base = block_to_point(b->pos);
     for (int lz = -1; lz < BLOCK_LEN; ++lz)
       for (int ly = -1; ly < BLOCK_LEN; ++ly)

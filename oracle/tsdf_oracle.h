@@ -36,15 +36,37 @@ typedef struct ora_stats {
   int32_t last_num_deleted;   /* successful block deletions (space carving) of the last integrate */
   int32_t last_num_candidates;/* unique missing keys attempted in the last allocate launch */
   int32_t active_blocks;      /* NUM_BLOCK - free */
+  int32_t last_cross_losses;  /* sharded grids: keys of the last allocate launch that lost a bucket
+                                 lock to a key another shard owns */
+  int32_t pool_exhausted;     /* sticky: an owned allocation found no free block */
 } ora_stats;
 
 /* voxel_tsdf.cu:309 TSDFGrid(voxel_size, truncation); num_block_bits replaces NUM_BLOCK_BITS=18
  * (voxel_mem.cuh:11) so tests can run small pools. */
 ora_grid* ora_create(float voxel_size, float truncation, int num_block_bits);
 void ora_destroy(ora_grid* g);
-/* Spatial sharding (not in the reference): the grid allocates only blocks whose
- * 4^3-block brick hashes to shard index (ora_block_owner == index). count <= 1: unsharded. */
+/* Spatial sharding (not in the reference): the grid becomes shard
+ * `index` of `count` of one volume. It keeps the whole hash index (entries of blocks another shard
+ * owns carry idx ORA_FOREIGN = 0x7FFFFFFF: occupied for Allocate / Delete, missing for readers)
+ * and holds voxels only for the blocks whose 4^3-block brick hashes to it (ora_block_owner). A
+ * shard integrates through the three phases below, with the union of every shard's keys and carve
+ * candidates between them; ora_integrate refuses it. count <= 1: one volume. */
 void ora_set_shard(ora_grid* g, int index, int count);
+/* phase 1: DDA over pixel rows [row_lo, row_hi): unique fully visible keys missing from the index
+ * with their smallest candidate order ((y W + x) << 8 | step); returns the count (outputs filled up
+ * to capacity). */
+int64_t ora_shard_keys(ora_grid* g, const float* depth, int W, int H, const float K[4],
+                       const float q[4], const float t[3], float max_depth, int row_lo, int row_hi,
+                       int16_t* keys_out, uint64_t* orders_out, int64_t capacity);
+/* phase 2: Allocate of the union of all shards' keys in candidate order, then visibility, update
+ * and carve test of the owned blocks; returns the owned carve candidates (entry order, outputs
+ * filled up to cand_cap). */
+int64_t ora_shard_update(ora_grid* g, const int16_t* keys, const uint64_t* orders, int64_t n,
+                         const uint8_t* rgb, const float* depth, const float* ht, const float* lt,
+                         int W, int H, const float K[4], const float q[4], const float t[3],
+                         float max_depth, int16_t* cand_pos, int32_t* cand_entry, int64_t cand_cap);
+/* phase 3: Delete of the union of all shards' carve candidates in entry order. */
+void ora_shard_delete(ora_grid* g, const int16_t* cand_pos, const int32_t* cand_entry, int64_t n);
 /* Marching cubes over the selected blocks (bounds as ora_query, NULL = all); 9 floats per
  * triangle into out (up to capacity triangles); returns the triangle count. See the .c. */
 int64_t ora_extract_mesh(const ora_grid* g, const float* bounds, float missing, int min_weight,

@@ -29,6 +29,8 @@ class OraStats(C.Structure):
         ("last_num_deleted", C.c_int32),
         ("last_num_candidates", C.c_int32),
         ("active_blocks", C.c_int32),
+        ("last_cross_losses", C.c_int32),
+        ("pool_exhausted", C.c_int32),
     ]
 
 
@@ -68,6 +70,13 @@ def lib():
         L.ora_pool_set_weight.argtypes = [P, C.c_int32, C.c_uint8]
         L.ora_pool_get_weights.argtypes = [P, C.c_int32, P]
         L.ora_set_shard.argtypes = [P, C.c_int, C.c_int]
+        L.ora_shard_keys.restype = C.c_int64
+        L.ora_shard_keys.argtypes = [P, P, C.c_int, C.c_int, P, P, P, C.c_float, C.c_int, C.c_int, P, P,
+                                     C.c_int64]
+        L.ora_shard_update.restype = C.c_int64
+        L.ora_shard_update.argtypes = [P, P, P, C.c_int64, P, P, P, P, C.c_int, C.c_int, P, P, P,
+                                       C.c_float, P, P, C.c_int64]
+        L.ora_shard_delete.argtypes = [P, P, P, C.c_int64]
         L.ora_extract_mesh.restype = C.c_int64
         L.ora_extract_mesh.argtypes = [P, P, C.c_float, C.c_int, P, C.c_int64]
         L.ora_block_owner.restype = C.c_uint32
@@ -138,6 +147,50 @@ class OracleGrid:
                                  _p(t), max_depth)
         if rc != 0:
             raise RuntimeError(f"ora_integrate -> {rc}")
+
+    # --- sharded frame (the engine's tsdf_integrate_shard_* in three phases) ---
+    @staticmethod
+    def _f32(*arrs):
+        return [None if a is None else np.ascontiguousarray(a, dtype=np.float32) for a in arrs]
+
+    def shard_keys(self, depth, K, q, t, max_depth, row_lo, row_hi):
+        """Phase 1: DDA over rows [row_lo, row_hi) -> (keys (n, 3) int16, orders (n,) uint64)."""
+        depth, K, q, t = self._f32(depth, K, q, t)
+        H, W = depth.shape
+        cap = max(1, W * max(0, min(row_hi, H) - max(row_lo, 0)) * 4)
+        keys = np.zeros((cap, 3), np.int16)
+        orders = np.zeros(cap, np.uint64)
+        n = lib().ora_shard_keys(self.h, _p(depth), W, H, _p(K), _p(q), _p(t), max_depth, row_lo, row_hi,
+                                 _p(keys), _p(orders), cap)
+        if n > cap:
+            keys = np.zeros((n, 3), np.int16)
+            orders = np.zeros(n, np.uint64)
+            n = lib().ora_shard_keys(self.h, _p(depth), W, H, _p(K), _p(q), _p(t), max_depth, row_lo,
+                                     row_hi, _p(keys), _p(orders), n)
+        return keys[:n].copy(), orders[:n].copy()
+
+    def shard_update(self, keys, orders, rgb, depth, ht, lt, max_depth, K, q, t):
+        """Phase 2: Allocate the union of the shards' keys, integrate the owned blocks ->
+        (carve candidate positions (m, 3) int16, their entries (m,) int32)."""
+        keys = np.ascontiguousarray(keys, dtype=np.int16).reshape(-1, 3)
+        orders = np.ascontiguousarray(orders, dtype=np.uint64)
+        rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+        depth, ht, lt, K, q, t = self._f32(depth, ht, lt, K, q, t)
+        H, W = depth.shape
+        cap = NUM_ENTRY
+        cpos = np.zeros((cap, 3), np.int16)
+        cent = np.zeros(cap, np.int32)
+        m = lib().ora_shard_update(self.h, _p(keys), _p(orders), keys.shape[0], _p(rgb), _p(depth), _p(ht),
+                                   _p(lt), W, H, _p(K), _p(q), _p(t), max_depth, _p(cpos), _p(cent), cap)
+        if m < 0:
+            raise RuntimeError("ora_shard_update failed")
+        return cpos[:m].copy(), cent[:m].copy()
+
+    def shard_delete(self, cand_pos, cand_entry):
+        """Phase 3: Delete the union of the shards' carve candidates (entry order)."""
+        p = np.ascontiguousarray(cand_pos, dtype=np.int16).reshape(-1, 3)
+        e = np.ascontiguousarray(cand_entry, dtype=np.int32)
+        lib().ora_shard_delete(self.h, _p(p), _p(e), e.shape[0])
 
     def raycast(self, K, W, H, q, t, max_depth):
         rgba = np.zeros((H, W, 4), np.uint8)

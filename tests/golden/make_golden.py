@@ -34,10 +34,15 @@ KAT = {
         {"key": [61, 16, 170], "bucket": (1 << 21) - 1},
         {"key": [63, 171, 45], "bucket": (1 << 21) - 1},
     ],
-    "collision": {  # voxel_hash_test.cu:137-155: one key per Allocate launch
-        "launches": [[[33, 180, 42]], [[61, 16, 170]], [[63, 171, 45]]],
+    "collision": {  # voxel_hash_test.cu:128-180: block_pos[0..3] -- three keys of the last bucket
+        # and {0, 0, 0} -- go to ONE Allocate<<<1, 4>>> launch (all four keys), three times
+        # (:139, :145, :151), with ResetLocks after each; the active count is 2, 3, 4 (:143, :149,
+        # :155) whatever order the four threads run in. Then the first voxel of each block gets
+        # rgb = weight = i (:157-161) and is retrieved (:171-179).
+        "keys": [[33, 180, 42], [61, 16, 170], [63, 171, 45], [0, 0, 0]],
+        "launches": 3,
         "active_after_each": [2, 3, 4],
-        "preallocated": [[0, 0, 0]],
+        "assign_rgbw": [[i, i, i, i] for i in range(4)],
     },
     "single": {  # voxel_hash_test.cu:56-92
         "allocate": [1, 1, 1], "retrieve_point": [8, 8, 8], "expect_block": [1, 1, 1],

@@ -1,10 +1,13 @@
 """Multi-rank (world_size 2, gloo, CPU) coverage of the N>1 path.
 
  - the bench's rank bookkeeping (tsdf_amd.dist): max-over-ranks timing, whole-job units, stream
-   offsets, shard assignment, and the routed-frame key exchange (all-to-all of the outboxes);
- - spatial sharding semantics on the CPU oracle: two shard engines fed the same frames own
-   disjoint block sets, each block lives on its owner, and the union equals the unsharded volume
-   with bit-identical voxels (integration of a block reads only its own state + the frame).
+   offsets, shard assignment, the slot all-gather of sharded frames, the ragged row gather;
+ - the sharded-volume protocol itself on the CPU oracle (tests/_shards.py restates the engine's
+   tsdf_integrate_shard_* phases): each rank is one shard of one volume, runs the DDA over its band
+   of pixel rows, and the ranks all-gather their new keys and their carve candidates over gloo.
+   Every rank's hash index equals the unsharded table, every block it holds equals the unsharded
+   block, and the union of the ranks' blocks is the unsharded volume -- at a size where keys of
+   the two ranks contend for bucket locks (cross-shard lock losses > 0, asserted).
 """
 import os
 import socket
@@ -13,7 +16,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-W, H, VOXEL, TRUNC, NB, FRAMES = 64, 48, 0.01, 0.04, 13, 4
+W, H, VOXEL, TRUNC, NB, FRAMES = 160, 120, 0.005, 0.03, 15, 3
 
 
 def _free_port():
@@ -24,17 +27,6 @@ def _free_port():
     return p
 
 
-def _live(ora):
-    d = ora.dump()
-    live = np.flatnonzero(d["entry_idx"] >= 0)
-    idx = d["entry_idx"][live]
-    pos = d["entry_pos"][live, :3]
-    order = np.lexsort(pos.T[::-1])
-    tsdf = d["tsdf"].reshape(-1, 512)[idx][order]
-    rgbw = d["rgbw"].reshape(-1, 512, 4)[idx][order]
-    return pos[order], tsdf, rgbw
-
-
 def _worker(rank, world, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
@@ -42,10 +34,12 @@ def _worker(rank, world, port):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (os.path.join(root, "tests"), os.path.join(root, "disinfect-slam_amd")):
         sys.path.insert(0, p)
+    import torch
     import torch.distributed as dist
     from tsdf_amd import dist as tdist
     from tsdf_amd import synth
-    from _oracle import OracleGrid, block_owner
+    from _oracle import OracleGrid, lib
+    from _shards import assert_shard_matches, row_slices
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -54,18 +48,16 @@ def _worker(rank, world, port):
         assert tdist.max_over_ranks(1.5 + rank) == 1.5 + world - 1
         assert tdist.sum_over_ranks([1, rank]) == [world, sum(range(world))]
         assert tdist.units("streams", 300, world) == 300 * world
-        assert tdist.units("sharded", 300, world) == 300
-        assert tdist.shard_of("sharded", rank, world) == (rank, world)
+        for mode in ("sharded", "routed"):
+            assert tdist.units(mode, 300, world) == 300
+            assert tdist.shard_of(mode, rank, world) == (rank, world)
         assert tdist.shard_of("streams", rank, world) == (0, 1)
-        assert tdist.units("routed", 300, world) == 300
-        assert tdist.shard_of("routed", rank, world) == (rank, world)
-        # routed frames' key exchange (bench --mode routed): inbox slot s = rank s's outbox slot rank
-        import torch
-        slot = 48
-        out = torch.stack([torch.full((slot,), rank * world + j, dtype=torch.uint8) for j in range(world)])
-        inbox = tdist.route_exchange(out, torch.empty_like(out))
+        # the exchange of sharded frames: slot all-gather in rank order
+        slot = torch.full((48,), rank + 7, dtype=torch.uint8)
+        out = torch.empty((world, 48), dtype=torch.uint8)
+        tdist.all_gather_slots(slot, out)
         for src in range(world):
-            assert bool((inbox[src] == src * world + rank).all()), (rank, src, inbox[src][:4])
+            assert bool((out[src] == src + 7).all()), (rank, src, out[src][:4])
         # render replicas (tsdf_amd.dist.render_sharded): all-gather-v of ragged record rows, rank order
         rows = np.full((rank + 1, 6160), rank + 1, np.uint8)
         rows[:, 0] = np.arange(rank + 1)
@@ -79,44 +71,45 @@ def _worker(rank, world, port):
         dist.all_gather_object(offs, tdist.stream_offset("streams", rank, world))
         assert len(set(offs)) == world
 
+        # ---- the sharded volume, one shard per rank ----
         cam = synth.camera(W, H, synth.TUM_FR1)
-        shard = OracleGrid(VOXEL, TRUNC, NB, shard_index=rank, shard_count=world)
+        shard = OracleGrid(VOXEL, TRUNC, NB)
+        lib().ora_set_shard(shard.h, rank, world)
+        full = OracleGrid(VOXEL, TRUNC, NB)  # every rank checks its own shard against one volume
+        lo, hi = row_slices(H, world)[rank]
+        cross = 0
         for f in range(FRAMES):
-            fr = synth.render(cam, 2 * f)
-            shard.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], 4.0, cam.K, fr["q"], fr["t"])
-        pos, tsdf, rgbw = _live(shard)
-        shard.close()
-        assert all(block_owner(*map(int, p), world) == rank for p in pos)
+            fr = synth.render(cam, f)
+            full.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], 4.0, cam.K, fr["q"], fr["t"])
+            keys, orders = shard.shard_keys(fr["depth"], cam.K, fr["q"], fr["t"], 4.0, lo, hi)
+            parts = [None] * world
+            dist.all_gather_object(parts, (keys, orders))  # the key all-gather
+            cpos, cent = shard.shard_update(np.concatenate([p[0] for p in parts]),
+                                            np.concatenate([p[1] for p in parts]), fr["rgb"],
+                                            fr["depth"], fr["ht"], fr["lt"], 4.0, cam.K, fr["q"], fr["t"])
+            cands = [None] * world
+            dist.all_gather_object(cands, (cpos, cent))  # the carve-candidate all-gather
+            shard.shard_delete(np.concatenate([c[0] for c in cands]), np.concatenate([c[1] for c in cands]))
+            cross += shard.stats()["last_cross_losses"]
+        fd = full.dump()
+        mine = assert_shard_matches(shard.dump(), fd, tag=f"rank {rank}")
+        assert mine and cross > 0, (len(mine), cross)
         # whole-volume Query of the sharded volume = union of the shard queries (SURVEY 8e gather)
-        qshard = OracleGrid(VOXEL, TRUNC, NB, shard_index=rank, shard_count=world)
-        for f in range(FRAMES):
-            fr = synth.render(cam, 2 * f)
-            qshard.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], 4.0, cam.K, fr["q"], fr["t"])
-        union = tdist.gather_query(qshard.query(None))
-        qshard.close()
-        sets = tdist.gather_block_sets(pos)
-        tsdfs = [None] * world
-        dist.all_gather_object(tsdfs, (tsdf, rgbw))
+        union = tdist.gather_query(shard.query(None))
+        fq = full.query(None)
+        sets = [None] * world
+        dist.all_gather_object(sets, sorted(mine))
         if rank == 0:
-            keys = [set(map(tuple, s.tolist())) for s in sets]
+            keys = [set(s) for s in sets]
             assert not (keys[0] & keys[1])
-            full = OracleGrid(VOXEL, TRUNC, NB)
-            for f in range(FRAMES):
-                fr = synth.render(cam, 2 * f)
-                full.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], 4.0, cam.K, fr["q"], fr["t"])
-            fpos, ftsdf, frgbw = _live(full)
-            fq = full.query(None)
-            full.close()
+            idx = fd["entry_idx"]
+            live = fd["entry_pos"][(idx >= 0), :3]
+            assert keys[0] | keys[1] == {tuple(map(int, p)) for p in live}
             srt = lambda a: a[np.lexsort(a.view(np.uint32).T[::-1])]
             assert union.shape == fq.shape and fq.shape[0] > 0
             np.testing.assert_array_equal(srt(union).view(np.uint32), srt(fq).view(np.uint32))
-            fkeys = list(map(tuple, fpos.tolist()))
-            assert set(fkeys) == keys[0] | keys[1]
-            where = {k: i for i, k in enumerate(fkeys)}
-            for s, (t, c) in zip(sets, tsdfs):
-                sel = [where[tuple(p)] for p in s.tolist()]
-                np.testing.assert_array_equal(t.view(np.uint32), ftsdf[sel].view(np.uint32))
-                np.testing.assert_array_equal(c, frgbw[sel])
+        shard.close()
+        full.close()
         dist.barrier()
     finally:
         dist.destroy_process_group()

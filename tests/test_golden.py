@@ -6,6 +6,7 @@ outputs, which pins the restatement against drift (parity unpinned vs the CUDA r
 which cannot run here -- SURVEY.md 8c).
 """
 import hashlib
+import itertools
 import json
 import os
 
@@ -24,14 +25,24 @@ def test_reference_kat_vectors():
     kat = json.load(open(os.path.join(GOLD, "kat_reference.json")))
     for h in kat["hash"]:
         assert hash_block(*h["key"]) == h["bucket"]
-    g = OracleGrid(0.01, 0.06, num_block_bits=12)
-    try:
-        g.hash_allocate(kat["collision"]["preallocated"])
-        for keys, n in zip(kat["collision"]["launches"], kat["collision"]["active_after_each"]):
-            g.hash_allocate(keys)
-            assert g.num_active_blocks() == n
-    finally:
-        g.close()
+    col = kat["collision"]
+    keys = np.asarray(col["keys"], np.int16)
+    # the reference's four threads race; the canonical linearisation must give 2 -> 3 -> 4 for
+    # every order of the launch's four keys
+    for perm in itertools.permutations(range(4)):
+        g = OracleGrid(0.01, 0.06, num_block_bits=12)
+        try:
+            for launch in range(col["launches"]):
+                g.hash_allocate(keys[list(perm)])  # all four keys, one Allocate launch
+                assert g.num_active_blocks() == col["active_after_each"][launch], (perm, launch)
+            points = keys.astype(np.int32) * 8  # the first voxel of each block (:157-161)
+            rgbw = np.asarray(col["assign_rgbw"], np.uint8)
+            assert g.hash_assign(points, rgbw) == 0
+            r = g.hash_retrieve(points)
+            np.testing.assert_array_equal(r["rgbw"], rgbw)
+            np.testing.assert_array_equal(r["block_pos_off"][:, :3], keys)
+        finally:
+            g.close()
 
 
 def run_oracle(G):

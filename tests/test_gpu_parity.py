@@ -171,35 +171,6 @@ def test_pool_exhaustion_is_reported():
         eng.close(), ora.close()
 
 
-def test_sharded_engines_match_sharded_oracles():
-    """SURVEY 8e option 1: two shard engines on one GPU (shard_index 0/1 of 2) fed the same frames
-    match the two oracle shards bit for bit (entries, pool, voxels)."""
-    import tsdf_amd
-    from tsdf_amd import synth
-    from _oracle import OracleGrid
-    W, H = 96, 72
-    cam = synth.camera(W, H, synth.TUM_FR1)
-    pairs = [(tsdf_amd.Engine(0.01, 0.04, max_width=W, max_height=H, num_block_bits=13,
-                              shard_index=i, shard_count=2),
-              OracleGrid(0.01, 0.04, 13, shard_index=i, shard_count=2)) for i in range(2)]
-    try:
-        for f in range(5):
-            fr = synth.render(cam, 2 * f)
-            for eng, ora in pairs:
-                eng.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K,
-                              tsdf_amd.SE3(fr["q"], fr["t"]), 4.0)
-                ora.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], 4.0, cam.K, fr["q"], fr["t"])
-        for i, (eng, ora) in enumerate(pairs):
-            compare(eng, ora, tag=f"shard {i}")
-            d = eng.dump(pool=False)
-            pos = d["entry_pos"][d["entry_idx"] >= 0, :3]
-            assert pos.shape[0] > 50
-            assert all(tsdf_amd.block_owner(*map(int, p), 2) == i for p in pos)
-    finally:
-        for eng, ora in pairs:
-            eng.close(), ora.close()
-
-
 @pytest.mark.parametrize("min_weight,bounded", [(0, False), (1, False), (1, True)])
 def test_marching_cubes_matches_oracle(min_weight, bounded):
     """GPU marching cubes (tsdf_extract_mesh) == the oracle's restatement, bit for bit and in

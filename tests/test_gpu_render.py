@@ -1,5 +1,9 @@
 """Raycast of a spatially sharded volume (SURVEY.md 8e raycast composite).
 
+The sharded volumes here are tsdf_amd.ShardGroup volumes (one GPU, exchanged slots), whose union is
+the unsharded volume (tests/test_gpu_sharded.py); the two-process test runs the same frames
+through tsdf_amd.dist.integrate_sharded over gloo.
+
 Every shard packs the blocks a raycast of the render camera can read (tsdf_render_blocks, a
 conservative view-pyramid selection), the union is imported into a scratch replica engine
 (tsdf_import_blocks) and rendered there with the unchanged raycast kernel. The images must equal the
@@ -15,12 +19,12 @@ W, H, VOXEL, TRUNC = 96, 72, 0.01, 0.04
 
 
 def _engines(G, nb_bits=13, w=W, h=H, voxel=VOXEL, trunc=TRUNC):
+    """(unsharded engine, G-shard group of one volume or None, replica engine)."""
     import tsdf_amd
     full = tsdf_amd.Engine(voxel, trunc, max_width=w, max_height=h, num_block_bits=nb_bits)
-    shards = [tsdf_amd.Engine(voxel, trunc, max_width=w, max_height=h, num_block_bits=nb_bits,
-                              shard_index=i, shard_count=G) for i in range(G)]
+    group = tsdf_amd.ShardGroup(G, voxel, trunc, max_width=w, max_height=h, num_block_bits=nb_bits) if G else None
     replica = tsdf_amd.Engine(voxel, trunc, max_width=w, max_height=h, num_block_bits=nb_bits)
-    return full, shards, replica
+    return full, group, replica
 
 
 def _integrate(engines, cam, frames, stride=2):
@@ -106,9 +110,10 @@ def test_sharded_render_equals_unsharded(G):
 
     from tsdf_amd import synth
     cam = synth.camera(W, H, synth.TUM_FR1)
-    full, shards, replica = _engines(G)
+    full, group, replica = _engines(G)
+    shards = group.engines
     try:
-        _integrate([full] + shards, cam, 6)
+        _integrate([full, group], cam, 6)
         for K, pose in _views(cam):
             parts = [e.render_blocks(K, W, H, pose, 4.0, device=True) for e in shards]
             assert sum(p.shape[0] for p in parts) == full.render_blocks(K, W, H, pose, 4.0).shape[0]
@@ -119,7 +124,7 @@ def test_sharded_render_equals_unsharded(G):
             np.testing.assert_array_equal(got[0], exp[0])
             np.testing.assert_array_equal(got[1], exp[1])
     finally:
-        _close(full, replica, *shards)
+        _close(full, replica, group)
 
 
 def test_sharded_render_bench_scale():
@@ -129,9 +134,10 @@ def test_sharded_render_bench_scale():
     from tsdf_amd import synth
     w, h, G = 640, 480, 8
     cam = synth.camera(w, h, synth.TUM_FR1)
-    full, shards, replica = _engines(G, nb_bits=16, w=w, h=h, voxel=0.005, trunc=0.03)
+    full, group, replica = _engines(G, nb_bits=16, w=w, h=h, voxel=0.005, trunc=0.03)
+    shards = group.engines
     try:
-        _integrate([full] + shards, cam, 12, stride=3)
+        _integrate([full, group], cam, 12, stride=3)
         fr = synth.render(cam, 20)
         import tsdf_amd
         pose = tsdf_amd.SE3(fr["q"], fr["t"])
@@ -143,7 +149,7 @@ def test_sharded_render_bench_scale():
         np.testing.assert_array_equal(got[0], exp[0])
         np.testing.assert_array_equal(got[1], exp[1])
     finally:
-        _close(full, replica, *shards)
+        _close(full, replica, group)
 
 
 def test_replica_random_views():
@@ -196,9 +202,10 @@ def test_sharded_mesh_equals_unsharded(G):
 
     from tsdf_amd import synth
     cam = synth.camera(W, H, synth.TUM_FR1)
-    full, shards, replica = _engines(G)
+    full, group, replica = _engines(G)
+    shards = group.engines
     try:
-        _integrate([full] + shards, cam, 6)
+        _integrate([full, group], cam, 6)
         xyz = full.query(None).view(np.float32).reshape(-1, 4)[:, :3]
         lo, hi = np.percentile(xyz, 20, axis=0), np.percentile(xyz, 80, axis=0)
         box = np.array([lo[0], hi[0], lo[1], hi[1], lo[2], hi[2]], np.float32)
@@ -218,7 +225,7 @@ def test_sharded_mesh_equals_unsharded(G):
         assert 0 < sel.shape[0] < full.stats()["active_blocks"]
         assert sel.shape[0] * 512 == full.query(box).shape[0]
     finally:
-        _close(full, replica, *shards)
+        _close(full, replica, group)
 
 
 def test_import_errors():
@@ -259,13 +266,19 @@ def _render_worker(rank, world, port, q):
     try:
         cam = synth.camera(W, H, synth.TUM_FR1)
         shard = tsdf_amd.Engine(VOXEL, TRUNC, max_width=W, max_height=H, num_block_bits=13,
-                                shard_index=rank, shard_count=world)
+                                shard_index=rank, shard_count=world,
+                                stream=torch.cuda.current_stream().cuda_stream)
         replica = tsdf_amd.Engine(VOXEL, TRUNC, max_width=W, max_height=H, num_block_bits=13)
         engines = [shard]
+        bufs = tdist.ShardBuffers(shard, world, key_cap=8192, cand_cap=4096)
         if rank == 0:
             full = tsdf_amd.Engine(VOXEL, TRUNC, max_width=W, max_height=H, num_block_bits=13)
             engines.append(full)
-        _integrate(engines, cam, 6)
+            _integrate([full], cam, 6)
+        for f in range(6):  # the sharded frames: key and candidate slots all-gathered over gloo
+            fr = synth.render(cam, 2 * f)
+            tdist.integrate_sharded(shard, bufs, fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K,
+                                    tsdf_amd.SE3(fr["q"], fr["t"]), 4.0)
         for K, pose in _views(cam):
             got = tdist.render_sharded(shard, replica, K, W, H, pose, 4.0, device=False)
             if rank == 0:
