@@ -7,13 +7,14 @@
 // candidates in pixel raster order then DDA step, with the exact bucket-lock semantics.
 #include "tsdf_block.h"
 #include "tsdf_kernels.h"
+#include "tsdf_resolve.h"
 
 namespace tsdf {
 
 // ---------------------------------------------------------------------------------------------
 // per-frame new-key set: open addressing on 64-bit packed keys, min candidate order per key
 // ---------------------------------------------------------------------------------------------
-__device__ void keyset_insert(unsigned long long* keys, uint32_t* orders, int32_t* list,
+__device__ void keyset_insert(unsigned long long* keys, uint32_t* orders, NkEnt* list,
                               int32_t* count, uint32_t* status, uint64_t key, uint32_t order) {
   uint32_t h = (uint32_t)mix64(key) & (kNewKeyCap - 1);
   for (int p = 0; p < 256; ++p) {
@@ -21,7 +22,10 @@ __device__ void keyset_insert(unsigned long long* keys, uint32_t* orders, int32_
     const unsigned long long cur = atomicCAS(&keys[h], 0ull, (unsigned long long)key);
     if (cur == 0ull) {
       const int s = atomicAdd(count, 1);
-      list[s] = (int32_t)h;
+      // the list entry carries the key (the resolver's prologue needs no second load for it),
+      // published for the workgroup that resolves at the end of this launch
+      st_co(&list[s].key, (unsigned long long)key);
+      st_co(&list[s].slot, (unsigned long long)h);
       atomicMin(&orders[h], order);
       return;
     }
@@ -67,17 +71,21 @@ __device__ __forceinline__ uint32_t tile_slot(uint64_t key) {
 
 // the two roles of k_ingest_dda share one LDS allocation
 template <int TS>
-union IngestLds {
-  struct {
-    unsigned long long key[TS];
-    uint32_t ord[TS];
-    uint16_t vis[4][TS / 4];
-  } tile;
-  struct {
-    uint32_t list[4][kVisChunk];
-    int cnt[kBands], base[kBands];
-    int npass;
-  } sweep;
+struct IngestLds {
+  union {
+    struct {
+      unsigned long long key[TS];
+      uint32_t ord[TS];
+      uint16_t vis[4][TS / 4];
+    } tile;
+    struct {
+      uint32_t list[4][kVisChunk];
+      int cnt[kBands], base[kBands];
+      int npass;
+    } sweep;
+    AllocLds res;  // the last-arriving workgroup's allocation resolve
+  } u;
+  int last;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -96,9 +104,9 @@ union IngestLds {
 template <int TS>
 __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, IngestLds<TS>& S) {
   const int lane = lane_id(), wave = threadIdx.x >> 6;
-  uint32_t* L = S.sweep.list[wave];
-  int* s_cnt = S.sweep.cnt;
-  int* s_base = S.sweep.base;
+  uint32_t* L = S.u.sweep.list[wave];
+  int* s_cnt = S.u.sweep.cnt;
+  int* s_base = S.u.sweep.base;
   const int grp = lane >> 3, corner = lane & 7;
   const int w = wg * 256 + wave * 64 + lane;
   const unsigned long long occ_all = D.occ[w];
@@ -106,11 +114,11 @@ __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, Inge
   const int incl = wave_incl_scan(cw);
   const int excl = incl - cw;
   const int wave_total = __shfl(incl, 63, 64);
-  if (threadIdx.x == 0) S.sweep.npass = 0;
+  if (threadIdx.x == 0) S.u.sweep.npass = 0;
   __syncthreads();
-  if (lane == 0) atomicMax(&S.sweep.npass, (wave_total + kVisChunk - 1) / kVisChunk);
+  if (lane == 0) atomicMax(&S.u.sweep.npass, (wave_total + kVisChunk - 1) / kVisChunk);
   __syncthreads();
-  const int npass = S.sweep.npass;
+  const int npass = S.u.sweep.npass;
   for (int pass = 0; pass < npass; ++pass) {
     if (threadIdx.x < kBands) s_cnt[threadIdx.x] = 0;
     // this pass lists the wave's live entries of rank [lo, lo + kVisChunk)
@@ -179,22 +187,14 @@ __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, Inge
 // grid: kVisWorkgroups sweep workgroups first (dispatched first, they overlap the tiles), then
 // one workgroup per 16x16 pixel tile (tiles_x per row, `tiles` in all)
 template <int TS>
-__device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
-                                           const float* __restrict__ depth,
-                                           const uint8_t* __restrict__ rgb,
-                                           const float* __restrict__ ht,
-                                           const float* __restrict__ lt, int tiles_x, int tiles) {
-  __shared__ IngestLds<TS> S;
-  if ((int)blockIdx.x < kVisWorkgroups) {
-    TSDF_STAMP(D, 2, 0);
-    vis_sweep(D, P, blockIdx.x, S);
-    TSDF_STAMP(D, 2, 1);
-    return;
-  }
-  const int tile = (int)blockIdx.x - kVisWorkgroups;
-  if (tile >= tiles) return;
-  unsigned long long* s_key = S.tile.key;
-  uint32_t* s_ord = S.tile.ord;
+__device__ __forceinline__ void ingest_tile(EngineDev& D, const FrameParams& P,
+                                            const float* __restrict__ depth,
+                                            const uint8_t* __restrict__ rgb,
+                                            const float* __restrict__ ht,
+                                            const float* __restrict__ lt, int tiles_x, int tile,
+                                            IngestLds<TS>& S) {
+  unsigned long long* s_key = S.u.tile.key;
+  uint32_t* s_ord = S.u.tile.ord;
   TSDF_STAMP(D, 0, 0);
   for (int i = threadIdx.x; i < TS; i += 256) {
     s_key[i] = 0ull;
@@ -281,7 +281,7 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
   // 8 at a time with 8 lanes per key, one block corner per lane (is_block_visible<true>), and the
   // fully visible ones are listed in LDS. The table probes and new-key inserts then run one key
   // per lane over that list, so the wave pays their memory latency once, not once per 8 keys.
-  uint16_t(*s_vis)[TS / 4] = S.tile.vis;
+  uint16_t(*s_vis)[TS / 4] = S.u.tile.vis;
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   const int grp = lane >> 3, corner = lane & 7;
   int nv = 0;
@@ -321,6 +321,61 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
   }
   TSDF_STAMP(D, 0, 5);
 }
+
+// a shard's split frame: the new-key set (this slice's keys) into the exchange slot, drained for
+// the merge of every shard's slots (k_resolve_alloc after the all-gather)
+__device__ void pack_keys_wg(const EngineDev& D, ShardRec* __restrict__ out, int cap) {
+  const int n = ld_co(&D.ctr->nk_count);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int h = (int)ld_co(&D.nk_list[i].slot);
+    const unsigned long long key = ld_co(&D.nk_list[i].key);
+    const uint32_t ord = ld_co(&D.nk_order[h]);
+    D.nk_key[h] = 0ull;
+    D.nk_order[h] = 0xFFFFFFFFu;
+    if (i < cap) {
+      ShardRec r;
+      unpack_key(key, r.x, r.y, r.z);
+      r.pad = 0;
+      r.val = ord;
+      r.zero = 0u;
+      out[1 + i] = r;
+    }
+  }
+  __syncthreads();  // every thread has read nk_count before it is reset
+  if (threadIdx.x == 0) {
+    ShardRec h{};
+    h.val = (uint32_t)min(n, cap);
+    out[0] = h;
+    if (n > cap) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_SHARD_OVERFLOW
+    D.ctr->nk_count = 0;
+  }
+}
+
+// grid: kVisWorkgroups sweep workgroups first (dispatched first, they overlap the tiles), then one
+// workgroup per 16x16 pixel tile (tiles_x per row, `tiles` in all). Every workgroup arrives at the
+// end; the last one resolves the frame's allocation (kTailResolve) or packs a shard's keys for the
+// exchange (kTailPack): block_allocate_kernel and VoxelHashTable::Allocate's launch in one.
+template <int TS>
+__device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
+                                           const float* __restrict__ depth,
+                                           const uint8_t* __restrict__ rgb,
+                                           const float* __restrict__ ht,
+                                           const float* __restrict__ lt, int tiles_x, int tiles) {
+  __shared__ IngestLds<TS> S;
+  if ((int)blockIdx.x < kVisWorkgroups) {
+    TSDF_STAMP(D, 2, 0);
+    vis_sweep(D, P, blockIdx.x, S);
+    TSDF_STAMP(D, 2, 1);
+  } else if ((int)blockIdx.x - kVisWorkgroups < tiles) {
+    ingest_tile<TS>(D, P, depth, rgb, ht, lt, tiles_x, (int)blockIdx.x - kVisWorkgroups, S);
+  }
+  if (!arrive_last(D.arrive + kArrIngest, 0ull, &S.last)) return;
+  if (threadIdx.x == 0) (void)arrive_collect(D.arrive + kArrIngest);
+  if (P.tail == kTailPack)
+    pack_keys_wg(D, P.slot, P.slot_cap);
+  else
+    resolve_alloc_wg(D, P, (uint32_t)P.W * (uint32_t)P.H * (uint32_t)P.maxs, 1, S.u.res);
+}
 template <int TS>
 __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
                                                     const float* __restrict__ depth,
@@ -342,50 +397,6 @@ template __global__ void k_ingest_dda<2048>(EngineDev, FrameParams, const float*
 template __global__ void k_ingest_dda_g<1024>(EngineDev, const FrameArgs*);
 template __global__ void k_ingest_dda_g<2048>(EngineDev, const FrameArgs*);
 
-// ---------------------------------------------------------------------------------------------
-// Sharded frames: the key exchange. k_key_pack drains this shard's new-key set
-// (its DDA slice's keys) into its outbox slot; after the all-gather, k_key_merge inserts every
-// shard's slot into the set with the smallest candidate order per key -- the set one volume's DDA
-// over the whole frame builds -- so every shard's allocation resolver makes the same decisions.
-// The senders probed the same index, so no probe is repeated here.
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_key_pack(EngineDev D, ShardRec* __restrict__ out, int cap) {
-  const int n = D.ctr->nk_count;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const int h = D.nk_list[i];
-    const unsigned long long key = D.nk_key[h];
-    const uint32_t ord = D.nk_order[h];
-    D.nk_key[h] = 0ull;  // the set is rebuilt from the exchanged slots
-    D.nk_order[h] = 0xFFFFFFFFu;
-    if (i < cap) {
-      ShardRec r;
-      unpack_key(key, r.x, r.y, r.z);
-      r.pad = 0;
-      r.val = ord;
-      r.zero = 0u;
-      out[1 + i] = r;
-    }
-  }
-  __syncthreads();  // every wave has read nk_count before it is reset
-  if (threadIdx.x == 0) {
-    ShardRec h{};
-    h.val = (uint32_t)min(n, cap);
-    out[0] = h;
-    if (n > cap) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_SHARD_OVERFLOW
-    D.ctr->nk_count = 0;
-  }
-}
-
-// grid (ceil(cap / 256), nshard): workgroup row s merges the slot shard s wrote
-__global__ __launch_bounds__(256) void k_key_merge(EngineDev D, const ShardRec* __restrict__ in, int cap) {
-  const ShardRec* slot = in + (size_t)blockIdx.y * (cap + 1);
-  const int n = min((int)slot[0].val, cap);
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const ShardRec r = slot[1 + i];
-  nk_insert(D, pack_key(r.x, r.y, r.z), r.val);
-}
-
 // test path: keys[n] in list order (one VoxelHashTable::Allocate launch, voxel_hash_test.cu)
 __global__ void k_keys_to_newset(EngineDev D, const int16_t* __restrict__ keys, int n) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -406,253 +417,29 @@ __global__ void k_import_keys(EngineDev D, const uint8_t* __restrict__ recs, int
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_resolve_alloc: one 1024-thread workgroup replays VoxelHashTable::Allocate in candidate order.
-// Every unique missing key K is evaluated against the current table:
-//   SLOT(B, s)   : an empty slot s of its bucket B                  -> takes lock B
-//   APPEND(L, C) : bucket full -> tail T of B's list (bucket L = T/2), first empty slot-0 entry E
-//                  after T (bucket C = E/2)                         -> takes lock L, then lock C
-// A key's outcome depends on earlier keys only through the buckets it locks (every table write
-// happens under those locks), so up to 1024 keys are evaluated speculatively, each claims its
-// buckets in an LDS table (smallest rank wins), and the longest prefix whose keys won all their
-// claims commits in parallel. The first key always wins, so each round commits >= 1 key.
-// Pool blocks are popped in commit order by prefix sum (AquireBlock, voxel_mem.cu:37-52).
-// frame_mode 1: append new blocks to this frame's visible-block lists flagged fresh (integrate
-// initialises them), 0: list them in D.fresh for k_fresh_init.
+// k_resolve_alloc: the allocation resolver (tsdf_resolve.h) as its own one-workgroup launch -- a
+// shard's split frame after the key all-gather (keys_in: every shard's slot, merged into the
+// new-key set first with the smallest candidate order per key, the set one volume's DDA over the
+// whole frame builds; the senders probed the same index, so no probe is repeated), and the
+// hash-level test / import path (frame_mode 0).
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void resolve_alloc(EngineDev D, FrameParams P, uint32_t range,
-                                              int frame_mode) {
-  __shared__ ResolveLds L;
-  const int t = threadIdx.x;
-  TSDF_STAMP(D, 1, 0);
-  // the counters are loaded together (one memory round trip) before anything waits on them
-  const int n = D.ctr->nk_count;
-  const int free0 = D.ctr->free_count;  // every thread: the pops index the stack top by it
-  uint32_t epoch0 = 0u;
-  if (t == 0) epoch0 = D.ctr->lock_epoch;
-  claims_clear(L);
-  if (t == 0) {
-    L.epoch = epoch0 + 1;
-    D.ctr->lock_epoch = L.epoch;
-    L.sfree = free0;
-    L.nfresh = 0;
-    L.nalloc = 0;
-  }
-  // One batch (the common case): (candidate order, list index) straight into the LDS batch, keys
-  // and set slots into LDS, plus the free-stack top the pops will read -- all in one round trip.
-  // Otherwise (order, slot) pairs go to a compact scratch array so every batch pass is one
-  // coalesced read.
-  const bool single = n <= kBatch;
-  if (single) {
-    for (int i = t; i < kLockSlots; i += kResolveThreads) L.lkey[i] = 0u;
-    const int npre = min(n, free0);
-    for (int i = t; i < npre; i += kResolveThreads) L.heap_top[i] = D.heap[free0 - 1 - i];
-    for (int i = t; i < n; i += kResolveThreads) {
-      const int h = D.nk_list[i];
-      L.batch[i] = ((unsigned long long)D.nk_order[h] << 32) | (uint32_t)i;
-      L.skey[i] = D.nk_key[h];
-      L.sslot[i] = h;
+__global__ __launch_bounds__(kRT) void k_resolve_alloc(EngineDev D, FrameParams P, uint32_t range,
+                                                       int frame_mode, const ShardRec* __restrict__ keys_in,
+                                                       int cap, int nshard) {
+  __shared__ AllocLds L;
+  if (keys_in) {
+    for (int s = 0; s < nshard; ++s) {
+      const ShardRec* slot = keys_in + (size_t)s * (cap + 1);
+      const int n = min((int)slot[0].val, cap);
+      for (int i = threadIdx.x; i < n; i += kRT) {
+        const ShardRec r = slot[1 + i];
+        nk_insert(D, pack_key(r.x, r.y, r.z), r.val);
+      }
     }
-  } else {
-    for (int i = t; i < n; i += kResolveThreads) {
-      const int h = D.nk_list[i];
-      D.pairs[i] = ((unsigned long long)D.nk_order[h] << 32) | (uint32_t)h;
-      D.pkey[i] = D.nk_key[h];
-    }
-  }
-  __syncthreads();
-  auto keyf = [&](int i) -> uint32_t { return (uint32_t)(D.pairs[i] >> 32); };
-  const int width = single ? 1 : stream_prepare(L, n, range, keyf);
-  const int nbatch = single ? (n > 0 ? 1 : 0) : ((n - 1) >> 10) + 1;
-  int rounds = 0;
-  TSDF_STAMP(D, 1, 1);
-  for (int j = 0; j < nbatch; ++j) {
-    int m;
-    if (single) {
-      m = n;
-      batch_sort(L, m, true);
-    } else {
-      m = stream_batch(L, n, width, j, keyf);
-    }
-    TSDF_STAMP(D, 1, 2);
-    if (t == 0) L.base = 0;
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    while (L.base < m) {
-      if (++rounds > n + 8) {  // unreachable: the first key of a round always commits
-        if (t == 0) atomicOr(&D.ctr->status, 8u);
-        j = nbatch;
-        break;
-      }
-      const int base = L.base;
-      const bool have = base + t < m;
-      int kind = 0, slot = 0, h = -1;
-      uint32_t B = 0, Lb = 0, C = 0, T = 0, E = 0;
-      int16_t kx = 0, ky = 0, kz = 0;
-      if (have) {
-        const int li = (int)(L.batch[base + t] & 0xFFFFFFFFu);
-        if (single) {
-          h = L.sslot[li];
-          unpack_key(L.skey[li], kx, ky, kz);
-        } else {
-          h = (int)(D.pairs[li] & 0xFFFFFFFFu);
-          unpack_key(D.pkey[li], kx, ky, kz);
-        }
-        B = hash_block(kx, ky, kz);
-        const Ent s0 = load_ent(D.table, 2 * B);
-        const Ent s1 = load_ent(D.table, 2 * B + 1);
-        if (s0.idx < 0) {
-          kind = 1;
-          slot = 0;
-        } else if (s1.idx < 0) {
-          kind = 1;
-          slot = 1;
-        } else {
-          kind = 2;
-          uint32_t last = 2 * B + 1;
-          Ent b = s1;
-          while (b.off) {
-            last = (uint32_t)(last + (int32_t)b.off) & kEntryMask;
-            b = load_ent(D.table, last);
-          }
-          T = last;
-          Lb = T >> 1;
-          uint32_t nx = T;
-          for (uint32_t p = 0; p < kNumEntry; ++p) {
-            nx = (nx + 1) & kEntryMask;
-            if ((nx & 1u) == 0u && load_ent(D.table, nx).idx < 0) break;
-          }
-          E = nx;
-          C = E >> 1;
-        }
-        if (kind == 1) {
-          claim(L, B, (uint32_t)t);
-        } else {
-          claim(L, Lb, (uint32_t)t);
-          claim(L, C, (uint32_t)t);
-        }
-      }
-      if (t == 0) L.first_dirty = kResolveThreads;
-      __syncthreads();
-      if (have) {
-        const bool clean = kind == 1 ? claim_winner(L, B) == (uint32_t)t
-                                     : (claim_winner(L, Lb) == (uint32_t)t &&
-                                        claim_winner(L, C) == (uint32_t)t);
-        if (!clean) atomicMin(&L.first_dirty, t);
-      }
-      __syncthreads();
-      const int first_dirty = L.first_dirty;
-      const bool commit = have && t < first_dirty;
-      bool ok = false;
-      if (commit && single) {  // the launch's locks in LDS (<= 2 x 2048 of the 8192 slots)
-        if (kind == 1)
-          ok = lock_take(L, B);
-        else if (lock_take(L, Lb))
-          ok = lock_take(L, C);
-      } else if (commit) {
-        const uint32_t ep = L.epoch;
-        if (kind == 1) {
-          if (D.lock_tag[B] != ep) {
-            D.lock_tag[B] = ep;
-            ok = true;
-          }
-        } else if (D.lock_tag[Lb] != ep) {
-          D.lock_tag[Lb] = ep;
-          if (D.lock_tag[C] != ep) {
-            D.lock_tag[C] = ep;
-            ok = true;
-          }
-        }
-      }
-      // Sharded volume: every shard commits every key's table change (the replicated index), and
-      // only the key's owner pops a pool block; the others store kForeignIdx.
-      const bool mine = ok && (P.shard_count <= 1 ||
-                               brick_owner(kx, ky, kz, (uint32_t)P.shard_count) == (uint32_t)P.shard_index);
-      int nok;
-      const int rank = block_excl_scan(mine ? 1 : 0, L.scan, &nok);
-      const int free_now = L.sfree;
-      if (ok) {
-        int32_t idx = kForeignIdx;
-        bool insert = true;
-        if (mine) {
-          const int hi = free_now - 1 - rank;
-          if (hi < 0) {
-            atomicOr(&D.ctr->status, 1u);  // TSDF_STATUS_POOL_EXHAUSTED
-            // one volume drops the insert; a shard keeps a voxel-less entry so that every
-            // shard's index stays the same
-            insert = P.shard_count > 1;
-          } else {
-            const int top = free0 - 1 - hi;  // pops so far this launch + rank
-            idx = single ? L.heap_top[top] : D.heap[hi];
-          }
-        }
-        if (insert) {
-          uint32_t e;
-          if (kind == 1) {
-            e = 2 * B + (uint32_t)slot;
-          } else {
-            const uint32_t wrap = E > T ? 0u : kNumEntry;
-            store_off(D.table, T, (int16_t)(E + wrap - T));
-            e = E;
-          }
-          store_ent(D.table, e, kx, ky, kz, 0, idx);
-          if (local_idx(idx)) {  // the occupancy bitmap lists the blocks this engine holds
-            atomicOr(&D.occ[e >> 6], 1ull << (e & 63));
-            if (frame_mode) {
-              // a new block has all 8 corners in view, so it is visible this frame: listed for
-              // the fresh-block integrate launch (the sweep in k_ingest_dda listed only the
-              // blocks that existed before), flagged fresh so it starts from AquireBlock's state
-              VisRec vr;
-              vr.x = kx;
-              vr.y = ky;
-              vr.z = kz;
-              vr.pad = 1;
-              vr.idx = idx;
-              vr.entry = (int32_t)e;
-              D.fresh_vis[L.nfresh + rank] = vr;
-            } else {
-              D.fresh[L.nfresh + rank] = idx;
-            }
-          }
-        }
-      }
-      if (commit) {
-        D.nk_key[h] = 0ull;
-        D.nk_order[h] = 0xFFFFFFFFu;
-      }
-      claims_clear(L);
-      __syncthreads();
-      if (t == 0) {
-        const int used = nok < free_now ? nok : (free_now > 0 ? free_now : 0);
-        L.sfree = free_now - used;
-        L.nfresh += used;
-        L.nalloc += used;
-        const int span = m - base < kResolveThreads ? m - base : kResolveThreads;
-        L.base = base + (first_dirty < span ? first_dirty : span);
-      }
-      __syncthreads();
-    }
   }
-  TSDF_STAMP(D, 1, 3);
-  __syncthreads();  // every thread's table / list writes precede the release below
-  if (t == 0) {
-    D.ctr->free_count = L.sfree;
-    D.ctr->n_fresh = L.nfresh;
-    D.ctr->nk_count = 0;
-    if (frame_mode) {
-      D.ctr->last_alloc = L.nalloc;
-      D.ctr->last_new_keys = n;
-      D.ctr->total_alloc += (unsigned long long)L.nalloc;
-    }
-  }
-}
-
-__global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc(EngineDev D, FrameParams P,
-                                                                   uint32_t range, int frame_mode) {
-  resolve_alloc(D, P, range, frame_mode);
-}
-__global__ __launch_bounds__(kResolveThreads) void k_resolve_alloc_g(EngineDev D,
-                                                                     const FrameArgs* __restrict__ A) {
-  const FrameParams P = A->P;
-  resolve_alloc(D, P, A->range, 1);
+  resolve_alloc_wg(D, P, range, frame_mode, L);
 }
 
 // AquireBlock's initialisation (voxel_mem.cu:43-51) for the hash-level test path

@@ -42,6 +42,13 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int* total) 
   *total = tot;
   return before + incl - v;
 }
+// workgroup barrier for LDS hand-offs only: global stores stay in flight (HIP's __syncthreads is a
+// release of all memory -- s_waitcnt vmcnt(0) -- and would drain every outstanding pool store)
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 __device__ __forceinline__ uint64_t mix64(uint64_t k) {
   k ^= k >> 33;
   k *= 0xff51afd7ed558ccdull;

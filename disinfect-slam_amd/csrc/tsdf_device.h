@@ -46,6 +46,9 @@ constexpr int kIntegrateGrid = 2048;  // k_integrate workgroups (persistent grid
 // k_integrate workgroup size: 4 waves, two per visible block (1024-thread workgroups measured
 // slower: 24.3 against 17.5 us)
 constexpr int kIntegrateThreads = 256;
+// carve candidates a k_integrate workgroup buffers in LDS before publishing them at its end (more
+// are published as they come)
+constexpr int kIntegrateCandBuf = 16;
 
 struct f3 {
   float x, y, z;
@@ -69,7 +72,13 @@ struct FrameParams {
   int maxs;                  // DDA samples reserved per pixel in the candidate order space
   int shard_index, shard_count;
   int tile_lo, tile_hi;      // pixel tiles whose DDA this engine runs (a shard's slice, else all)
+  int tail;                  // what the last workgroup of a frame kernel does (kTail*)
+  int slot_cap;              // kTailPack: records the exchange slot holds
+  struct ShardRec* slot;     // kTailPack: this shard's exchange slot (keys / carve candidates)
 };
+// the last-arriving workgroup of k_ingest_dda / k_integrate: resolve (allocation / carving) or, in a
+// shard's frame with an exchange after the kernel, pack the keys / candidates into the slot
+constexpr int kTailResolve = 0, kTailPack = 1;
 
 // Sharded volume: every shard keeps the whole hash index, so bucket locks and table
 // layout evolve exactly as in one volume; a block's voxels live only on its owner. The other
@@ -81,6 +90,13 @@ __device__ __host__ __forceinline__ bool local_idx(int32_t idx) { return idx >= 
 // one exchanged record of a sharded frame (16 B): a new block key with its candidate order, or a
 // carve candidate with its hash entry. A slot is (cap + 1) records, record 0 a header whose `val`
 // holds the count; an inbox is shard_count slots, slot s written by shard s.
+// one entry of the new-key list: the key and its new-key-set slot (16 B, published with two
+// 8-byte agent-scope stores)
+struct alignas(16) NkEnt {
+  unsigned long long key;
+  unsigned long long slot;
+};
+
 struct alignas(16) ShardRec {
   int16_t x, y, z, pad;
   uint32_t val;   // candidate order (keys) / hash entry (carve candidates) / count (header)

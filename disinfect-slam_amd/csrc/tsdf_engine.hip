@@ -16,6 +16,7 @@
 
 #include "disinfect_tsdf.h"
 #include "tsdf_kernels.h"
+#include "tsdf_resolve.h"
 
 using namespace tsdf;
 
@@ -149,9 +150,9 @@ namespace {
 void free_all(tsdf_engine* e) {
   EngineDev& D = e->D;
   void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.occ,
-                  D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs, D.pkey,      D.fresh,
+                  D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs, D.fresh,
                   e->fe_rgb, e->fe_depth, e->fe_mask, e->fe_out_rgb, e->fe_out_depth,
-                  D.vis,     D.band,    D.cand,     D.wg_upd, D.wg_end, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
+                  D.vis,     D.band,    D.cand,     D.arrive, D.fresh_vis, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
                   e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
                   e->t_i32,  e->t_u32,   e->t_f0,    e->t_f1,   e->t_s4};
@@ -198,6 +199,9 @@ FrameParams make_params(const tsdf_engine* e, const tsdf_intrinsics* K, int W, i
   P.shard_count = e->cfg.shard_count;
   P.tile_lo = 0;
   P.tile_hi = 1 << 30;
+  P.tail = kTailResolve;
+  P.slot_cap = 0;
+  P.slot = nullptr;
   return P;
 }
 
@@ -231,9 +235,10 @@ int ensure_test_cap(tsdf_engine* e, int n) {
   return TSDF_OK;
 }
 
+// the allocation resolver as its own launch: hash-level test path and imports (frame_mode 0)
 int launch_resolve_alloc(tsdf_engine* e, const FrameParams& P, uint32_t range, int frame_mode) {
-  hipLaunchKernelGGL(k_resolve_alloc, dim3(1), dim3(kResolveThreads), 0, e->stream, e->D, P, range,
-                     frame_mode);
+  hipLaunchKernelGGL(k_resolve_alloc, dim3(1), dim3(kRT), 0, e->stream, e->D, P, range, frame_mode,
+                     (const ShardRec*)nullptr, 0, 0);
   if (!frame_mode)
     hipLaunchKernelGGL(k_fresh_init, dim3(512), dim3(256), 0, e->stream, e->D);
   LAUNCH_OK("allocate");
@@ -320,6 +325,7 @@ bool init_state(tsdf_engine* e, bool with_pool = true) {
   ok &= hipMemsetAsync(D.nk_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
   ok &= hipMemsetAsync(D.band, 0, sizeof(int32_t) * kBands * kBandStride, s) == hipSuccess;
   ok &= hipMemsetAsync(D.visbits, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.arrive, 0, sizeof(unsigned long long) * kArriveWords, s) == hipSuccess;
   DevCounters c0{};
   c0.free_count = nb;
   ok &= hipMemcpyAsync(D.ctr, &c0, sizeof(c0), hipMemcpyHostToDevice, s) == hipSuccess;
@@ -394,14 +400,12 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.nk_key, kNewKeyCap);
   ALLOC(D.nk_order, kNewKeyCap);
   ALLOC(D.nk_list, kNewKeyCap);
-  ALLOC(D.pairs, kNewKeyCap);
-  ALLOC(D.pkey, kNewKeyCap);
+  ALLOC(D.pairs, std::max<size_t>(kNewKeyCap, (size_t)nb));
   ALLOC(D.fresh, kNewKeyCap);
   ALLOC(D.vis, (size_t)kBands * nb);
   ALLOC(D.band, kBands * kBandStride);
-  ALLOC(D.cand, nb);
-  ALLOC(D.wg_upd, 2 * kIntegrateGrid);
-  ALLOC(D.wg_end, 2 * kIntegrateGrid + 1);
+  ALLOC(D.cand, std::max(nb, 1024));  // >= the resolver's speculative prologue reads (kRB)
+  ALLOC(D.arrive, kArriveWords);
   ALLOC(D.fresh_vis, kNewKeyCap);
   {  // one resident wave of k_integrate workgroups: no second-round stragglers
     int per_cu = 0, ncu = 0;
@@ -470,7 +474,7 @@ namespace {
 // visibility of the existing blocks). *P / *ev carry the frame to the later phases.
 int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, const tsdf_pose* pose,
                  float max_depth, int slice_index, int slice_count, FrameParams* P,
-                 std::array<hipEvent_t, 5>** ev_out) {
+                 std::array<hipEvent_t, 5>** ev_out, void* keys_out = nullptr, int key_cap = 0) {
   if (!e || !f || !K || !pose || !f->depth || !f->rgb || f->width <= 0 || f->height <= 0 ||
       (int64_t)f->width * f->height > e->max_pixels || f->width > e->cfg.max_width ||
       f->height > e->cfg.max_height || (f->ht == nullptr) != (f->lt == nullptr) ||
@@ -508,6 +512,11 @@ int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, 
     P->tile_lo = std::min(tiles_y, slice_index * rows) * tiles_x;
     P->tile_hi = std::min(tiles_y, (slice_index + 1) * rows) * tiles_x;
   }
+  if (keys_out) {  // the last workgroup packs the keys for the exchange instead of resolving them
+    P->tail = kTailPack;
+    P->slot = reinterpret_cast<ShardRec*>(keys_out);
+    P->slot_cap = key_cap;
+  }
   std::array<hipEvent_t, 5>* ev = nullptr;
   if (e->profiling && (e->prof_calls++ % e->prof_every) == 0) {
     if (e->ev_used == e->events.size()) {
@@ -520,8 +529,8 @@ int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, 
   *ev_out = ev;
   if (ev && e->prof_mode == TSDF_PROFILE_PHASES) HIP_OK(hipEventRecord((*ev)[0], s));
   // ---- allocate (voxel_tsdf.cu:377-386) + visibility (:388-397) ----
-  // k_ingest_dda sweeps the blocks that already exist for visibility beside the DDA; the
-  // resolver inserts the new keys and appends the blocks it creates to the visible lists
+  // k_ingest_dda sweeps the blocks that already exist for visibility beside the DDA; its last
+  // workgroup resolves the new keys and appends the blocks it creates to the visible lists
   if (e->maxs <= 3)
     hipLaunchKernelGGL(k_ingest_dda<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, s, e->D, *P, depth,
                        rgb, ht, lt, tiles_x, tiles);
@@ -532,18 +541,20 @@ int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, 
   return TSDF_OK;
 }
 
-// Phase 2: ordered allocation of the new keys -> fused update (+ carve minimum).
-// (Measured and not kept: running the update of the existing blocks beside k_resolve_alloc, on a
-// second stream or as a dispatch without the AQL barrier bit that waits on a release flag for the
-// new blocks. The resolver's chain of dependent HBM round trips slows ~2.5x under the update's
-// memory load, and the stream fork / join costs more than it hides: 15-16k frames/s against 18k.)
-int frame_update(tsdf_engine* e, const FrameParams& P, std::array<hipEvent_t, 5>* ev) {
+// Phase 2: fused update (+ carve minimum); the last workgroup carves (kTailResolve) or packs a
+// shard's carve candidates into cands_out. (Measured and not kept in round 1: running the update of
+// the existing blocks beside the allocation resolver, on a second stream or as a dispatch without
+// the AQL barrier bit: the resolver's chain of dependent HBM round trips slows ~2.5x under the
+// update's memory load.)
+int frame_update(tsdf_engine* e, FrameParams P, std::array<hipEvent_t, 5>* ev, void* cands_out = nullptr,
+                 int cand_cap = 0) {
   hipStream_t s = e->stream;
   const bool all_ev = ev && e->prof_mode == TSDF_PROFILE_PHASES;
-  int rc = launch_resolve_alloc(e, P, (uint32_t)((size_t)P.W * P.H * e->maxs), 1);
-  if (rc) return rc;
   if (all_ev) HIP_OK(hipEventRecord((*ev)[1], s));
-  // ---- update (voxel_tsdf.cu:474-481) ----
+  P.tail = cands_out ? kTailPack : kTailResolve;
+  P.slot = reinterpret_cast<ShardRec*>(cands_out);
+  P.slot_cap = cand_cap;
+  // ---- update (voxel_tsdf.cu:474-481) + space carving (:483-488) ----
   if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
     // the two events are bound to the kernel's own dispatch packet (its begin / end timestamps,
     // the interval rocprofv3's kernel trace reports): no marker packets enter the stream
@@ -556,16 +567,7 @@ int frame_update(tsdf_engine* e, const FrameParams& P, std::array<hipEvent_t, 5>
     if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
   }
   LAUNCH_OK("k_integrate");
-  return TSDF_OK;
-}
-
-// Phase 3: space carving (voxel_tsdf.cu:483-488) of the candidates in D.cand.
-int frame_carve(tsdf_engine* e, std::array<hipEvent_t, 5>* ev) {
-  hipStream_t s = e->stream;
-  hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kResolveThreads), 0, s, e->D, e->D.cand,
-                     &e->D.ctr->n_cand, 0);
-  LAUNCH_OK("k_resolve_delete");
-  if (ev && e->prof_mode == TSDF_PROFILE_PHASES) HIP_OK(hipEventRecord((*ev)[4], s));
+  if (all_ev && !cands_out) HIP_OK(hipEventRecord((*ev)[4], s));
   return TSDF_OK;
 }
 
@@ -584,9 +586,7 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
   std::array<hipEvent_t, 5>* ev = nullptr;
   int rc = frame_ingest(e, f, K, pose, max_depth, 0, 1, &P, &ev);
   if (rc) return rc;
-  rc = frame_update(e, P, ev);
-  if (rc) return rc;
-  return frame_carve(e, ev);
+  return frame_update(e, P, ev);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -610,13 +610,13 @@ int tsdf_integrate_shard_begin(tsdf_engine* e, const tsdf_frame* f, const tsdf_i
   }
   FrameParams P;
   std::array<hipEvent_t, 5>* ev = nullptr;
-  int rc = frame_ingest(e, f, K, pose, max_depth, slice_index, slice_count, &P, &ev);
+  // split DDA: the last workgroup packs this slice's keys into keys_out; whole-frame DDA (no key
+  // exchange): it resolves the allocation right away, like one volume
+  int rc = frame_ingest(e, f, K, pose, max_depth, slice_index, slice_count, &P, &ev, keys_out, key_cap);
   if (rc) return rc;
-  if (keys_out) {
-    hipLaunchKernelGGL(k_key_pack, dim3(1), dim3(1024), 0, e->stream, e->D,
-                       reinterpret_cast<ShardRec*>(keys_out), key_cap);
-    LAUNCH_OK("k_key_pack");
-  }
+  P.tail = kTailResolve;
+  P.slot = nullptr;
+  P.slot_cap = 0;
   e->shard_P = P;
   e->shard_ev = ev;
   e->shard_keys_packed = keys_out != nullptr;
@@ -634,17 +634,15 @@ int tsdf_integrate_shard_update(tsdf_engine* e, const void* keys_in, int32_t key
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  hipStream_t s = e->stream;
-  if (keys_in) {
-    hipLaunchKernelGGL(k_key_merge, dim3((key_cap + 255) / 256, e->cfg.shard_count), dim3(256), 0, s, e->D,
-                       reinterpret_cast<const ShardRec*>(keys_in), key_cap);
-    LAUNCH_OK("k_key_merge");
+  if (keys_in) {  // merge every shard's keys, then the ordered allocation (one workgroup)
+    const FrameParams& P = e->shard_P;
+    hipLaunchKernelGGL(k_resolve_alloc, dim3(1), dim3(kRT), 0, e->stream, e->D, P,
+                       (uint32_t)((size_t)P.W * P.H * e->maxs), 1, reinterpret_cast<const ShardRec*>(keys_in),
+                       key_cap, e->cfg.shard_count);
+    LAUNCH_OK("k_resolve_alloc");
   }
-  int rc = frame_update(e, e->shard_P, e->shard_ev);
+  int rc = frame_update(e, e->shard_P, e->shard_ev, cands_out, cand_cap);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_cand_pack, dim3(1), dim3(1024), 0, s, e->D, reinterpret_cast<ShardRec*>(cands_out),
-                     cand_cap);
-  LAUNCH_OK("k_cand_pack");
   e->shard_phase = 2;
   return TSDF_OK;
 }
@@ -657,11 +655,14 @@ int tsdf_integrate_shard_end(tsdf_engine* e, const void* cands_in, int32_t cand_
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  hipLaunchKernelGGL(k_cand_gather, dim3(1), dim3(1024), 0, e->stream, e->D,
-                     reinterpret_cast<const ShardRec*>(cands_in), cand_cap, e->cfg.shard_count);
-  LAUNCH_OK("k_cand_gather");
+  hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kRT), 0, e->stream, e->D, (const VisRec*)e->D.cand,
+                     (const int32_t*)&e->D.ctr->n_cand, 0, reinterpret_cast<const ShardRec*>(cands_in),
+                     cand_cap, e->cfg.shard_count);
+  LAUNCH_OK("k_resolve_delete");
   e->shard_phase = 0;
-  return frame_carve(e, e->shard_ev);
+  std::array<hipEvent_t, 5>* ev = e->shard_ev;
+  if (ev && e->prof_mode == TSDF_PROFILE_PHASES) HIP_OK(hipEventRecord((*ev)[4], e->stream));
+  return TSDF_OK;
 }
 
 int tsdf_stream_wait(tsdf_engine* e, void* stream) {
@@ -777,11 +778,8 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
       hipLaunchKernelGGL(k_ingest_dda_g<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
     else
       hipLaunchKernelGGL(k_ingest_dda_g<2048>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
-    hipLaunchKernelGGL(k_resolve_alloc_g, dim3(1), dim3(kResolveThreads), 0, g->cap, e->D, A);
     hipLaunchKernelGGL((k_integrate_t<true>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, g->cap,
                        e->D, FrameParams{}, A);
-    hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kResolveThreads), 0, g->cap, e->D, e->D.cand,
-                       &e->D.ctr->n_cand, 0);
     if (render_width)
       hipLaunchKernelGGL(k_raycast_g, dim3((render_width + 15) / 16, (render_height + 15) / 16), dim3(256), 0,
                          g->cap, e->D, A);
@@ -1594,8 +1592,8 @@ int tsdf_hash_delete(tsdf_engine* e, const int16_t* keys, int n) {
   }
   HIP_OK(hipMemcpyAsync(e->t_recs, recs.data(), sizeof(VisRec) * n, hipMemcpyHostToDevice, e->stream));
   HIP_OK(hipMemcpyAsync(e->t_count, &n, sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
-  hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kResolveThreads), 0, e->stream, e->D,
-                     e->t_recs, e->t_count, 1);
+  hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kRT), 0, e->stream, e->D, (const VisRec*)e->t_recs,
+                     (const int32_t*)e->t_count, 1, (const ShardRec*)nullptr, 0, 0);
   LAUNCH_OK("k_resolve_delete");
   HIP_OK(hipStreamSynchronize(e->stream));
   return TSDF_OK;

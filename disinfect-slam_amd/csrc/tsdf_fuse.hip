@@ -1,6 +1,7 @@
 // tsdf_fuse.hip -- the fused integrate kernel and the space-carving resolver.
 #include "tsdf_block.h"
 #include "tsdf_kernels.h"
+#include "tsdf_resolve.h"
 
 namespace tsdf {
 
@@ -27,6 +28,66 @@ __device__ __forceinline__ void setu(uint4& v, int j, uint32_t f) {
   if (j == 0) v.x = f; else if (j == 1) v.y = f; else if (j == 2) v.z = f; else v.w = f;
 }
 
+// end of a frame's bookkeeping (after its carving): running totals, empty candidate / band lists
+__device__ void frame_end(const EngineDev& D) {
+  lds_barrier();
+  if (threadIdx.x == 0) {
+    D.ctr->total_visible += (unsigned long long)D.ctr->n_vis;
+    D.ctr->total_updated += D.ctr->last_updated;
+    D.ctr->frames += 1ull;
+    D.ctr->n_cand = 0;  // the next frame's lists start empty (its sweep runs before allocation)
+  }
+  if (threadIdx.x < kBands) D.band[threadIdx.x * kBandStride] = 0;
+}
+
+// a shard's frame: its carve candidates into the exchange slot
+__device__ void pack_cands_wg(const EngineDev& D, ShardRec* __restrict__ out, int cap) {
+  const int n = ld_co(&D.ctr->n_cand);
+  const unsigned long long* rq = reinterpret_cast<const unsigned long long*>(D.cand);
+  for (int i = threadIdx.x; i < min(n, cap); i += blockDim.x) {
+    const unsigned long long a = ld_co(&rq[2 * i]), b = ld_co(&rq[2 * i + 1]);
+    ShardRec r;
+    r.x = (int16_t)(a & 0xFFFF);
+    r.y = (int16_t)((a >> 16) & 0xFFFF);
+    r.z = (int16_t)((a >> 32) & 0xFFFF);
+    r.pad = 0;
+    r.val = (uint32_t)(b >> 32);  // hash entry
+    r.zero = 0u;
+    out[1 + i] = r;
+  }
+  if (threadIdx.x == 0) {
+    ShardRec h{};
+    h.val = (uint32_t)min(n, cap);
+    out[0] = h;
+    if (n > cap) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_SHARD_OVERFLOW
+  }
+}
+
+// The last-arriving workgroup of k_integrate: the frame's statistics (updated voxels from the
+// arrivals, the update's device-clock span, visible = listed by the sweep + created), then the
+// space carving of the candidates (voxel_tsdf.cu:483-488, kTailResolve) or, in a shard's frame,
+// the packing of its candidates for the exchange (kTailPack; k_resolve_delete follows it).
+__device__ __forceinline__ void integrate_tail(const EngineDev& D, const FrameParams& P, DeleteLds& L) {
+  const int t = threadIdx.x;
+  const int bc = t < kBands ? D.band[t * kBandStride] : 0;
+  int nband;
+  (void)wg_excl_scan(bc, L.scan, &nband);
+  if (t == 0) {
+    const unsigned long long upd = arrive_collect(D.arrive + kArrIntegrate);
+    const unsigned long long tend = __builtin_amdgcn_s_memrealtime();
+    D.ctr->last_updated = upd;
+    D.ctr->integrate_ticks += tend - ld_co(&D.arrive[kArrStart]);
+    D.ctr->n_vis = nband + D.ctr->n_fresh;
+  }
+  if (P.tail == kTailPack) {
+    pack_cands_wg(D, P.slot, P.slot_cap);
+  } else {
+    lds_barrier();
+    resolve_delete_wg(D, D.cand, &D.ctr->n_cand, 0, L);
+    frame_end(D);
+  }
+}
+
 // 64 VGPRs: 8 waves per SIMD (65 without the bound: 7). Graph: the graph-captured form reads its
 // camera from the FrameArgs block the graph's first node uploads.
 // The visible blocks are the sweep's band lists (blocks that existed before the frame) followed by
@@ -37,6 +98,10 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
   const FrameParams P = Graph ? A->P : Pv;
   __shared__ float s_min[4];
   __shared__ int s_upd[4];
+  __shared__ int s_last;
+  __shared__ int s_ncand, s_ovf;
+  __shared__ VisRec s_cand[kIntegrateCandBuf];  // this workgroup's carve candidates
+  __shared__ DeleteLds L;  // the last-arriving workgroup's carving resolve
   const int lane = lane_id();
   // wave-uniform (scalar) loop state: the band search, the list record and the fresh flag are
   // SALU / scalar loads instead of per-lane selects
@@ -57,10 +122,14 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
   const int off = (hf * 256 + lane * 4) * 4;
   const float neg_trunc = -P.trunc;
   int my_upd = 0;
+  if (threadIdx.x == 0) {  // (ordered before their first use by the pair loop's barrier)
+    s_ncand = 0;
+    s_ovf = 0;
+  }
   TSDF_STAMP(D, 3, 0);
-  // device-clock duration of this launch: start stamp by WG 0 (dispatched first), end stamp per WG;
-  // k_resolve_delete takes the max (bench cross-check of the HIP-event timing)
-  if (blockIdx.x == 0 && threadIdx.x == 0) D.wg_end[2 * kIntegrateGrid] = __builtin_amdgcn_s_memrealtime();
+  // device-clock duration of the update: start stamp by WG 0 (dispatched first), end = the last
+  // workgroup's arrival (bench cross-check of the HIP-event timing)
+  if (blockIdx.x == 0 && threadIdx.x == 0) st_co(&D.arrive[kArrStart], (unsigned long long)__builtin_amdgcn_s_memrealtime());
   // XCD-aware split (workgroups b and b + 8 share an XCD): group g = blockIdx % 8 takes the g-th
   // contiguous eighth of the block pairs in band order, a compact image region whose pixel
   // records stay resident in that XCD's L2.
@@ -232,267 +301,99 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
     }
     mn = wave_min(mn);
     if (lane == 0) s_min[wave] = mn;
-    __syncthreads();
+    lds_barrier();  // (LDS only: this pair's pool stores stay in flight)
     if (hf == 0 && lane == 0 && b < nvis) {
       const float m2 = fminf(s_min[wave], s_min[wave + 1]);
       if (m2 >= 0.9f) {  // space_carving_kernel threshold (voxel_tsdf.cu:227, :485)
-        const int k = atomicAdd(&D.ctr->n_cand, 1);
-        D.cand[k] = r;
+        const int k = atomicAdd(&s_ncand, 1);
+        if (k < kIntegrateCandBuf) {
+          s_cand[k] = r;
+        } else {  // buffer full (heavy carving): publish this one now
+          const int kg = atomicAdd(&D.ctr->n_cand, 1);
+          const unsigned long long* rv = reinterpret_cast<const unsigned long long*>(&r);
+          unsigned long long* dst = reinterpret_cast<unsigned long long*>(&D.cand[kg]);
+          st_co(&dst[0], rv[0]);
+          st_co(&dst[1], rv[1]);
+          s_ovf = 1;
+        }
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
-  // updated-voxel count: one plain store per workgroup, summed by k_resolve_delete (no atomics)
+  // updated-voxel count: the workgroup's total rides on its arrival (summed by the last arriver)
   const int tot = wave_sum(my_upd);
   if (lane == 0) s_upd[wave] = tot;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    D.wg_upd[blockIdx.x] = s_upd[0] + s_upd[1] + s_upd[2] + s_upd[3];
-    D.wg_end[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+  lds_barrier();
+  const unsigned long long wg_upd = (unsigned long long)(s_upd[0] + s_upd[1] + s_upd[2] + s_upd[3]);
+  // carve candidates: published (agent-scope stores) for the workgroup that resolves the carving at
+  // the end of this launch; only wave 0 publishes, so only it drains its stores before arriving
+  const int nc = min(s_ncand, kIntegrateCandBuf);
+  if (wave == 0 && nc > 0) {
+    int k0 = 0;
+    if (lane == 0) k0 = atomicAdd(&D.ctr->n_cand, nc);
+    k0 = __shfl(k0, 0, 64);
+    if (lane < nc) {
+      const unsigned long long* rv = reinterpret_cast<const unsigned long long*>(&s_cand[lane]);
+      unsigned long long* dst = reinterpret_cast<unsigned long long*>(&D.cand[k0 + lane]);
+      st_co(&dst[0], rv[0]);
+      st_co(&dst[1], rv[1]);
+    }
   }
   TSDF_STAMP(D, 3, 1);
+  // waves that published drain their stores before the workgroup arrives (wave 0: the buffer;
+  // the even waves' lane 0: overflow records)
+  const bool drain = (wave == 0 && nc > 0) || (s_ovf && (wave & 1) == 0);
+  if (arrive_last(D.arrive + kArrIntegrate, wg_upd, &s_last, drain)) integrate_tail(D, P, L);
 }
 template __global__ void k_integrate_t<false>(EngineDev, FrameParams, const FrameArgs*);
 template __global__ void k_integrate_t<true>(EngineDev, FrameParams, const FrameArgs*);
 
 // ---------------------------------------------------------------------------------------------
-// k_resolve_delete: VoxelHashTable::Delete (voxel_hash.cu:122-171) for every carve candidate in
-// hash-entry order (the reference deletes from the entry-ordered visible list). Slot-0 deletes are
-// lock free and touch only their own entry; list-head / list-element deletes lock the key's
-// bucket and only the first of them per bucket proceeds. The two kinds modify disjoint entries,
-// so a whole 1024-candidate round commits at once; ReleaseBlock's stack order is a prefix sum.
-// direct: the test path -- recs[0..*count) are keys in list order, one key per round.
+// k_resolve_delete: the carving resolver (tsdf_resolve.h) as its own one-workgroup launch -- a
+// shard's frame after the candidate all-gather (cands_in: every shard's slot, listed as D.cand --
+// the candidate set of one volume -- so every shard's index takes the same deletes), and the
+// hash-level test path (direct: the keys in list order, one per round).
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kResolveThreads) void k_resolve_delete(EngineDev D,
-                                                                    const VisRec* __restrict__ recs,
-                                                                    const int32_t* __restrict__ count,
-                                                                    int direct) {
-  __shared__ ResolveLds L;
-  __shared__ unsigned long long s_te[kResolveThreads / 64];
-  const int t = threadIdx.x;
-  TSDF_STAMP(D, 4, 0);
-  // every global value the prologue needs is loaded up front, so they share one memory round
-  // trip instead of four dependent ones (counters, per-workgroup sums, candidate count)
-  const int n = *count;
-  uint32_t epoch0 = 0u;
-  int free0 = 0;
-  unsigned long long t_start = 0ull;
-  int nfresh = 0;
-  if (t == 0) {
-    epoch0 = D.ctr->lock_epoch;
-    free0 = D.ctr->free_count;
-    if (!direct) {
-      t_start = D.wg_end[2 * kIntegrateGrid];
-      nfresh = D.ctr->n_fresh;
-    }
-  }
-  int u = 0, bc = 0;
-  unsigned long long te = 0ull;
-  if (!direct) {  // voxels updated by both k_integrate launches: sum of their per-workgroup counts
-    for (int i = t; i < D.integrate_grid; i += kResolveThreads) {
-      u += D.wg_upd[i];
-      te = max(te, D.wg_end[i]);  // device clock of the main launch
-    }
-    if (t < kBands) bc = D.band[t * kBandStride];  // visible = listed by the sweep + created
-  }
-  claims_clear(L);
-  if (t == 0) {
-    L.epoch = epoch0 + 1;
-    D.ctr->lock_epoch = L.epoch;
-    L.sfree = free0;
-    L.nalloc = 0;  // deletions
-  }
-  if (!direct) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) te = max(te, (unsigned long long)__shfl_xor(te, o, 64));
-    if ((t & 63) == 0) s_te[t >> 6] = te;
-    int tot, nband;
-    (void)block_excl_scan(u, L.scan, &tot);  // (its barriers also publish s_te)
-    (void)block_excl_scan(bc, L.scan, &nband);
-    if (t == 0) {
-      unsigned long long tend = 0ull;
-      for (int w = 0; w < kResolveThreads / 64; ++w) tend = max(tend, s_te[w]);
-      D.ctr->last_updated = (unsigned long long)tot;
-      D.ctr->integrate_ticks += tend - t_start;
-      D.ctr->n_vis = nband + nfresh;
-    }
-  }
-  __syncthreads();
-  auto keyf = [&](int i) -> uint32_t { return (uint32_t)recs[i].entry; };
-  const int width = direct ? 1 : stream_prepare(L, n, kNumEntry, keyf);
-  const int nbatch = direct ? n : (n <= kBatch ? (n > 0 ? 1 : 0) : ((n - 1) >> 10) + 1);
-  TSDF_STAMP(D, 4, 1);
-  for (int j = 0; j < nbatch; ++j) {
-    int m;
-    if (direct) {
-      if (t == 0) L.batch[0] = (unsigned long long)(uint32_t)j;
-      m = 1;
-      __syncthreads();
-    } else {
-      m = stream_batch(L, n, width, j, keyf);
-    }
-    for (int base = 0; base < m; base += kResolveThreads) {
-      const bool have = base + t < m;
-      int kind = 0;  // 1 slot 0, 2 list head, 3 list element
-      uint32_t A = 0, prev = 0, cur = 0;
-      Ent ecur = {}, eprev = {};
-      if (have) {
-        const VisRec r = recs[(int)(L.batch[base + t] & 0xFFFFFFFFu)];
-        A = hash_block(r.x, r.y, r.z);
-        const Ent s0 = load_ent(D.table, 2 * A);
-        if (s0.x == r.x && s0.y == r.y && s0.z == r.z && s0.idx >= 0) {
-          kind = 1;
-          cur = 2 * A;
-          ecur = s0;
-        } else {
-          const Ent hd = load_ent(D.table, 2 * A + 1);
-          if (hd.x == r.x && hd.y == r.y && hd.z == r.z && hd.idx >= 0) {
-            kind = 2;
-            prev = 2 * A + 1;
-            eprev = hd;
-            cur = (uint32_t)(prev + (int32_t)hd.off) & kEntryMask;  // element moved into the head
-            ecur = load_ent(D.table, cur);
-          } else {
-            uint32_t last = 2 * A + 1;
-            Ent bl = hd;
-            while (bl.off) {
-              const uint32_t c = (uint32_t)(last + (int32_t)bl.off) & kEntryMask;
-              const Ent bc = load_ent(D.table, c);
-              if (bc.x == r.x && bc.y == r.y && bc.z == r.z && bc.idx >= 0) {
-                kind = 3;
-                prev = last;
-                eprev = bl;
-                cur = c;
-                ecur = bc;
-                break;
-              }
-              last = c;
-              bl = bc;
-            }
-          }
-        }
-        if (kind >= 2) claim(L, A, (uint32_t)t);
-      }
-      __syncthreads();
-      bool ok = false;
-      int32_t released = -1;
-      if (kind == 1) {
-        ok = true;
-      } else if (kind >= 2 && claim_winner(L, A) == (uint32_t)t) {
-        ok = D.lock_tag[A] != L.epoch;
-        D.lock_tag[A] = L.epoch;
-      }
-      if (ok) {
-        if (kind == 1) {  // voxel_hash.cu:126-135
-          released = ecur.idx;
-          store_off_idx(D.table, cur, 0, -1);
-        } else if (kind == 2) {  // :137-152 (cur aliases the head when the list is empty)
-          released = eprev.idx;
-          const int16_t noff = ecur.off ? (int16_t)(eprev.off + ecur.off) : (int16_t)0;
-          store_ent(D.table, prev, ecur.x, ecur.y, ecur.z, noff, ecur.idx);
-          store_off_idx(D.table, cur, 0, -1);
-          // the next list element moved into the head entry: its occupancy bit moves with it
-          // (a shard lists only its own blocks; one volume's head bit simply stays set)
-          if (prev != cur) {
-            if (local_idx(ecur.idx))
-              atomicOr(&D.occ[prev >> 6], 1ull << (prev & 63));
-            else
-              atomicAnd(&D.occ[prev >> 6], ~(1ull << (prev & 63)));
-          }
-        } else {  // :154-170
-          released = ecur.idx;
-          const int16_t noff = ecur.off ? (int16_t)(eprev.off + ecur.off) : (int16_t)0;
-          store_off(D.table, prev, noff);
-          store_off_idx(D.table, cur, 0, -1);
-        }
-        atomicAnd(&D.occ[cur >> 6], ~(1ull << (cur & 63)));
-      }
-      // ReleaseBlock (voxel_mem.cu:54-59) of the blocks this engine holds (a shard deletes every
-      // shard's candidates from its index, and releases only its own pool blocks)
-      const bool rel = ok && local_idx(released);
-      int nok;
-      const int rank = block_excl_scan(rel ? 1 : 0, L.scan, &nok);
-      if (rel) D.heap[L.sfree + rank] = released;
-      claims_clear(L);
-      __syncthreads();
-      if (t == 0) {
-        L.sfree += nok;
-        L.nalloc += nok;
-      }
-      __syncthreads();
-    }
-  }
-  TSDF_STAMP(D, 4, 2);
-  if (t == 0) {
-    D.ctr->free_count = L.sfree;
-    if (!direct) {
-      D.ctr->last_deleted = L.nalloc;
-      D.ctr->total_deleted += (unsigned long long)L.nalloc;
-      D.ctr->total_visible += (unsigned long long)D.ctr->n_vis;
-      D.ctr->total_updated += D.ctr->last_updated;
-      D.ctr->frames += 1ull;
-      D.ctr->n_cand = 0;  // the next frame's lists start empty (its sweep runs before allocation)
-    }
-  }
-  if (!direct && t < kBands) D.band[t * kBandStride] = 0;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Sharded frames: the carve-candidate exchange. k_cand_pack writes this shard's
-// candidates (its own blocks) into its outbox slot; after the all-gather, k_cand_gather lists every
-// shard's slot as the delete resolver's input -- the candidate set of one volume -- so every
-// shard's index takes the same deletes (the resolver sorts by hash entry, the reference's order).
-// One workgroup each (a few hundred candidates per frame).
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_cand_pack(EngineDev D, ShardRec* __restrict__ out, int cap) {
-  const int n = D.ctr->n_cand;
-  for (int i = threadIdx.x; i < min(n, cap); i += blockDim.x) {
-    const VisRec c = D.cand[i];
-    ShardRec r;
-    r.x = c.x;
-    r.y = c.y;
-    r.z = c.z;
-    r.pad = 0;
-    r.val = (uint32_t)c.entry;
-    r.zero = 0u;
-    out[1 + i] = r;
-  }
-  if (threadIdx.x == 0) {
-    ShardRec h{};
-    h.val = (uint32_t)min(n, cap);
-    out[0] = h;
-    if (n > cap) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_SHARD_OVERFLOW
-  }
-}
-
-__global__ __launch_bounds__(1024) void k_cand_gather(EngineDev D, const ShardRec* __restrict__ in, int cap,
-                                                      int nshard) {
+__global__ __launch_bounds__(kRT) void k_resolve_delete(EngineDev D, const VisRec* __restrict__ recs,
+                                                        const int32_t* __restrict__ count, int direct,
+                                                        const ShardRec* __restrict__ cands_in, int cap,
+                                                        int nshard) {
+  __shared__ DeleteLds L;
   __shared__ int s_base[kMaxShards + 1];
-  if (threadIdx.x == 0) {
-    int run = 0;
+  if (cands_in) {
+    if (threadIdx.x == 0) {
+      int run = 0;
+      for (int s = 0; s < nshard; ++s) {
+        s_base[s] = run;
+        run += min((int)cands_in[(size_t)s * (cap + 1)].val, cap);
+      }
+      s_base[nshard] = run;
+      st_co(&D.ctr->n_cand, run);
+    }
+    __syncthreads();
+    unsigned long long* cq = reinterpret_cast<unsigned long long*>(D.cand);
     for (int s = 0; s < nshard; ++s) {
-      s_base[s] = run;
-      run += min((int)in[(size_t)s * (cap + 1)].val, cap);
+      const ShardRec* slot = cands_in + (size_t)s * (cap + 1) + 1;
+      const int n = s_base[s + 1] - s_base[s];
+      for (int i = threadIdx.x; i < n; i += kRT) {
+        const ShardRec r = slot[i];
+        VisRec c;
+        c.x = r.x;
+        c.y = r.y;
+        c.z = r.z;
+        c.pad = 0;
+        c.idx = -1;
+        c.entry = (int32_t)r.val;
+        const unsigned long long* cv = reinterpret_cast<const unsigned long long*>(&c);
+        st_co(&cq[2 * (s_base[s] + i)], cv[0]);
+        st_co(&cq[2 * (s_base[s] + i) + 1], cv[1]);
+      }
     }
-    s_base[nshard] = run;
-    D.ctr->n_cand = run;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
   }
-  __syncthreads();
-  for (int s = 0; s < nshard; ++s) {
-    const ShardRec* slot = in + (size_t)s * (cap + 1) + 1;
-    const int n = s_base[s + 1] - s_base[s];
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-      const ShardRec r = slot[i];
-      VisRec c;
-      c.x = r.x;
-      c.y = r.y;
-      c.z = r.z;
-      c.pad = 0;
-      c.idx = -1;
-      c.entry = (int32_t)r.val;
-      D.cand[s_base[s] + i] = c;
-    }
-  }
+  resolve_delete_wg(D, recs, count, direct, L);
+  if (!direct) frame_end(D);
 }
 
 }  // namespace tsdf

@@ -37,16 +37,14 @@ struct EngineDev {
   // per-frame allocation scratch
   unsigned long long* nk_key;   // kNewKeyCap new-key set
   uint32_t* nk_order;           // kNewKeyCap smallest candidate order per key
-  int32_t* nk_list;             // kNewKeyCap occupied slots
-  unsigned long long* pairs;    // kNewKeyCap (order << 32 | slot) resolver scratch
-  unsigned long long* pkey;     // kNewKeyCap packed key of pairs[i] (one load in the rounds)
+  NkEnt* nk_list;               // kNewKeyCap occupied slots with their keys
+  unsigned long long* pairs;    // max(kNewKeyCap, nblocks): resolver scratch (sort key << 32 | index)
   int32_t* fresh;               // pool indices acquired by the hash-level test path
   // visibility / carving
   VisRec* vis;                  // kBands x nblocks visible blocks (band-major, any order within)
   int32_t* band;                // kBands x kBandStride: record count of each band list
-  VisRec* cand;                 // carve candidates (any order; resolver sorts by entry)
-  int32_t* wg_upd;              // kIntegrateGrid per-workgroup updated-voxel counts
-  unsigned long long* wg_end;   // 2 x kIntegrateGrid + 1: per-WG end stamps, [2 kIntegrateGrid] = start
+  VisRec* cand;                 // max(nblocks, 1024) carve candidates (any order; sorted by entry)
+  unsigned long long* arrive;   // kArriveWords: last-arriver counters of the frame kernels
   VisRec* fresh_vis;            // kNewKeyCap blocks created this frame (k_resolve_alloc frame mode)
   // packed frame
   float4* pixA;                 // {depth, range, w_new, rgb}
@@ -77,29 +75,30 @@ __global__ void k_init_table(int4* table);
 __global__ void k_copy_words(uint32_t* dst, const uint32_t* src, int n);
 __global__ void k_init_heap(int32_t* heap, int n);
 __global__ void k_init_logodds(uint8_t* pool, int nb);
-// per frame (4 launches)
+// last-arriver counters (tsdf_resolve.h arrive_last), one 128-B line each: lines [0, 9) k_ingest_dda,
+// [16, 25) k_integrate, line 32 k_integrate's start stamp
+constexpr int kArrIngest = 0, kArrIntegrate = 16 * 16, kArrStart = 32 * 16, kArriveWords = 33 * 16;
+// per frame (2 launches; the resolvers run in the last workgroup of each)
 constexpr int kVisWorkgroups = kOccWords / 256;  // visibility-sweep workgroups of k_ingest_dda
 template <int TS>  // LDS key-set slots per tile (tsdf_alloc.hip): 1024 for maxs <= 3, else 2048
 __global__ void k_ingest_dda(EngineDev D, FrameParams P, const float* depth, const uint8_t* rgb,
                              const float* ht, const float* lt, int tiles_x, int tiles);
-__global__ void k_resolve_alloc(EngineDev D, FrameParams P, uint32_t range, int frame_mode);
+// standalone one-workgroup resolvers (sharded frames after an exchange; the hash-level test path).
+// keys_in: optional inbox of nshard key slots merged into the new-key set first.
+__global__ void k_resolve_alloc(EngineDev D, FrameParams P, uint32_t range, int frame_mode,
+                                const ShardRec* keys_in, int cap, int nshard);
 template <bool Graph>
 __global__ void k_integrate_t(EngineDev D, FrameParams P, const FrameArgs* A);
 // graph-captured forms of the frame kernels: identical bodies, arguments from FrameArgs
 template <int TS>
 __global__ void k_ingest_dda_g(EngineDev D, const FrameArgs* A);
-__global__ void k_resolve_alloc_g(EngineDev D, const FrameArgs* A);
 __global__ void k_raycast_g(EngineDev D, const FrameArgs* A);
-__global__ void k_resolve_delete(EngineDev D, const VisRec* recs, const int32_t* count,
-                                 int direct);
+// cands_in: optional inbox of nshard carve-candidate slots (then recs / count are D.cand / n_cand)
+__global__ void k_resolve_delete(EngineDev D, const VisRec* recs, const int32_t* count, int direct,
+                                 const ShardRec* cands_in, int cap, int nshard);
 // hash-level test path
 __global__ void k_keys_to_newset(EngineDev D, const int16_t* keys, int n);
-// sharded frames: key exchange and carve-candidate exchange
 constexpr int kMaxShards = 64;
-__global__ void k_key_pack(EngineDev D, ShardRec* out, int cap);
-__global__ void k_key_merge(EngineDev D, const ShardRec* in, int cap);
-__global__ void k_cand_pack(EngineDev D, ShardRec* out, int cap);
-__global__ void k_cand_gather(EngineDev D, const ShardRec* in, int cap, int nshard);
 // DISINFSystem::feed_rgbd_frame preprocessing (tsdf_frontend.hip); grid (ceil(w / 64), ceil(h / 4))
 __global__ void k_rgbd_half(const uint8_t* rgb, const uint16_t* depth, const uint8_t* mask, int W,
                             int H, float alpha, uint8_t* rgb_out, float* depth_out);

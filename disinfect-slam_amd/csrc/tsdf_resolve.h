@@ -1,0 +1,760 @@
+// tsdf_resolve.h -- the ordered allocation and carving resolvers as ONE-WORKGROUP device functions
+// (256 threads, <= 25 KiB of LDS).
+//
+// They run in two places:
+//  * fused into the frame kernels: the workgroup that arrives last at the end of k_ingest_dda runs
+//    the allocation resolver, the one that arrives last at the end of k_integrate runs the carving
+//    resolver -- so one frame is two launches (two kernel boundaries) instead of four;
+//  * as their own single-workgroup kernels (k_resolve_alloc / k_resolve_delete) where an exchange
+//    sits between the phases (sharded frames) and for the hash-level test path.
+//
+// Semantics (the canonical linearisation of the reference's racy launches):
+//  * allocation: VoxelHashTable::Allocate (voxel_hash.cu:58-120) of every new key in candidate
+//    order, <= 1 structural change per bucket per launch (losers dropped), AquireBlock pops
+//    heap[free - 1] in commit order (voxel_mem.cu:37-52);
+//  * carving: VoxelHashTable::Delete (voxel_hash.cu:122-171) of every candidate in hash-entry order;
+//    slot-0 deletes are lock free, list-head / element deletes lock the bucket.
+// Keys are processed in batches of <= kRB in order (a histogram threshold search over the global
+// scratch picks each batch when a launch has more); within a batch, rounds of 256 keys are
+// evaluated speculatively against the table, every key claims the buckets it would lock in an LDS
+// claim table (smallest rank wins), and the longest prefix of keys that won all their claims
+// commits (the first key always does).
+//
+// Cross-workgroup data of a fused launch (the new-key list, carve candidates) is published with
+// agent-scope atomic stores (global_store ... sc1) and read back with agent-scope atomic loads
+// (global_load ... sc1): the workgroup that arrives last has no kernel boundary between it and the
+// producers.
+#pragma once
+
+#include "tsdf_block.h"
+#include "tsdf_kernels.h"
+
+namespace tsdf {
+
+constexpr int kRT = 256;        // resolver workgroup size (= the ingest / integrate workgroup)
+constexpr int kRB = 2 * kRT;    // keys / candidates per ordered batch
+constexpr int kRHist = 1024;    // threshold-search bins (launches with more than kRB inputs)
+constexpr int kRClaim = 1024;   // claim slots, packed (bucket + 1) << 9 | rank (<= 512 per round)
+constexpr int kRLockA = 2048;   // LDS lock set of an allocation launch with <= kRLockKeysA keys
+constexpr int kRLockKeysA = 768;
+constexpr int kRLockD = 1024;   // LDS lock set of a carving launch with <= kRLockKeysD candidates
+constexpr int kRLockKeysD = 768;
+static_assert(kRT == 256, "resolver geometry");
+
+// cross-workgroup publish / consume inside one launch (agent scope, relaxed)
+template <class T>
+__device__ __forceinline__ T ld_co(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void st_co(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Last-arriver detection: every workgroup of the launch arrives once at its end; the function
+// returns true (in all threads) in the workgroup that arrives last. Arrivals go to 8 counters by
+// blockIdx % 8 (one per XCD under round-robin placement: no single hot word), each counter's last
+// arriver to a top counter. The high 24 bits of a counter count arrivals, the low 40 accumulate
+// `payload` (k_integrate: its updated-voxel count). Each thread drains its own memory operations
+// first, so everything it published (st_co) is complete before its workgroup arrives.
+// ---------------------------------------------------------------------------------------------
+constexpr int kArrLine = 16;  // u64 per 128-B line
+// drain: this wave published data (wave-uniform); other waves' outstanding stores stay in flight
+__device__ __forceinline__ bool arrive_last(unsigned long long* words, unsigned long long payload,
+                                            int* s_flag, bool drain = true) {
+  if (drain) __builtin_amdgcn_s_waitcnt(0);
+  lds_barrier();
+  if (threadIdx.x == 0) {
+    const uint32_t g = blockIdx.x & 7u, ngrp = gridDim.x < 8u ? gridDim.x : 8u;
+    const uint32_t expect = (gridDim.x - g + 7u) / 8u;
+    const unsigned long long old = __hip_atomic_fetch_add(&words[g * kArrLine], (1ull << 40) | payload,
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = 0;
+    if ((uint32_t)(old >> 40) + 1u == expect) {
+      const unsigned long long top = __hip_atomic_fetch_add(&words[8 * kArrLine], 1ull, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+      last = (uint32_t)top + 1u == ngrp;
+    }
+    *s_flag = last;
+  }
+  lds_barrier();
+  return *s_flag != 0;
+}
+// the last arriver, thread 0: the sum of the payloads; the counters are zeroed for the next launch
+__device__ __forceinline__ unsigned long long arrive_collect(unsigned long long* words) {
+  unsigned long long sum = 0ull;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) sum += ld_co(&words[g * kArrLine]) & ((1ull << 40) - 1ull);
+#pragma unroll
+  for (int g = 0; g < 9; ++g) st_co(&words[g * kArrLine], 0ull);
+  return sum;
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS helpers
+// ---------------------------------------------------------------------------------------------
+// claim table: slot = (bucket + 1) << 9 | rank; the smallest rank per bucket wins
+__device__ __forceinline__ void claim2(uint32_t* C, uint32_t bucket, uint32_t rank) {
+  uint32_t h = mix32(bucket) & (kRClaim - 1);
+  const uint32_t k = ((bucket + 1u) << 9) | rank;
+  for (int p = 0; p < kRClaim; ++p) {
+    const uint32_t prev = atomicCAS(&C[h], 0u, k);
+    if (prev == 0u) return;
+    if ((prev >> 9) == bucket + 1u) {
+      atomicMin(&C[h], k);
+      return;
+    }
+    h = (h + 1) & (kRClaim - 1);
+  }
+}
+__device__ __forceinline__ uint32_t claim2_winner(const uint32_t* C, uint32_t bucket) {
+  uint32_t h = mix32(bucket) & (kRClaim - 1);
+  for (int p = 0; p < kRClaim; ++p) {
+    const uint32_t v = C[h];
+    if ((v >> 9) == bucket + 1u) return v & 511u;
+    if (v == 0u) break;
+    h = (h + 1) & (kRClaim - 1);
+  }
+  return 0xFFFFFFFFu;
+}
+// VoxelHashTable's bucket lock within one launch, LDS form: true if this call took it
+template <int N>
+__device__ __forceinline__ bool lock_take2(uint32_t* S, uint32_t bucket) {
+  uint32_t h = mix32(bucket ^ 0x9E3779B9u) & (N - 1);
+  const uint32_t k = bucket + 1u;
+  for (int p = 0; p < N; ++p) {
+    const uint32_t prev = atomicCAS(&S[h], 0u, k);
+    if (prev == 0u) return true;
+    if (prev == k) return false;
+    h = (h + 1) & (N - 1);
+  }
+  return false;
+}
+template <int N>
+__device__ __forceinline__ bool lock_held(const uint32_t* S, uint32_t bucket) {
+  uint32_t h = mix32(bucket ^ 0x9E3779B9u) & (N - 1);
+  const uint32_t k = bucket + 1u;
+  for (int p = 0; p < N; ++p) {
+    const uint32_t v = S[h];
+    if (v == k) return true;
+    if (v == 0u) return false;
+    h = (h + 1) & (N - 1);
+  }
+  return false;
+}
+// HBM form (launches with more keys than the LDS set holds): "locked" == this launch's epoch
+__device__ __forceinline__ bool lock_take_hbm(uint32_t* tags, uint32_t bucket, uint32_t epoch) {
+  if (tags[bucket] == epoch) return false;
+  tags[bucket] = epoch;
+  return true;
+}
+
+// exclusive scan over the 256-thread workgroup; scratch >= 4 ints
+__device__ __forceinline__ int wg_excl_scan(int v, int* scratch, int* total) {
+  const int w = threadIdx.x >> 6;
+  const int incl = wave_incl_scan(v);
+  if (lane_id() == 63) scratch[w] = incl;
+  lds_barrier();
+  const int s0 = scratch[0], s1 = scratch[1], s2 = scratch[2], s3 = scratch[3];
+  lds_barrier();
+  *total = s0 + s1 + s2 + s3;
+  const int before = (w > 0 ? s0 : 0) + (w > 1 ? s1 : 0) + (w > 2 ? s2 : 0);
+  return before + incl - v;
+}
+
+// ascending sort of a[0..m) (m <= kRB, unique values) by rank counting: each thread ranks its two
+// elements against all m with broadcast LDS reads
+__device__ __forceinline__ void rank_sort(unsigned long long* a, unsigned long long* tmp, int m) {
+  const int t = threadIdx.x;
+  const unsigned long long x0 = t < m ? a[t] : ~0ull;
+  const unsigned long long x1 = t + kRT < m ? a[t + kRT] : ~0ull;
+  // the sort keys' high words are unique: compare those, two elements per 16-B broadcast read
+  const uint32_t h0 = (uint32_t)(x0 >> 32), h1 = (uint32_t)(x1 >> 32);
+  if (t == 0 && (m & 1)) a[m] = ~0ull;  // pad to pairs (a has kRB + 2 entries)
+  lds_barrier();
+  const uint4* a4 = reinterpret_cast<const uint4*>(a);
+  int r0 = 0, r1 = 0;
+  const int np = (m + 1) >> 1;
+  int j = 0;
+  for (; j + 8 <= np; j += 8) {  // 8 reads in flight per step (a dependent LDS read is ~50 cycles)
+    uint4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = a4[j + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      r0 += (v[u].y < h0) + (v[u].w < h0);
+      r1 += (v[u].y < h1) + (v[u].w < h1);
+    }
+  }
+  for (; j < np; ++j) {
+    const uint4 v = a4[j];
+    r0 += (v.y < h0) + (v.w < h0);
+    r1 += (v.y < h1) + (v.w < h1);
+  }
+  if (t < m) tmp[r0] = x0;
+  if (t + kRT < m) tmp[r1] = x1;
+  lds_barrier();
+  if (t < m) a[t] = tmp[t];
+  if (t + kRT < m) a[t + kRT] = tmp[t + kRT];
+  lds_barrier();
+}
+
+// Threshold search for multi-batch launches: keys[i] >> 32 (unique in [lo, range)) for i < n in
+// global scratch; returns thr > lo with count(lo <= key < thr) in [1, kRB] (some key remains).
+__device__ uint32_t batch_threshold(const unsigned long long* __restrict__ keys, int n, uint32_t lo,
+                                    uint32_t range, uint32_t* hist, int* scratch) {
+  uint32_t hi = range;
+  for (;;) {
+    const uint32_t w = (hi - lo + kRHist - 1) / kRHist;
+    for (int i = threadIdx.x; i < kRHist; i += kRT) hist[i] = 0u;
+    lds_barrier();
+    for (int i = threadIdx.x; i < n; i += kRT) {
+      const uint32_t o = (uint32_t)(keys[i] >> 32);
+      if (o >= lo && o < hi) atomicAdd(&hist[(o - lo) / w], 1u);
+    }
+    lds_barrier();
+    // inclusive prefix of the 1024 bins, 4 per thread
+    uint32_t c[4];
+    int local = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c[k] = hist[threadIdx.x * 4 + k];
+      local += (int)c[k];
+    }
+    int tot;
+    int run = wg_excl_scan(local, scratch, &tot);
+    // largest bin j whose inclusive prefix <= kRB
+    int best = -1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      run += (int)c[k];
+      if (run <= kRB) best = threadIdx.x * 4 + k;
+    }
+    lds_barrier();
+    if (threadIdx.x == 0) scratch[4] = -1;
+    lds_barrier();
+    if (best >= 0) atomicMax(&scratch[4], best);
+    lds_barrier();
+    const int j = scratch[4];
+    lds_barrier();
+    if (j >= 0) {
+      const unsigned long long thr = (unsigned long long)lo + (unsigned long long)(j + 1) * w;
+      return thr > hi ? hi : (uint32_t)thr;
+    }
+    hi = lo + w;  // the first bin alone holds more than kRB: narrow to it (w shrinks each time)
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Allocation resolver
+// ---------------------------------------------------------------------------------------------
+struct AllocLds {
+  alignas(16) unsigned long long batch[kRB + 2];  // (order << 32) | hint << 9 | p, ascending (+ pad)
+  unsigned long long bkey[kRB];   // packed key at position p
+  int32_t bslot[kRB];             // its new-key-set slot
+  int32_t heap_top[kRB];          // heap_top[i] = heap[free0 - 1 - i]
+  union {
+    uint32_t claim[kRClaim];
+    uint32_t hist[kRHist];
+    unsigned long long tmp[kRB];
+  } u;
+  uint32_t lock[kRLockA];
+  int scan[8];
+  int first_dirty, base, sfree, nfresh, nalloc, changed, m;
+};
+// batch low word: p (9 bits) | hint: bit 9 slot 0 empty, bit 10 slot 1 empty, bit 11 hint valid,
+// bits 16..31 slot 1's list offset -- the key's bucket as the prologue loaded it (the table as the
+// launch found it: valid until the first commit)
+constexpr uint32_t kHintS0 = 1u << 9, kHintS1 = 1u << 10, kHintValid = 1u << 11;
+
+// one key of an allocation round (registers)
+struct AKey {
+  bool have;
+  int kind, slot, p;  // kind 1: SLOT(B, slot); 2: APPEND(tail T, empty slot-0 entry E)
+  uint32_t B, T, E;
+  int16_t x, y, z;
+};
+
+// frame_mode 1: new blocks this engine holds are listed in D.fresh_vis (flagged fresh, visible this
+// frame); 0 (hash-level test path): their pool indices in D.fresh for k_fresh_init.
+__device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint32_t range, int frame_mode,
+                                 AllocLds& L) {
+  const int t = threadIdx.x;
+  TSDF_STAMP(D, 1, 0);
+  // ---- prologue, round trip 1: counters and (speculatively) the first kRB list entries ----
+  const int n = ld_co(&D.ctr->nk_count);
+  const int free0 = D.ctr->free_count;
+  const uint32_t epoch0 = D.ctr->lock_epoch;
+  unsigned long long k0 = ld_co(&D.nk_list[t].key), k1 = ld_co(&D.nk_list[t + kRT].key);
+  int32_t h0 = (int32_t)ld_co(&D.nk_list[t].slot), h1 = (int32_t)ld_co(&D.nk_list[t + kRT].slot);
+  const bool single = n <= kRB;
+  const bool lds_locks = n <= kRLockKeysA;
+  const uint32_t epoch = epoch0 + 1u;
+  if (lds_locks)
+    for (int i = t; i < kRLockA; i += kRT) L.lock[i] = 0u;
+  if (t == 0) {
+    D.ctr->lock_epoch = epoch;
+    L.sfree = free0;
+    L.nfresh = 0;
+    L.nalloc = 0;
+    L.changed = 0;
+  }
+  // ---- round trip 2: candidate orders, the keys' buckets, the free-stack top ----
+  {
+    const int npre = min(min(n, kRB), max(free0, 0));
+    for (int i = t; i < npre; i += kRT) L.heap_top[i] = D.heap[free0 - 1 - i];
+  }
+  if (single) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int p = t + r * kRT;
+      if (p < n) {
+        const unsigned long long key = r ? k1 : k0;
+        const int32_t h = r ? h1 : h0;
+        int16_t x, y, z;
+        unpack_key(key, x, y, z);
+        const uint32_t B = hash_block(x, y, z);
+        const uint32_t ord = ld_co(&D.nk_order[h]);
+        const Ent s0 = load_ent(D.table, 2 * B), s1 = load_ent(D.table, 2 * B + 1);
+        const uint32_t hint = (s0.idx < 0 ? kHintS0 : 0u) | (s1.idx < 0 ? kHintS1 : 0u) | kHintValid |
+                              ((uint32_t)(uint16_t)s1.off << 16);
+        L.bkey[p] = key;
+        L.bslot[p] = h;
+        L.batch[p] = ((unsigned long long)ord << 32) | hint | (uint32_t)p;
+      }
+    }
+  } else {
+    // scratch of every key: (order << 32) | list index, for the batch threshold search
+    for (int i = t; i < n; i += kRT) {
+      const int32_t h = (int32_t)ld_co(&D.nk_list[i].slot);
+      D.pairs[i] = ((unsigned long long)ld_co(&D.nk_order[h]) << 32) | (uint32_t)i;
+    }
+  }
+  if (single) lds_barrier(); else __syncthreads();  // (D.pairs: global)
+  TSDF_STAMP(D, 1, 1);
+  uint32_t lo = 0u;
+  int done = 0;
+  while (done < n) {
+    int m;
+    uint32_t thr = 0xFFFFFFFFu;
+    if (single) {
+      m = n;
+    } else {
+      if (n - done > kRB) thr = batch_threshold(D.pairs, n, lo, range, L.u.hist, L.scan);
+      // gather the batch [lo, thr) into LDS (list order; the sort below orders it)
+      if (t == 0) L.m = 0;
+      lds_barrier();
+      for (int i = t; i < n; i += kRT) {
+        const unsigned long long pr = D.pairs[i];
+        const uint32_t o = (uint32_t)(pr >> 32);
+        if (o >= lo && o < thr) {
+          const int p = atomicAdd(&L.m, 1);
+          const int li = (int)(pr & 0xFFFFFFFFu);
+          L.bkey[p] = ld_co(&D.nk_list[li].key);
+          L.bslot[p] = (int32_t)ld_co(&D.nk_list[li].slot);
+          L.batch[p] = (pr & 0xFFFFFFFF00000000ull) | (uint32_t)p;  // no hint: load the bucket
+        }
+      }
+      lds_barrier();
+      m = L.m;
+    }
+    rank_sort(L.batch, L.u.tmp, m);
+    TSDF_STAMP(D, 1, 2);
+    if (t == 0) L.base = 0;
+    lds_barrier();
+    while (L.base < m) {
+      // one round: the next min(kRB, m - base) keys in order, two per thread (ranks t, t + kRT)
+      const int base = L.base;
+      const int span = min(kRB, m - base);
+      for (int i = t; i < kRClaim; i += kRT) L.u.claim[i] = 0u;
+      if (t == 0) L.first_dirty = kRB;
+      lds_barrier();
+      AKey k[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        k[r] = AKey{};
+        const int rank = t + r * kRT;
+        if (rank < span) {
+          k[r].have = true;
+          const uint32_t lw = (uint32_t)L.batch[base + rank];
+          k[r].p = (int)(lw & 511u);
+          unpack_key(L.bkey[k[r].p], k[r].x, k[r].y, k[r].z);
+          const uint32_t B = hash_block(k[r].x, k[r].y, k[r].z);
+          k[r].B = B;
+          // the prologue's view of the bucket holds unless a commit of this launch wrote into it,
+          // and every such commit locked it
+          const bool fresh = (lw & kHintValid) && (lds_locks ? !lock_held<kRLockA>(L.lock, B) : !L.changed);
+          bool e0, e1;
+          int16_t off1;
+          if (fresh) {
+            e0 = (lw & kHintS0) != 0;
+            e1 = (lw & kHintS1) != 0;
+            off1 = (int16_t)(lw >> 16);
+          } else {
+            const Ent s0 = load_ent(D.table, 2 * B), s1 = load_ent(D.table, 2 * B + 1);
+            e0 = s0.idx < 0;
+            e1 = s1.idx < 0;
+            off1 = s1.off;
+          }
+          if (e0 || e1) {
+            k[r].kind = 1;
+            k[r].slot = e0 ? 0 : 1;
+            claim2(L.u.claim, B, (uint32_t)rank);
+          } else {  // APPEND: tail T of the list from slot 1, first empty slot-0 entry E after it
+            k[r].kind = 2;
+            uint32_t last = 2 * B + 1;
+            int16_t off = off1;
+            while (off) {
+              last = (uint32_t)(last + (int32_t)off) & kEntryMask;
+              off = load_ent(D.table, last).off;
+            }
+            k[r].T = last;
+            uint32_t nx = last;
+            for (uint32_t q = 0; q < kNumEntry; ++q) {
+              nx = (nx + 1) & kEntryMask;
+              if ((nx & 1u) == 0u && load_ent(D.table, nx).idx < 0) break;
+            }
+            k[r].E = nx;
+            claim2(L.u.claim, last >> 1, (uint32_t)rank);
+            claim2(L.u.claim, nx >> 1, (uint32_t)rank);
+          }
+        }
+      }
+      lds_barrier();
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        if (!k[r].have) continue;
+        const uint32_t rank = (uint32_t)(t + r * kRT);
+        const bool clean = k[r].kind == 1 ? claim2_winner(L.u.claim, k[r].B) == rank
+                                          : (claim2_winner(L.u.claim, k[r].T >> 1) == rank &&
+                                             claim2_winner(L.u.claim, k[r].E >> 1) == rank);
+        if (!clean) atomicMin(&L.first_dirty, (int)rank);
+      }
+      lds_barrier();
+      const int first_dirty = L.first_dirty;
+      bool ok[2] = {false, false}, mine[2] = {false, false};
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        if (!k[r].have || t + r * kRT >= first_dirty) continue;
+        // atomicExch(&bucket_locks_[b], LOCKED) == FREE, per launch; the keys committing together
+        // won all their claims, so they take distinct buckets
+        if (k[r].kind == 1) {
+          ok[r] = lds_locks ? lock_take2<kRLockA>(L.lock, k[r].B) : lock_take_hbm(D.lock_tag, k[r].B, epoch);
+        } else {
+          const uint32_t Lb = k[r].T >> 1, C = k[r].E >> 1;
+          if (lds_locks ? lock_take2<kRLockA>(L.lock, Lb) : lock_take_hbm(D.lock_tag, Lb, epoch))
+            ok[r] = lds_locks ? lock_take2<kRLockA>(L.lock, C) : lock_take_hbm(D.lock_tag, C, epoch);
+        }
+        // Sharded volume: every shard commits every key's table change (the replicated index), and
+        // only the key's owner pops a pool block; the others store kForeignIdx.
+        mine[r] = ok[r] && (P.shard_count <= 1 || brick_owner(k[r].x, k[r].y, k[r].z, (uint32_t)P.shard_count) ==
+                                                      (uint32_t)P.shard_index);
+      }
+      // pool pops in key order: rank among this round's owned commits (first half, then second)
+      int tot;
+      const int ex = wg_excl_scan((mine[0] ? 1 : 0) | (mine[1] ? 1 << 16 : 0), L.scan, &tot);
+      const int prank[2] = {ex & 0xFFFF, (tot & 0xFFFF) + (ex >> 16)};
+      const int nmine = (tot & 0xFFFF) + (tot >> 16);
+      const int free_now = L.sfree;
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        if (!k[r].have) continue;
+        if (ok[r]) {
+          int32_t idx = kForeignIdx;
+          bool insert = true;
+          if (mine[r]) {
+            const int hi = free_now - 1 - prank[r];
+            if (hi < 0) {
+              atomicOr(&D.ctr->status, 1u);  // TSDF_STATUS_POOL_EXHAUSTED
+              // one volume drops the insert; a shard keeps a voxel-less entry so that every
+              // shard's index stays the same
+              insert = P.shard_count > 1;
+            } else {
+              const int top = free0 - 1 - hi;  // pops so far this launch + rank
+              idx = top < kRB ? L.heap_top[top] : D.heap[hi];
+            }
+          }
+          if (insert) {
+            uint32_t e;
+            if (k[r].kind == 1) {
+              e = 2 * k[r].B + (uint32_t)k[r].slot;
+            } else {
+              const uint32_t T = k[r].T, E = k[r].E;
+              const uint32_t wrap = E > T ? 0u : kNumEntry;
+              store_off(D.table, T, (int16_t)(E + wrap - T));
+              e = E;
+            }
+            store_ent(D.table, e, k[r].x, k[r].y, k[r].z, 0, idx);
+            L.changed = 1;  // (a benign race: every writer stores 1)
+            if (local_idx(idx)) {  // the occupancy bitmap lists the blocks this engine holds
+              atomicOr(&D.occ[e >> 6], 1ull << (e & 63));
+              if (frame_mode) {
+                // a new block has all 8 corners in view, so it is visible this frame: listed for
+                // k_integrate after the blocks the visibility sweep listed, flagged fresh so it
+                // starts from AquireBlock's state
+                VisRec vr;
+                vr.x = k[r].x;
+                vr.y = k[r].y;
+                vr.z = k[r].z;
+                vr.pad = 1;
+                vr.idx = idx;
+                vr.entry = (int32_t)e;
+                D.fresh_vis[L.nfresh + prank[r]] = vr;
+              } else {
+                D.fresh[L.nfresh + prank[r]] = idx;
+              }
+            }
+          }
+        }
+        if (t + r * kRT < first_dirty) {  // processed: the key-set slot is empty for the next frame
+          D.nk_key[L.bslot[k[r].p]] = 0ull;
+          D.nk_order[L.bslot[k[r].p]] = 0xFFFFFFFFu;
+        }
+      }
+      // the table writes must be visible to the next round's loads; after the launch's last round
+      // nothing here reads them (the next kernel does, after the boundary)
+      if (first_dirty < span || base + span < m || done + m < n) __syncthreads(); else lds_barrier();
+      if (t == 0) {
+        const int used = nmine < free_now ? nmine : (free_now > 0 ? free_now : 0);
+        L.sfree = free_now - used;
+        L.nfresh += used;
+        L.nalloc += used;
+        L.base = base + (first_dirty < span ? first_dirty : span);
+      }
+      lds_barrier();
+    }
+    done += m;
+    lo = thr;
+  }
+  TSDF_STAMP(D, 1, 3);
+  if (t == 0) {
+    D.ctr->free_count = L.sfree;
+    D.ctr->n_fresh = L.nfresh;
+    D.ctr->nk_count = 0;
+    if (frame_mode) {
+      D.ctr->last_alloc = L.nalloc;
+      D.ctr->last_new_keys = n;
+      D.ctr->total_alloc += (unsigned long long)L.nalloc;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Carving resolver
+// ---------------------------------------------------------------------------------------------
+struct DeleteLds {
+  alignas(16) unsigned long long batch[kRB + 2];  // (entry << 32) | hint << 9 | p, ascending (+ pad)
+  unsigned long long bkey[kRB];   // packed key at position p
+  int32_t bidx0[kRB];             // slot 0's pool index when the hint says slot 0 holds the key
+  union {
+    uint32_t claim[kRClaim];
+    uint32_t hist[kRHist];
+    unsigned long long tmp[kRB];
+  } u;
+  uint32_t lock[kRLockD];
+  int scan[8];
+  int sfree, ndel, changed, m;
+};
+constexpr uint32_t kHintSlot0 = 1u << 9;  // (with kHintValid) slot 0 holds the key
+
+// Carve candidates recs[0..*count) (VisRec: key and hash entry; any order). direct: the hash-level
+// test path -- the candidates in list order, one per round (VoxelHashTable::Delete's launch of
+// voxel_hash_test.cu).
+__device__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__ recs,
+                                  const int32_t* __restrict__ count, int direct, DeleteLds& L) {
+  const int t = threadIdx.x;
+  TSDF_STAMP(D, 4, 0);
+  const int n = ld_co(count);
+  const int free0 = D.ctr->free_count;
+  const uint32_t epoch = D.ctr->lock_epoch + 1u;
+  const bool single = n <= kRB && !direct;
+  const bool lds_locks = n <= kRLockKeysD;
+  const unsigned long long* rq = reinterpret_cast<const unsigned long long*>(recs);
+  unsigned long long a0 = 0, b0 = 0, a1 = 0, b1 = 0;  // records t, t + kRT (speculative)
+  if (single) {
+    a0 = ld_co(&rq[2 * t]);
+    b0 = ld_co(&rq[2 * t + 1]);
+    a1 = ld_co(&rq[2 * (t + kRT)]);
+    b1 = ld_co(&rq[2 * (t + kRT) + 1]);
+  }
+  if (lds_locks)
+    for (int i = t; i < kRLockD; i += kRT) L.lock[i] = 0u;
+  if (t == 0) {
+    D.ctr->lock_epoch = epoch;
+    L.sfree = free0;
+    L.ndel = 0;
+    L.changed = 0;
+  }
+  if (single) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int p = t + r * kRT;
+      if (p < n) {
+        const unsigned long long a = r ? a1 : a0, b = r ? b1 : b0;
+        const int16_t x = (int16_t)(a & 0xFFFF), y = (int16_t)((a >> 16) & 0xFFFF),
+                      z = (int16_t)((a >> 32) & 0xFFFF);
+        const uint32_t entry = (uint32_t)(b >> 32);
+        const Ent s0 = load_ent(D.table, 2 * hash_block(x, y, z));
+        const bool in0 = s0.x == x && s0.y == y && s0.z == z && s0.idx >= 0;
+        L.bkey[p] = pack_key(x, y, z);
+        L.bidx0[p] = s0.idx;
+        L.batch[p] = ((unsigned long long)entry << 32) | (in0 ? kHintSlot0 : 0u) | kHintValid | (uint32_t)p;
+      }
+    }
+  } else if (!direct) {
+    for (int i = t; i < n; i += kRT)
+      D.pairs[i] = ((unsigned long long)(uint32_t)ld_co(&recs[i].entry) << 32) | (uint32_t)i;
+  }
+  if (single || direct) lds_barrier(); else __syncthreads();  // (D.pairs: global)
+  TSDF_STAMP(D, 4, 1);
+  uint32_t lo = 0u;
+  int done = 0;
+  while (done < n) {
+    int m;
+    uint32_t thr = 0xFFFFFFFFu;
+    if (single) {
+      m = n;
+      rank_sort(L.batch, L.u.tmp, m);
+    } else if (direct) {  // one candidate (list order) per round
+      if (t == 0) {
+        const VisRec r = recs[done];
+        L.bkey[0] = pack_key(r.x, r.y, r.z);
+        L.batch[0] = 0ull;
+      }
+      lds_barrier();
+      m = 1;
+    } else {
+      if (n - done > kRB) thr = batch_threshold(D.pairs, n, lo, kNumEntry, L.u.hist, L.scan);
+      if (t == 0) L.m = 0;
+      lds_barrier();
+      for (int i = t; i < n; i += kRT) {
+        const unsigned long long pr = D.pairs[i];
+        const uint32_t o = (uint32_t)(pr >> 32);
+        if (o >= lo && o < thr) {
+          const int p = atomicAdd(&L.m, 1);
+          const int li = (int)(pr & 0xFFFFFFFFu);
+          const unsigned long long a = ld_co(&rq[2 * li]);
+          L.bkey[p] = pack_key((int16_t)(a & 0xFFFF), (int16_t)((a >> 16) & 0xFFFF), (int16_t)((a >> 32) & 0xFFFF));
+          L.batch[p] = (pr & 0xFFFFFFFF00000000ull) | (uint32_t)p;
+        }
+      }
+      lds_barrier();
+      m = L.m;
+      rank_sort(L.batch, L.u.tmp, m);
+    }
+    // rounds of 256 candidates in entry order; the deletes of a round touch disjoint entries (slot-0
+    // deletes their own, list deletes one per bucket), so a whole round commits at once
+    for (int base = 0; base < m; base += kRT) {
+      for (int i = t; i < kRClaim; i += kRT) L.u.claim[i] = 0u;
+      lds_barrier();
+      const bool have = base + t < m;
+      int kind = 0;  // 1 slot 0, 2 list head, 3 list element
+      uint32_t A = 0, prev = 0, cur = 0;
+      Ent ecur = {}, eprev = {};
+      if (have) {
+        const unsigned long long v = L.batch[base + t];
+        const uint32_t lw = (uint32_t)v;
+        const int p = (int)(lw & 511u);
+        int16_t x, y, z;
+        unpack_key(L.bkey[p], x, y, z);
+        A = hash_block(x, y, z);
+        if ((lw & kHintValid) && (lw & kHintSlot0) && !L.changed) {  // slot 0 as loaded
+          kind = 1;
+          cur = 2 * A;
+          ecur.idx = L.bidx0[p];
+        } else {
+          const Ent s0 = load_ent(D.table, 2 * A);
+          if (s0.x == x && s0.y == y && s0.z == z && s0.idx >= 0) {
+            kind = 1;
+            cur = 2 * A;
+            ecur = s0;
+          } else {
+            const Ent hd = load_ent(D.table, 2 * A + 1);
+            if (hd.x == x && hd.y == y && hd.z == z && hd.idx >= 0) {
+              kind = 2;
+              prev = 2 * A + 1;
+              eprev = hd;
+              cur = (uint32_t)(prev + (int32_t)hd.off) & kEntryMask;  // element moved into the head
+              ecur = load_ent(D.table, cur);
+            } else {
+              uint32_t last = 2 * A + 1;
+              Ent bl = hd;
+              while (bl.off) {
+                const uint32_t c = (uint32_t)(last + (int32_t)bl.off) & kEntryMask;
+                const Ent bc = load_ent(D.table, c);
+                if (bc.x == x && bc.y == y && bc.z == z && bc.idx >= 0) {
+                  kind = 3;
+                  prev = last;
+                  eprev = bl;
+                  cur = c;
+                  ecur = bc;
+                  break;
+                }
+                last = c;
+                bl = bc;
+              }
+            }
+          }
+        }
+        if (kind >= 2) claim2(L.u.claim, A, (uint32_t)t);
+      }
+      lds_barrier();
+      bool ok = false;
+      int32_t released = -1;
+      if (kind == 1) {
+        ok = true;
+      } else if (kind >= 2 && claim2_winner(L.u.claim, A) == (uint32_t)t) {
+        ok = lds_locks ? lock_take2<kRLockD>(L.lock, A) : lock_take_hbm(D.lock_tag, A, epoch);
+      }
+      if (ok) {
+        if (kind == 1) {  // voxel_hash.cu:126-135
+          released = ecur.idx;
+          store_off_idx(D.table, cur, 0, -1);
+        } else if (kind == 2) {  // :137-152 (cur aliases the head when the list is empty)
+          released = eprev.idx;
+          const int16_t noff = ecur.off ? (int16_t)(eprev.off + ecur.off) : (int16_t)0;
+          store_ent(D.table, prev, ecur.x, ecur.y, ecur.z, noff, ecur.idx);
+          store_off_idx(D.table, cur, 0, -1);
+          // the next list element moved into the head entry: its occupancy bit moves with it
+          // (a shard lists only its own blocks; one volume's head bit simply stays set)
+          if (prev != cur) {
+            if (local_idx(ecur.idx))
+              atomicOr(&D.occ[prev >> 6], 1ull << (prev & 63));
+            else
+              atomicAnd(&D.occ[prev >> 6], ~(1ull << (prev & 63)));
+          }
+        } else {  // :154-170
+          released = ecur.idx;
+          const int16_t noff = ecur.off ? (int16_t)(eprev.off + ecur.off) : (int16_t)0;
+          store_off(D.table, prev, noff);
+          store_off_idx(D.table, cur, 0, -1);
+        }
+        atomicAnd(&D.occ[cur >> 6], ~(1ull << (cur & 63)));
+        L.changed = 1;
+      }
+      // ReleaseBlock (voxel_mem.cu:54-59) of the blocks this engine holds (a shard deletes every
+      // shard's candidates from its index, and releases only its own pool blocks)
+      const bool rel = ok && local_idx(released);
+      int nrel;
+      const int rank = wg_excl_scan(rel ? 1 : 0, L.scan, &nrel);
+      if (rel) D.heap[L.sfree + rank] = released;
+      if (base + kRT < m || done + m < n) __syncthreads(); else lds_barrier();
+      if (t == 0) {
+        L.sfree += nrel;
+        L.ndel += nrel;
+      }
+      lds_barrier();
+    }
+    done += m;
+    lo = thr;
+  }
+  TSDF_STAMP(D, 4, 2);
+  if (t == 0) D.ctr->free_count = L.sfree;
+  if (t == 0 && !direct) {
+    D.ctr->last_deleted = L.ndel;
+    D.ctr->total_deleted += (unsigned long long)L.ndel;
+  }
+}
+
+}  // namespace tsdf
