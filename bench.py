@@ -1,30 +1,35 @@
 #!/usr/bin/env python3
 """bench.py -- TSDF integrate frames/s on MI355X (BASELINE.json metric), one JSON line on rank 0.
 
-Workload (N=1): BASELINE.json configs[2] -- synthetic 640x480 depth + per-pixel high/low-touch
+Workload (N=1): BASELINE.json configs[2] (C3) -- synthetic 640x480 depth + per-pixel high/low-touch
 probability maps (the segmentation/inference output shape), fused TSDF + RGB + semantic integrate
-into a 5 mm voxel-hash volume (3 cm truncation, 4 m max depth, TUM fr1 intrinsics). One step =
-one TSDFGrid::Integrate of one frame: DDA block allocation, visibility, fused update, space
-carving. All frames are rendered on the GPU and resident in HBM before timing starts.
+into a 5 mm voxel-hash volume (3 cm truncation, 4 m max depth, TUM fr1 intrinsics). One step = one
+TSDFGrid::Integrate of one frame (voxel_tsdf.cu:347-375): DDA block allocation, visibility, fused
+update, space carving. All frames are rendered on the GPU and resident in HBM before timing starts.
 
-N>1 (launched by torch.distributed.run, one rank per GPU): default --mode streams runs one camera
-stream per GPU into that GPU's own volume (a multi-camera rig; no data-path collective), value =
-all frames integrated by all ranks / max rank time, scaling "weak". --mode sharded integrates ONE
-stream with the volume spatially sharded by 4^3-block bricks (each rank allocates and integrates
-only the blocks it owns), value = frames / max rank time, scaling "strong". --mode routed shards the
-same way but splits the block-allocation DDA by pixel-tile rows across ranks and routes each
-visible key to its owner with one RCCL all-to-all per frame (SURVEY.md 8e option 2), "strong".
+N>1 (torch.distributed.run, one rank per GPU) -- default --mode routed: ONE camera stream into ONE
+volume spatially sharded over the ranks. Every rank keeps the whole hash
+index and the voxels of its own 4^3-block bricks; rank r runs the block-allocation DDA over its band
+of pixel-tile rows, the frame's new keys and the carve candidates are all-gathered over RCCL, and
+each rank updates only its own blocks. value = frames / max rank time, scaling "strong"; the volume
+is the single-GPU volume block for block. --mode sharded: the same with every rank running the whole
+DDA (no key exchange). --mode streams: each rank integrates its own camera stream into its own volume
+(a multi-camera rig; weak scaling, no data-path collective). At N>1 the line carries the streams run
+as a labelled "secondary" object measured in the same job (--secondary none to skip).
 
-roofline: the fused integrate kernel (k_integrate). Algorithmic bytes per launch:
-N_vis * (512 * 12 + 12) voxel state + block metadata read, N_upd * 12 updated voxel state written,
-15 * W * H frame bytes read -- N_vis and N_upd are counted on device. Average launch duration from
-HIP start/stop events bound to every k_integrate launch of the timed region on the engine stream
-(hipExtLaunchKernel: the dispatch's own begin/end timestamps, the interval a rocprofv3 kernel
-trace reports); --marker-events times with marker events recorded around the launch instead (each
-carries a system-scope release, i.e. an L2 writeback, so it reads a few us longer). The in-kernel
-device clock of every launch is reported beside it.
-cpu_baseline: the single-threaded CPU oracle (oracle/tsdf_oracle.c, a restatement of the
-reference kernels incl. its full-table visibility scan) on a bounded sample of the same stream.
+roofline: SURVEY.md 8d. The frame-level fraction B_read * frames/s / (N * 8 TB/s) with
+B_read = 15 W H (frame) + N_vis * 6156 B (voxel state + metadata of every visible block), and the
+same with the updated voxels' writes; and the kernel-level entry of the fused update kernel
+k_integrate: algorithmic bytes per launch N_vis * 6156 + N_upd * 12 + 15 W H (N_vis, N_upd counted
+on device) / the kernel's average duration from HIP start/stop events bound to its dispatches on the
+engine stream. traffic: HBM bytes per launch from a rocprofv3 --pmc pass (FETCH_SIZE x2 + WRITE_SIZE,
+MI355X_MICROARCH.md gfx950 corrections) of THIS command over the same timed-window launches,
+accepted only when that pass integrated the same frames (equal N_vis / N_upd sums); otherwise null.
+The two resolvers run inside the ingest / update kernels' last-arriving workgroups: their device-clock
+spans are reported in "device_us_per_frame".
+cpu_baseline: the single-threaded CPU oracle (oracle/tsdf_oracle.c, a restatement of the reference
+kernels incl. its full-table visibility scan) on the first frames of this same stream (the GPU
+frames copied to the host), from an empty map.
 """
 from __future__ import annotations
 
@@ -39,6 +44,8 @@ sys.path.insert(0, os.path.join(ROOT, "disinfect-slam_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+BLOCK_READ_BYTES = 512 * 12 + 12  # voxel state + metadata of one visible block
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_integrate_r2.json")
 
 
 def parse():
@@ -52,40 +59,200 @@ def parse():
     p.add_argument("--trunc", type=float, default=0.03)
     p.add_argument("--max-depth", type=float, default=4.0)
     p.add_argument("--depth-only", action="store_true", help="config C2: ht = lt = NULL (ones)")
-    p.add_argument("--mode", choices=("streams", "sharded", "routed"), default="streams")
+    p.add_argument("--mode", choices=("routed", "sharded", "streams"), default="routed",
+                   help="N>1: routed (sharded volume, DDA split by tile rows, keys exchanged), sharded "
+                        "(sharded volume, whole-frame DDA on every rank), streams (one volume per rank)")
+    p.add_argument("--secondary", choices=("streams", "none"), default="streams",
+                   help="N>1: also measure the streams mode in the same job (labelled secondary)")
     p.add_argument("--loop", choices=("c3", "c5"), default="c3",
-                   help="c5: BASELINE config C5 -- per frame one hipGraph launch (integrate + raycast of "
-                        "the frame's camera), marching cubes of the whole volume every 30 frames")
+                   help="c5: BASELINE config C5 -- integrate + raycast of the frame's camera every frame, "
+                        "marching cubes of the whole volume every 30 frames (eager chain)")
     p.add_argument("--graph", action="store_true",
-                   help="c3 loop through the graph-captured frame (one hipGraph launch per frame)")
-    p.add_argument("--shard", default=None, metavar="I/G",
-                   help="single-GPU rehearsal of --mode sharded: run shard I of G alone (the G-GPU rate is "
-                        "the slowest shard's; every shard sees the whole frame)")
-    p.add_argument("--streams-per-gpu", type=int, default=1,
-                   help="camera streams per GPU, each its own engine (volume) and HIP stream; their "
-                        "frame chains overlap on the device (multi-camera rig; value counts all streams)")
-    p.add_argument("--key-cap", type=int, default=16384,
-                   help="sharded modes: key records per rank per frame (exchange slot size)")
-    p.add_argument("--cand-cap", type=int, default=8192,
-                   help="sharded modes: carve-candidate records per rank per frame")
+                   help="frames through the graph-captured frame (one hipGraph launch per frame)")
+    p.add_argument("--shard", default=None, metavar="G",
+                   help="single-GPU rehearsal of the routed sharded volume: G shard engines on this GPU "
+                        "exchanging their slots with device copies; reports the per-shard frame time")
+    p.add_argument("--key-cap", type=int, default=0,
+                   help="sharded modes: key records per rank per frame (0 = 32768 / G)")
+    p.add_argument("--cand-cap", type=int, default=0,
+                   help="sharded modes: carve-candidate records per rank per frame (0 = 16384 / G)")
     p.add_argument("--cpu-frames", type=int, default=-1, help="oracle sample size (-1 = auto)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--block-bits", type=int, default=18)
     p.add_argument("--event-every", type=int, default=8,
-                   help="HIP-event-time k_integrate on every n-th timed frame (a profiled dispatch "
-                        "runs ~1 us slower, so the loop samples)")
-    p.add_argument("--marker-events", action="store_true",
-                   help="time k_integrate with marker events recorded around the launch (each is a "
-                        "queue marker with a system-scope release: ~3 us of cache writeback each) "
-                        "instead of events bound to the kernel's dispatch")
+                   help="HIP-event-time k_integrate on every n-th timed frame (a dispatch with bound "
+                        "events runs ~1 us slower, so the loop samples)")
     p.add_argument("--no-events", action="store_true",
-                   help="diagnostic: no HIP events in the timed loop (roofline then unmeasured)")
+                   help="diagnostic: no HIP events in the timed loop (kernel roofline then from the "
+                        "device clock)")
     return p.parse_args()
+
+
+def workload_name(a):
+    W, H = a.width, a.height
+    if (W, H) == (640, 480):
+        w = "C2: 640x480 depth-only" if a.depth_only else "C3: 640x480 depth + ht/lt semantic"
+    else:
+        w = f"{W}x{H} depth{'' if a.depth_only else ' + ht/lt semantic'}"
+    if a.loop == "c5":
+        w = "C5: " + w + ", raycast every frame, marching cubes every 30 frames"
+    return (w + f", {a.voxel * 1000:g} mm voxel, {a.trunc * 100:g} cm truncation, {a.max_depth:g} m "
+            f"max depth, {'TUM fr1' if W <= 640 else 'L515 full-res'} intrinsics, orbit 1 cm + 0.5 deg/frame")
+
+
+class Run:
+    """One timed configuration on this rank: engines, the per-frame step, the timed loop."""
+
+    def __init__(self, a, mode, rank, world, dev, cam, frames, K, poses, dist):
+        import torch
+        import tsdf_amd
+        from tsdf_amd import dist as tdist
+        self.a, self.mode, self.world, self.dist, self.dev = a, mode, world, dist, dev
+        self.frames, self.K, self.poses = frames, K, poses
+        self.sharded = mode in ("routed", "sharded") and world > 1
+        si, sc = (rank, world) if self.sharded else (0, 1)
+        self.shard_index, self.shard_count = si, sc
+        self.stream = torch.cuda.current_stream()
+        self.eng = tsdf_amd.Engine(a.voxel, a.trunc, max_width=a.width, max_height=a.height,
+                                   num_block_bits=a.block_bits, device=torch.cuda.current_device(),
+                                   shard_index=si, shard_count=sc, stream=self.stream)
+        self.bufs = None
+        if self.sharded:  # exchange slots (RCCL all-gathers on this stream)
+            self.bufs = tdist.ShardBuffers(self.eng, sc, a.key_cap or max(1024, 32768 // sc),
+                                           a.cand_cap or max(1024, 16384 // sc), device=dev)
+        self.graph = None
+        self.replica = None
+        self.mesh_tris = []
+        W, H = a.width, a.height
+        self.rgba = self.normal = None
+        if a.loop == "c5":
+            self.rgba = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
+            self.normal = torch.zeros_like(self.rgba)
+            self.mesh_buf = torch.empty(9 * (8 << 20), dtype=torch.float32, device=dev)
+            if self.sharded:  # raycast / mesh composite of the sharded volume through a replica engine
+                self.replica = tsdf_amd.Engine(a.voxel, a.trunc, max_width=W, max_height=H,
+                                               num_block_bits=a.block_bits, device=torch.cuda.current_device(),
+                                               stream=self.stream)
+        if a.graph:
+            if self.sharded:
+                raise SystemExit("--graph takes a single volume per rank (streams mode or N=1)")
+            rw, rh = (W, H) if a.loop == "c5" else (0, 0)
+            self.graph = self.eng.frame_graph(W, H, rw, rh)
+
+    def step(self, i):
+        from tsdf_amd import dist as tdist
+        a, fr, K, pose = self.a, self.frames, self.K, self.poses[i]
+        ht = None if a.depth_only else fr["ht"][i]
+        lt = None if a.depth_only else fr["lt"][i]
+        c5 = a.loop == "c5"
+        if self.graph is not None:
+            self.graph.frame(fr["rgb"][i], fr["depth"][i], ht, lt, K, pose, a.max_depth,
+                             K if c5 else None, pose if c5 else None, self.rgba, self.normal)
+        elif self.sharded:
+            tdist.integrate_sharded(self.eng, self.bufs, fr["rgb"][i], fr["depth"][i], ht, lt, K, pose,
+                                    a.max_depth, split=self.mode == "routed")
+            if c5:
+                tdist.render_sharded(self.eng, self.replica, K, a.width, a.height, pose, a.max_depth,
+                                     rgba=self.rgba, normal=self.normal)
+        else:
+            self.eng.integrate(fr["rgb"][i], fr["depth"][i], ht, lt, K, pose, a.max_depth)
+            if c5:
+                self.eng.raycast(K, a.width, a.height, pose, a.max_depth, rgba=self.rgba, normal=self.normal)
+        if c5 and (i + 1) % 30 == 0:  # marching cubes of the whole volume, on device
+            if self.replica is not None:
+                n = tdist.mesh_sharded(self.eng, self.replica, None, 0.99, 0, out=self.mesh_buf).shape[0]
+            else:
+                n = self.eng.extract_mesh(None, 0.99, 0, out=self.mesh_buf).shape[0]
+            self.mesh_tris.append(int(n))
+
+    def timed(self):
+        """warmup, then exactly `steps` timed frames between barrier + synchronize; returns the
+        max-over-ranks elapsed seconds and this rank's profile of the timed window."""
+        import torch
+        from tsdf_amd import dist as tdist
+        a = self.a
+        for i in range(a.warmup):
+            self.step(i)
+        torch.cuda.synchronize()
+        if self.dist:
+            self.dist.barrier()
+        # start/stop events bound to every event_every-th k_integrate dispatch (hipExtLaunchKernel):
+        # the kernel's own begin/end timestamps, nothing added to the stream; the device-clock spans
+        # and the N_vis / N_upd sums cover every timed frame
+        self.eng.profile_begin(integrate_only=True, every=(1 << 30) if a.no_events else a.event_every,
+                               kernel_events=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(a.warmup, a.warmup + a.steps):
+            self.step(i)
+        t_enq = time.perf_counter()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if self.dist:
+            self.dist.barrier()
+        prof = self.eng.profile_end()
+        self.host_enqueue_ms = (t_enq - t0) / a.steps * 1e3
+        return tdist.max_over_ranks(t1 - t0, device=self.dev), prof
+
+    def close(self):
+        if self.graph is not None:
+            self.graph.close()
+        if self.replica is not None:
+            self.replica.close()
+        self.eng.close()
+
+
+def kernel_roofline(a, prof, n_frames):
+    """k_integrate: algorithmic bytes per launch / average launch duration (this rank)."""
+    W, H = a.width, a.height
+    img_bytes = (12 if a.depth_only else 15) * W * H
+    alg = (prof["sum_visible"] * BLOCK_READ_BYTES + prof["sum_updated"] * 12) / n_frames + img_bytes
+    if a.graph or a.no_events or prof["frames"] == 0:  # no (or one) dispatch event: the device clock
+        t = prof["ms_integrate_device"] / n_frames / 1e3
+        kind = "in-kernel device clock (first-workgroup start -> last arrival)"
+    else:
+        t = prof["ms_integrate"] / prof["frames"] / 1e3
+        kind = "HIP events bound to the k_integrate dispatch (hipExtLaunchKernel), engine stream"
+    achieved = alg / t / 1e9 if t > 0 else 0.0
+    return alg, t, achieved, kind
+
+
+def pmc_traffic(a, mode, world, prof):
+    """roofline.traffic from a rocprofv3 --pmc pass of this same command (profiles/, written by
+    scripts/summarize_prof.py): accepted only when the pass integrated the same frames."""
+    key = pmc_key(a, mode, world)
+    try:
+        runs = json.load(open(PMC_FILE))["runs"]
+    except (OSError, ValueError, KeyError):
+        return None, "no PMC file (profiles/pmc_integrate_r2.json)"
+    for r in runs:
+        if r.get("key") != key:
+            continue
+        if r.get("sum_visible") != prof["sum_visible"] or r.get("sum_updated") != prof["sum_updated"]:
+            return None, (f"PMC pass of this command saw N_vis/N_upd sums {r.get('sum_visible')}/"
+                          f"{r.get('sum_updated')}, this run {prof['sum_visible']}/{prof['sum_updated']}: rejected")
+        return r, "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes of this command, timed-window launches"
+    return None, "no PMC pass of this command in profiles/pmc_integrate_r2.json"
+
+
+def pmc_key(a, mode, world):
+    return {"width": a.width, "height": a.height, "voxel": a.voxel, "trunc": a.trunc,
+            "max_depth": a.max_depth, "depth_only": bool(a.depth_only), "block_bits": a.block_bits,
+            "steps": a.steps, "warmup": a.warmup, "mode": mode, "n_gpus": world, "loop": a.loop,
+            "graph": bool(a.graph)}
+
+
+def device_spans(prof, n):
+    us = lambda k: round(prof[k] / n * 1e3, 3)
+    return {"ingest_dda": us("ms_ingest_device"), "resolve_alloc": us("ms_resolve_alloc_device"),
+            "integrate": us("ms_integrate_device"), "resolve_delete": us("ms_resolve_delete_device"),
+            "note": "in-kernel 100 MHz clock, mean per timed frame: ingest = k_ingest_dda start -> "
+                    "last workgroup arrival; resolve_* = the resolvers in the last-arriving workgroups "
+                    "of k_ingest_dda / k_integrate; integrate = k_integrate start -> last arrival"}
 
 
 def main():
     a = parse()
-    import numpy as np
     import torch
 
     from tsdf_amd import dist as tdist
@@ -106,173 +273,100 @@ def main():
     import tsdf_amd
     from tsdf_amd import synth
 
-    cam = synth.camera(a.width, a.height,
-                       synth.TUM_FR1 if a.width <= 640 else synth.L515_FULL)
-    nphase = min(100, a.steps)  # untimed phase-breakdown pass after the timed region
-    nframes = a.warmup + a.steps + nphase
-    # streams mode: each rank's camera starts a third of an orbit apart (its own stream)
-    offset = tdist.stream_offset(a.mode, rank, world)
-    frames = synth.render_torch(cam, list(range(offset, offset + nframes)), device=dev)
-    torch.cuda.synchronize()
-    shard_index, shard_count = tdist.shard_of(a.mode, rank, world)
+    cam = synth.camera(a.width, a.height, synth.TUM_FR1 if a.width <= 640 else synth.L515_FULL)
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    nframes = a.warmup + a.steps
     if a.shard:
-        if world != 1:
-            raise SystemExit("--shard is a single-process rehearsal; use --mode sharded with N ranks")
-        shard_index, shard_count = (int(v) for v in a.shard.split("/"))
-        if not 0 <= shard_index < shard_count:
-            raise SystemExit("--shard I/G needs 0 <= I < G")
-    stream = torch.cuda.current_stream()
-    eng = tsdf_amd.Engine(a.voxel, a.trunc, max_width=a.width, max_height=a.height,
-                          num_block_bits=a.block_bits, device=torch.cuda.current_device(),
-                          shard_index=shard_index, shard_count=shard_count,
-                          stream=stream.cuda_stream)
-    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])  # ctypes struct cached once
-    poses = [tsdf_amd.SE3(frames["q"][i], frames["t"][i]) for i in range(nframes)]
+        return rehearsal(a, cam, K, dev)
+    mode = a.mode if world > 1 else "single"
 
-    routed = a.mode == "routed" and shard_count > 1 and not a.shard
-    # --streams-per-gpu: further engines, each on its own HIP stream with its own camera stream
-    extra = []
-    for k in range(1, a.streams_per_gpu):
-        if routed or a.loop == "c5" or a.graph or shard_count > 1:
-            raise SystemExit("--streams-per-gpu > 1 takes the eager c3 loop in streams mode")
-        off_k = offset + 97 * k  # a different stretch of the orbit per camera
-        fr_k = synth.render_torch(cam, list(range(off_k, off_k + nframes)), device=dev)
-        s_k = torch.cuda.Stream()
-        e_k = tsdf_amd.Engine(a.voxel, a.trunc, max_width=a.width, max_height=a.height,
-                              num_block_bits=a.block_bits, device=torch.cuda.current_device(),
-                              stream=s_k.cuda_stream)
-        extra.append((e_k, fr_k, [tsdf_amd.SE3(fr_k["q"][i], fr_k["t"][i]) for i in range(nframes)], s_k))
-    torch.cuda.synchronize()
-    if shard_count > 1:  # exchange slots of the sharded frame (RCCL all-gathers on this stream)
-        bufs = tdist.ShardBuffers(eng, shard_count, a.key_cap, a.cand_cap, device=dev)
+    def stream_frames(m):
+        off = tdist.stream_offset(m, rank, world)  # streams: each rank's camera a third of an orbit apart
+        fr = synth.render_torch(cam, list(range(off, off + nframes)), device=dev)
+        return fr, [tsdf_amd.SE3(fr["q"][i], fr["t"][i]) for i in range(nframes)]
 
-    use_graph = a.loop == "c5" or a.graph
-    if use_graph and routed:
-        raise SystemExit("--graph / --loop c5 take streams or sharded mode")
-    graph = None
-    mesh_tris = []
-    # C5 over a sharded volume: the graph frame integrates only; every frame's render is the raycast
-    # composite (tsdf_amd.dist.render_sharded: view-selected block records all-gathered over RCCL
-    # into a replica engine, raycast there), since one shard's own raycast sees only its blocks
-    composite = a.loop == "c5" and shard_count > 1
-    replica = None
-    if use_graph:
-        rw, rh = (a.width, a.height) if (a.loop == "c5" and not composite) else (0, 0)
-        graph = eng.frame_graph(a.width, a.height, rw, rh)
-        rgba = torch.zeros((a.height, a.width, 4), dtype=torch.uint8, device=dev) if rw else None
-        normal = torch.zeros_like(rgba) if rw else None
-        if composite:
-            replica = tsdf_amd.Engine(a.voxel, a.trunc, max_width=a.width, max_height=a.height,
-                                      num_block_bits=a.block_bits, device=torch.cuda.current_device(),
-                                      stream=stream.cuda_stream)
-            c_rgba = torch.zeros((a.height, a.width, 4), dtype=torch.uint8, device=dev)
-            c_normal = torch.zeros_like(c_rgba)
-        mesh_buf = torch.empty(9 * (8 << 20), dtype=torch.float32, device=dev) if a.loop == "c5" else None
-
-    def step(i):
-        ht = None if a.depth_only else frames["ht"][i]
-        lt = None if a.depth_only else frames["lt"][i]
-        if graph is not None:
-            graph.frame(frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i], a.max_depth,
-                        K if rgba is not None else None, poses[i] if rgba is not None else None, rgba, normal)
-            if replica is not None:
-                tdist.render_sharded(eng, replica, K, a.width, a.height, poses[i], a.max_depth,
-                                     rgba=c_rgba, normal=c_normal)
-            if a.loop == "c5" and (i + 1) % 30 == 0:  # marching cubes of the whole volume (on device)
-                if replica is not None:  # sharded: all blocks gathered into the replica first
-                    mesh_tris.append(int(tdist.mesh_sharded(eng, replica, None, 0.99, 0,
-                                                            out=mesh_buf).shape[0]))
-                else:
-                    mesh_tris.append(int(eng.extract_mesh(None, 0.99, 0, out=mesh_buf).shape[0]))
-        elif shard_count > 1:
-            tdist.integrate_sharded(eng, bufs, frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i],
-                                    a.max_depth, split=a.mode == "routed")
-        else:
-            eng.integrate(frames["rgb"][i], frames["depth"][i], ht, lt, K, poses[i], a.max_depth)
-        for e_k, fr_k, po_k, _ in extra:
-            e_k.integrate(fr_k["rgb"][i], fr_k["depth"][i], None if a.depth_only else fr_k["ht"][i],
-                          None if a.depth_only else fr_k["lt"][i], K, po_k[i], a.max_depth)
-
-    for i in range(a.warmup):
-        step(i)
+    frames, poses = stream_frames(mode)
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    if not a.no_events:
-        # default: start/stop events bound to every k_integrate dispatch (hipExtLaunchKernel) --
-        # the kernel's begin/end timestamps on the engine stream, nothing added to the stream.
-        # --marker-events: 2 marker events around the launch on every event_every-th frame
-        eng.profile_begin(integrate_only=True, every=a.event_every, kernel_events=not a.marker_events)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.warmup, a.warmup + a.steps):
-        step(i)
-    t_enq = time.perf_counter()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if dist:
-        dist.barrier()
-    if a.no_events:  # device-clock and counters still come from a profile window
-        eng.profile_begin(integrate_only=True)
-    prof = eng.profile_end()
-    # phase breakdown (all four phases event-bracketed) on the next frames of the stream, untimed
-    eng.profile_begin()
-    for i in range(a.warmup + a.steps, nframes):
-        if graph is not None:  # graph frames carry no events: the eager calls of the same frame
-            eng.integrate(frames["rgb"][i], frames["depth"][i], None if a.depth_only else frames["ht"][i],
-                          None if a.depth_only else frames["lt"][i], K, poses[i], a.max_depth)
-        else:
-            step(i)
-    torch.cuda.synchronize()
-    phases = eng.profile_end()
-    st = eng.stats()
-    elapsed = t1 - t0
-    elapsed = tdist.max_over_ranks(elapsed, device=dev)
-    value = tdist.units(a.mode, a.steps, world) * a.streams_per_gpu / elapsed
-    for e_k, _, _, _ in extra:
-        if e_k.stats()["status"] != 0:
-            raise SystemExit("a further stream's engine reported a status")
-
-    # ---- roofline of the fused integrate kernel (this rank's launches) ----
+    run = Run(a, mode, rank, world, dev, cam, frames, K, poses, dist)
+    elapsed, prof = run.timed()
+    st = run.eng.stats()
+    if st["status"] != 0:
+        raise SystemExit(f"engine status {st['status']:#x} after the timed run")
+    value = tdist.units(mode, a.steps, world) / elapsed
+    fps_stream = a.steps / elapsed  # frames/s of one stream (sharded: the job's only stream)
     W, H = a.width, a.height
     img_bytes = (12 if a.depth_only else 15) * W * H
-    alg_bytes = (prof["sum_visible"] * (512 * 12 + 12) + prof["sum_updated"] * 12) / a.steps + img_bytes
-    t_int = prof["ms_integrate"] / max(prof["frames"], 1) / 1e3
-    event_kind = "marker" if a.marker_events else "kernel-dispatch"
-    if graph is not None:  # graph frames carry no events: the in-kernel device clock
-        t_int = prof["ms_integrate_device"] / a.steps / 1e3
-        event_kind = "none (graph frames): device clock"
-    achieved = alg_bytes / t_int / 1e9 if t_int > 0 else 0.0
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_integrate_latest.json")
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            if pmc.get("width") == W and pmc.get("height") == H:
-                traffic = pmc.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+
+    # ---- kernel-level roofline (this rank's k_integrate) ----
+    alg, t_int, achieved, ev_kind = kernel_roofline(a, prof, a.steps)
+    pmc, pmc_src = pmc_traffic(a, mode, world, prof)
+    # ---- frame-level roofline, SURVEY.md 8d (whole job) ----
+    # bytes per frame of the job: sharded -- the ranks' visible blocks sum to the frame's, and every
+    # rank reads its frame; streams / single -- every rank its own frame
+    vis_sum, upd_sum = tdist.sum_over_ranks([prof["sum_visible"], prof["sum_updated"]], device=dev)
+    n_img = world  # every rank reads a frame per step (its own, or the shared one)
+    b_read = (vis_sum * BLOCK_READ_BYTES) / a.steps + n_img * img_bytes
+    b_write = upd_sum * 12 / a.steps
+    steps_per_s = a.steps / elapsed
+    frame_frac_read = b_read * steps_per_s / (world * HBM_PEAK_GBS * 1e9)
+    frame_frac_rw = (b_read + b_write) * steps_per_s / (world * HBM_PEAK_GBS * 1e9)
+    mesh_tris = run.mesh_tris[-1] if run.mesh_tris else None
+    host_enq = run.host_enqueue_ms
+    run.close()
+    del frames
+
+    secondary = None
+    if world > 1 and a.secondary == "streams" and mode != "streams":
+        fr2, po2 = stream_frames("streams")
+        torch.cuda.synchronize()
+        r2 = Run(a, "streams", rank, world, dev, cam, fr2, K, po2, dist)
+        el2, _ = r2.timed()
+        r2.close()
+        secondary = {"mode": "streams", "value": round(tdist.units("streams", a.steps, world) / el2, 2),
+                     "unit": "frames/s", "scaling": "weak",
+                     "ms_per_step": round(el2 / a.steps * 1e3, 4),
+                     "what": "each rank integrates its own camera stream into its own volume (multi-camera "
+                             "rig; no data-path collective); value = all ranks' frames / max rank time"}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(a, cam)
+        fr_host = synth.render_torch(cam, list(range(0, min(nframes, 80))), device=dev)
+        cpu = cpu_baseline(a, cam, fr_host)
 
     if rank == 0:
-        workload = ("C2: 640x480 depth-only" if a.depth_only else "C3: 640x480 depth + ht/lt semantic")
-        if (W, H) != (640, 480):
-            workload = f"{W}x{H} depth{'' if a.depth_only else ' + ht/lt semantic'}"
-        if a.streams_per_gpu > 1:
-            workload += f", {a.streams_per_gpu} camera streams per GPU (one volume each)"
         metric = "TSDF integrate frames/s (640x480 depth+label, 5mm voxel)"
         if a.loop == "c5":
             metric = ("C5 frame loop frames/s (integrate + raycast every frame, marching cubes every 30 "
-                      "frames, one hipGraph launch per frame)")
-            workload = "C5: " + workload
-            if replica is not None:
-                workload += (", sharded volume: per-frame raycast composite (view-selected block records "
-                             "all-gathered into a replica engine), marching cubes of the gathered volume")
-        elif graph is not None:
-            workload += " (hipGraph frame)"
+                      "frames)")
+        parallelism = "single" if world == 1 else f"{mode}{world}"
+        if a.graph:
+            parallelism += ", one hipGraph launch per frame"
+        roof = {
+            "kernel": "k_integrate",
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None if pmc is None else int(pmc["hbm_bytes_per_launch"]),
+            "traffic_read": None if pmc is None else int(pmc["fetch_bytes_per_launch"]),
+            "traffic_write": None if pmc is None else int(pmc["write_bytes_per_launch"]),
+            "traffic_source": pmc_src,
+            "alg_bytes_per_launch": int(alg),
+            "alg_read_bytes_per_launch": int(prof["sum_visible"] * BLOCK_READ_BYTES / a.steps + img_bytes),
+            "us_per_launch": round(t_int * 1e6, 3),
+            "event_timed_launches": prof["frames"],
+            "event_kind": ev_kind,
+            "us_per_launch_device_clock": round(prof["ms_integrate_device"] / a.steps * 1e3, 3),
+            "frame": {  # B_read * frames/s / (N x 8 TB/s)
+                "bytes_read_per_step": int(b_read),
+                "bytes_written_per_step": int(b_write),
+                "frac_read": round(frame_frac_read, 4),
+                "frac_read_write": round(frame_frac_rw, 4),
+                "def": "B_read = 15 W H per frame read + N_vis * 6156 B; write = N_upd * 12 B; "
+                       "fraction of N GPUs x 8 TB/s at the measured step rate",
+            },
+        }
         out = {
             "metric": metric,
             "value": round(value, 2),
@@ -282,91 +376,128 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak" if a.mode == "streams" else "strong",
+            "scaling": "weak" if mode == "streams" else ("strong" if world > 1 else "weak"),
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (analytic room scene rendered on GPU, resident in HBM)",
             "config": {
-                "workload": workload + f", {a.voxel * 1000:g} mm voxel, {a.trunc * 100:g} cm truncation, "
-                            f"{a.max_depth:g} m max depth, {'TUM fr1' if W <= 640 else 'L515 full-res'} intrinsics, "
-                            "orbit 1 cm + 0.5 deg/frame",
+                "workload": workload_name(a),
                 "width": W, "height": H, "voxel_m": a.voxel, "truncation_m": a.trunc,
                 "pool_blocks": 1 << a.block_bits,
-                "parallelism": (f"{a.mode}{world}" if world > 1 else
-                                f"shard {shard_index} of {shard_count} alone (sharded-mode rehearsal)"
-                                if shard_count > 1 else "single"),
+                "parallelism": parallelism,
             },
-            "roofline": {
-                "kernel": "k_integrate",
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "alg_bytes_per_launch": int(alg_bytes),
-                "us_per_launch": round(t_int * 1e6, 3),
-                # cross-check: first-WG start -> last-WG end from the in-kernel 100 MHz clock
-                # (what rocprofv3's kernel trace measures; the HIP events above also include the
-                # per-launch dispatch / completion overhead)
-                "event_timed_launches": prof["frames"],
-                "event_kind": event_kind,
-                "us_per_launch_device_clock": round(prof["ms_integrate_device"] / a.steps * 1e3, 3),
-                "achieved_device_clock": round(alg_bytes / (prof["ms_integrate_device"] / a.steps / 1e3) / 1e9, 1)
-                if prof["ms_integrate_device"] > 0 else None,
-            },
+            "roofline": roof,
             "cpu_baseline": cpu,
-            "phases_ms_per_frame": {  # separate untimed pass of nphase frames
-                "frames": nphase,
-                "allocate": round(phases["ms_allocate"] / nphase, 4),
-                "visibility": round(phases["ms_visible"] / nphase, 4),
-                "integrate": round(phases["ms_integrate"] / nphase, 4),
-                "carve": round(phases["ms_carve"] / nphase, 4),
-            },
-            "host_enqueue_ms_per_step": round((t_enq - t0) / a.steps * 1e3, 4),
+            "device_us_per_frame": device_spans(prof, a.steps),
+            "host_enqueue_ms_per_step": round(host_enq, 4),
+            "pmc_key": pmc_key(a, mode, world),  # what scripts/summarize_prof.py files a PMC pass under
+            "sum_visible": prof["sum_visible"],
+            "sum_updated": prof["sum_updated"],
             "avg_visible_blocks": round(prof["sum_visible"] / a.steps, 1),
-            "mesh_triangles": mesh_tris[-1] if mesh_tris else None,
             "avg_updated_voxels": round(prof["sum_updated"] / a.steps, 1),
             "active_blocks": st["active_blocks"],
+            "mesh_triangles": mesh_tris,
             "status": st["status"],
         }
+        if world > 1:
+            out["frames_per_s_per_stream"] = round(fps_stream, 2)
+        if secondary:
+            out["secondary"] = secondary
         print(json.dumps(out), flush=True)
-    if graph is not None:
-        graph.close()
-    for e_k, _, _, _ in extra:
-        e_k.close()
-    if replica is not None:
-        replica.close()
-    eng.close()
     if dist:
         dist.destroy_process_group()
 
 
-def cpu_baseline(a, cam):
-    """Single-thread oracle on the first frames of the same stream (empty map), host frames."""
-    import numpy as np
+def rehearsal(a, cam, K, dev):
+    """--shard G: the routed sharded volume's G shards on this one GPU (tsdf_amd.ShardGroup: slots
+    exchanged with device copies where a G-GPU job all-gathers them). The group's frame time is the
+    sum of the shards' own kernels; reported per shard as that time / G, beside each shard's in-kernel
+    device-clock spans (the slowest shard bounds a G-GPU job's frame, plus the two all-gathers)."""
+    import torch
 
+    import tsdf_amd
     from tsdf_amd import synth
+    G = int(a.shard)
+    nframes = a.warmup + a.steps
+    fr = synth.render_torch(cam, list(range(nframes)), device=dev)
+    poses = [tsdf_amd.SE3(fr["q"][i], fr["t"][i]) for i in range(nframes)]
+    grp = tsdf_amd.ShardGroup(G, a.voxel, a.trunc, max_width=a.width, max_height=a.height,
+                              num_block_bits=a.block_bits, device=torch.cuda.current_device(),
+                              key_cap=a.key_cap or max(1024, 32768 // G),
+                              cand_cap=a.cand_cap or max(1024, 16384 // G), split=a.mode != "sharded")
+
+    def step(i):
+        ht = None if a.depth_only else fr["ht"][i]
+        lt = None if a.depth_only else fr["lt"][i]
+        grp.integrate(fr["rgb"][i], fr["depth"][i], ht, lt, K, poses[i], a.max_depth)
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    for e in grp.engines:
+        e.profile_begin(integrate_only=True, every=1 << 30)
+    t0 = time.perf_counter()
+    for i in range(a.warmup, nframes):
+        step(i)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    profs = [e.profile_end() for e in grp.engines]
+    for e in grp.engines:
+        if e.stats()["status"]:
+            raise SystemExit("a shard engine reported a status")
+    n = a.steps
+    spans = [device_spans(p, n) for p in profs]
+    for s in spans:
+        s.pop("note")
+    dev_total = [sum(v for v in s.values()) for s in spans]
+    out = {
+        "metric": "sharded-volume rehearsal: per-shard frame time (one GPU, G shard engines)",
+        "value": round(el / n / G * 1e3, 4),
+        "unit": "ms/frame/shard",
+        "n_gpus": 1,
+        "steps": n,
+        "warmup": a.warmup,
+        "ms_per_step": round(el / n * 1e3, 4),
+        "higher_is_better": False,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (analytic room scene rendered on GPU, resident in HBM)",
+        "config": {"workload": workload_name(a), "width": a.width, "height": a.height,
+                   "parallelism": f"{G} {'routed' if a.mode != 'sharded' else 'sharded'} shards on one GPU"},
+        "shards": G,
+        "group_ms_per_frame": round(el / n * 1e3, 4),
+        "per_shard_device_us": spans,
+        "max_shard_device_us_per_frame": round(max(dev_total), 3),
+        "avg_visible_blocks_per_shard": [round(p["sum_visible"] / n, 1) for p in profs],
+    }
+    grp.close()
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline(a, cam, fr):
+    """Single-thread oracle on the first frames of the bench's own stream (GPU frames copied to the
+    host), from an empty map, ~20 s of CPU work."""
     from _oracle import OracleGrid
 
     ora = OracleGrid(a.voxel, a.trunc, a.block_bits)
+    host = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in fr.items()}
+    n_avail = host["depth"].shape[0]
     n = a.cpu_frames
     budget = 20.0
-    frames_done, spent = 0, 0.0
-    i = 0
-    while True:
-        if n >= 0 and frames_done >= n:
+    done, spent = 0, 0.0
+    while done < n_avail:
+        if n >= 0 and done >= n:
             break
-        if n < 0 and (spent >= budget or frames_done >= 60):
+        if n < 0 and spent >= budget:
             break
-        fr = synth.render(cam, i)
-        ht = None if a.depth_only else fr["ht"]
-        lt = None if a.depth_only else fr["lt"]
+        ht = None if a.depth_only else host["ht"][done]
+        lt = None if a.depth_only else host["lt"][done]
         t0 = time.perf_counter()
-        ora.integrate(fr["rgb"], fr["depth"], ht, lt, a.max_depth, cam.K, fr["q"], fr["t"])
+        ora.integrate(host["rgb"][done], host["depth"][done], ht, lt, a.max_depth, cam.K,
+                      host["q"][done], host["t"][done])
         spent += time.perf_counter() - t0
-        frames_done += 1
-        i += 1
+        done += 1
     ora.close()
     model = ""
     try:
@@ -377,12 +508,13 @@ def cpu_baseline(a, cam):
     except OSError:
         pass
     return {
-        "value": round(frames_done / spent, 4),
+        "value": round(done / spent, 4),
         "unit": "frames/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"first {frames_done} frames of the same {cam.width}x{cam.height} stream from an empty "
-                  f"map, single thread, oracle/tsdf_oracle.c -O2 (host: {model}, nproc={os.cpu_count()})",
+        "sample": f"frames 0..{done - 1} of this bench's own {cam.width}x{cam.height} stream (GPU-rendered "
+                  f"frames copied to the host) from an empty map, single thread, oracle/tsdf_oracle.c -O2 "
+                  f"(host: {model}, nproc={os.cpu_count()})",
     }
 
 

@@ -362,6 +362,9 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
                                            const float* __restrict__ ht,
                                            const float* __restrict__ lt, int tiles_x, int tiles) {
   __shared__ IngestLds<TS> S;
+  // device-clock span of the ingest (WG 0 is dispatched first; the end is the last arrival)
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    st_co(&D.arrive[kArrStart + 8], (unsigned long long)__builtin_amdgcn_s_memrealtime());
   if ((int)blockIdx.x < kVisWorkgroups) {
     TSDF_STAMP(D, 2, 0);
     vis_sweep(D, P, blockIdx.x, S);
@@ -370,7 +373,10 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
     ingest_tile<TS>(D, P, depth, rgb, ht, lt, tiles_x, (int)blockIdx.x - kVisWorkgroups, S);
   }
   if (!arrive_last(D.arrive + kArrIngest, 0ull, &S.last)) return;
-  if (threadIdx.x == 0) (void)arrive_collect(D.arrive + kArrIngest);
+  if (threadIdx.x == 0) {
+    (void)arrive_collect(D.arrive + kArrIngest);
+    D.ctr->ingest_ticks += __builtin_amdgcn_s_memrealtime() - ld_co(&D.arrive[kArrStart + 8]);
+  }
   if (P.tail == kTailPack)
     pack_keys_wg(D, P.slot, P.slot_cap);
   else

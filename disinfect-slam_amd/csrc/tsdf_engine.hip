@@ -128,7 +128,7 @@ struct tsdf_engine {
   int64_t prof_calls = 0;    // integrate calls since profile_begin
   std::vector<std::array<hipEvent_t, 5>> events;
   size_t ev_used = 0;
-  unsigned long long prof_vis0 = 0, prof_upd0 = 0, prof_ticks0 = 0;
+  unsigned long long prof_vis0 = 0, prof_upd0 = 0, prof_ticks0 = 0, prof_ing0 = 0, prof_ra0 = 0, prof_rd0 = 0;
   // sharded frame (tsdf_integrate_shard_*): 0 idle, 1 after _begin, 2 after _update
   hipEvent_t order_ev = nullptr;  // tsdf_stream_wait / _signal
   int shard_phase = 0;
@@ -1296,6 +1296,9 @@ int tsdf_profile_begin(tsdf_engine* e, int mode, int every) {
   e->prof_vis0 = e->h_ctr->total_visible;
   e->prof_upd0 = e->h_ctr->total_updated;
   e->prof_ticks0 = e->h_ctr->integrate_ticks;
+  e->prof_ing0 = e->h_ctr->ingest_ticks;
+  e->prof_ra0 = e->h_ctr->resolve_alloc_ticks;
+  e->prof_rd0 = e->h_ctr->resolve_delete_ticks;
   e->ev_used = 0;
   e->profiling = true;
   return TSDF_OK;
@@ -1322,6 +1325,9 @@ int tsdf_profile_end(tsdf_engine* e, tsdf_profile* o) {
   o->sum_visible = (int64_t)(e->h_ctr->total_visible - e->prof_vis0);
   o->sum_updated = (int64_t)(e->h_ctr->total_updated - e->prof_upd0);
   o->ms_integrate_device = (double)(e->h_ctr->integrate_ticks - e->prof_ticks0) * 1e-5;
+  o->ms_ingest_device = (double)(e->h_ctr->ingest_ticks - e->prof_ing0) * 1e-5;
+  o->ms_resolve_alloc_device = (double)(e->h_ctr->resolve_alloc_ticks - e->prof_ra0) * 1e-5;
+  o->ms_resolve_delete_device = (double)(e->h_ctr->resolve_delete_ticks - e->prof_rd0) * 1e-5;
   return TSDF_OK;
 }
 

@@ -282,6 +282,7 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
                                  AllocLds& L) {
   const int t = threadIdx.x;
   TSDF_STAMP(D, 1, 0);
+  const unsigned long long tick0 = __builtin_amdgcn_s_memrealtime();
   // ---- prologue, round trip 1: counters and (speculatively) the first kRB list entries ----
   const int n = ld_co(&D.ctr->nk_count);
   const int free0 = D.ctr->free_count;
@@ -529,6 +530,7 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
   }
   TSDF_STAMP(D, 1, 3);
   if (t == 0) {
+    D.ctr->resolve_alloc_ticks += __builtin_amdgcn_s_memrealtime() - tick0;
     D.ctr->free_count = L.sfree;
     D.ctr->n_fresh = L.nfresh;
     D.ctr->nk_count = 0;
@@ -565,6 +567,7 @@ __device__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__
                                   const int32_t* __restrict__ count, int direct, DeleteLds& L) {
   const int t = threadIdx.x;
   TSDF_STAMP(D, 4, 0);
+  const unsigned long long tick0 = __builtin_amdgcn_s_memrealtime();
   const int n = ld_co(count);
   const int free0 = D.ctr->free_count;
   const uint32_t epoch = D.ctr->lock_epoch + 1u;
@@ -750,7 +753,10 @@ __device__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__
     lo = thr;
   }
   TSDF_STAMP(D, 4, 2);
-  if (t == 0) D.ctr->free_count = L.sfree;
+  if (t == 0) {
+    D.ctr->free_count = L.sfree;
+    D.ctr->resolve_delete_ticks += __builtin_amdgcn_s_memrealtime() - tick0;
+  }
   if (t == 0 && !direct) {
     D.ctr->last_deleted = L.ndel;
     D.ctr->total_deleted += (unsigned long long)L.ndel;

@@ -87,6 +87,9 @@ class Profile(C.Structure):
         ("sum_updated", C.c_int64),
         ("ms_integrate_device", C.c_double),
         ("calls", C.c_int64),
+        ("ms_ingest_device", C.c_double),
+        ("ms_resolve_alloc_device", C.c_double),
+        ("ms_resolve_delete_device", C.c_double),
     ]
 
 

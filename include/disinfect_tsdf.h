@@ -109,6 +109,11 @@ typedef struct tsdf_profile { /* device time of the integrate phases between beg
                                  dispatch overhead the HIP events of ms_integrate include) */
   int64_t calls;       /* all integrate calls between begin and end (sum_* and the device
                           clock cover all of them; the ms_* event times only `frames`) */
+  /* in-kernel 100 MHz clock, summed over the calls (the two resolvers run inside the ingest and
+     update kernels' last-arriving workgroups, so no kernel trace can time them apart): */
+  double ms_ingest_device;          /* k_ingest_dda start -> its last workgroup's arrival */
+  double ms_resolve_alloc_device;   /* ordered allocation resolve (VoxelHashTable::Allocate) */
+  double ms_resolve_delete_device;  /* ordered carving resolve (VoxelHashTable::Delete) */
 } tsdf_profile;
 
 /* ---- engine lifetime: TSDFGrid::TSDFGrid / ~TSDFGrid (voxel_tsdf.cu:309-345) ---- */

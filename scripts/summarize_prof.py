@@ -1,9 +1,14 @@
 #!/usr/bin/env python3
 """Summarise a scripts/profile_integrate.sh run: per-kernel trace stats + PMC HBM bytes.
 
+  summarize_prof.py <out_dir>            -> <out_dir>/summary.json, <out_dir>/pmc_entry.json, table
+  summarize_prof.py --merge <entry.json> <profiles/pmc_integrate_r2.json>
+
 gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KiB;
 FETCH_SIZE reports half the bytes of wide coalesced reads, so it is doubled.
-Writes <out>/summary.json and prints a table.
+The PMC means are over the k_integrate dispatches of the bench's timed window only (launches
+[warmup, warmup + steps) in dispatch order), and the entry carries the bench's pmc_key and the
+N_vis / N_upd sums of that window, which bench.py matches before it reports roofline.traffic.
 """
 import csv
 import glob
@@ -15,7 +20,7 @@ import sys
 
 
 def find(pattern):
-    m = glob.glob(pattern, recursive=True)
+    m = sorted(glob.glob(pattern, recursive=True))
     return m[0] if m else None
 
 
@@ -35,74 +40,99 @@ def kname(full):
     'k_integrate' (the eager instantiation; the graph one is 'k_integrate_graph')."""
     n = full.split("(")[0].replace("tsdf::", "")
     n = re.sub(r"^void ", "", n)
-    return re.sub(r"k_integrate_t<true(, false)?>", "k_integrate_graph", re.sub(r"k_integrate_t<false(, false)?>", "k_integrate", n))
+    n = re.sub(r"k_integrate_t<false(, false)?>", "k_integrate", n)
+    return re.sub(r"k_integrate_t<true(, false)?>", "k_integrate_graph", n)
+
+
+def window(rows, b):
+    """rows (dispatch id, value) of one kernel -> the bench's timed-window launches."""
+    rows = sorted(rows)
+    w, k = b["warmup"], b["steps"]
+    return [v for _, v in rows[w:w + k]]
 
 
 def main(out):
     res = {"kernels": {}, "pmc": {}}
     st = find(os.path.join(out, "trace", "**", "*kernel_stats.csv"))
+    b0 = bench_line(os.path.join(out, "trace_bench.log"))
     if st:
         for r in csv.DictReader(open(st)):
-            if not re.search(r"tsdf::", r["Name"]):
+            if "tsdf::" not in r["Name"]:
                 continue
-            name = kname(r["Name"])
-            res["kernels"][name] = {
+            res["kernels"][kname(r["Name"])] = {
                 "calls": int(r["Calls"]),
                 "avg_us": float(r["AverageNs"]) / 1e3,
                 "min_us": float(r["MinNs"]) / 1e3,
                 "max_us": float(r["MaxNs"]) / 1e3,
                 "total_ms": float(r["TotalDurationNs"]) / 1e6,
             }
-    # per-dispatch trace: k_integrate durations inside the bench's timed window (launches
-    # [warmup, warmup + steps) of the kernel), the same launches the bench's HIP events bracket
     tr = find(os.path.join(out, "trace", "**", "*kernel_trace.csv"))
-    b0 = bench_line(os.path.join(out, "trace_bench.log"))
     if tr and b0:
-        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(tr))
-                if kname(r["Kernel_Name"]) == "k_integrate"]
-        w, k = b0["warmup"], b0["steps"]
-        win = durs[w:w + k]
-        if win:
-            res["integrate_timed_window"] = {"launches": len(win), "avg_us": statistics.mean(win) / 1e3,
-                                             "event_avg_us": b0["roofline"]["us_per_launch"]}
+        per = {}
+        for r in csv.DictReader(open(tr)):
+            per.setdefault(kname(r["Kernel_Name"]), []).append(
+                (int(r["Dispatch_Id"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+        res["timed_window"] = {}
+        for name, rows in per.items():
+            if not name.startswith("k_") or len(rows) < b0["warmup"] + b0["steps"]:
+                continue
+            win = window(rows, b0)
+            res["timed_window"][name] = {"launches": len(win), "avg_us": statistics.mean(win) / 1e3,
+                                         "min_us": min(win) / 1e3, "max_us": max(win) / 1e3}
+        res["bench_event_us_per_launch"] = b0["roofline"]["us_per_launch"]
+    pmc_lines = {}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         f = find(os.path.join(out, f"pmc_{c}", "**", "*counter_collection.csv"))
-        if not f:
+        b = bench_line(os.path.join(out, f"pmc_{c}_bench.log"))
+        if not f or not b:
             continue
-        vals = {}
+        pmc_lines[c] = b
+        per = {}
         for r in csv.DictReader(open(f)):
             kn = r.get("Kernel_Name", "")
             if "tsdf::" not in kn or r.get("Counter_Name") != c:
                 continue
-            name = kname(kn)
-            vals.setdefault(name, []).append(float(r["Counter_Value"]))
-        for name, v in vals.items():
-            kib = statistics.mean(v)
-            corr = 2.0 if c == "FETCH_SIZE" else 1.0
-            res["pmc"].setdefault(name, {})[c] = {"mean_kib_raw": kib, "bytes_per_launch": kib * 1024 * corr,
-                                                   "dispatches": len(v)}
-    b = bench_line(os.path.join(out, "trace_bench.log")) or bench_line(os.path.join(out, "pmc_FETCH_SIZE_bench.log"))
-    if b:
-        res["bench"] = b
+            per.setdefault(kname(kn), []).append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+        corr = 2.0 if c == "FETCH_SIZE" else 1.0
+        for name, rows in per.items():
+            win = window(rows, b) if len(rows) >= b["warmup"] + b["steps"] else [v for _, v in sorted(rows)]
+            res["pmc"].setdefault(name, {})[c] = {
+                "bytes_per_launch": statistics.mean(win) * 1024 * corr, "dispatches": len(win),
+                "timed_window": len(rows) >= b["warmup"] + b["steps"]}
+    if b0:
+        res["bench"] = b0
     ki = res["pmc"].get("k_integrate", {})
     if "FETCH_SIZE" in ki and "WRITE_SIZE" in ki:
-        res["integrate_hbm_bytes_per_launch"] = ki["FETCH_SIZE"]["bytes_per_launch"] + ki["WRITE_SIZE"]["bytes_per_launch"]
-        if b:
-            res["integrate_alg_bytes_per_launch"] = b["roofline"]["alg_bytes_per_launch"]
+        bf, bw = pmc_lines["FETCH_SIZE"], pmc_lines["WRITE_SIZE"]
+        same = (bf["sum_visible"], bf["sum_updated"]) == (bw["sum_visible"], bw["sum_updated"])
+        if b0:
+            same = same and (b0["sum_visible"], b0["sum_updated"]) == (bf["sum_visible"], bf["sum_updated"])
+        fetch, write = ki["FETCH_SIZE"]["bytes_per_launch"], ki["WRITE_SIZE"]["bytes_per_launch"]
+        entry = {"key": bf["pmc_key"], "sum_visible": bf["sum_visible"], "sum_updated": bf["sum_updated"],
+                 "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
+                 "hbm_bytes_per_launch": fetch + write,
+                 "alg_bytes_per_launch": bf["roofline"]["alg_bytes_per_launch"],
+                 "alg_read_bytes_per_launch": bf["roofline"]["alg_read_bytes_per_launch"],
+                 "launches": ki["FETCH_SIZE"]["dispatches"], "passes_saw_same_frames": same,
+                 "note": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and --pmc WRITE_SIZE, separate passes of "
+                         "the bench command; mean over the timed-window k_integrate dispatches"}
+        res["integrate_pmc_entry"] = entry
+        json.dump(entry, open(os.path.join(out, "pmc_entry.json"), "w"), indent=1)
+        if not same:
+            print("WARNING: the passes integrated different frames (N_vis/N_upd sums differ)")
+        print(f"k_integrate PMC (timed window, {entry['launches']} launches): fetch {fetch / 1e6:.3f} MB, "
+              f"write {write / 1e6:.3f} MB, total {(fetch + write) / 1e6:.3f} MB vs algorithmic "
+              f"{entry['alg_bytes_per_launch'] / 1e6:.3f} MB (read {entry['alg_read_bytes_per_launch'] / 1e6:.3f})")
     json.dump(res, open(os.path.join(out, "summary.json"), "w"), indent=1)
-    if "integrate_hbm_bytes_per_launch" in res and b:
-        # the file bench.py reads for roofline.traffic (same workload only)
-        json.dump({"width": b["config"]["width"], "height": b["config"]["height"],
-                   "hbm_bytes_per_launch": res["integrate_hbm_bytes_per_launch"],
-                   "fetch_bytes_per_launch": ki["FETCH_SIZE"]["bytes_per_launch"],
-                   "write_bytes_per_launch": ki["WRITE_SIZE"]["bytes_per_launch"],
-                   "note": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, separate passes, "
-                           "mean over all k_integrate dispatches of the bench command"},
-                  open(os.path.join(out, "pmc_integrate_latest.json"), "w"), indent=1)
-    if "integrate_timed_window" in res:
-        t = res["integrate_timed_window"]
-        print(f"k_integrate timed window: {t['launches']} launches avg {t['avg_us']:.2f}us "
-              f"(bench HIP events {t['event_avg_us']:.2f}us)")
+    if b0:
+        d = b0.get("device_us_per_frame", {})
+        print("bench: %.1f frames/s, %.4f ms/step; device us/frame: %s" % (
+            b0["value"], b0["ms_per_step"], {k: v for k, v in d.items() if k != "note"}))
+    for name, t in sorted(res.get("timed_window", {}).items()):
+        print(f"{name} timed window: {t['launches']} launches avg {t['avg_us']:.2f}us "
+              f"(min {t['min_us']:.2f}, max {t['max_us']:.2f})")
+    if "bench_event_us_per_launch" in res:
+        print(f"bench HIP events (k_integrate): {res['bench_event_us_per_launch']:.2f}us")
     for k, v in sorted(res["kernels"].items(), key=lambda kv: -kv[1]["total_ms"]):
         p = res["pmc"].get(k, {})
         fb = p.get("FETCH_SIZE", {}).get("bytes_per_launch")
@@ -113,5 +143,18 @@ def main(out):
               f"max={v['max_us']:9.2f} fetch={fs} write={ws}")
 
 
+def merge(entry_path, table_path):
+    e = json.load(open(entry_path))
+    try:
+        t = json.load(open(table_path))
+    except (OSError, ValueError):
+        t = {"runs": []}
+    t["runs"] = [r for r in t["runs"] if r.get("key") != e["key"]] + [e]
+    json.dump(t, open(table_path, "w"), indent=1)
+
+
 if __name__ == "__main__":
-    main(sys.argv[1])
+    if sys.argv[1] == "--merge":
+        merge(sys.argv[2], sys.argv[3])
+    else:
+        main(sys.argv[1])
