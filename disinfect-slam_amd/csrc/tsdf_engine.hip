@@ -101,6 +101,13 @@ struct tsdf_engine {
   // raycast / query / test scratch
   uchar4* rc_rgba = nullptr;
   uchar4* rc_norm = nullptr;
+  // raycast view grid (tsdf_kernels.h ViewGrid): cells, the two brick bitmaps, generation
+  uint32_t* vg_cell = nullptr;
+  int64_t vg_cap = 0;  // cells
+  uint8_t* vg_flags = nullptr;
+  uint32_t* vg_bits = nullptr;
+  uint32_t vg_gen = 0;
+  uint64_t vg_calls = 0;
   VisRec* q_sel = nullptr;
   int32_t* q_count = nullptr;
   float4* q_out = nullptr;
@@ -154,6 +161,7 @@ void free_all(tsdf_engine* e) {
                   e->fe_rgb, e->fe_depth, e->fe_mask, e->fe_out_rgb, e->fe_out_depth,
                   D.vis,     D.band,    D.cand,     D.arrive, D.fresh_vis, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
+                  e->vg_cell, e->vg_flags, e->vg_bits,
                   e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
                   e->t_i32,  e->t_u32,   e->t_f0,    e->t_f1,   e->t_s4};
   for (void* p : ptrs)
@@ -428,6 +436,10 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(e->s_lt, e->max_pixels);
   ALLOC(e->rc_rgba, e->max_pixels);
   ALLOC(e->rc_norm, e->max_pixels);
+  ALLOC(e->vg_flags, (size_t)kViewBitmapWords * 32);
+  ALLOC(e->vg_bits, kViewBitmapWords);
+  if (hipMemset(e->vg_flags, 0, (size_t)kViewBitmapWords * 32) != hipSuccess)
+    return fail(TSDF_ERR_HIP);
   ALLOC(e->q_sel, nb);
   ALLOC(e->q_count, 1);
   ALLOC(e->m_counts, nb);
@@ -693,6 +705,55 @@ int tsdf_get_stream(tsdf_engine* e, void** stream) {
   return TSDF_OK;
 }
 
+namespace {
+
+// The view grid of one raycast of camera P (tsdf_kernels.h ViewGrid). Its cube reaches every voxel
+// a ray can read: positions up to max_step * step_size / voxel grid units from the camera centre
+// (|direction| = 1 up to rounding), plus the binary search, the +-1 gradient neighbours and the
+// rounding to the nearest voxel (2.5 voxels). n = 0 (hash lookups) when the cube would exceed
+// kViewMaxN cells per axis, the brick bitmap `lds_words` of LDS, or the pool a cell's index bits.
+int view_grid_for(tsdf_engine* e, const FrameParams& P, float step_size, int lds_words, ViewGrid* V) {
+  *V = ViewGrid{};
+  V->flags = e->vg_flags;
+  V->bits = e->vg_bits;
+  const double max_step = std::ceil((double)P.max_depth / (double)step_size);
+  const double reach = max_step * (double)step_size / (double)P.voxel * (1.0 + 1e-5) + 2.5;
+  const int half = (int)std::ceil(reach / kBlockLen) + 1;
+  const int n = 2 * half + 1;
+  const int nb = (n + 3) / 4, ns = (nb + 3) / 4;
+  const int nbw = (nb * nb * nb + 31) / 32, nw = nbw + (ns * ns * ns + 31) / 32;
+  if (!(reach < 1e6) || n > kViewMaxN || nw > lds_words ||
+      e->D.nblocks > (1 << kViewIdxBits))
+    return TSDF_OK;
+  const int64_t cells = (int64_t)n * n * n;
+  if (cells > e->vg_cap) {
+    if (e->vg_cell) HIP_OK(hipFree(e->vg_cell));
+    e->vg_cell = nullptr;
+    e->vg_cap = 0;
+    HIP_OK(hipMalloc(&e->vg_cell, (size_t)cells * 4));
+    HIP_OK(hipMemsetAsync(e->vg_cell, 0, (size_t)cells * 4, e->stream));
+    e->vg_cap = cells;
+    e->vg_gen = 0;
+  }
+  if (e->vg_gen == kViewGenMax) {  // generations exhausted: stale cells must not match gen 1 again
+    HIP_OK(hipMemsetAsync(e->vg_cell, 0, (size_t)e->vg_cap * 4, e->stream));
+    e->vg_gen = 0;
+  }
+  e->vg_gen += 1;
+  e->vg_calls += 1;
+  V->cell = e->vg_cell;
+  V->n = n;
+  V->nb = nb;
+  V->ns = ns;
+  V->nbw = nbw;
+  V->nw = nw;
+  V->half = half;
+  V->gen = e->vg_gen;
+  return TSDF_OK;
+}
+
+}  // namespace
+
 // ---------------------------------------------------------------------------------------------
 // Graph-captured frame loop (BASELINE config C5): the whole per-frame sequence -- argument upload,
 // k_ingest_dda, k_resolve_alloc, k_integrate, k_resolve_delete and (optionally) k_raycast -- is one
@@ -780,9 +841,12 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
       hipLaunchKernelGGL(k_ingest_dda_g<2048>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
     hipLaunchKernelGGL((k_integrate_t<true>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, g->cap,
                        e->D, FrameParams{}, A);
-    if (render_width)
+    if (render_width) {
+      hipLaunchKernelGGL(k_view_grid_g, dim3(kOccWords / 256), dim3(256), 0, g->cap, e->D, A);
+      hipLaunchKernelGGL(k_view_pack_g, dim3(kViewPackGrid), dim3(256), 0, g->cap, A);
       hipLaunchKernelGGL(k_raycast_g, dim3((render_width + 15) / 16, (render_height + 15) / 16), dim3(256), 0,
                          g->cap, e->D, A);
+    }
     if ((err = hipStreamEndCapture(g->cap, &g->graph[k])) != hipSuccess) return fail(err, "hipStreamEndCapture");
     if ((err = hipGraphInstantiate(&g->exec[k], g->graph[k], nullptr, nullptr, 0)) != hipSuccess)
       return fail(err, "hipGraphInstantiate");
@@ -820,6 +884,10 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
   a.rgba = reinterpret_cast<uchar4*>(rgba);
   a.normal = reinterpret_cast<uchar4*>(normal);
   a.step_size = e->cfg.truncation / 2;
+  if (g->RW) {
+    int rc = view_grid_for(e, a.R, a.step_size, kViewGraphBitmapWords, &a.V);
+    if (rc) return rc;
+  }
   a.range = (uint32_t)((size_t)f->width * f->height * e->maxs);
   a.tiles_x = (f->width + 15) / 16;
   a.tiles = a.tiles_x * ((f->height + 15) / 16);
@@ -942,6 +1010,7 @@ int tsdf_feed_rgbd_frame(tsdf_engine* e, const uint8_t* rgb, const uint16_t* dep
   return tsdf_integrate(e, &f, K, cam_T_world, max_depth);
 }
 
+
 int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const tsdf_pose* pose,
                  float max_depth, uint8_t* rgba, uint8_t* normal, int mem_kind) {
   TraceRange trace_("tsdf_raycast");
@@ -954,8 +1023,19 @@ int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const t
   const FrameParams P = make_params(e, K, W, H, pose, max_depth);
   uchar4* o1 = mem_kind == TSDF_MEM_DEVICE ? reinterpret_cast<uchar4*>(rgba) : (rgba ? e->rc_rgba : nullptr);
   uchar4* o2 = mem_kind == TSDF_MEM_DEVICE ? reinterpret_cast<uchar4*>(normal) : (normal ? e->rc_norm : nullptr);
-  hipLaunchKernelGGL(k_raycast, dim3((W + 15) / 16, (H + 15) / 16), dim3(256), 0, e->stream, e->D,
-                     P, e->cfg.truncation / 2, o1, o2);
+  const float step = e->cfg.truncation / 2;
+  ViewGrid V;
+  int rc = view_grid_for(e, P, step, kViewBitmapWords, &V);
+  if (rc) return rc;
+  if (V.n) {
+    hipLaunchKernelGGL(k_view_grid, dim3(kOccWords / 256), dim3(256), 0, e->stream, e->D, P, V);
+    LAUNCH_OK("k_view_grid");
+    hipLaunchKernelGGL(k_view_pack, dim3(kViewPackGrid), dim3(256), 0, e->stream, V);
+    LAUNCH_OK("k_view_pack");
+  }
+  const size_t lds = V.n ? (size_t)V.nw * 4 : 0;
+  hipLaunchKernelGGL(k_raycast, dim3((W + 15) / 16, (H + 15) / 16), dim3(256), lds, e->stream, e->D,
+                     P, step, V, o1, o2);
   LAUNCH_OK("k_raycast");
   if (mem_kind == TSDF_MEM_HOST) {
     const size_t bytes = (size_t)W * H * 4;

@@ -111,34 +111,180 @@ __global__ __launch_bounds__(256) void k_vis_emit(EngineDev D, VisRec* __restric
 // ---------------------------------------------------------------------------------------------
 // raycast (ray_cast_kernel, voxel_tsdf.cu:232-307), nearest-voxel lookups
 // ---------------------------------------------------------------------------------------------
-struct VoxRef {
-  const uint8_t* blk;
-  int o;
-};
-__device__ __forceinline__ bool voxel_ref(const EngineDev& D, int16_t px, int16_t py, int16_t pz,
-                                          VoxRef& ref) {
-  const int16_t bx = (int16_t)(px >> kBlockLenBits), by = (int16_t)(py >> kBlockLenBits),
-                bz = (int16_t)(pz >> kBlockLenBits);
-  const int32_t e = find_local(D.table, bx, by, bz);
-  if (e < 0) return false;
-  const int32_t idx = D.table[e].z;
-  ref.blk = D.pool + (size_t)idx * kBlockBytes;
-  ref.o = (px & 7) + (py & 7) * kBlockLen + (pz & 7) * kBlockLen * kBlockLen;
-  return true;
+// View grid of the call (tsdf_kernels.h ViewGrid): every live block inside the cube gets its
+// generation-tagged pool index, and its brick's and superbrick's flag bytes are set -- plain byte
+// stores of 1 (any number of writers agree), where atomics on shared bitmap words would serialise
+// across the XCDs. One thread per occupancy word. k_view_pack then packs the flags into bits.
+__device__ __forceinline__ void view_grid(const EngineDev& D, const FrameParams& P, const ViewGrid& V) {
+  if (V.n == 0) return;
+  const int w = blockIdx.x * 256 + threadIdx.x;
+  const int ox = view_origin(P.wt.x, P.voxel, V.half), oy = view_origin(P.wt.y, P.voxel, V.half),
+            oz = view_origin(P.wt.z, P.voxel, V.half);
+  unsigned long long occ = D.occ[w];
+  while (occ) {
+    const int b = __ffsll((long long)occ) - 1;
+    occ &= occ - 1;
+    const Ent en = load_ent(D.table, (uint32_t)(w * 64 + b));
+    const int lx = en.x - ox, ly = en.y - oy, lz = en.z - oz;
+    if ((unsigned)lx >= (unsigned)V.n || (unsigned)ly >= (unsigned)V.n || (unsigned)lz >= (unsigned)V.n ||
+        !local_idx(en.idx))
+      continue;
+    V.cell[((size_t)lz * V.n + ly) * V.n + lx] = (V.gen << kViewIdxBits) | (uint32_t)en.idx;
+    V.flags[((lz >> 2) * V.nb + (ly >> 2)) * V.nb + (lx >> 2)] = 1;
+    V.flags[V.nbw * 32 + ((lz >> 4) * V.ns + (ly >> 4)) * V.ns + (lx >> 4)] = 1;
+  }
 }
-__device__ __forceinline__ float retrieve_tsdf(const EngineDev& D, int16_t x, int16_t y, int16_t z) {
-  VoxRef r;
-  if (!voxel_ref(D, x, y, z, r)) return 1.0f;  // VoxelTSDF() default (voxel_types.cu:9)
-  return reinterpret_cast<const float*>(r.blk)[r.o];
+__global__ __launch_bounds__(256) void k_view_grid(EngineDev D, FrameParams P, ViewGrid V) {
+  view_grid(D, P, V);
+}
+__global__ __launch_bounds__(256) void k_view_grid_g(EngineDev D, const FrameArgs* __restrict__ A) {
+  view_grid(D, A->R, A->V);
+}
+// one bitmap word per thread from its 32 flag bytes, which it zeroes for the next call
+__device__ __forceinline__ void view_pack(const ViewGrid& V) {
+  const int w = blockIdx.x * 256 + threadIdx.x;
+  if (V.n == 0 || w >= V.nw) return;
+  uint4* f = reinterpret_cast<uint4*>(V.flags + (size_t)w * 32);
+  const uint4 a = f[0], b = f[1];
+  const uint32_t in[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t word = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) word |= ((in[k] >> (8 * j)) & 1u) << (4 * k + j);
+  V.bits[w] = word;
+  if (a.x | a.y | a.z | a.w) f[0] = make_uint4(0, 0, 0, 0);
+  if (b.x | b.y | b.z | b.w) f[1] = make_uint4(0, 0, 0, 0);
+}
+__global__ __launch_bounds__(256) void k_view_pack(ViewGrid V) { view_pack(V); }
+__global__ __launch_bounds__(256) void k_view_pack_g(const FrameArgs* __restrict__ A) { view_pack(A->V); }
+
+// One ray's block cache (the reference's per-thread VoxelBlock cache, voxel_hash.cuh:124-161): the
+// block of the last lookup and its pool index (-1: missing), and the empty region around it: 0 none,
+// 1 its brick holds no block, 2 its superbrick holds none.
+struct RayCache {
+  int bx, by, bz;
+  int32_t idx;
+  int empty;
+};
+struct RayView {
+  const uint32_t* cell;
+  const uint32_t* bits;  // LDS copy of the bitmaps (bricks, then superbricks)
+  int n, nb, ns, nbw, ox, oy, oz;
+  uint32_t gen;
+};
+__device__ __forceinline__ void ray_block(const EngineDev& D, const RayView& R, RayCache& c, int bx,
+                                          int by, int bz) {
+  if (bx == c.bx && by == c.by && bz == c.bz) return;
+  c.bx = bx;
+  c.by = by;
+  c.bz = bz;
+  c.empty = 0;
+  const int lx = bx - R.ox, ly = by - R.oy, lz = bz - R.oz;
+  const int n = R.n;
+  if ((unsigned)lx < (unsigned)n && (unsigned)ly < (unsigned)n && (unsigned)lz < (unsigned)n) {
+    const int k = ((lz >> 2) * R.nb + (ly >> 2)) * R.nb + (lx >> 2);
+    if (!((R.bits[k >> 5] >> (k & 31)) & 1u)) {
+      c.idx = -1;
+      const int q = ((lz >> 4) * R.ns + (ly >> 4)) * R.ns + (lx >> 4);
+      c.empty = ((R.bits[R.nbw + (q >> 5)] >> (q & 31)) & 1u) ? 1 : 2;
+      return;
+    }
+    const uint32_t v = R.cell[((size_t)lz * n + ly) * n + lx];
+    c.idx = (v >> kViewIdxBits) == R.gen ? (int32_t)(v & ((1u << kViewIdxBits) - 1)) : -1;
+    return;
+  }
+  const int32_t e = find_local(D.table, (int16_t)bx, (int16_t)by, (int16_t)bz);  // outside the grid / none
+  c.idx = e < 0 ? -1 : D.table[e].z;
+}
+__device__ __forceinline__ int voxel_off(int16_t px, int16_t py, int16_t pz) {
+  return (px & 7) + (py & 7) * kBlockLen + (pz & 7) * kBlockLen * kBlockLen;
+}
+// Retrieve<VoxelTSDF>(point, cache).tsdf: VoxelTSDF() default +1 (voxel_types.cu:9) when missing
+__device__ __forceinline__ float ray_tsdf(const EngineDev& D, const RayView& R, RayCache& c, int16_t px,
+                                          int16_t py, int16_t pz) {
+  ray_block(D, R, c, px >> kBlockLenBits, py >> kBlockLenBits, pz >> kBlockLenBits);
+  if (c.idx < 0) return 1.0f;
+  return reinterpret_cast<const float*>(D.pool + (size_t)c.idx * kBlockBytes)[voxel_off(px, py, pz)];
 }
 
-__device__ __forceinline__ void raycast(EngineDev D, FrameParams P, float step_size,
-                                        uchar4* __restrict__ rgba, uchar4* __restrict__ normal) {
-  const int x = blockIdx.x * 16 + (threadIdx.x & 15);
-  const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
-  if (x >= P.W || y >= P.H) return;
-  const int idx = y * P.W + x;
-  const f3 pc = pixel_ray(P, x, y);
+// The hit of ray_cast_kernel (voxel_tsdf.cu:259-300) at position hp: binary search between
+// hp - step and hp, the voxel's colour / probability and the central-difference normal.
+__device__ __forceinline__ void ray_shade(const EngineDev& D, const RayView& R, RayCache& c, f3 hp, f3 sg,
+                                       f3 dw, uchar4* __restrict__ rgba, uchar4* __restrict__ normal, int idx) {
+  f3 p1 = {hp.x - sg.x, hp.y - sg.y, hp.z - sg.z};
+  f3 p2 = hp;
+  f3 mid = {(p1.x + p2.x) / 2, (p1.y + p2.y) / 2, (p1.z + p2.z) / 2};
+  for (;;) {
+    const f3 dd = {p1.x - p2.x, p1.y - p2.y, p1.z - p2.z};
+    if (!((double)dot3(dd, dd) > .1)) break;
+    if (ray_tsdf(D, R, c, f2s(roundf(mid.x)), f2s(roundf(mid.y)), f2s(roundf(mid.z))) < 0)
+      p2 = mid;
+    else
+      p1 = mid;
+    mid.x = (p1.x + p2.x) / 2;
+    mid.y = (p1.y + p2.y) / 2;
+    mid.z = (p1.z + p2.z) / 2;
+  }
+  const int16_t fx = f2s(roundf(mid.x)), fy = f2s(roundf(mid.y)), fz = f2s(roundf(mid.z));
+  uint32_t col = 0;
+  float prob = 0.0f;  // VoxelRGBW() / VoxelSEGM() defaults
+  ray_block(D, R, c, fx >> kBlockLenBits, fy >> kBlockLenBits, fz >> kBlockLenBits);
+  if (c.idx >= 0) {
+    const uint8_t* blk = D.pool + (size_t)c.idx * kBlockBytes;
+    const int o = voxel_off(fx, fy, fz);
+    col = reinterpret_cast<const uint32_t*>(blk + kRgbwOffset)[o];
+    prob = prob_of_logodds(reinterpret_cast<const float*>(blk + kProbOffset)[o]);
+  }
+  const float gxp = ray_tsdf(D, R, c, (int16_t)(fx + 1), fy, fz);
+  const float gxn = ray_tsdf(D, R, c, (int16_t)(fx - 1), fy, fz);
+  const float gyp = ray_tsdf(D, R, c, fx, (int16_t)(fy + 1), fz);
+  const float gyn = ray_tsdf(D, R, c, fx, (int16_t)(fy - 1), fz);
+  const float gzp = ray_tsdf(D, R, c, fx, fy, (int16_t)(fz + 1));
+  const float gzn = ray_tsdf(D, R, c, fx, fy, (int16_t)(fz - 1));
+  const f3 nr = {gxp - gxn, gyp - gyn, gzp - gzn};
+  const f3 nd = {-dw.x, -dw.y, -dw.z};
+  const float diff = fmaxf(dot3(nr, nd) / sqrtf(dot3(nr, nr)), 0.0f);
+  const float alpha = (float)((double)fmaxf((float)((double)prob - 0.5), 0.0f) / .5);
+  const float oma = 1 - alpha;
+  if (rgba)
+    rgba[idx] = make_uchar4(f2u8(alpha * 255 + oma * (float)(col & 0xFF)), f2u8(oma * (float)((col >> 8) & 0xFF)),
+                            f2u8(oma * (float)((col >> 16) & 0xFF)), 255);
+  const float sh = oma * diff * 255;
+  if (normal) normal[idx] = make_uchar4(f2u8(alpha * 255 + sh), f2u8(sh), f2u8(sh), 255);
+}
+
+__device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P, float step_size,
+                                        const ViewGrid& V, uint32_t* sbits, uchar4* __restrict__ rgba,
+                                        uchar4* __restrict__ normal) {
+  // stage the bitmaps (all threads, before any ray returns)
+  const int nw = V.n ? V.nw : 0;
+  for (int i = threadIdx.x; i < nw; i += 256) sbits[i] = V.bits[i];
+  __syncthreads();
+  // XCD-aware tiles: workgroups wg and wg + 8 share an XCD (and its L2), so XCD g takes the g-th
+  // contiguous run of 16x16 tiles in raster order -- neighbouring rays' blocks stay in one L2
+  const int gx = gridDim.x, nwg = gx * gridDim.y, wg = blockIdx.y * gx + blockIdx.x;
+  const int g = wg & 7, tile = g * (nwg >> 3) + min(g, nwg & 7) + (wg >> 3);
+  const int x = (tile % gx) * 16 + (threadIdx.x & 15);
+  const int y = (tile / gx) * 16 + (threadIdx.x >> 4);
+  const bool valid = x < P.W && y < P.H;
+  const int idx = valid ? y * P.W + x : 0;
+  RayView R;
+  R.cell = V.cell;
+  R.bits = sbits;
+  R.n = V.n;
+  R.nb = V.nb;
+  R.ns = V.ns;
+  R.nbw = V.nbw;
+  R.gen = V.gen;
+  R.ox = view_origin(P.wt.x, P.voxel, V.half);
+  R.oy = view_origin(P.wt.y, P.voxel, V.half);
+  R.oz = view_origin(P.wt.z, P.voxel, V.half);
+  RayCache c;
+  c.bx = c.by = c.bz = 0x7FFFFFFF;  // no block (block coordinates are int16)
+  c.idx = -1;
+  c.empty = 0;
+  const f3 pc = pixel_ray(P, valid ? x : 0, valid ? y : 0);
   const float nn = dot3(pc, pc);
   f3 dc = pc;
   if (nn > 0) {
@@ -149,68 +295,66 @@ __device__ __forceinline__ void raycast(EngineDev D, FrameParams P, float step_s
   }
   const f3 dw = qrot(P.wq, dc);
   const f3 sg = {dw.x * step_size / P.voxel, dw.y * step_size / P.voxel, dw.z * step_size / P.voxel};
-  const int max_step = f2i(ceilf(P.max_depth / step_size));
+  const int max_step = f2i(ceilf(P.max_depth / step_size));  // wave-uniform
   f3 pos = {P.wt.x / P.voxel, P.wt.y / P.voxel, P.wt.z / P.voxel};
-  float prev = retrieve_tsdf(D, f2s(roundf(pos.x)), f2s(roundf(pos.y)), f2s(roundf(pos.z)));
+  bool done = !valid;
+  float prev = 1.0f;
+  if (valid) prev = ray_tsdf(D, R, c, f2s(roundf(pos.x)), f2s(roundf(pos.y)), f2s(roundf(pos.z)));
   pos.x += sg.x;
   pos.y += sg.y;
   pos.z += sg.z;
-  for (int i = 1; i < max_step; ++i) {
-    const float cur = retrieve_tsdf(D, f2s(roundf(pos.x)), f2s(roundf(pos.y)), f2s(roundf(pos.z)));
-    if (prev > 0 && cur <= 0 && (double)(prev - cur) <= 1.5) {
-      f3 p1 = {pos.x - sg.x, pos.y - sg.y, pos.z - sg.z};
-      f3 p2 = pos;
-      f3 mid = {(p1.x + p2.x) / 2, (p1.y + p2.y) / 2, (p1.z + p2.z) / 2};
-      for (;;) {
-        const f3 dd = {p1.x - p2.x, p1.y - p2.y, p1.z - p2.z};
-        if (!((double)dot3(dd, dd) > .1)) break;
-        if (retrieve_tsdf(D, f2s(roundf(mid.x)), f2s(roundf(mid.y)), f2s(roundf(mid.z))) < 0)
-          p2 = mid;
-        else
-          p1 = mid;
-        mid.x = (p1.x + p2.x) / 2;
-        mid.y = (p1.y + p2.y) / 2;
-        mid.z = (p1.z + p2.z) / 2;
+  // Region of the last lookup, as float bounds x in (lo, hi) per axis of the positions that surely
+  // round into it: the missing block or the empty brick / superbrick around it (reads +1: no lookup,
+  // no hit), or the present block (only the voxel offset and its load). The lanes of a wave step
+  // together (a tight per-lane loop through empty regions measured slower: the lanes' dependent
+  // loads then no longer overlap in time -- the kernel is bound by those load chains).
+  f3 rlo = {1.f, 1.f, 1.f}, rhi = {0.f, 0.f, 0.f};
+  int32_t ridx = -1;  // pool index of the present block of the region, -1 missing
+  int i = 1;
+  while (i < max_step && !done) {
+    const bool inside = pos.x > rlo.x && pos.x < rhi.x && pos.y > rlo.y && pos.y < rhi.y && pos.z > rlo.z &&
+                        pos.z < rhi.z;
+    const int16_t px = round_s16(pos.x), py = round_s16(pos.y), pz = round_s16(pos.z);
+    if (!inside) {
+      ray_block(D, R, c, px >> kBlockLenBits, py >> kBlockLenBits, pz >> kBlockLenBits);
+      ridx = c.idx;
+      const int sh = c.idx >= 0 ? 0 : c.empty == 2 ? 4 : c.empty == 1 ? 2 : 0;  // 2^sh blocks per axis
+      const int rx = (sh ? R.ox + (((c.bx - R.ox) >> sh) << sh) : c.bx) * kBlockLen;
+      const int ry = (sh ? R.oy + (((c.by - R.oy) >> sh) << sh) : c.by) * kBlockLen;
+      const int rz = (sh ? R.oz + (((c.bz - R.oz) >> sh) << sh) : c.bz) * kBlockLen;
+      const float len = (float)(kBlockLen << sh);
+      rlo = {(float)rx - 0.5f, (float)ry - 0.5f, (float)rz - 0.5f};
+      rhi = {rlo.x + len, rlo.y + len, rlo.z + len};
+    }
+    float cur = 1.0f;
+    if (ridx >= 0) {
+      cur = reinterpret_cast<const float*>(D.pool + (size_t)ridx * kBlockBytes)[voxel_off(px, py, pz)];
+      if (prev > 0 && cur <= 0 && (double)(prev - cur) <= 1.5) {
+        ray_shade(D, R, c, pos, sg, dw, rgba, normal, idx);
+        done = true;
       }
-      const int16_t fx = f2s(roundf(mid.x)), fy = f2s(roundf(mid.y)), fz = f2s(roundf(mid.z));
-      uint32_t c = 0;
-      float prob = 0.0f;  // VoxelRGBW() / VoxelSEGM() defaults
-      VoxRef ref;
-      if (voxel_ref(D, fx, fy, fz, ref)) {
-        c = reinterpret_cast<const uint32_t*>(ref.blk + kRgbwOffset)[ref.o];
-        prob = prob_of_logodds(reinterpret_cast<const float*>(ref.blk + kProbOffset)[ref.o]);
-      }
-      const f3 nr = {retrieve_tsdf(D, (int16_t)(fx + 1), fy, fz) - retrieve_tsdf(D, (int16_t)(fx - 1), fy, fz),
-                     retrieve_tsdf(D, fx, (int16_t)(fy + 1), fz) - retrieve_tsdf(D, fx, (int16_t)(fy - 1), fz),
-                     retrieve_tsdf(D, fx, fy, (int16_t)(fz + 1)) - retrieve_tsdf(D, fx, fy, (int16_t)(fz - 1))};
-      const f3 nd = {-dw.x, -dw.y, -dw.z};
-      const float diff = fmaxf(dot3(nr, nd) / sqrtf(dot3(nr, nr)), 0.0f);
-      const float alpha = (float)((double)fmaxf((float)((double)prob - 0.5), 0.0f) / .5);
-      const float oma = 1 - alpha;
-      if (rgba)
-        rgba[idx] = make_uchar4(f2u8(alpha * 255 + oma * (float)(c & 0xFF)),
-                                f2u8(oma * (float)((c >> 8) & 0xFF)),
-                                f2u8(oma * (float)((c >> 16) & 0xFF)), 255);
-      const float sh = oma * diff * 255;
-      if (normal) normal[idx] = make_uchar4(f2u8(alpha * 255 + sh), f2u8(sh), f2u8(sh), 255);
-      return;
     }
     prev = cur;
     pos.x += sg.x;
     pos.y += sg.y;
     pos.z += sg.z;
+    ++i;
   }
-  if (rgba) rgba[idx] = make_uchar4(0, 0, 0, 0);
-  if (normal) normal[idx] = make_uchar4(0, 0, 0, 0);
+  if (valid && !done) {
+    if (rgba) rgba[idx] = make_uchar4(0, 0, 0, 0);
+    if (normal) normal[idx] = make_uchar4(0, 0, 0, 0);
+  }
 }
-__global__ __launch_bounds__(256) void k_raycast(EngineDev D, FrameParams P, float step_size,
-                                                 uchar4* __restrict__ rgba,
-                                                 uchar4* __restrict__ normal) {
-  raycast(D, P, step_size, rgba, normal);
+__global__ __launch_bounds__(256) void k_raycast(EngineDev D, FrameParams P, float step_size, ViewGrid V,
+                                                 uchar4* __restrict__ rgba, uchar4* __restrict__ normal) {
+  extern __shared__ uint32_t sbits[];
+  raycast(D, P, step_size, V, sbits, rgba, normal);
 }
 __global__ __launch_bounds__(256) void k_raycast_g(EngineDev D, const FrameArgs* __restrict__ A) {
+  __shared__ uint32_t sbits[kViewGraphBitmapWords];
   const FrameParams R = A->R;
-  raycast(D, R, A->step_size, A->rgba, A->normal);
+  const ViewGrid V = A->V;
+  raycast(D, R, A->step_size, V, sbits, A->rgba, A->normal);
 }
 
 // download_tsdf_kernel (voxel_tsdf.cu:34-46): one workgroup of 512 threads per selected block

@@ -55,6 +55,33 @@ struct EngineDev {
   unsigned long long* dbg;      // diagnostic stamps (DIAG builds), else unused
 };
 
+// View grid of one raycast: a dense cube of n^3 block cells around the camera, wide
+// enough for every voxel a ray of the call can read (marched length + binary search + gradient
+// neighbours), each cell the block's pool index tagged with the call's generation (stale cells of
+// earlier calls read as missing, so nothing is cleared per call), plus occupancy bitmaps of its
+// 4^3-block bricks and 16^3-block superbricks that the raycast workgroups stage in LDS to skip empty
+// space. n == 0: no grid (a view too deep for it); the raycast then looks every block up in the hash
+// table.
+constexpr int kViewIdxBits = 22;                  // pool index bits of a cell (gen in the top 10)
+constexpr uint32_t kViewGenMax = 1023u;           // generations 1..1023, then the cells are zeroed
+constexpr int kViewMaxN = 256;                    // cells per axis at most (64 bricks per axis)
+constexpr int kViewBitmapWords = (kViewMaxN / 4) * (kViewMaxN / 4) * (kViewMaxN / 4) / 32 +
+                                 (kViewMaxN / 16) * (kViewMaxN / 16) * (kViewMaxN / 16) / 32;
+constexpr int kViewGraphBitmapWords = 4608;       // LDS bitmap words of the graph's raycast node
+struct ViewGrid {
+  uint32_t* cell;          // n^3: gen << kViewIdxBits | pool index
+  uint8_t* flags;          // kViewBitmapWords * 32 bytes: brick / superbrick occupied (1), word w's bits
+                           // at bytes [32 w, 32 w + 32); zero between calls (k_view_pack clears them)
+  uint32_t* bits;          // the packed bitmaps: nb^3 brick bits, then ns^3 superbrick bits
+  int n, nb, ns, half;     // cells, bricks (ceil(n / 4)), superbricks (ceil(nb / 4)) per axis
+  int nbw, nw;             // brick words, all bitmap words
+  uint32_t gen;
+};
+// origin (block coordinates) of the view grid of camera centre wt: both kernels compute it alike
+__device__ __forceinline__ int view_origin(float wt, float voxel, int half) {
+  return (f2i(floorf(wt / voxel)) >> kBlockLenBits) - half;
+}
+
 // per-frame arguments of the graph-captured frame loop (tsdf_graph_*): the graph's first node
 // copies them from a pinned host slot, every graph kernel reads its camera / frame pointers here
 struct FrameArgs {
@@ -67,6 +94,7 @@ struct FrameArgs {
   uchar4* rgba;
   uchar4* normal;
   float step_size;  // raycast step (truncation / 2)
+  ViewGrid V;       // the raycast node's view grid (n == 0: hash lookups)
   uint32_t range;   // candidate order space W * H * maxs
   int tiles_x, tiles;
 };
@@ -112,8 +140,15 @@ template <bool Emit>
 __global__ void k_mesh(EngineDev D, const VisRec* sel, MeshParams M, int32_t* counts,
                        const int32_t* offsets, float* out);
 __global__ void k_scan_counts(const int32_t* counts, int n, int32_t* offsets, int64_t* total);
-__global__ void k_raycast(EngineDev D, FrameParams P, float step_size, uchar4* rgba,
+__global__ void k_raycast(EngineDev D, FrameParams P, float step_size, ViewGrid V, uchar4* rgba,
                           uchar4* normal);
+// view grid of a raycast: grid kOccWords / 256 workgroups of 256
+__global__ void k_view_grid(EngineDev D, FrameParams P, ViewGrid V);
+__global__ void k_view_grid_g(EngineDev D, const FrameArgs* A);
+// flags -> bits (and the flags cleared): kViewPackGrid workgroups of 256, one word per thread
+constexpr int kViewPackGrid = (kViewBitmapWords + 255) / 256;
+__global__ void k_view_pack(ViewGrid V);
+__global__ void k_view_pack_g(const FrameArgs* A);
 __global__ void k_query_count(EngineDev D, int use_bounds, short4 lo, short4 hi);
 __global__ void k_vis_emit(EngineDev D, VisRec* out, int32_t* out_count);
 __global__ void k_query_download(EngineDev D, const VisRec* sel, float voxel, float4* out);

@@ -1,11 +1,12 @@
 // tsdf_selfcheck.hip -- test-only library (libtsdf_selfcheck.so): checks the engine's fast exact
 // quotient helpers (tsdf_device.h: round_quot_i/_u8/_pos2, div_pair, quot_const, quot_for_cmp,
-// f2i / f2u8) bit-for-bit against the
+// f2i / f2u8 / round_s16) bit-for-bit against the
 // correctly rounded IEEE divide and the saturating conversions, on the GPU, over exhaustive and
 // adversarial input sets. Not part of the product library; tests/test_gpu_numerics.py drives it.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
 
 #include "tsdf_device.h"
 
@@ -144,7 +145,7 @@ __global__ void k_convert(uint32_t lo, uint32_t hi, unsigned long long* bad, uin
                        : t <= -2147483648.0f ? (-2147483647 - 1) : (int32_t)t;
     const int32_t es = f != f ? 0 : t >= 32767.0f ? 32767 : t <= -32768.0f ? -32768 : (int32_t)t;
     const uint32_t eu = !(t > 0.0f) ? 0u : t >= 255.0f ? 255u : (uint32_t)t;
-    if (f2i(f) != ei || f2s(f) != es || f2u8(f) != eu) {
+    if (f2i(f) != ei || f2s(f) != es || f2u8(f) != eu || round_s16(f) != f2s(roundf(f))) {
       atomicAdd(bad, 1ull);
       atomicMin(first, bits);
     }
@@ -158,7 +159,12 @@ struct Out {
 
 int finish(Out* d, unsigned long long* bad, uint32_t* first) {
   Out h{};
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  hipError_t err = hipGetLastError();
+  if (err == hipSuccess) err = hipDeviceSynchronize();
+  if (err != hipSuccess) {
+    std::fprintf(stderr, "tsdf_selfcheck: %s\n", hipGetErrorString(err));
+    return -2;
+  }
   if (hipMemcpy(&h, d, sizeof(Out), hipMemcpyDeviceToHost) != hipSuccess) return -1;
   (void)hipFree(d);
   *bad = h.bad;
@@ -168,9 +174,13 @@ int finish(Out* d, unsigned long long* bad, uint32_t* first) {
 
 Out* start() {
   Out* d = nullptr;
-  if (hipMalloc(&d, sizeof(Out)) != hipSuccess) return nullptr;
+  hipError_t err = hipMalloc(&d, sizeof(Out));
   Out h{0ull, 0xFFFFFFFFu};
-  if (hipMemcpy(d, &h, sizeof(Out), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+  if (err == hipSuccess) err = hipMemcpy(d, &h, sizeof(Out), hipMemcpyHostToDevice);
+  if (err != hipSuccess) {
+    std::fprintf(stderr, "tsdf_selfcheck: %s\n", hipGetErrorString(err));
+    return nullptr;
+  }
   return d;
 }
 

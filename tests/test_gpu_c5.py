@@ -1,0 +1,137 @@
+"""BASELINE configs C5 and C3 at their workload against the CPU oracle:
+
+ - the 640x480 render() stream integrated for 30 frames into a 2^18-block pool, eager engine and
+   oracle compared every 10 frames (hash table, free stack, every voxel);
+ - C5 on the same stream: the graph-captured frame (integrate + raycast of the frame's camera in one
+   hipGraph launch) and the eager chain render every frame identically, the 640x480 raycast equals
+   the oracle's at frames 0, 14 and 29, and marching cubes at frame 30 equals the oracle's mesh bit
+   for bit (tsdf_extract_mesh, voxel_tsdf.cu's caller ros_offline.cc:279-287);
+ - the raycast view grid (tsdf_kernels.h ViewGrid) against the hash-lookup path it replaces: views
+   too deep for the grid, cameras outside the volume, and more calls than the grid has generations.
+"""
+import numpy as np
+import pytest
+
+from test_gpu_parity import compare
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_render(rgba, nrm, rgba_o, nrm_o, tag):
+    hit = rgba[..., 3] == 255
+    assert np.array_equal(rgba[..., 3], rgba_o[..., 3]), f"{tag}: hit mask differs"
+    # colour / shading within 1 LSB (log-odds probability state)
+    assert np.abs(rgba.astype(int) - rgba_o).max() <= 1, tag
+    assert np.abs(nrm.astype(int) - nrm_o).max() <= 1, tag
+    return hit.mean()
+
+
+def test_c5_640x480_stream_graph_eager_oracle():
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    from _oracle import OracleGrid
+    W, H, n = 640, 480, 30
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    a = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=18)
+    b = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=18)
+    ora = OracleGrid(0.005, 0.03, 18)
+    g = b.frame_graph(W, H, W, H)
+    try:
+        img = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(4)]
+        dev = {}
+        for i in range(n):
+            fr = synth.render(cam, i)
+            pose = tsdf_amd.SE3(fr["q"], fr["t"])
+            for k in ("rgb", "depth", "ht", "lt"):  # the graph takes device frames
+                dev[k] = torch.from_numpy(fr[k]).to("cuda")
+            a.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, pose, 4.0)
+            a.raycast(K, W, H, pose, 4.0, rgba=img[0], normal=img[1])
+            g.frame(dev["rgb"], dev["depth"], dev["ht"], dev["lt"], K, pose, 4.0, K, pose, img[2], img[3])
+            ora.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], 4.0, cam.K, fr["q"], fr["t"])
+            torch.cuda.synchronize()
+            assert torch.equal(img[0], img[2]) and torch.equal(img[1], img[3]), f"frame {i}: graph != eager"
+            s, so = a.stats(), ora.stats()
+            assert s["status"] == 0 and b.stats()["status"] == 0
+            for k in ("last_num_visible", "last_num_updated", "last_num_deleted", "active_blocks"):
+                assert s[k] == so[k] == b.stats()[k], (i, k, s[k], so[k])
+            if i in (0, 14, n - 1):
+                ro, no = ora.raycast(cam.K, W, H, fr["q"], fr["t"], 4.0)
+                frac = _check_render(img[0].cpu().numpy(), img[1].cpu().numpy(), ro, no, f"frame {i}")
+                assert frac > 0.5
+            if (i + 1) % 10 == 0:
+                compare(a, ora, tag=f"frame {i}")
+        # marching cubes every 30 frames (C5): the whole volume
+        m_a = a.extract_mesh(None, 0.99, 0)
+        m_b = b.extract_mesh(None, 0.99, 0)
+        m_o = ora.extract_mesh(None, 0.99, 0)
+        assert m_a.shape[0] > 100000
+        np.testing.assert_array_equal(np.asarray(m_a).view(np.uint32), np.asarray(m_o).view(np.uint32))
+        np.testing.assert_array_equal(np.asarray(m_b).view(np.uint32), np.asarray(m_o).view(np.uint32))
+    finally:
+        g.close()
+        a.close(), b.close(), ora.close()
+
+
+@pytest.mark.parametrize("max_depth", [2.0, 4.0, 9.0])
+def test_raycast_view_grid_depths_and_outside_cameras(max_depth):
+    """4 m and 2 m use the view grid, 9 m exceeds it (hash lookups); cameras inside the volume,
+    behind it and far outside it (no block within reach) render like the oracle."""
+    import tsdf_amd
+    from tsdf_amd import synth
+    from _oracle import OracleGrid
+    W, H = 160, 120
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    eng = tsdf_amd.Engine(0.01, 0.04, max_width=W, max_height=H, num_block_bits=15)
+    ora = OracleGrid(0.01, 0.04, 15)
+    try:
+        for f in range(0, 24, 3):
+            fr = synth.render(cam, f)
+            eng.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, tsdf_amd.SE3(fr["q"], fr["t"]), 4.0)
+            ora.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], 4.0, cam.K, fr["q"], fr["t"])
+        rng = np.random.default_rng(5)
+        views = [synth.pose(f)[1] for f in (2, 11, 40)]
+        for _ in range(3):  # random orientations at random places, some far outside the room
+            q = rng.normal(size=4)
+            q = (q / np.linalg.norm(q)).astype(np.float32)
+            t = rng.uniform(-12, 12, size=3).astype(np.float32)
+            views.append((q, t))
+        hits = 0.0
+        for q, t in views:
+            rgba, nrm = eng.raycast(cam.K, W, H, tsdf_amd.SE3(q, t), max_depth)
+            ro, no = ora.raycast(cam.K, W, H, q, t, max_depth)
+            hits += _check_render(rgba, nrm, ro, no, f"view {q} {t} depth {max_depth}")
+        assert hits > 0.5
+    finally:
+        eng.close(), ora.close()
+
+
+def test_raycast_view_grid_generations_wrap():
+    """More raycasts than the view grid has generations (1023): cells of earlier calls never read
+    as this call's blocks, also after blocks were carved away and the cells were zeroed."""
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H = 32, 24
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    eng = tsdf_amd.Engine(0.01, 0.04, max_width=W, max_height=H, num_block_bits=14)
+    try:
+        fr = synth.render(cam, 0)
+        pose = tsdf_amd.SE3(fr["q"], fr["t"])
+        eng.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, pose, 4.0)
+        ref = eng.raycast(cam.K, W, H, pose, 4.0)
+        assert (ref[0][..., 3] == 255).mean() > 0.5
+        away = tsdf_amd.SE3(fr["q"], np.asarray(fr["t"]) + np.float32(0.5))
+        for i in range(1100):
+            img = eng.raycast(cam.K, W, H, pose if i % 2 else away, 4.0)
+            if i % 2 and i % 97 == 1:
+                assert np.array_equal(img[0], ref[0]) and np.array_equal(img[1], ref[1]), i
+        eng.reset()  # every block gone: the same view must now see nothing
+        img = eng.raycast(cam.K, W, H, pose, 4.0)
+        assert (img[0][..., 3] == 0).all()
+        eng.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, pose, 4.0)
+        img = eng.raycast(cam.K, W, H, pose, 4.0)
+        assert np.array_equal(img[0], ref[0]) and np.array_equal(img[1], ref[1])
+    finally:
+        eng.close()

@@ -11,7 +11,8 @@ The integrate and ingest kernels replace the 11-op IEEE divide where an exact sh
    (voxel_visible's frustum test); adversarial samples at both thresholds;
  - div_pair(a, b, rcp(b))     -- the IEEE divide expansion without its range scaling (tsdf
    running average); every a in the fast range against fixed divisors, 2^28 random pairs;
- - f2i / f2s / f2u8 via v_cvt_{i,u}32_f32 -- checked on every float bit pattern.
+ - f2i / f2s / f2u8 via v_cvt_{i,u}32_f32, and round_s16 (= f2s(roundf(f)), the raycast's voxel
+   rounding) -- checked on every float bit pattern.
 Each must agree bit for bit with the correctly rounded divide / cvt.rzi semantics.
 """
 import ctypes as C
@@ -27,6 +28,11 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def lib():
+    # torch's HIP runtime first (conftest._torch_hip_first runs after module fixtures): loaded before
+    # it, this library would bring up the /opt/rocm runtime as a second one in the process
+    import torch
+    if torch.cuda.is_available():
+        torch.zeros(1, device="cuda")
     L = C.CDLL(LIB)
     u32, u64, f = C.c_uint32, C.c_uint64, C.c_float
     P64, P32 = C.POINTER(C.c_ulonglong), C.POINTER(C.c_uint32)
