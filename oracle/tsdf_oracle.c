@@ -11,7 +11,6 @@
  */
 #include "tsdf_oracle.h"
 
-#include "../disinfect-slam_amd/csrc/tsdf_mc_tables.h" /* generated case table (data only) */
 
 #include <math.h>
 #include <stdlib.h>
@@ -984,9 +983,11 @@ void ora_pool_get_weights(const ora_grid* g, int32_t b, uint8_t* out) {
  *  - order: blocks in hash-entry order, cells of a block by (z, y, x) of c in [8b - 1, 8b + 7]^3,
  *    triangles in case-table order; vertex on edge (a, b): t = va / (va - vb), p = pa + t (pb - pa)
  *    along the edge's axis. Output: 9 floats per triangle. */
-static const int8_t kOraMcEdge[12][2] = TSDF_MC_EDGE_INIT;
-static const uint8_t kOraMcNumTri[256] = TSDF_MC_NUM_TRI_INIT;
-static const int8_t kOraMcTri[256][3 * TSDF_MC_MAX_TRI] = TSDF_MC_TRI_INIT;
+/* the case table: derived by ora_mc_cases.c (not the product's header; tests/test_mc_table.py
+ * checks the two are equal) */
+const int8_t* ora_mc_tri(void);
+const uint8_t* ora_mc_ntri(void);
+int ora_mc_edge(int e, int s);
 
 static int block_selected(const ora_grid* g, s3 blk, const int16_t* bb, int64_t* e_out) {
   const int64_t e = hash_find(g, blk);
@@ -1039,13 +1040,13 @@ int64_t ora_extract_mesh(const ora_grid* g, const float* bounds, float missing, 
           int cube = 0;
           for (int i = 0; i < 8; ++i)
             if (val[i] < 0) cube |= 1 << i;
-          const int nt = kOraMcNumTri[cube];
+          const int nt = ora_mc_ntri()[cube];
           for (int t = 0; t < nt; ++t) {
             if (out && n < capacity) {
               float* w = &out[n * 9];
               for (int k = 0; k < 3; ++k) {
-                const int ed = kOraMcTri[cube][3 * t + k];
-                const int a = kOraMcEdge[ed][0], bc = kOraMcEdge[ed][1];
+                const int ed = ora_mc_tri()[cube * 15 + 3 * t + k];
+                const int a = ora_mc_edge(ed, 0), bc = ora_mc_edge(ed, 1);
                 const int gx = base.x + lx, gy = base.y + ly, gz = base.z + lz;
                 float pa[3] = {(float)(gx + (a & 1)) * g->voxel + half,
                                (float)(gy + ((a >> 1) & 1)) * g->voxel + half,

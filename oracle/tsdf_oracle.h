@@ -71,6 +71,9 @@ void ora_shard_delete(ora_grid* g, const int16_t* cand_pos, const int32_t* cand_
  * triangle into out (up to capacity triangles); returns the triangle count. See the .c. */
 int64_t ora_extract_mesh(const ora_grid* g, const float* bounds, float missing, int min_weight,
                          float* out, int64_t capacity);
+/* the oracle's own marching-cubes case table (ora_mc_cases.c): edges 12 x 2 corner pairs, triangle
+ * counts per case, triangles 256 x 15 edge indices (-1 padded); returns the triangles per case */
+int ora_mc_table(int8_t* edges, uint8_t* ntri, int8_t* tri);
 uint32_t ora_block_owner(int16_t x, int16_t y, int16_t z, uint32_t shards);
 
 /* voxel_tsdf.cu:347-375 TSDFGrid::Integrate. rgb: HxWx3 u8; depth/ht/lt: HxW f32 (ht/lt may be

@@ -95,6 +95,22 @@ def edge_mid(k):
     return (P[a] + P[b]) / 2
 
 
+P2 = [tuple(2 * int(v) for v in P[i]) for i in range(8)]  # corners in doubled integer coordinates
+
+
+def edge_mid2(k):
+    a, b = EDGES[k]
+    return tuple(P2[a][j] // 2 + P2[b][j] // 2 for j in range(3))
+
+
+def sub(u, v):
+    return tuple(u[j] - v[j] for j in range(3))
+
+
+def cross(u, v):
+    return (u[1] * v[2] - u[2] * v[1], u[2] * v[0] - u[0] * v[2], u[0] * v[1] - u[1] * v[0])
+
+
 def triangulations(poly):
     """All triangulations of a polygon (vertex list, boundary order kept), recursive on the
     triangle that contains the edge poly[0]-poly[-1]."""
@@ -110,12 +126,39 @@ def triangulations(poly):
 
 
 def tri_score(case, t):
-    """How well triangle t (edge indices) faces away from the inside endpoints of its edges."""
-    a, b, d = (edge_mid(k) for k in t)
-    n = np.cross(b - a, d - a)
-    n = n / (np.linalg.norm(n) + 1e-30)
-    ins = [P[i] for k in t for i in EDGES[k] if (case >> i) & 1]
-    return np.dot(n, (a + b + d) / 3 - np.mean(ins, 0))
+    """How well triangle t (edge indices) faces away from the inside endpoints of its edges: the
+    cosine-like n . (centroid - mean of the inside corners) / |n|, kept exact as (N, D, Q) with
+    score = N / (D sqrt(Q)) in doubled integer coordinates (edge midpoints are on the half grid)."""
+    a, b, d = (edge_mid2(k) for k in t)
+    n = cross(sub(b, a), sub(d, a))
+    ins = [P2[i] for k in t for i in EDGES[k] if (case >> i) & 1]
+    k = len(ins)
+    c = [k * (a[j] + b[j] + d[j]) - 3 * sum(p[j] for p in ins) for j in range(3)]
+    return (sum(n[j] * c[j] for j in range(3)), 3 * k, sum(v * v for v in n))
+
+
+def score_less(s, t):
+    """s < t for exact scores (N, D, Q): N1 / (D1 sqrt Q1) < N2 / (D2 sqrt Q2); Q = 0 reads 0."""
+    (n1, d1, q1), (n2, d2, q2) = s, t
+    if q1 == 0:
+        n1, d1, q1 = 0, 1, 1
+    if q2 == 0:
+        n2, d2, q2 = 0, 1, 1
+    A, B = n1 * d2, n2 * d1            # compare A sqrt(q2) with B sqrt(q1)
+    if (A >= 0) != (B >= 0):
+        return A < 0
+    if A >= 0:
+        return A * A * q2 < B * B * q1
+    return A * A * q2 > B * B * q1
+
+
+def min_score(case, ts):
+    m = None
+    for t in ts:
+        v = tri_score(case, t)
+        if m is None or score_less(v, m):
+            m = v
+    return m
 
 
 def tris_for(case, flip):
@@ -128,8 +171,12 @@ def tris_for(case, flip):
         if flip is None:  # orientation probe: plain fan
             tris += [(loop[0], loop[i], loop[i + 1]) for i in range(1, len(loop) - 1)]
             continue
-        # the triangulation whose worst triangle is best oriented (first one on ties)
-        best = max(cands, key=lambda ts: min(tri_score(case, t) for t in ts))
+        # the triangulation whose worst triangle is best oriented (the first one on exact ties)
+        best, best_s = None, None
+        for ts in cands:
+            m = min_score(case, ts)
+            if best is None or score_less(best_s, m):
+                best, best_s = ts, m
         tris += best
     return tris
 

@@ -1,8 +1,9 @@
-"""The generated marching-cubes table (disinfect-slam_amd/csrc/tsdf_mc_tables.h) yields closed,
+"""The generated marching-cubes table (disinfect-slam_amd/csrc/tsdf_mc_tables.h) equals the one the
+oracle derives on its own (oracle/ora_mc_cases.c), and yields closed,
 consistently oriented surfaces: on random scalar fields whose border is outside, every mesh edge
 (a pair of grid-edge vertices) is shared by exactly two triangles with opposite directions, and
 on a sphere every normal points outward. This is what "crack free" means for the table the
-oracle and the HIP kernel share (KrisLibrary's own table is not available: parity unpinned)."""
+oracle and the HIP kernel both use (KrisLibrary's own table is not available: parity unpinned)."""
 import os
 import re
 
@@ -85,3 +86,22 @@ def test_every_case_uses_exactly_its_crossing_edges():
         cross = {k for k, (a, b) in enumerate(EDGE) if ((c >> a) & 1) != ((c >> b) & 1)}
         assert used == cross
         assert all(k == -1 for k in TRI[c][3 * NTRI[c]:])
+
+
+def test_oracle_derives_the_same_table():
+    """The oracle's case table (oracle/ora_mc_cases.c, derived from the cube's geometry in C) and
+    the product's (csrc/tsdf_mc_tables.h, scripts/gen_mc_tables.py in Python) are equal entry for
+    entry: the oracle no longer includes the product's table, so a wrong entry in either shows up
+    here and in the GPU-vs-oracle mesh parity."""
+    import ctypes as C
+
+    from _oracle import LIB_PATH as ORACLE_LIB
+    L = C.CDLL(ORACLE_LIB)
+    e = np.zeros(24, np.int8)
+    n = np.zeros(256, np.uint8)
+    t = np.zeros(256 * 15, np.int8)
+    assert L.ora_mc_table(e.ctypes.data_as(C.c_void_p), n.ctypes.data_as(C.c_void_p),
+                          t.ctypes.data_as(C.c_void_p)) == 5
+    np.testing.assert_array_equal(e.reshape(12, 2), np.asarray(EDGE))
+    np.testing.assert_array_equal(n, np.asarray(NTRI))
+    np.testing.assert_array_equal(t.reshape(256, 15), np.asarray(TRI))
