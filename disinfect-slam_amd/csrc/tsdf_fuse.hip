@@ -291,11 +291,20 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
 #if defined(TSDF_EXP) && (TSDF_EXP & 4)  // experiment build: no pool state stores
       if (upd_mask < 0) {
 #else
-      if (upd_mask || fresh) {
+      if (upd_mask == 0xF || fresh) {
 #endif
+        // all four voxels written (a fresh block's untouched voxels get AquireBlock's state)
         pool_st(blk + off, ts);
         pool_st(blk + kProbOffset + off, pr);
         pool_stu(blk + kRgbwOffset + off, cw);
+      } else if (upd_mask) {  // only the updated voxels' words: writes stay N_upd x 12 B
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (upd_mask & (1 << j)) {
+            reinterpret_cast<float*>(blk + off)[j] = comp(ts, j);
+            reinterpret_cast<float*>(blk + kProbOffset + off)[j] = comp(pr, j);
+            reinterpret_cast<uint32_t*>(blk + kRgbwOffset + off)[j] = compu(cw, j);
+          }
       }
       my_upd += __popc(upd_mask);
     }
