@@ -13,7 +13,7 @@ for rep in 1 2; do
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][0])
 r = d['roofline']
-print(f"{sys.argv[2]:>10} fps={d['value']:9.1f} ms/step={d['ms_per_step']:.4f} integ_evt={r['us_per_launch']:.2f}us dev={r.get('us_per_launch_device_clock')}us frac={r['frac']:.3f} phases={d['phases_ms_per_frame']}")
+print(f"{sys.argv[2]:>10} fps={d['value']:9.1f} ms/step={d['ms_per_step']:.4f} integ_evt={r['us_per_launch']:.2f}us dev={r.get('us_per_launch_device_clock')}us frac={r['frac']:.3f} dev={d['device_us_per_frame']}")
 PY
   done
 done

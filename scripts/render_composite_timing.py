@@ -21,11 +21,13 @@ K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
 poses = [tsdf_amd.SE3(fr['q'][i], fr['t'][i]) for i in range(N + 1)]
 mk = lambda **kw: tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, **kw)
 full = mk()
-shards = [mk(shard_index=i, shard_count=G) for i in range(G)]
+group = tsdf_amd.ShardGroup(G, 0.005, 0.03, max_width=W, max_height=H, num_block_bits=18,
+                            key_cap=32768 // G, cand_cap=16384 // G)
+shards = group.engines
 replica = mk()
 for i in range(N):
-    for e in [full] + shards:
-        e.integrate(fr['rgb'][i], fr['depth'][i], fr['ht'][i], fr['lt'][i], K, poses[i], 4.0)
+    full.integrate(fr['rgb'][i], fr['depth'][i], fr['ht'][i], fr['lt'][i], K, poses[i], 4.0)
+    group.integrate(fr['rgb'][i], fr['depth'][i], fr['ht'][i], fr['lt'][i], K, poses[i], 4.0)
 torch.cuda.synchronize()
 pose = poses[N]
 rgba = torch.zeros((H, W, 4), dtype=torch.uint8, device='cuda')
