@@ -95,26 +95,28 @@ __device__ __forceinline__ unsigned long long arrive_collect(unsigned long long*
 // LDS helpers
 // ---------------------------------------------------------------------------------------------
 // claim table: slot = (bucket + 1) << 9 | rank; the smallest rank per bucket wins
+template <int NC = kRClaim>
 __device__ __forceinline__ void claim2(uint32_t* C, uint32_t bucket, uint32_t rank) {
-  uint32_t h = mix32(bucket) & (kRClaim - 1);
+  uint32_t h = mix32(bucket) & (NC - 1);
   const uint32_t k = ((bucket + 1u) << 9) | rank;
-  for (int p = 0; p < kRClaim; ++p) {
+  for (int p = 0; p < NC; ++p) {
     const uint32_t prev = atomicCAS(&C[h], 0u, k);
     if (prev == 0u) return;
     if ((prev >> 9) == bucket + 1u) {
       atomicMin(&C[h], k);
       return;
     }
-    h = (h + 1) & (kRClaim - 1);
+    h = (h + 1) & (NC - 1);
   }
 }
+template <int NC = kRClaim>
 __device__ __forceinline__ uint32_t claim2_winner(const uint32_t* C, uint32_t bucket) {
-  uint32_t h = mix32(bucket) & (kRClaim - 1);
-  for (int p = 0; p < kRClaim; ++p) {
+  uint32_t h = mix32(bucket) & (NC - 1);
+  for (int p = 0; p < NC; ++p) {
     const uint32_t v = C[h];
     if ((v >> 9) == bucket + 1u) return v & 511u;
     if (v == 0u) break;
-    h = (h + 1) & (kRClaim - 1);
+    h = (h + 1) & (NC - 1);
   }
   return 0xFFFFFFFFu;
 }
@@ -163,15 +165,17 @@ __device__ __forceinline__ int wg_excl_scan(int v, int* scratch, int* total) {
   return before + incl - v;
 }
 
-// ascending sort of a[0..m) (m <= kRB, unique values) by rank counting: each thread ranks its two
-// elements against all m with broadcast LDS reads
+// ascending sort of a[0..m) (m <= RB, unique values) by rank counting: each thread ranks its one
+// (RB = kRT) or two (RB = 2 kRT) elements against all m with broadcast LDS reads
+template <int RB = kRB>
 __device__ __forceinline__ void rank_sort(unsigned long long* a, unsigned long long* tmp, int m) {
+  static_assert(RB == kRT || RB == 2 * kRT, "rank_sort geometry");
   const int t = threadIdx.x;
   const unsigned long long x0 = t < m ? a[t] : ~0ull;
-  const unsigned long long x1 = t + kRT < m ? a[t + kRT] : ~0ull;
+  const unsigned long long x1 = RB > kRT && t + kRT < m ? a[t + kRT] : ~0ull;
   // the sort keys' high words are unique: compare those, two elements per 16-B broadcast read
   const uint32_t h0 = (uint32_t)(x0 >> 32), h1 = (uint32_t)(x1 >> 32);
-  if (t == 0 && (m & 1)) a[m] = ~0ull;  // pad to pairs (a has kRB + 2 entries)
+  if (t == 0 && (m & 1)) a[m] = ~0ull;  // pad to pairs (a has RB + 2 entries)
   lds_barrier();
   const uint4* a4 = reinterpret_cast<const uint4*>(a);
   int r0 = 0, r1 = 0;
@@ -193,15 +197,16 @@ __device__ __forceinline__ void rank_sort(unsigned long long* a, unsigned long l
     r1 += (v.y < h1) + (v.w < h1);
   }
   if (t < m) tmp[r0] = x0;
-  if (t + kRT < m) tmp[r1] = x1;
+  if (RB > kRT && t + kRT < m) tmp[r1] = x1;
   lds_barrier();
   if (t < m) a[t] = tmp[t];
-  if (t + kRT < m) a[t + kRT] = tmp[t + kRT];
+  if (RB > kRT && t + kRT < m) a[t + kRT] = tmp[t + kRT];
   lds_barrier();
 }
 
 // Threshold search for multi-batch launches: keys[i] >> 32 (unique in [lo, range)) for i < n in
-// global scratch; returns thr > lo with count(lo <= key < thr) in [1, kRB] (some key remains).
+// global scratch; returns thr > lo with count(lo <= key < thr) in [1, RB] (some key remains).
+template <int RB = kRB>
 __device__ uint32_t batch_threshold(const unsigned long long* __restrict__ keys, int n, uint32_t lo,
                                     uint32_t range, uint32_t* hist, int* scratch) {
   uint32_t hi = range;
@@ -224,12 +229,12 @@ __device__ uint32_t batch_threshold(const unsigned long long* __restrict__ keys,
     }
     int tot;
     int run = wg_excl_scan(local, scratch, &tot);
-    // largest bin j whose inclusive prefix <= kRB
+    // largest bin j whose inclusive prefix <= RB
     int best = -1;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       run += (int)c[k];
-      if (run <= kRB) best = threadIdx.x * 4 + k;
+      if (run <= RB) best = threadIdx.x * 4 + k;
     }
     lds_barrier();
     if (threadIdx.x == 0) scratch[4] = -1;
@@ -242,27 +247,34 @@ __device__ uint32_t batch_threshold(const unsigned long long* __restrict__ keys,
       const unsigned long long thr = (unsigned long long)lo + (unsigned long long)(j + 1) * w;
       return thr > hi ? hi : (uint32_t)thr;
     }
-    hi = lo + w;  // the first bin alone holds more than kRB: narrow to it (w shrinks each time)
+    hi = lo + w;  // the first bin alone holds more than RB: narrow to it (w shrinks each time)
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 // Allocation resolver
 // ---------------------------------------------------------------------------------------------
-struct AllocLds {
-  alignas(16) unsigned long long batch[kRB + 2];  // (order << 32) | hint << 9 | p, ascending (+ pad)
-  unsigned long long bkey[kRB];   // packed key at position p
-  int32_t bslot[kRB];             // its new-key-set slot
-  int32_t heap_top[kRB];          // heap_top[i] = heap[free0 - 1 - i]
+// RB keys per round: kRB (the frame kernels' tails, the standalone kernel) or kRT (the deferred
+// resolve inside k_integrate, whose LDS budget is the update's: ~14 KiB instead of ~24).
+template <int RB>
+struct AllocLdsT {
+  static constexpr int kClaim = 2 * RB, kLock = 4 * RB, kLockKeys = 3 * RB / 2;
+  alignas(16) unsigned long long batch[RB + 2];  // (order << 32) | hint << 9 | p, ascending (+ pad)
+  unsigned long long bkey[RB];   // packed key at position p
+  int32_t bslot[RB];             // its new-key-set slot
+  int32_t heap_top[RB];          // heap_top[i] = heap[free0 - 1 - i]
   union {
-    uint32_t claim[kRClaim];
+    uint32_t claim[kClaim];
     uint32_t hist[kRHist];
-    unsigned long long tmp[kRB];
+    unsigned long long tmp[RB];
   } u;
-  uint32_t lock[kRLockA];
+  uint32_t lock[kLock];
   int scan[8];
   int first_dirty, base, sfree, nfresh, nalloc, changed, m;
 };
+using AllocLds = AllocLdsT<kRB>;
+static_assert(AllocLds::kClaim == kRClaim && AllocLds::kLock == kRLockA && AllocLds::kLockKeys == kRLockKeysA,
+              "resolver geometry");
 // batch low word: p (9 bits) | hint: bit 9 slot 0 empty, bit 10 slot 1 empty, bit 11 hint valid,
 // bits 16..31 slot 1's list offset -- the key's bucket as the prologue loaded it (the table as the
 // launch found it: valid until the first commit)
@@ -278,22 +290,25 @@ struct AKey {
 
 // frame_mode 1: new blocks this engine holds are listed in D.fresh_vis (flagged fresh, visible this
 // frame); 0 (hash-level test path): their pool indices in D.fresh for k_fresh_init.
+template <int RB>
 __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint32_t range, int frame_mode,
-                                 AllocLds& L) {
+                                 AllocLdsT<RB>& L) {
+  constexpr int NR = RB / kRT;  // keys per thread and round
+  constexpr int NC = AllocLdsT<RB>::kClaim, NL = AllocLdsT<RB>::kLock;
   const int t = threadIdx.x;
   TSDF_STAMP(D, 1, 0);
   const unsigned long long tick0 = __builtin_amdgcn_s_memrealtime();
-  // ---- prologue, round trip 1: counters and (speculatively) the first kRB list entries ----
+  // ---- prologue, round trip 1: counters and (speculatively) the first RB list entries ----
   const int n = ld_co(&D.ctr->nk_count);
   const int free0 = D.ctr->free_count;
   const uint32_t epoch0 = D.ctr->lock_epoch;
-  unsigned long long k0 = ld_co(&D.nk_list[t].key), k1 = ld_co(&D.nk_list[t + kRT].key);
-  int32_t h0 = (int32_t)ld_co(&D.nk_list[t].slot), h1 = (int32_t)ld_co(&D.nk_list[t + kRT].slot);
-  const bool single = n <= kRB;
-  const bool lds_locks = n <= kRLockKeysA;
+  unsigned long long k0 = ld_co(&D.nk_list[t].key), k1 = NR > 1 ? ld_co(&D.nk_list[t + kRT].key) : 0ull;
+  int32_t h0 = (int32_t)ld_co(&D.nk_list[t].slot), h1 = NR > 1 ? (int32_t)ld_co(&D.nk_list[t + kRT].slot) : 0;
+  const bool single = n <= RB;
+  const bool lds_locks = n <= AllocLdsT<RB>::kLockKeys;
   const uint32_t epoch = epoch0 + 1u;
   if (lds_locks)
-    for (int i = t; i < kRLockA; i += kRT) L.lock[i] = 0u;
+    for (int i = t; i < NL; i += kRT) L.lock[i] = 0u;
   if (t == 0) {
     D.ctr->lock_epoch = epoch;
     L.sfree = free0;
@@ -303,12 +318,12 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
   }
   // ---- round trip 2: candidate orders, the keys' buckets, the free-stack top ----
   {
-    const int npre = min(min(n, kRB), max(free0, 0));
+    const int npre = min(min(n, RB), max(free0, 0));
     for (int i = t; i < npre; i += kRT) L.heap_top[i] = D.heap[free0 - 1 - i];
   }
   if (single) {
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < NR; ++r) {
       const int p = t + r * kRT;
       if (p < n) {
         const unsigned long long key = r ? k1 : k0;
@@ -342,7 +357,7 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
     if (single) {
       m = n;
     } else {
-      if (n - done > kRB) thr = batch_threshold(D.pairs, n, lo, range, L.u.hist, L.scan);
+      if (n - done > RB) thr = batch_threshold<RB>(D.pairs, n, lo, range, L.u.hist, L.scan);
       // gather the batch [lo, thr) into LDS (list order; the sort below orders it)
       if (t == 0) L.m = 0;
       lds_barrier();
@@ -360,20 +375,20 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
       lds_barrier();
       m = L.m;
     }
-    rank_sort(L.batch, L.u.tmp, m);
+    rank_sort<RB>(L.batch, L.u.tmp, m);
     TSDF_STAMP(D, 1, 2);
     if (t == 0) L.base = 0;
     lds_barrier();
     while (L.base < m) {
-      // one round: the next min(kRB, m - base) keys in order, two per thread (ranks t, t + kRT)
+      // one round: the next min(RB, m - base) keys in order, NR per thread (ranks t, t + kRT)
       const int base = L.base;
-      const int span = min(kRB, m - base);
-      for (int i = t; i < kRClaim; i += kRT) L.u.claim[i] = 0u;
-      if (t == 0) L.first_dirty = kRB;
+      const int span = min(RB, m - base);
+      for (int i = t; i < NC; i += kRT) L.u.claim[i] = 0u;
+      if (t == 0) L.first_dirty = RB;
       lds_barrier();
-      AKey k[2];
+      AKey k[NR];
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
+      for (int r = 0; r < NR; ++r) {
         k[r] = AKey{};
         const int rank = t + r * kRT;
         if (rank < span) {
@@ -385,7 +400,7 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
           k[r].B = B;
           // the prologue's view of the bucket holds unless a commit of this launch wrote into it,
           // and every such commit locked it
-          const bool fresh = (lw & kHintValid) && (lds_locks ? !lock_held<kRLockA>(L.lock, B) : !L.changed);
+          const bool fresh = (lw & kHintValid) && (lds_locks ? !lock_held<NL>(L.lock, B) : !L.changed);
           bool e0, e1;
           int16_t off1;
           if (fresh) {
@@ -401,7 +416,7 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
           if (e0 || e1) {
             k[r].kind = 1;
             k[r].slot = e0 ? 0 : 1;
-            claim2(L.u.claim, B, (uint32_t)rank);
+            claim2<NC>(L.u.claim, B, (uint32_t)rank);
           } else {  // APPEND: tail T of the list from slot 1, first empty slot-0 entry E after it
             k[r].kind = 2;
             uint32_t last = 2 * B + 1;
@@ -417,35 +432,37 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
               if ((nx & 1u) == 0u && load_ent(D.table, nx).idx < 0) break;
             }
             k[r].E = nx;
-            claim2(L.u.claim, last >> 1, (uint32_t)rank);
-            claim2(L.u.claim, nx >> 1, (uint32_t)rank);
+            claim2<NC>(L.u.claim, last >> 1, (uint32_t)rank);
+            claim2<NC>(L.u.claim, nx >> 1, (uint32_t)rank);
           }
         }
       }
       lds_barrier();
+      TSDF_STAMP(D, 1, 3);
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
+      for (int r = 0; r < NR; ++r) {
         if (!k[r].have) continue;
         const uint32_t rank = (uint32_t)(t + r * kRT);
-        const bool clean = k[r].kind == 1 ? claim2_winner(L.u.claim, k[r].B) == rank
-                                          : (claim2_winner(L.u.claim, k[r].T >> 1) == rank &&
-                                             claim2_winner(L.u.claim, k[r].E >> 1) == rank);
+        const bool clean = k[r].kind == 1 ? claim2_winner<NC>(L.u.claim, k[r].B) == rank
+                                          : (claim2_winner<NC>(L.u.claim, k[r].T >> 1) == rank &&
+                                             claim2_winner<NC>(L.u.claim, k[r].E >> 1) == rank);
         if (!clean) atomicMin(&L.first_dirty, (int)rank);
       }
       lds_barrier();
+      TSDF_STAMP(D, 1, 4);
       const int first_dirty = L.first_dirty;
       bool ok[2] = {false, false}, mine[2] = {false, false};
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
+      for (int r = 0; r < NR; ++r) {
         if (!k[r].have || t + r * kRT >= first_dirty) continue;
         // atomicExch(&bucket_locks_[b], LOCKED) == FREE, per launch; the keys committing together
         // won all their claims, so they take distinct buckets
         if (k[r].kind == 1) {
-          ok[r] = lds_locks ? lock_take2<kRLockA>(L.lock, k[r].B) : lock_take_hbm(D.lock_tag, k[r].B, epoch);
+          ok[r] = lds_locks ? lock_take2<NL>(L.lock, k[r].B) : lock_take_hbm(D.lock_tag, k[r].B, epoch);
         } else {
           const uint32_t Lb = k[r].T >> 1, C = k[r].E >> 1;
-          if (lds_locks ? lock_take2<kRLockA>(L.lock, Lb) : lock_take_hbm(D.lock_tag, Lb, epoch))
-            ok[r] = lds_locks ? lock_take2<kRLockA>(L.lock, C) : lock_take_hbm(D.lock_tag, C, epoch);
+          if (lds_locks ? lock_take2<NL>(L.lock, Lb) : lock_take_hbm(D.lock_tag, Lb, epoch))
+            ok[r] = lds_locks ? lock_take2<NL>(L.lock, C) : lock_take_hbm(D.lock_tag, C, epoch);
         }
         // Sharded volume: every shard commits every key's table change (the replicated index), and
         // only the key's owner pops a pool block; the others store kForeignIdx.
@@ -459,7 +476,7 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
       const int nmine = (tot & 0xFFFF) + (tot >> 16);
       const int free_now = L.sfree;
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
+      for (int r = 0; r < NR; ++r) {
         if (!k[r].have) continue;
         if (ok[r]) {
           int32_t idx = kForeignIdx;
@@ -473,7 +490,7 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
               insert = P.shard_count > 1;
             } else {
               const int top = free0 - 1 - hi;  // pops so far this launch + rank
-              idx = top < kRB ? L.heap_top[top] : D.heap[hi];
+              idx = top < RB ? L.heap_top[top] : D.heap[hi];
             }
           }
           if (insert) {
@@ -516,6 +533,7 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
       // the table writes must be visible to the next round's loads; after the launch's last round
       // nothing here reads them (the next kernel does, after the boundary)
       if (first_dirty < span || base + span < m || done + m < n) __syncthreads(); else lds_barrier();
+      TSDF_STAMP(D, 1, 5);
       if (t == 0) {
         const int used = nmine < free_now ? nmine : (free_now > 0 ? free_now : 0);
         L.sfree = free_now - used;
@@ -528,7 +546,7 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
     done += m;
     lo = thr;
   }
-  TSDF_STAMP(D, 1, 3);
+  TSDF_STAMP(D, 1, 6);
   if (t == 0) {
     D.ctr->resolve_alloc_ticks += __builtin_amdgcn_s_memrealtime() - tick0;
     D.ctr->free_count = L.sfree;

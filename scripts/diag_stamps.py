@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "disinfect-slam_amd"))
 
 KERNELS = {0: ("ingest", ["lds_init", "pix_write", "dda", "barrier", "sweep"]),
-           1: ("resolve_alloc", ["prepare", "batch0", "resolve"]),
+           1: ("resolve_alloc", ["prepare", "sort", "claim", "dirty", "commit", "rest"]),
            2: ("vis (in ingest)", ["all"]),
            3: ("integrate", ["all"]),
            4: ("resolve_delete", ["sum+prepare", "rounds"])}
