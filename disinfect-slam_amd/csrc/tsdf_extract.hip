@@ -311,9 +311,20 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
   f3 rlo = {1.f, 1.f, 1.f}, rhi = {0.f, 0.f, 0.f};
   int32_t ridx = -1;  // pool index of the present block of the region, -1 missing
   int i = 1;
+#ifdef TSDF_DIAG_STAMPS
+  // diagnostic step statistics (per lane and per wave), summed per workgroup into D.dbg kernel 5
+  int d_it = 0, d_blk = 0, d_ld = 0, dw_blk = 0, dw_ld = 0;
+#endif
   while (i < max_step && !done) {
     const bool inside = pos.x > rlo.x && pos.x < rhi.x && pos.y > rlo.y && pos.y < rhi.y && pos.z > rlo.z &&
                         pos.z < rhi.z;
+#ifdef TSDF_DIAG_STAMPS
+    d_it += 1;
+    d_blk += !inside;
+    d_ld += ridx >= 0;
+    dw_blk += __ballot(!inside) != 0ull;
+    dw_ld += __ballot(ridx >= 0) != 0ull;
+#endif
     const int16_t px = round_s16(pos.x), py = round_s16(pos.y), pz = round_s16(pos.z);
     if (!inside) {
       ray_block(D, R, c, px >> kBlockLenBits, py >> kBlockLenBits, pz >> kBlockLenBits);
@@ -344,6 +355,30 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
     if (rgba) rgba[idx] = make_uchar4(0, 0, 0, 0);
     if (normal) normal[idx] = make_uchar4(0, 0, 0, 0);
   }
+#ifdef TSDF_DIAG_STAMPS
+  if (D.dbg) {
+    int mx_it = d_it, mx_blk = dw_blk, mx_ld = dw_ld;
+    for (int o = 32; o > 0; o >>= 1) {
+      mx_it = max(mx_it, __shfl_xor(mx_it, o, 64));
+      mx_blk = max(mx_blk, __shfl_xor(mx_blk, o, 64));
+      mx_ld = max(mx_ld, __shfl_xor(mx_ld, o, 64));
+    }
+    const unsigned wg = blockIdx.y * gridDim.x + blockIdx.x;
+    if (wg < (unsigned)kDiagMaxWg) {
+      unsigned long long* q = D.dbg + ((size_t)5 * kDiagMaxWg + wg) * kDiagStamps;
+      atomicAdd(&q[0], (unsigned long long)d_it);
+      atomicAdd(&q[1], (unsigned long long)d_blk);
+      atomicAdd(&q[2], (unsigned long long)d_ld);
+      atomicAdd(&q[6], (unsigned long long)(valid && done));
+      if (lane_id() == 0) {
+        atomicAdd(&q[3], (unsigned long long)mx_it);
+        atomicAdd(&q[4], (unsigned long long)mx_blk);
+        atomicAdd(&q[5], (unsigned long long)mx_ld);
+        atomicAdd(&q[7], 1ull);
+      }
+    }
+  }
+#endif
 }
 __global__ __launch_bounds__(256) void k_raycast(EngineDev D, FrameParams P, float step_size, ViewGrid V,
                                                  uchar4* __restrict__ rgba, uchar4* __restrict__ normal) {
