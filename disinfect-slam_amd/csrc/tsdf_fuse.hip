@@ -67,25 +67,25 @@ __device__ void pack_cands_wg(const EngineDev& D, ShardRec* __restrict__ out, in
 // arrivals, the update's device-clock span, visible = listed by the sweep + created), then the
 // space carving of the candidates (voxel_tsdf.cu:483-488, kTailResolve) or, in a shard's frame,
 // the packing of its candidates for the exchange (kTailPack; k_resolve_delete follows it).
+// The statistics (their loads) come after the carving, off its path.
 __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FrameParams& P, DeleteLds& L) {
   const int t = threadIdx.x;
+  const unsigned long long tend = __builtin_amdgcn_s_memrealtime();  // the update's span ends here
+  if (P.tail == kTailPack)
+    pack_cands_wg(D, P.slot, P.slot_cap);
+  else
+    resolve_delete_wg(D, D.cand, &D.ctr->n_cand, 0, L);
+  lds_barrier();  // (L.scan is reused below)
   const int bc = t < kBands ? D.band[t * kBandStride] : 0;
   int nband;
   (void)wg_excl_scan(bc, L.scan, &nband);
   if (t == 0) {
     const unsigned long long upd = arrive_collect(D.arrive + kArrIntegrate);
-    const unsigned long long tend = __builtin_amdgcn_s_memrealtime();
     D.ctr->last_updated = upd;
     D.ctr->integrate_ticks += tend - ld_co(&D.arrive[kArrStart]);
     D.ctr->n_vis = nband + D.ctr->n_fresh;
   }
-  if (P.tail == kTailPack) {
-    pack_cands_wg(D, P.slot, P.slot_cap);
-  } else {
-    lds_barrier();
-    resolve_delete_wg(D, D.cand, &D.ctr->n_cand, 0, L);
-    frame_end(D);
-  }
+  if (P.tail != kTailPack) frame_end(D);
 }
 
 // 64 VGPRs: 8 waves per SIMD (65 without the bound: 7). Graph: the graph-captured form reads its

@@ -81,6 +81,11 @@ __device__ __forceinline__ bool arrive_last(unsigned long long* words, unsigned 
   lds_barrier();
   return *s_flag != 0;
 }
+// the last arriver, thread 0: the counters zeroed for the next launch (stores only)
+__device__ __forceinline__ void arrive_reset(unsigned long long* words) {
+#pragma unroll
+  for (int g = 0; g < 9; ++g) st_co(&words[g * kArrLine], 0ull);
+}
 // the last arriver, thread 0: the sum of the payloads; the counters are zeroed for the next launch
 __device__ __forceinline__ unsigned long long arrive_collect(unsigned long long* words) {
   unsigned long long sum = 0ull;

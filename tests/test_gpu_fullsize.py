@@ -112,3 +112,42 @@ def test_bench_stream_full_size_invariants_and_determinism():
         assert np.array_equal(a[k].reshape(-1, 512)[pidx].view(np.uint32),
                               b[k].reshape(-1, 512)[pidx].view(np.uint32)), k
     assert np.array_equal(cw, b["rgbw"].reshape(-1, 512, 4)[pidx])
+
+
+def test_bench_stream_oracle_parity_40_frames():
+    """The bench's own stream (synth.render_torch: the GPU-rendered 640x480 orbit bench.py integrates,
+    frames 0..39, 2^18-block pool) against the CPU oracle fed the same frames copied to the host:
+    per-frame counts every frame, the hash table, free stack and every voxel at frames 20 and 40
+    (VERDICT r1 weak item 5)."""
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    from _oracle import OracleGrid
+
+    def host(x):
+        return x.cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
+
+    W, H, n = 640, 480, 40
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    fr = synth.render_torch(cam, list(range(n)), device="cuda")
+    eng = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=18)
+    ora = OracleGrid(0.005, 0.03, 18)
+    try:
+        for i in range(n):
+            q, t = fr["q"][i], fr["t"][i]
+            eng.integrate(fr["rgb"][i], fr["depth"][i], fr["ht"][i], fr["lt"][i], K, tsdf_amd.SE3(q, t), 4.0)
+            ora.integrate(host(fr["rgb"][i]), host(fr["depth"][i]), host(fr["ht"][i]), host(fr["lt"][i]), 4.0,
+                          cam.K, host(q), host(t))
+            torch.cuda.synchronize()
+            s, so = eng.stats(), ora.stats()
+            assert s["status"] == 0, s
+            for k in ("last_num_visible", "last_num_updated", "last_num_deleted", "active_blocks"):
+                assert s[k] == so[k], (i, k, s[k], so[k])
+            if (i + 1) % 20 == 0:
+                compare(eng, ora, tag=f"bench stream frame {i}")
+        assert eng.stats()["active_blocks"] > 8000
+    finally:
+        eng.close()
+        ora.close()
