@@ -78,6 +78,10 @@ def parse():
                    help="sharded modes: carve-candidate records per rank per frame (0 = 16384 / G)")
     p.add_argument("--cpu-frames", type=int, default=-1, help="oracle sample size (-1 = auto)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                   help="process-group backend for N > 1: nccl (RCCL over xGMI, one GPU per rank) or gloo "
+                        "(a rehearsal of the multi-rank code path; ranks may share a GPU, exchanges staged "
+                        "through the host -- not a performance number)")
     p.add_argument("--block-bits", type=int, default=18)
     p.add_argument("--event-every", type=int, default=8,
                    help="HIP-event-time k_integrate on every n-th timed frame (a dispatch with bound "
@@ -264,8 +268,12 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "gloo":  # rehearsal: ranks share the box's GPUs round-robin
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -339,6 +347,8 @@ def main():
             metric = ("C5 frame loop frames/s (integrate + raycast every frame, marching cubes every 30 "
                       "frames)")
         parallelism = "single" if world == 1 else f"{mode}{world}"
+        if world > 1 and a.backend == "gloo":
+            parallelism += " (gloo rehearsal, ranks sharing GPUs: not a performance number)"
         if a.graph:
             parallelism += ", one hipGraph launch per frame"
         roof = {
