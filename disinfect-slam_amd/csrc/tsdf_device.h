@@ -181,12 +181,13 @@ __device__ __forceinline__ int32_t f2i(float f) {  // cvt.rzi.s32.f32
 }
 // f2s(roundf(f)) in a few operations: for 1/2 <= |f| < 2^22, f + copysign(1/2, f) truncates to
 // roundf(f) (the sum is exact, or rounds without reaching the next integer); |f| < 1/2 gives 0 (the
-// sum could round up to 1); larger |f| saturates the int16 result either way (NaN -> 0 as f2s).
-// tests/test_gpu_numerics.py checks it on every float.
+// sum could round up to 1); from 2^15 on the int16 result saturates either way, so no other range
+// needs its own form (NaN -> 0 as f2s). Written as selects on the converted value: the ternary on
+// the float operand compiled to three exec-masked branches per call, and the raycast rounds three
+// coordinates per march step. tests/test_gpu_numerics.py checks it on every float.
 __device__ __forceinline__ int16_t round_s16(float f) {
-  const float a = fabsf(f);
-  const float g = a < 0.5f ? 0.0f : a < 4194304.0f ? f + __builtin_copysignf(0.5f, f) : f;
-  return (int16_t)min(32767, max(-32768, f2i(g)));
+  const int r = min(32767, max(-32768, f2i(f + __builtin_copysignf(0.5f, f))));
+  return (int16_t)(fabsf(f) < 0.5f ? 0 : r);
 }
 
 __device__ __forceinline__ int16_t f2s(float f) {  // cvt.rzi.s16.f32
