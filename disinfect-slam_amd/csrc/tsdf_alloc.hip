@@ -264,9 +264,9 @@ __device__ __forceinline__ void ingest_tile(EngineDev& D, const FrameParams& P,
           atomicOr(&D.ctr->status, 4u);  // TSDF_STATUS_DDA_OVERFLOW
           break;
         }
-        const int16_t kx = (int16_t)(f2s(roundf(pos.x)) >> kBlockLenBits);
-        const int16_t ky = (int16_t)(f2s(roundf(pos.y)) >> kBlockLenBits);
-        const int16_t kz = (int16_t)(f2s(roundf(pos.z)) >> kBlockLenBits);
+        const int16_t kx = (int16_t)(round_s16(pos.x) >> kBlockLenBits);
+        const int16_t ky = (int16_t)(round_s16(pos.y) >> kBlockLenBits);
+        const int16_t kz = (int16_t)(round_s16(pos.z) >> kBlockLenBits);
         pos.x += st.x;
         pos.y += st.y;
         pos.z += st.z;

@@ -183,11 +183,13 @@ __device__ __forceinline__ void ray_block(const EngineDev& D, const RayView& R, 
   const int lx = bx - R.ox, ly = by - R.oy, lz = bz - R.oz;
   const int n = R.n;
   if ((unsigned)lx < (unsigned)n && (unsigned)ly < (unsigned)n && (unsigned)lz < (unsigned)n) {
+    // brick and superbrick words read together (one LDS round trip, not two in sequence)
     const int k = ((lz >> 2) * R.nb + (ly >> 2)) * R.nb + (lx >> 2);
-    if (!((R.bits[k >> 5] >> (k & 31)) & 1u)) {
+    const int q = ((lz >> 4) * R.ns + (ly >> 4)) * R.ns + (lx >> 4);
+    const uint32_t wb = R.bits[k >> 5], ws = R.bits[R.nbw + (q >> 5)];
+    if (!((wb >> (k & 31)) & 1u)) {
       c.idx = -1;
-      const int q = ((lz >> 4) * R.ns + (ly >> 4)) * R.ns + (lx >> 4);
-      c.empty = ((R.bits[R.nbw + (q >> 5)] >> (q & 31)) & 1u) ? 1 : 2;
+      c.empty = 2 - (int)((ws >> (q & 31)) & 1u);
       return;
     }
     const uint32_t v = R.cell[((size_t)lz * n + ly) * n + lx];
@@ -218,7 +220,7 @@ __device__ __forceinline__ void ray_shade(const EngineDev& D, const RayView& R, 
   for (;;) {
     const f3 dd = {p1.x - p2.x, p1.y - p2.y, p1.z - p2.z};
     if (!((double)dot3(dd, dd) > .1)) break;
-    if (ray_tsdf(D, R, c, f2s(roundf(mid.x)), f2s(roundf(mid.y)), f2s(roundf(mid.z))) < 0)
+    if (ray_tsdf(D, R, c, round_s16(mid.x), round_s16(mid.y), round_s16(mid.z)) < 0)
       p2 = mid;
     else
       p1 = mid;
@@ -226,7 +228,7 @@ __device__ __forceinline__ void ray_shade(const EngineDev& D, const RayView& R, 
     mid.y = (p1.y + p2.y) / 2;
     mid.z = (p1.z + p2.z) / 2;
   }
-  const int16_t fx = f2s(roundf(mid.x)), fy = f2s(roundf(mid.y)), fz = f2s(roundf(mid.z));
+  const int16_t fx = round_s16(mid.x), fy = round_s16(mid.y), fz = round_s16(mid.z);
   uint32_t col = 0;
   float prob = 0.0f;  // VoxelRGBW() / VoxelSEGM() defaults
   ray_block(D, R, c, fx >> kBlockLenBits, fy >> kBlockLenBits, fz >> kBlockLenBits);
@@ -299,7 +301,7 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
   f3 pos = {P.wt.x / P.voxel, P.wt.y / P.voxel, P.wt.z / P.voxel};
   bool done = !valid;
   float prev = 1.0f;
-  if (valid) prev = ray_tsdf(D, R, c, f2s(roundf(pos.x)), f2s(roundf(pos.y)), f2s(roundf(pos.z)));
+  if (valid) prev = ray_tsdf(D, R, c, round_s16(pos.x), round_s16(pos.y), round_s16(pos.z));
   pos.x += sg.x;
   pos.y += sg.y;
   pos.z += sg.z;
@@ -329,10 +331,12 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
     if (!inside) {
       ray_block(D, R, c, px >> kBlockLenBits, py >> kBlockLenBits, pz >> kBlockLenBits);
       ridx = c.idx;
-      const int sh = c.idx >= 0 ? 0 : c.empty == 2 ? 4 : c.empty == 1 ? 2 : 0;  // 2^sh blocks per axis
-      const int rx = (sh ? R.ox + (((c.bx - R.ox) >> sh) << sh) : c.bx) * kBlockLen;
-      const int ry = (sh ? R.oy + (((c.by - R.oy) >> sh) << sh) : c.by) * kBlockLen;
-      const int rz = (sh ? R.oz + (((c.bz - R.oz) >> sh) << sh) : c.bz) * kBlockLen;
+      // 2^sh blocks per axis: 0 for a block (present, or missing in an occupied brick), 2 for an
+      // empty brick, 4 for an empty superbrick (c.empty 0 / 1 / 2); selects, not branches
+      const int sh = 2 * c.empty;
+      const int rx = (R.ox + (((c.bx - R.ox) >> sh) << sh)) * kBlockLen;
+      const int ry = (R.oy + (((c.by - R.oy) >> sh) << sh)) * kBlockLen;
+      const int rz = (R.oz + (((c.bz - R.oz) >> sh) << sh)) * kBlockLen;
       const float len = (float)(kBlockLen << sh);
       rlo = {(float)rx - 0.5f, (float)ry - 0.5f, (float)rz - 0.5f};
       rhi = {rlo.x + len, rlo.y + len, rlo.z + len};
