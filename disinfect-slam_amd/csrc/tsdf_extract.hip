@@ -327,26 +327,30 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
     dw_blk += __ballot(!inside) != 0ull;
     dw_ld += __ballot(ridx >= 0) != 0ull;
 #endif
-    const int16_t px = round_s16(pos.x), py = round_s16(pos.y), pz = round_s16(pos.z);
-    if (!inside) {
-      ray_block(D, R, c, px >> kBlockLenBits, py >> kBlockLenBits, pz >> kBlockLenBits);
-      ridx = c.idx;
-      // 2^sh blocks per axis: 0 for a block (present, or missing in an occupied brick), 2 for an
-      // empty brick, 4 for an empty superbrick (c.empty 0 / 1 / 2); selects, not branches
-      const int sh = 2 * c.empty;
-      const int rx = (R.ox + (((c.bx - R.ox) >> sh) << sh)) * kBlockLen;
-      const int ry = (R.oy + (((c.by - R.oy) >> sh) << sh)) * kBlockLen;
-      const int rz = (R.oz + (((c.bz - R.oz) >> sh) << sh)) * kBlockLen;
-      const float len = (float)(kBlockLen << sh);
-      rlo = {(float)rx - 0.5f, (float)ry - 0.5f, (float)rz - 0.5f};
-      rhi = {rlo.x + len, rlo.y + len, rlo.z + len};
-    }
+    // a lane inside an empty region reads +1 and needs nothing else this step (no rounding either:
+    // when every lane of the wave is there, the wave skips the block below)
     float cur = 1.0f;
-    if (ridx >= 0) {
-      cur = reinterpret_cast<const float*>(D.pool + (size_t)ridx * kBlockBytes)[voxel_off(px, py, pz)];
-      if (prev > 0 && cur <= 0 && (double)(prev - cur) <= 1.5) {
-        ray_shade(D, R, c, pos, sg, dw, rgba, normal, idx);
-        done = true;
+    if (!inside || ridx >= 0) {
+      const int16_t px = round_s16(pos.x), py = round_s16(pos.y), pz = round_s16(pos.z);
+      if (!inside) {
+        ray_block(D, R, c, px >> kBlockLenBits, py >> kBlockLenBits, pz >> kBlockLenBits);
+        ridx = c.idx;
+        // 2^sh blocks per axis: 0 for a block (present, or missing in an occupied brick), 2 for an
+        // empty brick, 4 for an empty superbrick (c.empty 0 / 1 / 2); selects, not branches
+        const int sh = 2 * c.empty;
+        const int rx = (R.ox + (((c.bx - R.ox) >> sh) << sh)) * kBlockLen;
+        const int ry = (R.oy + (((c.by - R.oy) >> sh) << sh)) * kBlockLen;
+        const int rz = (R.oz + (((c.bz - R.oz) >> sh) << sh)) * kBlockLen;
+        const float len = (float)(kBlockLen << sh);
+        rlo = {(float)rx - 0.5f, (float)ry - 0.5f, (float)rz - 0.5f};
+        rhi = {rlo.x + len, rlo.y + len, rlo.z + len};
+      }
+      if (ridx >= 0) {
+        cur = reinterpret_cast<const float*>(D.pool + (size_t)ridx * kBlockBytes)[voxel_off(px, py, pz)];
+        if (prev > 0 && cur <= 0 && (double)(prev - cur) <= 1.5) {
+          ray_shade(D, R, c, pos, sg, dw, rgba, normal, idx);
+          done = true;
+        }
       }
     }
     prev = cur;
