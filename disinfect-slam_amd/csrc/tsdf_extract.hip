@@ -300,6 +300,8 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
   const int max_step = f2i(ceilf(P.max_depth / step_size));  // wave-uniform
   f3 pos = {P.wt.x / P.voxel, P.wt.y / P.voxel, P.wt.z / P.voxel};
   bool done = !valid;
+  bool hit = false;
+  f3 hit_pos = pos;
   float prev = 1.0f;
   if (valid) prev = ray_tsdf(D, R, c, round_s16(pos.x), round_s16(pos.y), round_s16(pos.z));
   pos.x += sg.x;
@@ -348,7 +350,8 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
       if (ridx >= 0) {
         cur = reinterpret_cast<const float*>(D.pool + (size_t)ridx * kBlockBytes)[voxel_off(px, py, pz)];
         if (prev > 0 && cur <= 0 && (double)(prev - cur) <= 1.5) {
-          ray_shade(D, R, c, pos, sg, dw, rgba, normal, idx);
+          hit_pos = pos;  // shaded after the march (below)
+          hit = true;
           done = true;
         }
       }
@@ -359,7 +362,13 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
     pos.z += sg.z;
     ++i;
   }
-  if (valid && !done) {
+  // The hits are shaded together after the march: inside it, the lanes of a wave hit at different
+  // steps, and each step with a hit ran the whole shading (binary search + 7 lookups) for a few lanes.
+  // The shading reads only the static volume (the block cache is a memo), so where it runs changes
+  // nothing.
+  if (hit) {
+    ray_shade(D, R, c, hit_pos, sg, dw, rgba, normal, idx);
+  } else if (valid) {
     if (rgba) rgba[idx] = make_uchar4(0, 0, 0, 0);
     if (normal) normal[idx] = make_uchar4(0, 0, 0, 0);
   }
