@@ -367,7 +367,11 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
   // The shading reads only the static volume (the block cache is a memo), so where it runs changes
   // nothing.
   if (hit) {
+#if defined(TSDF_EXP) && (TSDF_EXP & 8)  // experiment build: no shading (timing of the march alone)
+    if (rgba) rgba[idx] = make_uchar4(255, 255, 255, 255);
+#else
     ray_shade(D, R, c, hit_pos, sg, dw, rgba, normal, idx);
+#endif
   } else if (valid) {
     if (rgba) rgba[idx] = make_uchar4(0, 0, 0, 0);
     if (normal) normal[idx] = make_uchar4(0, 0, 0, 0);
