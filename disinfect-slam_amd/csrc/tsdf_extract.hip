@@ -267,8 +267,11 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
   // contiguous run of 16x16 tiles in raster order -- neighbouring rays' blocks stay in one L2
   const int gx = gridDim.x, nwg = gx * gridDim.y, wg = blockIdx.y * gx + blockIdx.x;
   const int g = wg & 7, tile = g * (nwg >> 3) + min(g, nwg & 7) + (wg >> 3);
-  const int x = (tile % gx) * 16 + (threadIdx.x & 15);
-  const int y = (tile / gx) * 16 + (threadIdx.x >> 4);
+  // each wave an 8x8 quadrant of the tile: a tighter ray bundle than 16x4 rows, whose lanes leave
+  // their regions at closer steps (101.3 vs 103.8 us at C5)
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  const int x = (tile % gx) * 16 + (wv & 1) * 8 + (ln & 7);
+  const int y = (tile / gx) * 16 + (wv >> 1) * 8 + (ln >> 3);
   const bool valid = x < P.W && y < P.H;
   const int idx = valid ? y * P.W + x : 0;
   RayView R;
