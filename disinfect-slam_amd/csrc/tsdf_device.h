@@ -129,7 +129,7 @@ struct DevCounters {
   unsigned long long frames;
   unsigned long long integrate_ticks;  // sum of k_integrate device durations (100 MHz clock)
   int32_t n_keys_in;      // sharded frames: key records merged from the exchange (last frame)
-  int32_t pad0;
+  int32_t n_pend;         // a shard's owned entries left without voxels (pool exhausted) this frame
   unsigned long long ingest_ticks;          // k_ingest_dda start -> last arrival (100 MHz clock)
   unsigned long long resolve_alloc_ticks;   // resolve_alloc_wg durations
   unsigned long long resolve_delete_ticks;  // resolve_delete_wg durations

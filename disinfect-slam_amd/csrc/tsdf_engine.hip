@@ -159,7 +159,7 @@ void free_all(tsdf_engine* e) {
   void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.occ,
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs, D.fresh,
                   e->fe_rgb, e->fe_depth, e->fe_mask, e->fe_out_rgb, e->fe_out_depth,
-                  D.vis,     D.band,    D.cand,     D.arrive, D.fresh_vis, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
+                  D.vis,     D.band,    D.cand,     D.arrive, D.fresh_vis, D.pend, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
                   e->vg_cell, e->vg_flags, e->vg_bits,
                   e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
@@ -412,9 +412,11 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.fresh, kNewKeyCap);
   ALLOC(D.vis, (size_t)kBands * nb);
   ALLOC(D.band, kBands * kBandStride);
-  ALLOC(D.cand, std::max(nb, 1024));  // >= the resolver's speculative prologue reads (kRB)
+  D.cand_cap = std::max(nb, 1024);  // >= the resolver's speculative prologue reads (kRB)
+  ALLOC(D.cand, D.cand_cap);
   ALLOC(D.arrive, kArriveWords);
   ALLOC(D.fresh_vis, kNewKeyCap);
+  ALLOC(D.pend, kNewKeyCap);
   {  // one resident wave of k_integrate workgroups: no second-round stragglers
     int per_cu = 0, ncu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate_t<false>, kIntegrateThreads, 0) != hipSuccess ||
@@ -674,6 +676,21 @@ int tsdf_integrate_shard_end(tsdf_engine* e, const void* cands_in, int32_t cand_
   e->shard_phase = 0;
   std::array<hipEvent_t, 5>* ev = e->shard_ev;
   if (ev && e->prof_mode == TSDF_PROFILE_PHASES) HIP_OK(hipEventRecord((*ev)[4], e->stream));
+  return TSDF_OK;
+}
+
+int tsdf_integrate_shard_abort(tsdf_engine* e) {
+  TraceRange trace_("tsdf_integrate_shard_abort");
+  if (!e || !sharded(e)) {
+    set_error("tsdf_integrate_shard_abort: not a shard engine");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  if (e->shard_phase == 0) return TSDF_OK;  // nothing pending
+  HIP_OK(hipSetDevice(e->device));
+  e->shard_phase = 0;
+  e->shard_ev = nullptr;
+  hipLaunchKernelGGL(k_shard_abort, dim3(1), dim3(256), 0, e->stream, e->D);
+  LAUNCH_OK("k_shard_abort");
   return TSDF_OK;
 }
 

@@ -36,16 +36,29 @@ __device__ void frame_end(const EngineDev& D) {
     D.ctr->total_updated += D.ctr->last_updated;
     D.ctr->frames += 1ull;
     D.ctr->n_cand = 0;  // the next frame's lists start empty (its sweep runs before allocation)
+    D.ctr->n_pend = 0;
   }
   if (threadIdx.x < kBands) D.band[threadIdx.x * kBandStride] = 0;
 }
 
-// a shard's frame: its carve candidates into the exchange slot
+// a shard's frame: its carve candidates into the exchange slot, then the owned entries its
+// exhausted pool left without voxels this frame (D.pend, written by the allocation resolver before
+// this launch)
 __device__ void pack_cands_wg(const EngineDev& D, ShardRec* __restrict__ out, int cap) {
-  const int n = ld_co(&D.ctr->n_cand);
+  const int nc = ld_co(&D.ctr->n_cand);
+  const int np = min(D.ctr->n_pend, (int)kNewKeyCap);
+  const int n = nc + np;
   const unsigned long long* rq = reinterpret_cast<const unsigned long long*>(D.cand);
   for (int i = threadIdx.x; i < min(n, cap); i += blockDim.x) {
-    const unsigned long long a = ld_co(&rq[2 * i]), b = ld_co(&rq[2 * i + 1]);
+    unsigned long long a, b;
+    if (i < nc) {
+      a = ld_co(&rq[2 * i]);
+      b = ld_co(&rq[2 * i + 1]);
+    } else {
+      const unsigned long long* pq = reinterpret_cast<const unsigned long long*>(D.pend + (i - nc));
+      a = pq[0];
+      b = pq[1];
+    }
     ShardRec r;
     r.x = (int16_t)(a & 0xFFFF);
     r.y = (int16_t)((a >> 16) & 0xFFFF);
@@ -60,6 +73,30 @@ __device__ void pack_cands_wg(const EngineDev& D, ShardRec* __restrict__ out, in
     h.val = (uint32_t)min(n, cap);
     out[0] = h;
     if (n > cap) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_SHARD_OVERFLOW
+  }
+}
+
+// tsdf_integrate_shard_abort (one workgroup): the per-frame state of a sharded frame that will not
+// complete back to "between frames" -- the new-key set (slots listed in the new-key list), the
+// visible-band counts, candidate / fresh / pending counts and the arrival counters. Structural
+// changes a phase already committed stay (TSDF_STATUS_SHARD_ABORTED tells the caller the shards may
+// differ: restore a snapshot).
+__global__ __launch_bounds__(256) void k_shard_abort(EngineDev D) {
+  const int n = min(D.ctr->nk_count, (int)kNewKeyCap);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int h = (int)D.nk_list[i].slot;
+    D.nk_key[h] = 0ull;
+    D.nk_order[h] = 0xFFFFFFFFu;
+  }
+  if (threadIdx.x < kBands) D.band[threadIdx.x * kBandStride] = 0;
+  for (int i = threadIdx.x; i < kArriveWords; i += blockDim.x) D.arrive[i] = 0ull;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    D.ctr->nk_count = 0;
+    D.ctr->n_cand = 0;
+    D.ctr->n_fresh = 0;
+    D.ctr->n_pend = 0;
+    D.ctr->status |= 32u;  // TSDF_STATUS_SHARD_ABORTED
   }
 }
 
@@ -371,13 +408,22 @@ __global__ __launch_bounds__(kRT) void k_resolve_delete(EngineDev D, const VisRe
   __shared__ int s_base[kMaxShards + 1];
   if (cands_in) {
     if (threadIdx.x == 0) {
+      // the union is listed in D.cand (cand_cap records; the resolver's D.pairs scratch holds at
+      // least as many): more candidates than that is a shard overflow, the rest are dropped
       int run = 0;
+      bool ovf = false;
       for (int s = 0; s < nshard; ++s) {
         s_base[s] = run;
-        run += min((int)cands_in[(size_t)s * (cap + 1)].val, cap);
+        int n = min((int)cands_in[(size_t)s * (cap + 1)].val, cap);
+        if (n > D.cand_cap - run) {
+          n = D.cand_cap - run;
+          ovf = true;
+        }
+        run += n;
       }
       s_base[nshard] = run;
       st_co(&D.ctr->n_cand, run);
+      if (ovf) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_SHARD_OVERFLOW
     }
     __syncthreads();
     unsigned long long* cq = reinterpret_cast<unsigned long long*>(D.cand);
@@ -404,5 +450,6 @@ __global__ __launch_bounds__(kRT) void k_resolve_delete(EngineDev D, const VisRe
   resolve_delete_wg(D, recs, count, direct, L);
   if (!direct) frame_end(D);
 }
+
 
 }  // namespace tsdf

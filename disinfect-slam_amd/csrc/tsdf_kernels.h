@@ -43,9 +43,12 @@ struct EngineDev {
   // visibility / carving
   VisRec* vis;                  // kBands x nblocks visible blocks (band-major, any order within)
   int32_t* band;                // kBands x kBandStride: record count of each band list
-  VisRec* cand;                 // max(nblocks, 1024) carve candidates (any order; sorted by entry)
+  VisRec* cand;                 // cand_cap carve candidates (any order; sorted by entry)
+  int32_t cand_cap;             // records D.cand holds: max(nblocks, 1024) (<= the D.pairs scratch)
   unsigned long long* arrive;   // kArriveWords: last-arriver counters of the frame kernels
   VisRec* fresh_vis;            // kNewKeyCap blocks created this frame (k_resolve_alloc frame mode)
+  VisRec* pend;                 // kNewKeyCap: a shard's owned entries its exhausted pool left without
+                                // voxels this frame (ctr->n_pend); carved in the same frame
   // packed frame
   float4* pixA;                 // {depth, range, w_new, rgb}
   float* pixB;                  // log2 ht - log2 lt (base-2 log-odds of the pixel)
@@ -131,6 +134,8 @@ constexpr int kMaxShards = 64;
 __global__ void k_rgbd_half(const uint8_t* rgb, const uint16_t* depth, const uint8_t* mask, int W,
                             int H, float alpha, uint8_t* rgb_out, float* depth_out);
 __global__ void k_fresh_init(EngineDev D);
+// tsdf_integrate_shard_abort: a pending sharded frame's per-frame state back to "between frames"
+__global__ void k_shard_abort(EngineDev D);
 // extraction
 struct MeshParams {
   float voxel, missing;

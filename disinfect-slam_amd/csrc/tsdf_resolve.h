@@ -509,6 +509,22 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
               e = E;
             }
             store_ent(D.table, e, k[r].x, k[r].y, k[r].z, 0, idx);
+            if (mine[r] && idx == kForeignIdx) {
+              // a shard's owned entry without voxels (its pool is exhausted): listed for this
+              // frame's carving, so no voxel-less owned entry outlives the frame and the key is
+              // retried once the DDA meets it again (one volume drops the insert instead)
+              const int pk = atomicAdd(&D.ctr->n_pend, 1);
+              if (pk < (int)kNewKeyCap) {
+                VisRec pr;
+                pr.x = k[r].x;
+                pr.y = k[r].y;
+                pr.z = k[r].z;
+                pr.pad = 0;
+                pr.idx = kForeignIdx;
+                pr.entry = (int32_t)e;
+                D.pend[pk] = pr;
+              }
+            }
             L.changed = 1;  // (a benign race: every writer stores 1)
             if (local_idx(idx)) {  // the occupancy bitmap lists the blocks this engine holds
               atomicOr(&D.occ[e >> 6], 1ull << (e & 63));

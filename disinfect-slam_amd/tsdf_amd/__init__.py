@@ -19,8 +19,8 @@ import numpy as np
 
 from . import _lib
 from ._lib import (SHARD_RECORD_BYTES, STATUS_DDA_OVERFLOW, STATUS_NEWKEY_OVERFLOW,
-                   STATUS_POOL_EXHAUSTED, STATUS_SHARD_OVERFLOW, TSDF_MEM_DEVICE, TSDF_MEM_HOST,
-                   TSDFError)
+                   STATUS_POOL_EXHAUSTED, STATUS_SHARD_ABORTED, STATUS_SHARD_OVERFLOW, TSDF_MEM_DEVICE,
+                   TSDF_MEM_HOST, TSDFError)
 
 NUM_ENTRY = 1 << 22
 NUM_BUCKET = 1 << 21
@@ -32,6 +32,7 @@ VOXEL_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("tsdf", "<f4"
 __all__ = [
     "CameraIntrinsics", "CameraParams", "SE3", "BoundingCube", "TSDFGrid", "Engine", "ShardGroup",
     "VOXEL_DTYPE", "TSDFError", "hash_block", "block_owner", "load_library", "FOREIGN_IDX",
+    "STATUS_SHARD_ABORTED",
 ]
 FOREIGN_IDX = 0x7FFFFFFF  # a shard's index entry of a block another shard holds (kForeignIdx)
 
@@ -241,9 +242,12 @@ class Engine:
         h = C.c_void_p()
         _lib.check(L.tsdf_create(C.byref(cfg), device, C.byref(h)), "tsdf_create")
         self._h = h
-        # an engine on its own stream orders itself after / before torch's current stream around
-        # every call that reads / writes a torch device tensor (tsdf_stream_wait / _signal)
-        self._own_stream = stream is None
+        # the engine orders its stream after / before torch's current stream around every call that
+        # reads / writes a torch device tensor (tsdf_stream_wait / _signal) whenever the two differ
+        # (an engine-owned stream, or a caller's stream other than torch's current one)
+        es = C.c_void_p()
+        _lib.check(L.tsdf_get_stream(h, C.byref(es)), "tsdf_get_stream")
+        self._stream = int(es.value or 0)
         self.voxel_size = voxel_size
         self.truncation = truncation
         self.num_blocks = int(L.tsdf_num_blocks(h))
@@ -340,20 +344,27 @@ class Engine:
         return FrameGraph(self, width, height, render_width, render_height)
 
     # ---- stream ordering with torch (device tensors on torch's current stream) ----
+    def _torch_stream(self, tensors):
+        """torch's current stream when it differs from the engine stream and a device tensor is
+        involved, else None (same stream: already ordered)."""
+        if not any(_is_torch_cuda(t) for t in tensors if t is not None):
+            return None
+        import torch
+        cur = int(torch.cuda.current_stream().cuda_stream or 0)
+        return None if cur == self._stream else cur
+
     def _wait_torch(self, *tensors):
         """Engine stream waits for torch's current stream when a device tensor goes in."""
-        if self._own_stream and any(_is_torch_cuda(t) for t in tensors if t is not None):
-            import torch
-            _lib.check(_lib.load().tsdf_stream_wait(self._h, C.c_void_p(torch.cuda.current_stream().cuda_stream)),
-                       "tsdf_stream_wait")
+        cur = self._torch_stream(tensors)
+        if cur is not None:
+            _lib.check(_lib.load().tsdf_stream_wait(self._h, C.c_void_p(cur)), "tsdf_stream_wait")
 
     def _signal_torch(self, *tensors):
         """Torch's current stream waits for the engine when a device tensor it wrote / reads is
         handed back (or may be freed by the caller)."""
-        if self._own_stream and any(_is_torch_cuda(t) for t in tensors if t is not None):
-            import torch
-            _lib.check(_lib.load().tsdf_stream_signal(self._h, C.c_void_p(torch.cuda.current_stream().cuda_stream)),
-                       "tsdf_stream_signal")
+        cur = self._torch_stream(tensors)
+        if cur is not None:
+            _lib.check(_lib.load().tsdf_stream_signal(self._h, C.c_void_p(cur)), "tsdf_stream_signal")
 
     # ---- sharded frames (SURVEY 8e; tsdf_integrate_shard_*) ----
     @staticmethod
@@ -402,6 +413,11 @@ class Engine:
         _lib.check(_lib.load().tsdf_integrate_shard_end(self._h, _ptr(cands_in), cand_cap),
                    "tsdf_integrate_shard_end")
         self._signal_torch(cands_in)
+
+    def integrate_shard_abort(self):
+        """Abort a pending sharded frame (tsdf_integrate_shard_abort): the engine is between frames
+        again; STATUS_SHARD_ABORTED is set because shards may have diverged (restore snapshots)."""
+        _lib.check(_lib.load().tsdf_integrate_shard_abort(self._h), "tsdf_integrate_shard_abort")
 
     def integrate(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float):
         dev = _is_torch_cuda(depth)
@@ -675,6 +691,14 @@ class ShardGroup:
         self.cands_exchanged = 0  # carve-candidate records likewise
 
     def integrate(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float, count=False):
+        try:
+            self._integrate(rgb, depth, ht, lt, K, cam_T_world, max_depth, count)
+        except Exception:
+            for e in self.engines:  # no shard stays stuck mid-frame (the caller sees the error)
+                e.integrate_shard_abort()
+            raise
+
+    def _integrate(self, rgb, depth, ht, lt, K, cam_T_world, max_depth, count):
         G = self.G
         for i, e in enumerate(self.engines):
             if self.split:

@@ -20,6 +20,7 @@ STATUS_NEWKEY_OVERFLOW = 2
 STATUS_DDA_OVERFLOW = 4
 STATUS_RESOLVE_ABORT = 8
 STATUS_SHARD_OVERFLOW = 16
+STATUS_SHARD_ABORTED = 32
 SHARD_RECORD_BYTES = 16
 
 
@@ -101,7 +102,7 @@ EXPORTS = [
     "tsdf_pool_acquire", "tsdf_pool_release", "tsdf_pool_set_weight", "tsdf_pool_get_weights",
     "tsdf_hash_block", "tsdf_block_owner", "tsdf_error_string", "tsdf_last_error",
     "tsdf_shard_slot_bytes", "tsdf_integrate_shard_begin", "tsdf_integrate_shard_update",
-    "tsdf_integrate_shard_end", "tsdf_stream_wait", "tsdf_stream_signal", "tsdf_get_stream",
+    "tsdf_integrate_shard_end", "tsdf_integrate_shard_abort", "tsdf_stream_wait", "tsdf_stream_signal", "tsdf_get_stream",
     "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame", "tsdf_graph_destroy",
     "tsdf_snapshot_bytes", "tsdf_snapshot_save", "tsdf_snapshot_load",
     "tsdf_render_blocks", "tsdf_import_blocks", "tsdf_reset", "tsdf_pack_blocks",
@@ -133,6 +134,7 @@ def load(path: str | None = None):
                                              C.c_int32, C.c_int32, P, C.c_int32]
     L.tsdf_integrate_shard_update.argtypes = [P, P, C.c_int32, P, C.c_int32]
     L.tsdf_integrate_shard_end.argtypes = [P, P, C.c_int32]
+    L.tsdf_integrate_shard_abort.argtypes = [P]
     L.tsdf_stream_wait.argtypes = [P, P]
     L.tsdf_stream_signal.argtypes = [P, P]
     L.tsdf_get_stream.argtypes = [P, C.POINTER(P)]
@@ -181,7 +183,7 @@ def load(path: str | None = None):
     L.tsdf_last_error.argtypes = []
     for name in ("tsdf_create", "tsdf_destroy", "tsdf_integrate", "tsdf_raycast", "tsdf_query",
                  "tsdf_integrate_shard_begin", "tsdf_integrate_shard_update", "tsdf_integrate_shard_end",
-                 "tsdf_stream_wait", "tsdf_stream_signal", "tsdf_get_stream",
+                 "tsdf_integrate_shard_abort", "tsdf_stream_wait", "tsdf_stream_signal", "tsdf_get_stream",
                  "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame",
                  "tsdf_graph_destroy", "tsdf_snapshot_bytes", "tsdf_snapshot_save", "tsdf_snapshot_load",
                  "tsdf_extract_mesh",

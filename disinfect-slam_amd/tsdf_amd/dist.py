@@ -69,6 +69,15 @@ def integrate_sharded(engine, bufs, rgb, depth, ht, lt, K, cam_T_world, max_dept
         rank, world = dist.get_rank(), dist.get_world_size()
     else:
         rank, world = 0, 1
+    try:
+        _integrate_sharded(engine, bufs, rgb, depth, ht, lt, K, cam_T_world, max_depth, split, rank, world)
+    except Exception:
+        # a failed exchange (e.g. a collective timeout) must not leave the engine mid-frame
+        engine.integrate_shard_abort()
+        raise
+
+
+def _integrate_sharded(engine, bufs, rgb, depth, ht, lt, K, cam_T_world, max_depth, split, rank, world):
     if split:
         engine.integrate_shard_begin(rgb, depth, ht, lt, K, cam_T_world, max_depth, rank, world,
                                      bufs.keys_out, bufs.key_cap)

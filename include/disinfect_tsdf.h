@@ -37,6 +37,7 @@ extern "C" {
 #define TSDF_STATUS_DDA_OVERFLOW 4u    /* a DDA ray took more samples than sized for */
 #define TSDF_STATUS_RESOLVE_ABORT 8u   /* allocation resolver made no progress (internal error) */
 #define TSDF_STATUS_SHARD_OVERFLOW 16u /* a sharded frame had more keys / candidates than a slot holds */
+#define TSDF_STATUS_SHARD_ABORTED 32u  /* a pending sharded frame was aborted (the shards may differ) */
 
 typedef struct tsdf_engine tsdf_engine;
 typedef struct tsdf_graph tsdf_graph;
@@ -160,6 +161,11 @@ int tsdf_integrate_shard_begin(tsdf_engine* e, const tsdf_frame* frame, const ts
 int tsdf_integrate_shard_update(tsdf_engine* e, const void* keys_in, int32_t key_cap, void* cands_out,
                                 int32_t cand_cap);
 int tsdf_integrate_shard_end(tsdf_engine* e, const void* cands_in, int32_t cand_cap);
+/* Abort a pending sharded frame (e.g. a failed exchange between the phases): the engine returns to
+ * "between frames" so later calls (a new frame, reset, snapshot_load, ...) work again. Structural
+ * changes a phase already made stay, so the shards may no longer agree: TSDF_STATUS_SHARD_ABORTED is
+ * set, and the caller should restore every shard from a snapshot (or reset). No pending frame: OK. */
+int tsdf_integrate_shard_abort(tsdf_engine* e);
 
 /* Stream ordering with a caller's HIP stream (e.g. torch's current stream) for device buffers
  * passed to an engine that runs on its own stream: tsdf_stream_wait makes the engine stream wait

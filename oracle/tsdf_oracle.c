@@ -54,6 +54,11 @@ struct ora_grid {
   int32_t* vis;    /* visible_blocks_ entry indices (entry order) */
   ora_stats st;
   int shard_index, shard_count; /* spatial sharding (not in the reference) */
+  /* a shard's entries of owned keys its exhausted pool could not give voxels this frame: carved in
+   * the same frame (appended to its candidates), so no voxel-less owned entry outlives the frame */
+  s3* pend_pos;
+  int32_t* pend_entry;
+  int64_t n_pend, pend_cap;
 };
 
 /* ---------------- float math (utils/cuda/camera.cuh, lie_group.cuh, Eigen 3.3) ------------- */
@@ -220,6 +225,18 @@ static int new_block(ora_grid* g, s3 key, int32_t* idx) {
   *idx = pool_acquire(g);
   return 1;
 }
+/* a shard's owned entry without voxels (pool exhausted): listed for this frame's carving */
+static void note_pending(ora_grid* g, s3 key, int32_t idx, uint32_t e) {
+  if (g->shard_count <= 1 || idx != ORA_FOREIGN || !owns(g, key)) return;
+  if (g->n_pend == g->pend_cap) {
+    g->pend_cap = g->pend_cap ? 2 * g->pend_cap : 256;
+    g->pend_pos = (s3*)realloc(g->pend_pos, sizeof(s3) * (size_t)g->pend_cap);
+    g->pend_entry = (int32_t*)realloc(g->pend_entry, sizeof(int32_t) * (size_t)g->pend_cap);
+  }
+  g->pend_pos[g->n_pend] = key;
+  g->pend_entry[g->n_pend] = (int32_t)e;
+  g->n_pend++;
+}
 
 /* voxel_hash.cu:58-120 VoxelHashTable::Allocate, executed as one step of a sequential launch. */
 static int hash_allocate(ora_grid* g, s3 key) {
@@ -248,6 +265,7 @@ static int hash_allocate(ora_grid* g, s3 key) {
         b->pos = key;
         b->offset = 0;
         b->idx = idx;
+        note_pending(g, key, idx, e0 + (uint32_t)i);
         return 1;
       }
       g->st.last_cross_losses += cross;
@@ -275,6 +293,7 @@ static int hash_allocate(ora_grid* g, s3 key) {
         bn->pos = key;
         bn->offset = 0;
         bn->idx = idx;
+        note_pending(g, key, idx, next);
         return 1;
       }
       g->st.last_cross_losses += cross;
@@ -421,7 +440,7 @@ ora_grid* ora_create(float voxel_size, float truncation, int num_block_bits) {
 void ora_destroy(ora_grid* g) {
   if (!g) return;
   free(g->table); free(g->locks); free(g->heap); free(g->tsdf); free(g->prob); free(g->rgbw);
-  free(g->range); free(g->vis);
+  free(g->range); free(g->vis); free(g->pend_pos); free(g->pend_entry);
   free(g);
 }
 
@@ -734,9 +753,19 @@ int64_t ora_shard_update(ora_grid* g, const int16_t* keys, const uint64_t* order
     cand_pos[3 * i + 2] = cpos[i].z;
     cand_entry[i] = cent[i];
   }
+  /* + the owned entries left without voxels by an exhausted pool (carved this frame) */
+  int64_t ntot = nc;
+  for (int64_t j = 0; j < g->n_pend; ++j, ++ntot)
+    if (ntot < cand_cap) {
+      cand_pos[3 * ntot + 0] = g->pend_pos[j].x;
+      cand_pos[3 * ntot + 1] = g->pend_pos[j].y;
+      cand_pos[3 * ntot + 2] = g->pend_pos[j].z;
+      cand_entry[ntot] = g->pend_entry[j];
+    }
+  g->n_pend = 0;
   free(cpos);
   free(cent);
-  return nc;
+  return ntot;
 }
 
 void ora_shard_delete(ora_grid* g, const int16_t* cand_pos, const int32_t* cand_entry, int64_t n) {

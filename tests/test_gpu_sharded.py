@@ -202,3 +202,124 @@ def test_sharded_snapshot_resume():
         assert_union_equals([e.dump() for e in other.engines], full.dump(), tag="resumed")
     finally:
         group.close(), other.close(), full.close(), u.close()
+
+
+def _no_owned_voxelless_entries(group):
+    """No shard keeps an entry of a block it owns without voxels (an exhausted owner's
+    kForeignIdx entry would hide the key from the DDA forever)."""
+    import tsdf_amd
+    for i, e in enumerate(group.engines):
+        d = e.dump(pool=False)
+        foreign = np.flatnonzero(d["entry_idx"] == tsdf_amd.FOREIGN_IDX)
+        for p in d["entry_pos"][foreign, :3]:
+            assert tsdf_amd.block_owner(int(p[0]), int(p[1]), int(p[2]), group.G) != i, \
+                f"shard {i} owns block {tuple(p)} but holds no voxels for it"
+
+
+def test_sharded_pool_exhaustion_matches_oracle_shards():
+    """Shard pools far smaller than the scene: owned keys an exhausted pool cannot hold are carved in
+    the same frame on every shard (the key is retried when the DDA meets it again, as one volume
+    retries a dropped insert). Every shard stays bit-exact against the oracle's shard, and no shard
+    is left with a voxel-less entry of a block it owns."""
+    import tsdf_amd
+    from tsdf_amd import synth
+    from _oracle import OracleGrid, lib
+    W, H, G, bits = 160, 120, 3, 8
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    group = tsdf_amd.ShardGroup(G, 0.005, 0.03, max_width=W, max_height=H, num_block_bits=bits)
+    oshards = []
+    for i in range(G):
+        o = OracleGrid(0.005, 0.03, bits)
+        lib().ora_set_shard(o.h, i, G)
+        oshards.append(o)
+    try:
+        exhausted = 0
+        for f in range(8):
+            fr = synth.render(cam, 2 * f)
+            group.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, tsdf_amd.SE3(fr["q"], fr["t"]), MAXD)
+            oracle_shard_frame(oshards, fr, cam, MAXD, split=True)
+            st = group.stats()
+            assert all(s["status"] & ~tsdf_amd.STATUS_POOL_EXHAUSTED == 0 for s in st), st
+            exhausted += sum(bool(s["status"] & tsdf_amd.STATUS_POOL_EXHAUSTED) for s in st)
+            for i, o in enumerate(oshards):
+                compare(group.engines[i], o, tag=f"frame {f} shard {i}/{G}")
+            _no_owned_voxelless_entries(group)
+        assert exhausted > 0, "the pools never ran out: the test would not exercise exhaustion"
+    finally:
+        group.close()
+        for o in oshards:
+            o.close()
+
+
+def test_sharded_candidate_union_overflow_is_clamped():
+    """the union of the shards' candidate slots can exceed the records a shard's
+    carving list holds (max(pool, 1024)). It is clamped with TSDF_STATUS_SHARD_OVERFLOW instead of
+    being written past the list; later frames still run and every pool index stays in range."""
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H, G, bits = 640, 480, 8, 10
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    group = tsdf_amd.ShardGroup(G, 0.005, 0.03, max_width=W, max_height=H, num_block_bits=bits,
+                                key_cap=16384, cand_cap=16384)
+    try:
+        cap = max(1 << bits, 1024)
+        prev, big = 0, False
+        for f in range(4):
+            fr = synth.render(cam, 4 * f)
+            group.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, tsdf_amd.SE3(fr["q"], fr["t"]),
+                            MAXD, count=True)
+            n = group.cands_exchanged - prev
+            prev = group.cands_exchanged
+            st = group.stats()
+            if n > cap:
+                big = True
+                assert all(s["status"] & tsdf_amd.STATUS_SHARD_OVERFLOW for s in st), (f, n, st)
+            for e in group.engines:
+                e.stats(clear_status=True)
+        assert big, "no frame exchanged more candidates than the list holds"
+        for e in group.engines:
+            d = e.dump(pool=False)
+            idx = d["entry_idx"]
+            ok = (idx == -1) | (idx == tsdf_amd.FOREIGN_IDX) | ((idx >= 0) & (idx < (1 << bits)))
+            assert ok.all()
+    finally:
+        group.close()
+
+
+def test_shard_abort_returns_engine_between_frames():
+    """a failed exchange between the phases must not strand the engine in a pending frame.
+    tsdf_integrate_shard_abort clears it (STATUS_SHARD_ABORTED set); new frames, snapshots and reset
+    work again."""
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H, G, cap = 96, 72, 2, 4096
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    fr = synth.render(cam, 0)
+    pose = tsdf_amd.SE3(fr["q"], fr["t"])
+    e = tsdf_amd.Engine(0.01, 0.04, max_width=W, max_height=H, num_block_bits=12, shard_index=0,
+                        shard_count=G)
+    slot = lambda n=1: torch.zeros((n, tsdf_amd.Engine.shard_slot_bytes(cap)), dtype=torch.uint8, device="cuda")
+    try:
+        e.integrate_shard_abort()  # nothing pending: a no-op
+        assert e.stats()["status"] == 0
+        for phases in (1, 2):
+            keys, cands = slot(G), slot(G)
+            e.integrate_shard_begin(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, pose, MAXD, 0, G, keys[0], cap)
+            if phases == 2:
+                e.integrate_shard_update(keys, cap, cands[0], cap)
+            with pytest.raises(tsdf_amd.TSDFError):
+                e.snapshot()
+            e.integrate_shard_abort()
+            assert e.stats(clear_status=True)["status"] & tsdf_amd.STATUS_SHARD_ABORTED
+            e.snapshot()
+        e.reset()
+        # a whole frame runs after the aborts, and the per-frame state was cleared (no stale keys)
+        keys, cands = slot(G), slot(G)
+        e.integrate_shard_begin(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, pose, MAXD, 0, G, keys[0], cap)
+        e.integrate_shard_update(keys, cap, cands[0], cap)
+        e.integrate_shard_end(cands, cap)
+        assert e.stats()["status"] == 0 and e.stats()["active_blocks"] > 0
+    finally:
+        e.close()
