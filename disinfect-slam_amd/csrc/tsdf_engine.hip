@@ -412,7 +412,11 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.fresh, kNewKeyCap);
   ALLOC(D.vis, (size_t)kBands * nb);
   ALLOC(D.band, kBands * kBandStride);
-  D.cand_cap = std::max(nb, 1024);  // >= the resolver's speculative prologue reads (kRB)
+  // carve candidates of one frame: a shard's list takes every shard's (their visible blocks and the
+  // entries exhausted pools left without voxels), so it is sized like the resolver's D.pairs scratch;
+  // more are clamped with TSDF_STATUS_SHARD_OVERFLOW. TSDF_CAND_CAP (tests) sets a smaller list.
+  D.cand_cap = (int32_t)std::max<size_t>(kNewKeyCap, (size_t)nb);
+  if (const char* v = std::getenv("TSDF_CAND_CAP")) D.cand_cap = std::min(D.cand_cap, std::max(1024, std::atoi(v)));
   ALLOC(D.cand, D.cand_cap);
   ALLOC(D.arrive, kArriveWords);
   ALLOC(D.fresh_vis, kNewKeyCap);

@@ -44,7 +44,7 @@ struct EngineDev {
   VisRec* vis;                  // kBands x nblocks visible blocks (band-major, any order within)
   int32_t* band;                // kBands x kBandStride: record count of each band list
   VisRec* cand;                 // cand_cap carve candidates (any order; sorted by entry)
-  int32_t cand_cap;             // records D.cand holds: max(nblocks, 1024) (<= the D.pairs scratch)
+  int32_t cand_cap;             // records D.cand holds (<= the D.pairs scratch, >= 1024)
   unsigned long long* arrive;   // kArriveWords: last-arriver counters of the frame kernels
   VisRec* fresh_vis;            // kNewKeyCap blocks created this frame (k_resolve_alloc frame mode)
   VisRec* pend;                 // kNewKeyCap: a shard's owned entries its exhausted pool left without

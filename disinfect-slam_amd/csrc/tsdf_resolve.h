@@ -293,6 +293,225 @@ struct AKey {
   int16_t x, y, z;
 };
 
+// ---------------------------------------------------------------------------------------------
+// One-wave fast path of the allocation resolver for launches with <= 64 new keys (the steady state
+// of a frame stream: ~50-80 new keys per 640x480 frame). The same rounds as resolve_alloc_wg --
+// candidate order, speculative evaluation against the table, the longest prefix whose buckets are
+// pairwise distinct commits -- with one key per lane and wave-level operations instead of LDS
+// tables and workgroup barriers: the rank of each key by readlane comparisons and a ds_permute
+// into rank order, the first conflicting rank by readlane comparisons of the claimed buckets, pool
+// pops by the lane-mask prefix count of the committing owned keys. Only the launch's bucket locks
+// live in LDS (a 256-slot set; <= 2 locks per key).
+// ---------------------------------------------------------------------------------------------
+constexpr int kWaveKeys = 64;
+constexpr int kWaveLockSlots = 256;
+// Measured (r3, same box, interleaved): 7.25 us per frame against the workgroup resolver's 6.75 --
+// the readlane rank / conflict loops cost more VALU latency than the barriers they replace. Kept for
+// A/B builds (-DTSDF_WAVE_RESOLVE); off by default.
+#ifdef TSDF_WAVE_RESOLVE
+__device__ constexpr bool resolve_wave_off() { return false; }
+#else
+__device__ constexpr bool resolve_wave_off() { return true; }
+#endif
+
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+  return (1ull << lane_id()) - 1ull;
+}
+// lane `rank` receives v (ranks distinct in [0, 64))
+__device__ __forceinline__ uint32_t push_to(uint32_t v, int rank) {
+  return (uint32_t)__builtin_amdgcn_ds_permute(rank << 2, (int)v);
+}
+
+__device__ void resolve_alloc_wave(const EngineDev& D, const FrameParams& P, int frame_mode, int n, int free0,
+                                   unsigned long long key_in, int32_t slot_in, uint32_t* lockset,
+                                   unsigned long long tick0) {
+  const int l = lane_id();
+  // ---- round trip 2: candidate orders, the keys' buckets, the free-stack top ----
+  uint32_t ord = 0xFFFFFFFFu, hint = 0u;
+  if (l < n) {
+    int16_t x, y, z;
+    unpack_key(key_in, x, y, z);
+    const uint32_t B = hash_block(x, y, z);
+    ord = ld_co(&D.nk_order[slot_in]);
+    const Ent s0 = load_ent(D.table, 2 * B), s1 = load_ent(D.table, 2 * B + 1);
+    hint = (s0.idx < 0 ? 1u : 0u) | (s1.idx < 0 ? 2u : 0u) | ((uint32_t)(uint16_t)s1.off << 16);
+  }
+  const int32_t htop = l < min(n, max(free0, 0)) ? D.heap[free0 - 1 - l] : 0;  // heap[free0 - 1 - l]
+  for (int i = l; i < kWaveLockSlots; i += 64) lockset[i] = 0u;
+  // ---- keys into candidate order: lane r <- the key of rank r (orders are unique per key) ----
+  int rank = 0;
+#pragma unroll 16
+  for (int j = 0; j < 64; ++j) {
+    const uint32_t oj = __builtin_amdgcn_readlane(ord, j);
+    rank += (oj < ord) || (oj == ord && j < l);
+  }
+  const unsigned long long key =
+      ((unsigned long long)push_to((uint32_t)(key_in >> 32), rank) << 32) | push_to((uint32_t)key_in, rank);
+  const int32_t slot = (int32_t)push_to((uint32_t)slot_in, rank);
+  const uint32_t hint0 = push_to(hint, rank);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");  // (the lock set cleared above)
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+  const bool have = l < n;
+  int16_t x = 0, y = 0, z = 0;
+  uint32_t B = 0;
+  if (have) {
+    unpack_key(key, x, y, z);
+    B = hash_block(x, y, z);
+  }
+  const bool owned = have && (P.shard_count <= 1 ||
+                              brick_owner(x, y, z, (uint32_t)P.shard_count) == (uint32_t)P.shard_index);
+  int base = 0, sfree = free0, nfresh = 0;
+  bool first_round = true;
+  while (base < n) {  // wave-uniform
+    const bool act = have && l >= base;
+    int kind = 0;
+    uint32_t b1 = 0xFFFFFFFFu, b2 = 0xFFFFFFFFu, T = 0, E = 0;
+    int sl = 0;
+    if (act) {
+      // the prologue's view of the bucket holds unless a commit of this launch wrote into it, and
+      // every such commit locked it
+      bool e0, e1;
+      int16_t off1;
+      if (first_round || !lock_held<kWaveLockSlots>(lockset, B)) {
+        e0 = (hint0 & 1u) != 0;
+        e1 = (hint0 & 2u) != 0;
+        off1 = (int16_t)(hint0 >> 16);
+      } else {
+        const Ent s0 = load_ent(D.table, 2 * B), s1 = load_ent(D.table, 2 * B + 1);
+        e0 = s0.idx < 0;
+        e1 = s1.idx < 0;
+        off1 = s1.off;
+      }
+      if (e0 || e1) {  // SLOT (voxel_hash.cu:79-91)
+        kind = 1;
+        sl = e0 ? 0 : 1;
+        b1 = b2 = B;
+      } else {  // APPEND (:93-119): tail T of the list from slot 1, first empty slot-0 entry E after it
+        kind = 2;
+        uint32_t last = 2 * B + 1;
+        int16_t off = off1;
+        while (off) {
+          last = (uint32_t)(last + (int32_t)off) & kEntryMask;
+          off = load_ent(D.table, last).off;
+        }
+        T = last;
+        uint32_t nx = last;
+        for (uint32_t q = 0; q < kNumEntry; ++q) {
+          nx = (nx + 1) & kEntryMask;
+          if ((nx & 1u) == 0u && load_ent(D.table, nx).idx < 0) break;
+        }
+        E = nx;
+        b1 = T >> 1;
+        b2 = E >> 1;
+      }
+    }
+    // first rank (>= base) whose buckets meet an earlier key's of this round: the keys before it
+    // take pairwise distinct buckets, so their locks and commits do not interact
+    bool dirty = false;
+    for (int j = base; j < n; ++j) {  // wave-uniform bounds
+      const uint32_t c1 = __builtin_amdgcn_readlane(b1, j), c2 = __builtin_amdgcn_readlane(b2, j);
+      dirty |= j < l && (c1 == b1 || c1 == b2 || c2 == b1 || c2 == b2);
+    }
+    const unsigned long long dm = __ballot(act && dirty);
+    const int fd = dm ? __ffsll((long long)dm) - 1 : 64;
+    const bool proc = act && l < fd;
+    // atomicExch(&bucket_locks_[b], LOCKED) == FREE within the launch (locks of earlier rounds hold)
+    bool ok = false;
+    if (proc) {
+      if (kind == 1)
+        ok = lock_take2<kWaveLockSlots>(lockset, B);
+      else if (lock_take2<kWaveLockSlots>(lockset, b1))
+        ok = lock_take2<kWaveLockSlots>(lockset, b2);
+    }
+    // pool pops in key order among the committing keys this engine holds
+    const bool mine = ok && owned;
+    const unsigned long long mm = __ballot(mine);
+    const int prank = __popcll(mm & lanemask_lt());
+    const int nmine = __popcll(mm);
+    const int hi = sfree - 1 - prank;
+    const int top = free0 - 1 - hi;  // pops so far this launch + rank (< n <= 64)
+    const int32_t popped = __shfl(htop, top & 63, 64);
+    if (ok) {
+      int32_t idx = kForeignIdx;
+      bool insert = true;
+      if (mine) {
+        if (hi < 0) {
+          atomicOr(&D.ctr->status, 1u);  // TSDF_STATUS_POOL_EXHAUSTED
+          insert = P.shard_count > 1;    // (see resolve_alloc_wg)
+        } else {
+          idx = popped;
+        }
+      }
+      if (insert) {
+        uint32_t e;
+        if (kind == 1) {
+          e = 2 * B + (uint32_t)sl;
+        } else {
+          const uint32_t wrap = E > T ? 0u : kNumEntry;
+          store_off(D.table, T, (int16_t)(E + wrap - T));
+          e = E;
+        }
+        store_ent(D.table, e, x, y, z, 0, idx);
+        if (mine && idx == kForeignIdx) {  // voxel-less owned entry: carved this frame
+          const int pk = atomicAdd(&D.ctr->n_pend, 1);
+          if (pk < (int)kNewKeyCap) {
+            VisRec pr;
+            pr.x = x;
+            pr.y = y;
+            pr.z = z;
+            pr.pad = 0;
+            pr.idx = kForeignIdx;
+            pr.entry = (int32_t)e;
+            D.pend[pk] = pr;
+          }
+        }
+        if (local_idx(idx)) {
+          atomicOr(&D.occ[e >> 6], 1ull << (e & 63));
+          if (frame_mode) {  // fresh and visible this frame (see resolve_alloc_wg)
+            VisRec vr;
+            vr.x = x;
+            vr.y = y;
+            vr.z = z;
+            vr.pad = 1;
+            vr.idx = idx;
+            vr.entry = (int32_t)e;
+            D.fresh_vis[nfresh + prank] = vr;
+          } else {
+            D.fresh[nfresh + prank] = idx;
+          }
+        }
+      }
+    }
+    if (proc) {  // processed: the key-set slot is empty for the next frame
+      D.nk_key[slot] = 0ull;
+      D.nk_order[slot] = 0xFFFFFFFFu;
+    }
+    const int used = nmine < sfree ? nmine : (sfree > 0 ? sfree : 0);
+    sfree -= used;
+    nfresh += used;
+    base = min(fd, n);
+    first_round = false;
+    if (base < n) {  // the next round reloads buckets this one wrote
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    }
+  }
+  if (l == 0) {
+    D.ctr->resolve_alloc_ticks += __builtin_amdgcn_s_memrealtime() - tick0;
+    D.ctr->free_count = sfree;
+    D.ctr->n_fresh = nfresh;
+    D.ctr->nk_count = 0;
+    if (frame_mode) {
+      D.ctr->last_alloc = nfresh;
+      D.ctr->last_new_keys = n;
+      D.ctr->total_alloc += (unsigned long long)nfresh;
+    }
+  }
+}
+
 // frame_mode 1: new blocks this engine holds are listed in D.fresh_vis (flagged fresh, visible this
 // frame); 0 (hash-level test path): their pool indices in D.fresh for k_fresh_init.
 template <int RB>
@@ -312,6 +531,12 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
   const bool single = n <= RB;
   const bool lds_locks = n <= AllocLdsT<RB>::kLockKeys;
   const uint32_t epoch = epoch0 + 1u;
+  if (n <= kWaveKeys && !resolve_wave_off()) {  // one-wave fast path; the other waves are done
+    static_assert(AllocLdsT<RB>::kLock >= kWaveLockSlots, "lock set");
+    if (t == 0) D.ctr->lock_epoch = epoch;
+    if (t < 64) resolve_alloc_wave(D, P, frame_mode, n, free0, k0, h0, L.lock, tick0);
+    return;
+  }
   if (lds_locks)
     for (int i = t; i < NL; i += kRT) L.lock[i] = 0u;
   if (t == 0) {

@@ -239,7 +239,7 @@ def test_sharded_pool_exhaustion_matches_oracle_shards():
             group.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, tsdf_amd.SE3(fr["q"], fr["t"]), MAXD)
             oracle_shard_frame(oshards, fr, cam, MAXD, split=True)
             st = group.stats()
-            assert all(s["status"] & ~tsdf_amd.STATUS_POOL_EXHAUSTED == 0 for s in st), st
+            assert all((s["status"] & ~tsdf_amd.STATUS_POOL_EXHAUSTED) == 0 for s in st), [s["status"] for s in st]
             exhausted += sum(bool(s["status"] & tsdf_amd.STATUS_POOL_EXHAUSTED) for s in st)
             for i, o in enumerate(oshards):
                 compare(group.engines[i], o, tag=f"frame {f} shard {i}/{G}")
@@ -253,16 +253,20 @@ def test_sharded_pool_exhaustion_matches_oracle_shards():
 
 def test_sharded_candidate_union_overflow_is_clamped():
     """the union of the shards' candidate slots can exceed the records a shard's
-    carving list holds (max(pool, 1024)). It is clamped with TSDF_STATUS_SHARD_OVERFLOW instead of
+    carving list holds. It is clamped with TSDF_STATUS_SHARD_OVERFLOW instead of
     being written past the list; later frames still run and every pool index stays in range."""
     import tsdf_amd
     from tsdf_amd import synth
-    W, H, G, bits = 640, 480, 8, 10
+    import os
+    W, H, G, bits, cap = 640, 480, 8, 8, 1024  # pools of 256: thousands of voxel-less entries to carve
     cam = synth.camera(W, H, synth.TUM_FR1)
-    group = tsdf_amd.ShardGroup(G, 0.005, 0.03, max_width=W, max_height=H, num_block_bits=bits,
-                                key_cap=16384, cand_cap=16384)
+    os.environ["TSDF_CAND_CAP"] = str(cap)  # a 1024-record carving list (default: 2^17)
     try:
-        cap = max(1 << bits, 1024)
+        group = tsdf_amd.ShardGroup(G, 0.005, 0.03, max_width=W, max_height=H, num_block_bits=bits,
+                                    key_cap=16384, cand_cap=16384)
+    finally:
+        del os.environ["TSDF_CAND_CAP"]
+    try:
         prev, big = 0, False
         for f in range(4):
             fr = synth.render(cam, 4 * f)
