@@ -51,9 +51,11 @@ __device__ void nk_insert(const EngineDev& D, uint64_t key, uint32_t order) {
 //     an LDS hash set with their smallest candidate order (y*W + x)*maxs + i
 //  3. each unique key once: all-8-corners visibility (is_block_visible<true>), table probe;
 //     missing keys go to the global new-key set.
-// Steps 2-3 run only for tiles in [P.tile_lo, P.tile_hi) (a sharded frame's pixel slice; every
-// tile otherwise). A shard probes its copy of the whole hash index, so its keys are exactly the
-// ones one volume's DDA finds in those tiles, whichever shard owns them.
+// The launch covers tiles [P.tile_lo, P.tile_hi): every tile of the frame, or a sharded frame's
+// pixel slice. Step 1 runs only when P.pack_pixels (one volume); a shard's k_integrate gathers the
+// raw frame, so a shard runs the DDA of its slice and nothing else per pixel. A shard probes its
+// copy of the whole hash index, so its keys are exactly the ones one volume's DDA finds in those
+// tiles, whichever shard owns them.
 // ---------------------------------------------------------------------------------------------
 // LDS key-set slots per 16x16 tile: TS > 256 pixels x maxs. 1024 for maxs <= 3 (the reference's
 // 6x truncation / voxel ratio: 2-3 samples per pixel) keeps the workgroup at 16.5 KiB of LDS, so 9
@@ -223,19 +225,18 @@ __device__ __forceinline__ void ingest_tile(EngineDev& D, const FrameParams& P,
   if (x < P.W && y < P.H) {
     const int i = y * P.W + x;
     const float d = depth[i];
-    const uint32_t c = (uint32_t)rgb[3 * i] | ((uint32_t)rgb[3 * i + 1] << 8) |
-                       ((uint32_t)rgb[3 * i + 2] << 16);
-    const float h = ht ? ht[i] : 1.0f;
-    const float l = lt ? lt[i] : 1.0f;
     const f3 pc = pixel_ray(P, x, y);
     const float range = sqrtf(dot3(pc, pc));  // img_depth_to_range (voxel_tsdf.cu:120)
-    const float w_new = (1.0f - quot_const(d, P.max_depth, P.inv_max_depth)) * 4.0f;
-    D.pixA[i] = make_float4(d, range, w_new, __uint_as_float(c));
-    // base-2 log-odds of the pixel (k_integrate); the hardware log2 (1 ulp) is far inside the
-    // 1e-4 prob tolerance and still gives exactly 0 when ht == lt
-    D.pixB[i] = __log2f(h) - __log2f(l);
+    if (P.pack_pixels) {  // (a shard's k_integrate reads the raw frame instead)
+      const uint32_t c = (uint32_t)rgb[3 * i] | ((uint32_t)rgb[3 * i + 1] << 8) |
+                         ((uint32_t)rgb[3 * i + 2] << 16);
+      const float h = ht ? ht[i] : 1.0f;
+      const float l = lt ? lt[i] : 1.0f;
+      D.pixA[i] = make_float4(d, range, pixel_w_new(P, d), __uint_as_float(c));
+      D.pixB[i] = pixel_logodds(h, l);
+    }
     TSDF_STAMP(D, 0, 2);
-    if (tile >= P.tile_lo && tile < P.tile_hi && !(d == 0 || d > P.max_depth)) {
+    if (!(d == 0 || d > P.max_depth)) {
       const f3 pcd = {pc.x * d, pc.y * d, pc.z * d};
       const f3 pw = se3_apply(P.wq, P.wt, pcd);
       // pc / range (IEEE quotients; pc.z = 1): the Newton-refined pair division, exact in range
@@ -314,7 +315,6 @@ __device__ __forceinline__ void ingest_tile(EngineDev& D, const FrameParams& P,
   }
   TSDF_STAMP(D, 0, 3);
   __syncthreads();
-  if (tile < P.tile_lo || tile >= P.tile_hi) return;  // pixel records only (workgroup-uniform)
   TSDF_STAMP(D, 0, 4);
   // Each wave sweeps its 64-slot strips; the few occupied slots of a strip (ballot) are tested
   // 8 at a time with 8 lanes per key, one block corner per lane (is_block_visible<true>), and the
@@ -408,8 +408,8 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
     TSDF_STAMP(D, 2, 0);
     vis_sweep(D, P, blockIdx.x, S);
     TSDF_STAMP(D, 2, 1);
-  } else if ((int)blockIdx.x - kVisWorkgroups < tiles) {
-    ingest_tile<TS>(D, P, depth, rgb, ht, lt, tiles_x, (int)blockIdx.x - kVisWorkgroups, S);
+  } else if ((int)blockIdx.x - kVisWorkgroups < tiles) {  // tiles [P.tile_lo, P.tile_lo + tiles)
+    ingest_tile<TS>(D, P, depth, rgb, ht, lt, tiles_x, P.tile_lo + (int)blockIdx.x - kVisWorkgroups, S);
   }
   if (!arrive_last(D.arrive + kArrIngest, 0ull, &S.last)) return;
   const unsigned long long tend = __builtin_amdgcn_s_memrealtime();

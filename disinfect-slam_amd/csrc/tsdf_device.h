@@ -75,6 +75,12 @@ struct FrameParams {
   int tail;                  // what the last workgroup of a frame kernel does (kTail*)
   int slot_cap;              // kTailPack: records the exchange slot holds
   struct ShardRec* slot;     // kTailPack: this shard's exchange slot (keys / carve candidates)
+  int pack_pixels;           // the ingest writes the pixel records (one volume); else k_integrate
+                             // gathers the raw frame below (a shard: no whole-frame pass)
+  const float* depth;        // the frame (device pointers)
+  const uint8_t* rgb;
+  const float* ht;           // NULL: ones (tsdf_module.cc:29-33)
+  const float* lt;
 };
 // the last-arriving workgroup of k_ingest_dda / k_integrate: resolve (allocation / carving) or, in a
 // shard's frame with an exchange after the kernel, pack the keys / candidates into the slot
@@ -496,5 +502,15 @@ __device__ __forceinline__ f3 pixel_ray(const FrameParams& P, int x, int y) {
   pc.z = 1.0f;
   return pc;
 }
+// the per-pixel terms of tsdf_integrate_kernel's update (voxel_tsdf.cu:174-201), computed once per
+// pixel into the pixel records (one volume) or per voxel from the raw frame (a shard): the same
+// operations either way, so the results are identical
+//   w_new = (1 - d / max_depth) * 4
+__device__ __forceinline__ float pixel_w_new(const FrameParams& P, float d) {
+  return (1.0f - quot_const(d, P.max_depth, P.inv_max_depth)) * 4.0f;
+}
+//   base-2 log-odds of the pixel's ht / lt; the hardware log2 (1 ulp) is far inside the 1e-4 prob
+//   tolerance and still gives exactly 0 when ht == lt
+__device__ __forceinline__ float pixel_logodds(float h, float l) { return __log2f(h) - __log2f(l); }
 
 }  // namespace tsdf

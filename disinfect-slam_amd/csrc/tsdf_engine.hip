@@ -210,6 +210,11 @@ FrameParams make_params(const tsdf_engine* e, const tsdf_intrinsics* K, int W, i
   P.tail = kTailResolve;
   P.slot_cap = 0;
   P.slot = nullptr;
+  P.pack_pixels = 1;
+  P.depth = nullptr;
+  P.rgb = nullptr;
+  P.ht = nullptr;
+  P.lt = nullptr;
   return P;
 }
 
@@ -423,7 +428,10 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.pend, kNewKeyCap);
   {  // one resident wave of k_integrate workgroups: no second-round stragglers
     int per_cu = 0, ncu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate_t<false>, kIntegrateThreads, 0) != hipSuccess ||
+    // (a shard's raw-frame variant is sized by its own occupancy)
+    const void* kfn = cfg.shard_count > 1 ? reinterpret_cast<const void*>(k_integrate_t<false, true>)
+                                          : reinterpret_cast<const void*>(k_integrate_t<false, false>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kIntegrateThreads, 0) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
       return fail(TSDF_ERR_HIP);
     if (const char* v = std::getenv("TSDF_INTEGRATE_WG_PER_CU")) per_cu = std::min(per_cu, std::atoi(v));  // tuning
@@ -524,12 +532,21 @@ int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, 
     return TSDF_ERR_INVALID_ARG;
   }
   *P = make_params(e, K, W, H, pose, max_depth);
-  const int tiles_x = (W + 15) / 16, tiles_y = (H + 15) / 16, tiles = tiles_x * tiles_y;
+  P->depth = depth;
+  P->rgb = rgb;
+  P->ht = ht;
+  P->lt = lt;
+  // a shard's k_integrate reads the raw frame: no whole-frame pixel pass in its ingest
+  P->pack_pixels = e->cfg.shard_count > 1 ? 0 : 1;
+  const int tiles_x = (W + 15) / 16, tiles_y = (H + 15) / 16;
+  P->tile_lo = 0;
+  P->tile_hi = tiles_x * tiles_y;
   if (slice_count > 1) {  // contiguous bands of tile rows
     const int rows = (tiles_y + slice_count - 1) / slice_count;
     P->tile_lo = std::min(tiles_y, slice_index * rows) * tiles_x;
     P->tile_hi = std::min(tiles_y, (slice_index + 1) * rows) * tiles_x;
   }
+  const int tiles = P->tile_hi - P->tile_lo;  // the launch covers the DDA's tiles only
   if (keys_out) {  // the last workgroup packs the keys for the exchange instead of resolving them
     P->tail = kTailPack;
     P->slot = reinterpret_cast<ShardRec*>(keys_out);
@@ -573,14 +590,15 @@ int frame_update(tsdf_engine* e, FrameParams P, std::array<hipEvent_t, 5>* ev, v
   P.slot = reinterpret_cast<ShardRec*>(cands_out);
   P.slot_cap = cand_cap;
   // ---- update (voxel_tsdf.cu:474-481) + space carving (:483-488) ----
+  auto kfn = P.pack_pixels ? k_integrate_t<false, false> : k_integrate_t<false, true>;
   if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
     // the two events are bound to the kernel's own dispatch packet (its begin / end timestamps,
     // the interval rocprofv3's kernel trace reports): no marker packets enter the stream
-    hipExtLaunchKernelGGL(k_integrate_t<false>, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
+    hipExtLaunchKernelGGL(kfn, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
                           (*ev)[2], (*ev)[3], 0, e->D, P, (const FrameArgs*)nullptr);
   } else {
     if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
-    hipLaunchKernelGGL((k_integrate_t<false>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
+    hipLaunchKernelGGL(kfn, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
                        e->D, P, (const FrameArgs*)nullptr);
     if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
   }
@@ -860,7 +878,7 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
       hipLaunchKernelGGL(k_ingest_dda_g<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
     else
       hipLaunchKernelGGL(k_ingest_dda_g<2048>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
-    hipLaunchKernelGGL((k_integrate_t<true>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, g->cap,
+    hipLaunchKernelGGL((k_integrate_t<true, false>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, g->cap,
                        e->D, FrameParams{}, A);
     if (render_width) {
       hipLaunchKernelGGL(k_view_grid_g, dim3(kOccWords / 256), dim3(256), 0, g->cap, e->D, A);

@@ -129,7 +129,10 @@ __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FramePa
 // camera from the FrameArgs block the graph's first node uploads.
 // The visible blocks are the sweep's band lists (blocks that existed before the frame) followed by
 // the blocks k_resolve_alloc created (D.fresh_vis, flagged fresh).
-template <bool Graph>
+// Raw: a shard's frame -- the pixel terms come from the raw frame (depth, rgb, ht, lt gathers) and
+// are computed per voxel with the ingest's operations (pixel_w_new, pixel_logodds, the range of
+// pixel_ray), instead of from pixel records packed for the whole frame.
+template <bool Graph, bool Raw>
 __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_integrate_t(
     EngineDev D, FrameParams Pv, const FrameArgs* __restrict__ A) {
   const FrameParams P = Graph ? A->P : Pv;
@@ -265,8 +268,15 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
           // unconditional gathers at a clamped index (pixel 0 when out of the image): no exec-
           // masked region around the loads, so all 8 stay in flight until pass 2
           const int img = inb[j] ? vv[e] * P.W + uu[e] : 0;
-          px[j] = D.pixA[img];
-          lg[j] = D.pixB[img];
+          if (Raw) {  // x: depth, y: pixel x, z: pixel y, w: rgb (range / w_new computed in pass 2)
+            const uint32_t c = (uint32_t)P.rgb[3 * img] | ((uint32_t)P.rgb[3 * img + 1] << 8) |
+                               ((uint32_t)P.rgb[3 * img + 2] << 16);
+            px[j] = make_float4(P.depth[img], __int_as_float(uu[e]), __int_as_float(vv[e]), __uint_as_float(c));
+            lg[j] = P.ht ? pixel_logodds(P.ht[img], P.lt[img]) : 0.0f;
+          } else {
+            px[j] = D.pixA[img];
+            lg[j] = D.pixB[img];
+          }
 #endif
         }
       }
@@ -276,8 +286,17 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const int j0 = 2 * k, j1 = 2 * k + 1;
-        const v2f d = v2(px[j0].x, px[j1].x), rng = v2(px[j0].y, px[j1].y);
-        const v2f w_new = v2(px[j0].z, px[j1].z);
+        const v2f d = v2(px[j0].x, px[j1].x);
+        v2f rng, w_new;
+        if (Raw) {  // the ingest's per-pixel terms (identical operations)
+          const f3 r0 = pixel_ray(P, __float_as_int(px[j0].y), __float_as_int(px[j0].z));
+          const f3 r1 = pixel_ray(P, __float_as_int(px[j1].y), __float_as_int(px[j1].z));
+          rng = v2(sqrtf(dot3(r0, r0)), sqrtf(dot3(r1, r1)));
+          w_new = v2(pixel_w_new(P, d.x), pixel_w_new(P, d.y));
+        } else {
+          rng = v2(px[j0].y, px[j1].y);
+          w_new = v2(px[j0].z, px[j1].z);
+        }
         const uint32_t n0 = __float_as_uint(px[j0].w), n1 = __float_as_uint(px[j1].w);
         const v2f sdf = rng * (d - hzs[k]);
         const bool a0 = inb[j0] && !(d.x == 0 || d.x > P.max_depth) && sdf.x > neg_trunc;
@@ -391,8 +410,10 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
   const bool drain = (wave == 0 && nc > 0) || (s_ovf && (wave & 1) == 0);
   if (arrive_last(D.arrive + kArrIntegrate, wg_upd, &s_last, drain)) integrate_tail(D, P, L);
 }
-template __global__ void k_integrate_t<false>(EngineDev, FrameParams, const FrameArgs*);
-template __global__ void k_integrate_t<true>(EngineDev, FrameParams, const FrameArgs*);
+template __global__ void k_integrate_t<false, false>(EngineDev, FrameParams, const FrameArgs*);
+template __global__ void k_integrate_t<true, false>(EngineDev, FrameParams, const FrameArgs*);
+template __global__ void k_integrate_t<false, true>(EngineDev, FrameParams, const FrameArgs*);
+template __global__ void k_integrate_t<true, true>(EngineDev, FrameParams, const FrameArgs*);
 
 // ---------------------------------------------------------------------------------------------
 // k_resolve_delete: the carving resolver (tsdf_resolve.h) as its own one-workgroup launch -- a

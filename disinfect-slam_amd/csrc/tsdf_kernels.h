@@ -118,7 +118,7 @@ __global__ void k_ingest_dda(EngineDev D, FrameParams P, const float* depth, con
 // keys_in: optional inbox of nshard key slots merged into the new-key set first.
 __global__ void k_resolve_alloc(EngineDev D, FrameParams P, uint32_t range, int frame_mode,
                                 const ShardRec* keys_in, int cap, int nshard);
-template <bool Graph>
+template <bool Graph, bool Raw>
 __global__ void k_integrate_t(EngineDev D, FrameParams P, const FrameArgs* A);
 // graph-captured forms of the frame kernels: identical bodies, arguments from FrameArgs
 template <int TS>
