@@ -78,6 +78,10 @@ def parse():
                    help="sharded modes: carve-candidate records per rank per frame (0 = 16384 / G)")
     p.add_argument("--cpu-frames", type=int, default=-1, help="oracle sample size (-1 = auto)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--broadcast-frames", action="store_true",
+                   help="sharded modes: rank 0 broadcasts every frame to the other ranks inside the timed "
+                        "loop (one camera feeding the node); otherwise each rank holds the stream and the "
+                        "broadcast is timed beside the line")
     p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                    help="process-group backend for N > 1: nccl (RCCL over xGMI, one GPU per rank) or gloo "
                         "(a rehearsal of the multi-rank code path; ranks may share a GPU, exchanges staged "
@@ -137,11 +141,14 @@ class Run:
                 self.replica = tsdf_amd.Engine(a.voxel, a.trunc, max_width=W, max_height=H,
                                                num_block_bits=a.block_bits, device=torch.cuda.current_device(),
                                                stream=self.stream)
+        self.sgraph = None
         if a.graph:
-            if self.sharded:
-                raise SystemExit("--graph takes a single volume per rank (streams mode or N=1)")
-            rw, rh = (W, H) if a.loop == "c5" else (0, 0)
-            self.graph = self.eng.frame_graph(W, H, rw, rh)
+            if self.sharded:  # a shard's frame as three captured segments around the exchanges
+                split = mode == "routed"
+                self.sgraph = self.eng.shard_frame_graph(W, H, rank if split else 0, world if split else 1)
+            else:
+                rw, rh = (W, H) if a.loop == "c5" else (0, 0)
+                self.graph = self.eng.frame_graph(W, H, rw, rh)
 
     def step(self, i):
         from tsdf_amd import dist as tdist
@@ -153,8 +160,12 @@ class Run:
             self.graph.frame(fr["rgb"][i], fr["depth"][i], ht, lt, K, pose, a.max_depth,
                              K if c5 else None, pose if c5 else None, self.rgba, self.normal)
         elif self.sharded:
+            if a.broadcast_frames:  # the camera's frame reaches every rank from rank 0 (in the timed region)
+                for t in (fr["rgb"][i], fr["depth"][i], ht, lt):
+                    if t is not None:
+                        self.dist.broadcast(t, src=0)
             tdist.integrate_sharded(self.eng, self.bufs, fr["rgb"][i], fr["depth"][i], ht, lt, K, pose,
-                                    a.max_depth, split=self.mode == "routed")
+                                    a.max_depth, split=self.mode == "routed", graph=self.sgraph)
             if c5:
                 tdist.render_sharded(self.eng, self.replica, K, a.width, a.height, pose, a.max_depth,
                                      rgba=self.rgba, normal=self.normal)
@@ -201,6 +212,8 @@ class Run:
     def close(self):
         if self.graph is not None:
             self.graph.close()
+        if self.sgraph is not None:
+            self.sgraph.close()
         if self.replica is not None:
             self.replica.close()
         self.eng.close()
@@ -286,6 +299,8 @@ def main():
     nframes = a.warmup + a.steps
     if a.shard:
         return rehearsal(a, cam, K, dev)
+    if a.broadcast_frames and a.backend == "gloo":
+        raise SystemExit("--broadcast-frames broadcasts device frames (RCCL); gloo is host-only")
     mode = a.mode if world > 1 else "single"
 
     def stream_frames(m):
@@ -320,6 +335,13 @@ def main():
     frame_frac_rw = (b_read + b_write) * steps_per_s / (world * HBM_PEAK_GBS * 1e9)
     mesh_tris = run.mesh_tris[-1] if run.mesh_tris else None
     host_enq = run.host_enqueue_ms
+    exch = None
+    if run.sharded:  # bytes this rank moved per frame (rank 0's view)
+        ks, cs = run.bufs.keys_out.numel(), run.bufs.cands_out.numel()
+        exch = {"key_slot_bytes_allgathered": ks * world if mode == "routed" else 0,
+                "cand_slot_bytes_allgathered": cs * world,
+                "frames_broadcast_in_timed_loop": bool(a.broadcast_frames)}
+        exch.update({k: v for k, v in tdist.last_exchange.items()})
     run.close()
     del frames
 
@@ -336,6 +358,9 @@ def main():
                      "what": "each rank integrates its own camera stream into its own volume (multi-camera "
                              "rig; no data-path collective); value = all ranks' frames / max rank time"}
 
+    bcast = None
+    if world > 1 and mode in ("routed", "sharded"):
+        bcast = frame_broadcast_ms(a, dist, None, dev)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         fr_host = synth.render_torch(cam, list(range(0, min(nframes, 80))), device=dev)
@@ -411,11 +436,41 @@ def main():
         }
         if world > 1:
             out["frames_per_s_per_stream"] = round(fps_stream, 2)
+        if bcast is not None:
+            out["frame_broadcast_ms"] = bcast
+        if exch:
+            out["exchange_per_rank"] = exch
         if secondary:
             out["secondary"] = secondary
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def frame_broadcast_ms(a, dist, _unused, dev, reps=20):
+    """Time of rank 0 broadcasting one frame (rgb u8 + depth / ht / lt f32) to every rank -- what a
+    single camera feeding an N-GPU sharded volume adds per frame (reported beside the line unless
+    --broadcast-frames puts it in the timed loop)."""
+    import torch
+    W, H = a.width, a.height
+    bufs = [torch.zeros((H, W, 3), dtype=torch.uint8, device=dev)] + \
+           [torch.zeros((H, W), dtype=torch.float32, device=dev) for _ in range(1 if a.depth_only else 3)]
+    if a.backend == "gloo":
+        bufs = [b.cpu() for b in bufs]
+    for b in bufs:
+        dist.broadcast(b, src=0)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for b in bufs:
+            dist.broadcast(b, src=0)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    from tsdf_amd import dist as tdist
+    return {"ms_per_frame": round(tdist.max_over_ranks(el, device=dev) / reps * 1e3, 4),
+            "bytes_per_frame": int(sum(b.numel() * b.element_size() for b in bufs)),
+            "backend": a.backend}
 
 
 def rehearsal(a, cam, K, dev):
@@ -434,7 +489,8 @@ def rehearsal(a, cam, K, dev):
     grp = tsdf_amd.ShardGroup(G, a.voxel, a.trunc, max_width=a.width, max_height=a.height,
                               num_block_bits=a.block_bits, device=torch.cuda.current_device(),
                               key_cap=a.key_cap or max(1024, 32768 // G),
-                              cand_cap=a.cand_cap or max(1024, 16384 // G), split=a.mode != "sharded")
+                              cand_cap=a.cand_cap or max(1024, 16384 // G), split=a.mode != "sharded",
+                              graph=(a.width, a.height) if a.graph else None)
 
     def step(i):
         ht = None if a.depth_only else fr["ht"][i]

@@ -468,9 +468,9 @@ __global__ void k_import_keys(EngineDev D, const uint8_t* __restrict__ recs, int
 // whole frame builds; the senders probed the same index, so no probe is repeated), and the
 // hash-level test / import path (frame_mode 0).
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kRT) void k_resolve_alloc(EngineDev D, FrameParams P, uint32_t range,
-                                                       int frame_mode, const ShardRec* __restrict__ keys_in,
-                                                       int cap, int nshard) {
+__device__ __forceinline__ void resolve_alloc_merged(EngineDev D, const FrameParams& P, uint32_t range,
+                                                     int frame_mode, const ShardRec* __restrict__ keys_in,
+                                                     int cap, int nshard) {
   __shared__ AllocLdsT<kIngestRB> L;
   if (keys_in) {
     for (int s = 0; s < nshard; ++s) {
@@ -485,6 +485,15 @@ __global__ __launch_bounds__(kRT) void k_resolve_alloc(EngineDev D, FrameParams 
     __syncthreads();
   }
   resolve_alloc_wg(D, P, range, frame_mode, L);
+}
+__global__ __launch_bounds__(kRT) void k_resolve_alloc(EngineDev D, FrameParams P, uint32_t range,
+                                                       int frame_mode, const ShardRec* __restrict__ keys_in,
+                                                       int cap, int nshard) {
+  resolve_alloc_merged(D, P, range, frame_mode, keys_in, cap, nshard);
+}
+__global__ __launch_bounds__(kRT) void k_resolve_alloc_g(EngineDev D, const FrameArgs* __restrict__ A) {
+  const FrameParams P = A->P;
+  resolve_alloc_merged(D, P, A->range, 1, A->keys_in, A->key_cap, A->nshard);
 }
 
 // AquireBlock's initialisation (voxel_mem.cu:43-51) for the hash-level test path

@@ -81,6 +81,7 @@ struct FrameParams {
   const uint8_t* rgb;
   const float* ht;           // NULL: ones (tsdf_module.cc:29-33)
   const float* lt;
+  int row0, nrows;           // raycast: the rows [row0, row0 + nrows) of the W x H camera it renders
 };
 // the last-arriving workgroup of k_ingest_dda / k_integrate: resolve (allocation / carving) or, in a
 // shard's frame with an exchange after the kernel, pack the keys / candidates into the slot

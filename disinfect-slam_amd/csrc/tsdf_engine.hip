@@ -112,6 +112,13 @@ struct tsdf_engine {
   int32_t* q_count = nullptr;
   float4* q_out = nullptr;
   int64_t q_out_cap = 0;
+  // grouped selections (render bands / halo destinations): per group a bitmap, its per-workgroup
+  // counts, the emitted list and its count
+  unsigned long long* g_visbits = nullptr;
+  int32_t* g_wgcnt = nullptr;
+  VisRec* g_sel = nullptr;
+  int32_t* g_count = nullptr;
+  int g_cap = 0;  // groups
   // mesh extraction scratch
   int32_t* m_counts = nullptr;
   int32_t* m_offsets = nullptr;
@@ -161,7 +168,7 @@ void free_all(tsdf_engine* e) {
                   e->fe_rgb, e->fe_depth, e->fe_mask, e->fe_out_rgb, e->fe_out_depth,
                   D.vis,     D.band,    D.cand,     D.arrive, D.fresh_vis, D.pend, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
-                  e->vg_cell, e->vg_flags, e->vg_bits,
+                  e->vg_cell, e->vg_flags, e->vg_bits, e->g_visbits, e->g_wgcnt, e->g_sel, e->g_count,
                   e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
                   e->t_i32,  e->t_u32,   e->t_f0,    e->t_f1,   e->t_s4};
   for (void* p : ptrs)
@@ -211,6 +218,8 @@ FrameParams make_params(const tsdf_engine* e, const tsdf_intrinsics* K, int W, i
   P.slot_cap = 0;
   P.slot = nullptr;
   P.pack_pixels = 1;
+  P.row0 = 0;
+  P.nrows = H;
   P.depth = nullptr;
   P.rgb = nullptr;
   P.ht = nullptr;
@@ -802,13 +811,17 @@ int view_grid_for(tsdf_engine* e, const FrameParams& P, float step_size, int lds
 // ---------------------------------------------------------------------------------------------
 struct tsdf_graph {
   static constexpr int kSlots = 4;
+  static constexpr int kSegs = 3;  // a shard's frame: begin / update / end around the exchanges
   tsdf_engine* e = nullptr;
   int W = 0, H = 0, RW = 0, RH = 0;
+  bool shard = false;     // a shard engine's graph (tsdf_graph_create_shard)
+  int slice_index = 0, slice_count = 1;
+  int cur = -1;           // a shard's frame in flight: its slot
   hipStream_t cap = nullptr;  // capture stream (the engine stream may be a legacy default stream)
   FrameArgs* d_args = nullptr;
   FrameArgs* h_args = nullptr;  // pinned
-  hipGraph_t graph[kSlots] = {};
-  hipGraphExec_t exec[kSlots] = {};
+  hipGraph_t graph[kSlots][kSegs] = {};
+  hipGraphExec_t exec[kSlots][kSegs] = {};
   hipEvent_t done[kSlots] = {};
   bool used[kSlots] = {};
   int next = 0;
@@ -818,8 +831,10 @@ namespace {
 
 void graph_free(tsdf_graph* g) {
   for (int i = 0; i < tsdf_graph::kSlots; ++i) {
-    if (g->exec[i]) (void)hipGraphExecDestroy(g->exec[i]);
-    if (g->graph[i]) (void)hipGraphDestroy(g->graph[i]);
+    for (int j = 0; j < tsdf_graph::kSegs; ++j) {
+      if (g->exec[i][j]) (void)hipGraphExecDestroy(g->exec[i][j]);
+      if (g->graph[i][j]) (void)hipGraphDestroy(g->graph[i][j]);
+    }
     if (g->done[i]) (void)hipEventDestroy(g->done[i]);
   }
   if (g->d_args) (void)hipFree(g->d_args);
@@ -833,8 +848,7 @@ void graph_free(tsdf_graph* g) {
 int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, int render_height,
                       tsdf_graph** out) {
   if (e && e->cfg.shard_count > 1) {
-    set_error("tsdf_graph_create: graph frames are for a whole volume (a shard integrates through "
-              "tsdf_integrate_shard_*)");
+    set_error("tsdf_graph_create: a shard's graph frames are tsdf_graph_create_shard / tsdf_graph_shard_*");
     return TSDF_ERR_INVALID_ARG;
   }
   if (!e || !out || width <= 0 || height <= 0 || width > e->cfg.max_width || height > e->cfg.max_height ||
@@ -886,11 +900,166 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
       hipLaunchKernelGGL(k_raycast_g, dim3((render_width + 15) / 16, (render_height + 15) / 16), dim3(256), 0,
                          g->cap, e->D, A);
     }
-    if ((err = hipStreamEndCapture(g->cap, &g->graph[k])) != hipSuccess) return fail(err, "hipStreamEndCapture");
-    if ((err = hipGraphInstantiate(&g->exec[k], g->graph[k], nullptr, nullptr, 0)) != hipSuccess)
+    if ((err = hipStreamEndCapture(g->cap, &g->graph[k][0])) != hipSuccess) return fail(err, "hipStreamEndCapture");
+    if ((err = hipGraphInstantiate(&g->exec[k][0], g->graph[k][0], nullptr, nullptr, 0)) != hipSuccess)
       return fail(err, "hipGraphInstantiate");
   }
   *out = g;
+  return TSDF_OK;
+}
+
+// A shard's graph frame: three captured segments per args slot -- (0) the args upload + k_ingest_dda_g
+// over the slice (its tail packs the slice's keys into keys_out; slice_count 1: it resolves them, no
+// key exchange), (1) k_resolve_alloc_g merging the key inbox (split DDA only) + the raw-frame
+// k_integrate (its tail packs the carve candidates into cands_out), (2) k_resolve_delete_g of the
+// candidate inbox. The caller's exchanges (RCCL all-gathers on the engine stream) run between them:
+// stream-ordered collectives of another library cannot be recorded into the engine's graphs.
+int tsdf_graph_create_shard(tsdf_engine* e, int width, int height, int slice_index, int slice_count,
+                            tsdf_graph** out) {
+  if (!e || !out || e->cfg.shard_count < 2 || width <= 0 || height <= 0 || width > e->cfg.max_width ||
+      height > e->cfg.max_height || slice_count < 1 || slice_index < 0 || slice_index >= slice_count) {
+    set_error("tsdf_graph_create_shard: invalid argument (a shard engine; the slice of its DDA)");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  auto* g = new tsdf_graph();
+  g->e = e;
+  g->W = width;
+  g->H = height;
+  g->shard = true;
+  g->slice_index = slice_index;
+  g->slice_count = slice_count;
+  auto fail = [&](hipError_t err, const char* what) {
+    set_error(what, err);
+    graph_free(g);
+    return TSDF_ERR_HIP;
+  };
+  hipError_t err;
+  if ((err = hipStreamCreateWithFlags(&g->cap, hipStreamNonBlocking)) != hipSuccess) return fail(err, "graph stream");
+  if ((err = hipMalloc(&g->d_args, sizeof(FrameArgs) * tsdf_graph::kSlots)) != hipSuccess) return fail(err, "graph args");
+  if ((err = hipHostMalloc(&g->h_args, sizeof(FrameArgs) * tsdf_graph::kSlots)) != hipSuccess)
+    return fail(err, "graph host args");
+  std::memset(g->h_args, 0, sizeof(FrameArgs) * tsdf_graph::kSlots);
+  const int tiles_x = (width + 15) / 16, tiles_y = (height + 15) / 16;
+  const int rows = (tiles_y + slice_count - 1) / slice_count;
+  const int tiles = (std::min(tiles_y, (slice_index + 1) * rows) - std::min(tiles_y, slice_index * rows)) * tiles_x;
+  if ((err = hipStreamSynchronize(e->stream)) != hipSuccess) return fail(err, "graph sync");
+  for (int k = 0; k < tsdf_graph::kSlots; ++k) {
+    const FrameArgs* A = g->d_args + k;
+    if ((err = hipEventCreateWithFlags(&g->done[k], hipEventDisableTiming)) != hipSuccess) return fail(err, "graph event");
+    for (int seg = 0; seg < tsdf_graph::kSegs; ++seg) {
+      if ((err = hipStreamBeginCapture(g->cap, hipStreamCaptureModeThreadLocal)) != hipSuccess)
+        return fail(err, "hipStreamBeginCapture");
+      if (seg == 0) {
+        hipLaunchKernelGGL(k_copy_words, dim3(1), dim3(64), 0, g->cap, reinterpret_cast<uint32_t*>(g->d_args + k),
+                           reinterpret_cast<const uint32_t*>(g->h_args + k), (int)(sizeof(FrameArgs) / 4));
+        if (e->maxs <= 3)
+          hipLaunchKernelGGL(k_ingest_dda_g<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
+        else
+          hipLaunchKernelGGL(k_ingest_dda_g<2048>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
+      } else if (seg == 1) {
+        if (slice_count > 1)
+          hipLaunchKernelGGL(k_resolve_alloc_g, dim3(1), dim3(kRT), 0, g->cap, e->D, A);
+        hipLaunchKernelGGL((k_integrate_t<true, true>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0,
+                           g->cap, e->D, FrameParams{}, A);
+      } else {
+        hipLaunchKernelGGL(k_resolve_delete_g, dim3(1), dim3(kRT), 0, g->cap, e->D, A);
+      }
+      if ((err = hipStreamEndCapture(g->cap, &g->graph[k][seg])) != hipSuccess) return fail(err, "hipStreamEndCapture");
+      if ((err = hipGraphInstantiate(&g->exec[k][seg], g->graph[k][seg], nullptr, nullptr, 0)) != hipSuccess)
+        return fail(err, "hipGraphInstantiate");
+    }
+  }
+  *out = g;
+  return TSDF_OK;
+}
+
+int tsdf_graph_shard_begin(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* K, const tsdf_pose* pose,
+                           float max_depth, void* keys_out, const void* keys_in, int32_t key_cap, void* cands_out,
+                           const void* cands_in, int32_t cand_cap) {
+  TraceRange trace_("tsdf_graph_shard_begin");
+  const bool split = g && g->slice_count > 1;
+  if (!g || !g->shard || !f || !K || !pose || f->mem_kind != TSDF_MEM_DEVICE || f->width != g->W ||
+      f->height != g->H || !f->depth || !f->rgb || (f->ht == nullptr) != (f->lt == nullptr) || !cands_out ||
+      !cands_in || cand_cap < 1 || (split && (!keys_out || !keys_in || key_cap < 1))) {
+    set_error("tsdf_graph_shard_begin: invalid argument (a shard graph; device frame of its size; the key "
+              "slot / inbox of a split DDA and the candidate slot / inbox)");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  tsdf_engine* e = g->e;
+  if (e->shard_phase != 0) {
+    set_error("tsdf_graph_shard_begin: a sharded frame is pending");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  const int k = g->next;
+  g->next = (k + 1) % tsdf_graph::kSlots;
+  if (g->used[k]) HIP_OK(hipEventSynchronize(g->done[k]));  // slot k's upload has run
+  FrameArgs& a = g->h_args[k];
+  a = FrameArgs{};
+  a.P = make_params(e, K, f->width, f->height, pose, max_depth);
+  FrameParams& P = a.P;
+  P.depth = f->depth;
+  P.rgb = f->rgb;
+  P.ht = f->ht;
+  P.lt = f->lt;
+  P.pack_pixels = 0;  // a shard's k_integrate reads the raw frame
+  const int tiles_x = (f->width + 15) / 16, tiles_y = (f->height + 15) / 16;
+  const int rows = (tiles_y + g->slice_count - 1) / g->slice_count;
+  P.tile_lo = std::min(tiles_y, g->slice_index * rows) * tiles_x;
+  P.tile_hi = std::min(tiles_y, (g->slice_index + 1) * rows) * tiles_x;
+  if (split) {
+    P.tail = kTailPack;
+    P.slot = reinterpret_cast<ShardRec*>(keys_out);
+    P.slot_cap = key_cap;
+  }
+  a.depth = f->depth;
+  a.rgb = f->rgb;
+  a.ht = f->ht;
+  a.lt = f->lt;
+  a.range = (uint32_t)((size_t)f->width * f->height * e->maxs);
+  a.tiles_x = tiles_x;
+  a.tiles = P.tile_hi - P.tile_lo;
+  a.keys_out = reinterpret_cast<ShardRec*>(keys_out);
+  a.keys_in = reinterpret_cast<const ShardRec*>(keys_in);
+  a.key_cap = key_cap;
+  a.cands_out = reinterpret_cast<ShardRec*>(cands_out);
+  a.cands_in = reinterpret_cast<const ShardRec*>(cands_in);
+  a.cand_cap = cand_cap;
+  a.nshard = e->cfg.shard_count;
+  HIP_OK(hipGraphLaunch(g->exec[k][0], e->stream));
+  // the host slot is read by segment 0's upload only (segments 1 and 2 read the device copy, which
+  // only segment 0 of the slot's next use rewrites, after them on the stream)
+  HIP_OK(hipEventRecord(g->done[k], e->stream));
+  g->used[k] = true;
+  g->cur = k;
+  e->shard_phase = 1;
+  return TSDF_OK;
+}
+
+int tsdf_graph_shard_update(tsdf_graph* g) {
+  TraceRange trace_("tsdf_graph_shard_update");
+  if (!g || !g->shard || g->cur < 0 || g->e->shard_phase != 1) {
+    set_error("tsdf_graph_shard_update: no graph frame begun");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(g->e->device));
+  HIP_OK(hipGraphLaunch(g->exec[g->cur][1], g->e->stream));
+  g->e->shard_phase = 2;
+  return TSDF_OK;
+}
+
+int tsdf_graph_shard_end(tsdf_graph* g) {
+  TraceRange trace_("tsdf_graph_shard_end");
+  if (!g || !g->shard || g->cur < 0 || g->e->shard_phase != 2) {
+    set_error("tsdf_graph_shard_end: no graph frame updated");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  tsdf_engine* e = g->e;
+  HIP_OK(hipSetDevice(e->device));
+  HIP_OK(hipGraphLaunch(g->exec[g->cur][2], e->stream));
+  g->cur = -1;
+  e->shard_phase = 0;
   return TSDF_OK;
 }
 
@@ -898,8 +1067,8 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
                      float max_depth, const tsdf_intrinsics* render_K, const tsdf_pose* render_pose,
                      uint8_t* rgba, uint8_t* normal) {
   TraceRange trace_("tsdf_graph_frame");
-  if (!g || !f || !K || !pose || f->mem_kind != TSDF_MEM_DEVICE || f->width != g->W || f->height != g->H ||
-      !f->depth || !f->rgb || (f->ht == nullptr) != (f->lt == nullptr) ||
+  if (!g || g->shard || !f || !K || !pose || f->mem_kind != TSDF_MEM_DEVICE || f->width != g->W ||
+      f->height != g->H || !f->depth || !f->rgb || (f->ht == nullptr) != (f->lt == nullptr) ||
       (g->RW && (!render_K || !render_pose))) {
     set_error("tsdf_graph_frame: invalid argument (device frame of the graph's size)");
     return TSDF_ERR_INVALID_ARG;
@@ -930,7 +1099,7 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
   a.range = (uint32_t)((size_t)f->width * f->height * e->maxs);
   a.tiles_x = (f->width + 15) / 16;
   a.tiles = a.tiles_x * ((f->height + 15) / 16);
-  HIP_OK(hipGraphLaunch(g->exec[k], e->stream));
+  HIP_OK(hipGraphLaunch(g->exec[k][0], e->stream));
   HIP_OK(hipEventRecord(g->done[k], e->stream));
   g->used[k] = true;
   return TSDF_OK;
@@ -1050,16 +1219,18 @@ int tsdf_feed_rgbd_frame(tsdf_engine* e, const uint8_t* rgb, const uint16_t* dep
 }
 
 
-int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const tsdf_pose* pose,
-                 float max_depth, uint8_t* rgba, uint8_t* normal, int mem_kind) {
-  TraceRange trace_("tsdf_raycast");
-  if (!e || !K || !pose || W <= 0 || H <= 0 || (int64_t)W * H > e->max_pixels ||
-      (mem_kind != TSDF_MEM_HOST && mem_kind != TSDF_MEM_DEVICE)) {
+namespace {
+int raycast_impl(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const tsdf_pose* pose,
+                 float max_depth, int row0, int nrows, uint8_t* rgba, uint8_t* normal, int mem_kind) {
+  if (!e || !K || !pose || W <= 0 || H <= 0 || (int64_t)W * H > e->max_pixels || row0 < 0 || nrows < 1 ||
+      row0 + nrows > H || (mem_kind != TSDF_MEM_HOST && mem_kind != TSDF_MEM_DEVICE)) {
     set_error("tsdf_raycast: invalid argument");
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  const FrameParams P = make_params(e, K, W, H, pose, max_depth);
+  FrameParams P = make_params(e, K, W, H, pose, max_depth);
+  P.row0 = row0;
+  P.nrows = nrows;
   uchar4* o1 = mem_kind == TSDF_MEM_DEVICE ? reinterpret_cast<uchar4*>(rgba) : (rgba ? e->rc_rgba : nullptr);
   uchar4* o2 = mem_kind == TSDF_MEM_DEVICE ? reinterpret_cast<uchar4*>(normal) : (normal ? e->rc_norm : nullptr);
   const float step = e->cfg.truncation / 2;
@@ -1073,16 +1244,29 @@ int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const t
     LAUNCH_OK("k_view_pack");
   }
   const size_t lds = V.n ? (size_t)V.nw * 4 : 0;
-  hipLaunchKernelGGL(k_raycast, dim3((W + 15) / 16, (H + 15) / 16), dim3(256), lds, e->stream, e->D,
+  hipLaunchKernelGGL(k_raycast, dim3((W + 15) / 16, (nrows + 15) / 16), dim3(256), lds, e->stream, e->D,
                      P, step, V, o1, o2);
   LAUNCH_OK("k_raycast");
   if (mem_kind == TSDF_MEM_HOST) {
-    const size_t bytes = (size_t)W * H * 4;
+    const size_t bytes = (size_t)W * nrows * 4;
     if (rgba) HIP_OK(hipMemcpyAsync(rgba, e->rc_rgba, bytes, hipMemcpyDeviceToHost, e->stream));
     if (normal) HIP_OK(hipMemcpyAsync(normal, e->rc_norm, bytes, hipMemcpyDeviceToHost, e->stream));
     HIP_OK(hipStreamSynchronize(e->stream));
   }
   return TSDF_OK;
+}
+}  // namespace
+
+int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const tsdf_pose* pose,
+                 float max_depth, uint8_t* rgba, uint8_t* normal, int mem_kind) {
+  TraceRange trace_("tsdf_raycast");
+  return raycast_impl(e, K, W, H, pose, max_depth, 0, H, rgba, normal, mem_kind);
+}
+
+int tsdf_raycast_rows(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const tsdf_pose* pose,
+                      float max_depth, int row0, int nrows, uint8_t* rgba, uint8_t* normal, int mem_kind) {
+  TraceRange trace_("tsdf_raycast_rows");
+  return raycast_impl(e, K, W, H, pose, max_depth, row0, nrows, rgba, normal, mem_kind);
 }
 
 int tsdf_query(tsdf_engine* e, const float* bounds, tsdf_voxel* out, int64_t capacity,
@@ -1168,6 +1352,31 @@ int tsdf_reset(tsdf_engine* e) {
   return TSDF_OK;
 }
 
+namespace {
+// the render cull of camera P (tsdf_render_blocks): the pixel-centre pyramid of rows [r0, r1) grown
+// by one lookup's reach, cut at the marched length
+RenderCull render_cull(const tsdf_engine* e, const FrameParams& P, int W, int r0, int r1) {
+  // ray_cast_kernel's march (voxel_tsdf.cu:248-250): max_step samples truncation / 2 apart
+  const double step = (double)(e->cfg.truncation / 2);
+  const double max_step = std::ceil((double)P.max_depth / step);
+  RenderCull C{};
+  C.a0 = P.icx;
+  C.a1 = (float)(W - 1) * P.ifx + P.icx;
+  C.b0 = (float)r0 * P.ify + P.icy;  // the rays' own y / z slopes (pixel_ray's float operations)
+  C.b1 = (float)(r1 - 1) * P.ify + P.icy;
+  C.na0 = std::sqrt(1.0f + C.a0 * C.a0);
+  C.na1 = std::sqrt(1.0f + C.a1 * C.a1);
+  C.nb0 = std::sqrt(1.0f + C.b0 * C.b0);
+  C.nb1 = std::sqrt(1.0f + C.b1 * C.b1);
+  // bounding sphere of the voxel centres (3.5 sqrt 3 voxels) + nearest-voxel rounding (sqrt 3 / 2)
+  // + the +-1 gradient neighbours = 7.93 voxels; 10 leaves room for float error
+  C.reach = 10.0f * e->cfg.voxel_size;
+  C.len = (float)(max_step * step) + C.reach;
+  return C;
+}
+
+}  // namespace
+
 int tsdf_render_blocks(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H,
                        const tsdf_pose* pose, float max_depth, void* out, int64_t capacity,
                        int64_t* count, int mem_kind) {
@@ -1179,22 +1388,7 @@ int tsdf_render_blocks(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H,
   }
   HIP_OK(hipSetDevice(e->device));
   const FrameParams P = make_params(e, K, W, H, pose, max_depth);
-  // ray_cast_kernel's march (voxel_tsdf.cu:248-250): max_step samples truncation / 2 apart
-  const double step = (double)(e->cfg.truncation / 2);
-  const double max_step = std::ceil((double)max_depth / step);
-  RenderCull C{};
-  C.a0 = P.icx;
-  C.a1 = (float)(W - 1) * P.ifx + P.icx;
-  C.b0 = P.icy;
-  C.b1 = (float)(H - 1) * P.ify + P.icy;
-  C.na0 = std::sqrt(1.0f + C.a0 * C.a0);
-  C.na1 = std::sqrt(1.0f + C.a1 * C.a1);
-  C.nb0 = std::sqrt(1.0f + C.b0 * C.b0);
-  C.nb1 = std::sqrt(1.0f + C.b1 * C.b1);
-  // bounding sphere of the voxel centres (3.5 sqrt 3 voxels) + nearest-voxel rounding (sqrt 3 / 2)
-  // + the +-1 gradient neighbours = 7.93 voxels; 10 leaves room for float error
-  C.reach = 10.0f * e->cfg.voxel_size;
-  C.len = (float)(max_step * step) + C.reach;
+  const RenderCull C = render_cull(e, P, W, 0, H);
   hipStream_t s = e->stream;
   hipLaunchKernelGGL(k_render_count, dim3(kOccWords / 256), dim3(256), 0, s, e->D, P, C);
   hipLaunchKernelGGL(k_vis_emit, dim3(kOccWords / 256), dim3(256), 0, s, e->D, e->q_sel,
@@ -1210,6 +1404,128 @@ int tsdf_render_blocks(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H,
     return TSDF_ERR_CAPACITY;
   }
   return pack_selected(e, nsel, out, mem_kind, "tsdf_render_blocks");
+}
+
+namespace {
+int ensure_groups(tsdf_engine* e, int n) {
+  if (n <= e->g_cap) return TSDF_OK;
+  (void)hipFree(e->g_visbits);
+  (void)hipFree(e->g_wgcnt);
+  (void)hipFree(e->g_sel);
+  (void)hipFree(e->g_count);
+  e->g_visbits = nullptr;
+  e->g_wgcnt = nullptr;
+  e->g_sel = nullptr;
+  e->g_count = nullptr;
+  e->g_cap = 0;
+  HIP_OK(dmalloc(&e->g_visbits, (size_t)n * kOccWords));
+  HIP_OK(dmalloc(&e->g_wgcnt, (size_t)n * (kOccWords / 256)));
+  HIP_OK(dmalloc(&e->g_sel, (size_t)n * e->D.nblocks));
+  HIP_OK(dmalloc(&e->g_count, (size_t)n));
+  e->g_cap = n;
+  return TSDF_OK;
+}
+
+// the groups of S: selection, per-group lists (entry order) and their counts (one host round trip);
+// then, when out != NULL, the records group by group (TSDF_BLOCK_RECORD_BYTES each) into out
+int group_records(tsdf_engine* e, const FrameParams& P, const GroupSel& S, void* out, int64_t capacity,
+                  int64_t* counts, int mem_kind, const char* what) {
+  int rc = ensure_groups(e, S.ngroups);
+  if (rc) return rc;
+  hipStream_t s = e->stream;
+  hipLaunchKernelGGL(k_group_count, dim3(kOccWords / 256), dim3(256), 0, s, e->D, P, S, e->g_visbits,
+                     e->g_wgcnt);
+  for (int g = 0; g < S.ngroups; ++g) {
+    EngineDev Dg = e->D;
+    Dg.visbits = e->g_visbits + (size_t)g * kOccWords;
+    Dg.wgcnt = e->g_wgcnt + (size_t)g * (kOccWords / 256);
+    hipLaunchKernelGGL(k_vis_emit, dim3(kOccWords / 256), dim3(256), 0, s, Dg, e->g_sel + (size_t)g * e->D.nblocks,
+                       e->g_count + g);
+  }
+  LAUNCH_OK(what);
+  std::vector<int32_t> n(S.ngroups);
+  HIP_OK(hipMemcpyAsync(n.data(), e->g_count, sizeof(int32_t) * S.ngroups, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  int64_t total = 0;
+  for (int g = 0; g < S.ngroups; ++g) {
+    counts[g] = n[g];
+    total += n[g];
+  }
+  if (!out || total == 0) return TSDF_OK;
+  if (capacity < total) {
+    set_error("grouped block records: capacity too small");
+    return TSDF_ERR_CAPACITY;
+  }
+  uint8_t* dst = reinterpret_cast<uint8_t*>(out);
+  uint8_t* tmp = nullptr;
+  if (mem_kind == TSDF_MEM_HOST) {
+    HIP_OK(dmalloc(&tmp, (size_t)total * kBlockRecBytes));
+    dst = tmp;
+  }
+  int64_t off = 0;
+  for (int g = 0; g < S.ngroups; ++g) {
+    if (n[g])
+      hipLaunchKernelGGL(k_render_pack, dim3(n[g]), dim3(256), 0, s, e->D, e->g_sel + (size_t)g * e->D.nblocks,
+                         dst + (size_t)off * kBlockRecBytes);
+    off += n[g];
+  }
+  hipError_t err = hipGetLastError();
+  if (err == hipSuccess && tmp) err = hipMemcpyAsync(out, tmp, (size_t)total * kBlockRecBytes, hipMemcpyDeviceToHost, s);
+  if (err == hipSuccess) err = hipStreamSynchronize(s);
+  if (tmp) (void)hipFree(tmp);
+  if (err != hipSuccess) {
+    set_error(what, err);
+    return TSDF_ERR_HIP;
+  }
+  return TSDF_OK;
+}
+}  // namespace
+
+int tsdf_render_bands(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const tsdf_pose* pose,
+                      float max_depth, int nbands, const int32_t* rows, void* out, int64_t capacity,
+                      int64_t* counts, int mem_kind) {
+  TraceRange trace_("tsdf_render_bands");
+  bool ok = e && K && pose && counts && rows && W > 0 && H > 0 && max_depth > 0 && nbands >= 1 &&
+            nbands <= kMaxGroups && (mem_kind == TSDF_MEM_HOST || mem_kind == TSDF_MEM_DEVICE);
+  for (int b = 0; ok && b < nbands; ++b) ok = rows[b] >= 0 && rows[b] < rows[b + 1] && rows[b + 1] <= H;
+  if (!ok) {
+    set_error("tsdf_render_bands: invalid argument (1..64 bands of increasing rows within the image)");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  const FrameParams P = make_params(e, K, W, H, pose, max_depth);
+  GroupSel S{};
+  S.mode = kGroupBands;
+  S.ngroups = nbands;
+  S.cull = render_cull(e, P, W, 0, H);
+  for (int b = 0; b < nbands; ++b) {
+    const RenderCull C = render_cull(e, P, W, rows[b], rows[b + 1]);
+    S.b0[b] = C.b0;
+    S.b1[b] = C.b1;
+    S.nb0[b] = C.nb0;
+    S.nb1[b] = C.nb1;
+  }
+  return group_records(e, P, S, out, capacity, counts, mem_kind, "tsdf_render_bands");
+}
+
+int tsdf_pack_halo(tsdf_engine* e, void* out, int64_t capacity, int64_t* counts, int mem_kind) {
+  TraceRange trace_("tsdf_pack_halo");
+  if (!e || !counts || e->cfg.shard_count < 2 || (mem_kind != TSDF_MEM_HOST && mem_kind != TSDF_MEM_DEVICE)) {
+    set_error("tsdf_pack_halo: invalid argument (a shard engine)");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  if (e->shard_phase != 0) {
+    set_error("tsdf_pack_halo: a sharded frame is pending");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  FrameParams P{};
+  P.shard_index = e->cfg.shard_index;
+  P.shard_count = e->cfg.shard_count;
+  GroupSel S{};
+  S.mode = kGroupHalo;
+  S.ngroups = e->cfg.shard_count;
+  return group_records(e, P, S, out, capacity, counts, mem_kind, "tsdf_pack_halo");
 }
 
 int tsdf_pack_blocks(tsdf_engine* e, const float* bounds, void* out, int64_t capacity,
@@ -1315,10 +1631,11 @@ int tsdf_import_blocks(tsdf_engine* e, const void* records, int64_t n, int mem_k
   return done(TSDF_OK);
 }
 
-int tsdf_extract_mesh(tsdf_engine* e, const float* bounds, float missing_tsdf, int min_weight,
-                      float* triangles, int64_t capacity, int64_t* num_triangles, int mem_kind) {
-  TraceRange trace_("tsdf_extract_mesh");
-  if (!e || !num_triangles || (mem_kind != TSDF_MEM_HOST && mem_kind != TSDF_MEM_DEVICE)) {
+namespace {
+int extract_mesh_impl(tsdf_engine* e, const float* bounds, float missing_tsdf, int min_weight, int own_index,
+                      int own_count, float* triangles, int64_t capacity, int64_t* num_triangles, int mem_kind) {
+  if (!e || !num_triangles || (mem_kind != TSDF_MEM_HOST && mem_kind != TSDF_MEM_DEVICE) || own_count < 1 ||
+      own_count > kMaxShards || own_index < 0 || own_index >= own_count) {
     set_error("tsdf_extract_mesh: invalid argument");
     return TSDF_ERR_INVALID_ARG;
   }
@@ -1340,7 +1657,7 @@ int tsdf_extract_mesh(tsdf_engine* e, const float* bounds, float missing_tsdf, i
   HIP_OK(hipStreamSynchronize(s));
   *num_triangles = 0;
   if (nsel == 0) return TSDF_OK;
-  const MeshParams M{e->cfg.voxel_size, missing_tsdf, min_weight};
+  const MeshParams M{e->cfg.voxel_size, missing_tsdf, min_weight, own_index, own_count};
   hipLaunchKernelGGL(k_mesh<false>, dim3(nsel), dim3(256), 0, s, e->D, e->q_sel, M, e->m_counts,
                      (const int32_t*)nullptr, (float*)nullptr);
   hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, e->m_counts, nsel, e->m_offsets,
@@ -1374,6 +1691,22 @@ int tsdf_extract_mesh(tsdf_engine* e, const float* bounds, float missing_tsdf, i
                           hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
   return TSDF_OK;
+}
+}  // namespace
+
+int tsdf_extract_mesh(tsdf_engine* e, const float* bounds, float missing_tsdf, int min_weight,
+                      float* triangles, int64_t capacity, int64_t* num_triangles, int mem_kind) {
+  TraceRange trace_("tsdf_extract_mesh");
+  return extract_mesh_impl(e, bounds, missing_tsdf, min_weight, 0, 1, triangles, capacity, num_triangles,
+                           mem_kind);
+}
+
+int tsdf_extract_mesh_owned(tsdf_engine* e, const float* bounds, float missing_tsdf, int min_weight,
+                            int shard_index, int shard_count, float* triangles, int64_t capacity,
+                            int64_t* num_triangles, int mem_kind) {
+  TraceRange trace_("tsdf_extract_mesh_owned");
+  return extract_mesh_impl(e, bounds, missing_tsdf, min_weight, shard_index, shard_count, triangles, capacity,
+                           num_triangles, mem_kind);
 }
 
 int tsdf_get_stats(tsdf_engine* e, tsdf_stats* o, int clear_status) {

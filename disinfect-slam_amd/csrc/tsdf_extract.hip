@@ -269,11 +269,14 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
   const int g = wg & 7, tile = g * (nwg >> 3) + min(g, nwg & 7) + (wg >> 3);
   // each wave an 8x8 quadrant of the tile: a tighter ray bundle than 16x4 rows, whose lanes leave
   // their regions at closer steps (101.3 vs 103.8 us at C5)
+  // rows [P.row0, P.row0 + P.nrows) of the W x H camera (a band of a sharded render, else all);
+  // the outputs hold the band's rows only
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int x = (tile % gx) * 16 + (wv & 1) * 8 + (ln & 7);
-  const int y = (tile / gx) * 16 + (wv >> 1) * 8 + (ln >> 3);
-  const bool valid = x < P.W && y < P.H;
-  const int idx = valid ? y * P.W + x : 0;
+  const int yb = (tile / gx) * 16 + (wv >> 1) * 8 + (ln >> 3);
+  const int y = P.row0 + yb;
+  const bool valid = x < P.W && yb < P.nrows && y < P.H;
+  const int idx = valid ? yb * P.W + x : 0;
   RayView R;
   R.cell = V.cell;
   R.bits = sbits;
@@ -455,6 +458,65 @@ __device__ __forceinline__ bool render_needs(const FrameParams& P, const RenderC
          C.a1 * c.z - c.x >= -C.reach * C.na1 && c.y - C.b0 * c.z >= -C.reach * C.nb0 &&
          C.b1 * c.z - c.y >= -C.reach * C.nb1 && dot3(c, c) <= C.len * C.len;
 }
+// ---------------------------------------------------------------------------------------------
+// Grouped selections of a shard's own blocks for the sharded extraction: one pass over
+// the occupancy bitmap sets, per group g, a selection bitmap visbits + g * kOccWords and its
+// per-workgroup counts wgcnt + g * (kOccWords / 256); k_vis_emit then lists each group in entry
+// order. A block may belong to several groups.
+//  kGroupBands: group b = image band b of the render camera -- the block can be read by a ray of
+//    the band's rows (render_needs against the band's sub-pyramid: the top / bottom planes of its
+//    first and last rows);
+//  kGroupHalo: group d = shard d != this one owns one of the block's 26 neighbours -- d's marching
+//    cubes of its own blocks read this block (cells reach one sample into every neighbour, and a
+//    cell's block is decided by which neighbours exist).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_group_count(EngineDev D, FrameParams P, GroupSel S,
+                                                     unsigned long long* __restrict__ visbits,
+                                                     int32_t* __restrict__ wgcnt) {
+  __shared__ int scratch[4][kMaxGroups];
+  const int w = blockIdx.x * 256 + threadIdx.x;
+  // this thread's word of every group's bitmap (thread-exclusive: plain read-modify-writes)
+  for (int g = 0; g < S.ngroups; ++g) visbits[(size_t)g * kOccWords + w] = 0ull;
+  unsigned long long occ = D.occ[w];
+  while (occ) {
+    const int b = __ffsll((long long)occ) - 1;
+    occ &= occ - 1;
+    const Ent en = load_ent(D.table, (uint32_t)(w * 64 + b));
+    unsigned long long groups = 0ull;
+    if (S.mode == kGroupBands) {
+      RenderCull C = S.cull;
+      for (int g = 0; g < S.ngroups; ++g) {
+        C.b0 = S.b0[g];
+        C.b1 = S.b1[g];
+        C.nb0 = S.nb0[g];
+        C.nb1 = S.nb1[g];
+        if (render_needs(P, C, en)) groups |= 1ull << g;
+      }
+    } else {
+      for (int n = 0; n < 27; ++n) {
+        if (n == 13) continue;
+        const int16_t nx = (int16_t)(en.x + n % 3 - 1), ny = (int16_t)(en.y + (n / 3) % 3 - 1),
+                      nz = (int16_t)(en.z + n / 9 - 1);
+        if (find_entry(D.table, nx, ny, nz) >= 0)
+          groups |= 1ull << brick_owner(nx, ny, nz, (uint32_t)P.shard_count);
+      }
+      groups &= ~(1ull << P.shard_index);
+    }
+    while (groups) {
+      const int g = __ffsll((long long)groups) - 1;
+      groups &= groups - 1;
+      visbits[(size_t)g * kOccWords + w] |= 1ull << b;
+    }
+  }
+  for (int g = 0; g < S.ngroups; ++g) {
+    const int c = wave_sum(__popcll(visbits[(size_t)g * kOccWords + w]));
+    if (lane_id() == 0) scratch[threadIdx.x >> 6][g] = c;
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g < S.ngroups; g += 256)
+    wgcnt[(size_t)g * (kOccWords / 256) + blockIdx.x] = scratch[0][g] + scratch[1][g] + scratch[2][g] + scratch[3][g];
+}
+
 // selection into D.visbits + per-workgroup counts; k_vis_emit then lists it in entry order
 __global__ __launch_bounds__(256) void k_render_count(EngineDev D, FrameParams P, RenderCull C) {
   __shared__ int scratch[4];

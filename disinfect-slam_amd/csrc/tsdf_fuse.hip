@@ -135,7 +135,14 @@ __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FramePa
 template <bool Graph, bool Raw>
 __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_integrate_t(
     EngineDev D, FrameParams Pv, const FrameArgs* __restrict__ A) {
-  const FrameParams P = Graph ? A->P : Pv;
+  FrameParams P = Graph ? A->P : Pv;
+  if (Graph && A->cands_out) {  // a shard's graph frame: the tail packs the carve candidates
+    P.tail = kTailPack;
+    P.slot = A->cands_out;
+    P.slot_cap = A->cand_cap;
+  } else if (Graph) {
+    P.tail = kTailResolve;
+  }
   __shared__ float s_min[4];
   __shared__ int s_upd[4];
   __shared__ int s_last;
@@ -421,10 +428,10 @@ template __global__ void k_integrate_t<true, true>(EngineDev, FrameParams, const
 // the candidate set of one volume -- so every shard's index takes the same deletes), and the
 // hash-level test path (direct: the keys in list order, one per round).
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kRT) void k_resolve_delete(EngineDev D, const VisRec* __restrict__ recs,
-                                                        const int32_t* __restrict__ count, int direct,
-                                                        const ShardRec* __restrict__ cands_in, int cap,
-                                                        int nshard) {
+__device__ __forceinline__ void resolve_delete_merged(EngineDev D, const VisRec* __restrict__ recs,
+                                                      const int32_t* __restrict__ count, int direct,
+                                                      const ShardRec* __restrict__ cands_in, int cap,
+                                                      int nshard) {
   __shared__ DeleteLds L;
   __shared__ int s_base[kMaxShards + 1];
   if (cands_in) {
@@ -470,6 +477,15 @@ __global__ __launch_bounds__(kRT) void k_resolve_delete(EngineDev D, const VisRe
   }
   resolve_delete_wg(D, recs, count, direct, L);
   if (!direct) frame_end(D);
+}
+__global__ __launch_bounds__(kRT) void k_resolve_delete(EngineDev D, const VisRec* __restrict__ recs,
+                                                        const int32_t* __restrict__ count, int direct,
+                                                        const ShardRec* __restrict__ cands_in, int cap,
+                                                        int nshard) {
+  resolve_delete_merged(D, recs, count, direct, cands_in, cap, nshard);
+}
+__global__ __launch_bounds__(kRT) void k_resolve_delete_g(EngineDev D, const FrameArgs* __restrict__ A) {
+  resolve_delete_merged(D, D.cand, &D.ctr->n_cand, 0, A->cands_in, A->cand_cap, A->nshard);
 }
 
 

@@ -100,6 +100,13 @@ struct FrameArgs {
   ViewGrid V;       // the raycast node's view grid (n == 0: hash lookups)
   uint32_t range;   // candidate order space W * H * maxs
   int tiles_x, tiles;
+  // a shard's graph frame (tsdf_graph_shard_*): the exchange slots of its three segments
+  ShardRec* keys_out;        // k_ingest_dda_g's tail packs the slice's keys here (P.tail / P.slot)
+  const ShardRec* keys_in;   // k_resolve_alloc_g merges the all-gathered key slots
+  int key_cap;
+  ShardRec* cands_out;       // k_integrate_t<true, .>'s tail packs the carve candidates here
+  const ShardRec* cands_in;  // k_resolve_delete_g merges the all-gathered candidate slots
+  int cand_cap, nshard;
 };
 
 __global__ void k_init_table(int4* table);
@@ -118,6 +125,9 @@ __global__ void k_ingest_dda(EngineDev D, FrameParams P, const float* depth, con
 // keys_in: optional inbox of nshard key slots merged into the new-key set first.
 __global__ void k_resolve_alloc(EngineDev D, FrameParams P, uint32_t range, int frame_mode,
                                 const ShardRec* keys_in, int cap, int nshard);
+// graph-captured forms of a shard's standalone resolvers (arguments from FrameArgs)
+__global__ void k_resolve_alloc_g(EngineDev D, const FrameArgs* A);
+__global__ void k_resolve_delete_g(EngineDev D, const FrameArgs* A);
 template <bool Graph, bool Raw>
 __global__ void k_integrate_t(EngineDev D, FrameParams P, const FrameArgs* A);
 // graph-captured forms of the frame kernels: identical bodies, arguments from FrameArgs
@@ -140,6 +150,8 @@ __global__ void k_shard_abort(EngineDev D);
 struct MeshParams {
   float voxel, missing;
   int min_weight;
+  int own_index, own_count;  // own_count > 1: only blocks whose brick owner is own_index emit (a
+                             // shard's part of a sharded mesh; the other selected blocks are its halo)
 };
 template <bool Emit>
 __global__ void k_mesh(EngineDev D, const VisRec* sel, MeshParams M, int32_t* counts,
@@ -166,6 +178,16 @@ struct RenderCull {
   float len;                 // marched ray length + reach (m)
 };
 __global__ void k_render_count(EngineDev D, FrameParams P, RenderCull C);
+// grouped selections (render bands / marching-cubes halo destinations), tsdf_extract.hip
+constexpr int kMaxGroups = 64;
+constexpr int kGroupBands = 0, kGroupHalo = 1;
+struct GroupSel {
+  int mode, ngroups;
+  RenderCull cull;                 // kGroupBands: the camera's pyramid (b0 / b1 per band below)
+  float b0[kMaxGroups], b1[kMaxGroups], nb0[kMaxGroups], nb1[kMaxGroups];
+};
+__global__ void k_group_count(EngineDev D, FrameParams P, GroupSel S, unsigned long long* visbits,
+                              int32_t* wgcnt);
 __global__ void k_render_pack(EngineDev D, const VisRec* sel, uint8_t* out);
 __global__ void k_import_keys(EngineDev D, const uint8_t* recs, int n);
 __global__ void k_import_payload(EngineDev D, const uint8_t* recs, int32_t* missing);

@@ -221,6 +221,55 @@ class FrameGraph:
         except Exception:
             pass
 
+class ShardFrameGraph:
+    """A shard engine's graph-captured sharded frame (tsdf_graph_create_shard): begin / update / end
+    as three graph launches around the caller's two exchanges. Device frames and device slots."""
+
+    def __init__(self, eng, width, height, slice_index=0, slice_count=1):
+        self._eng = eng
+        self.width, self.height = width, height
+        self.split = slice_count > 1
+        h = C.c_void_p()
+        _lib.check(_lib.load().tsdf_graph_create_shard(eng._h, width, height, slice_index, slice_count,
+                                                       C.byref(h)), "tsdf_graph_create_shard")
+        self._g = h
+
+    def begin(self, rgb, depth, ht, lt, K, cam_T_world, max_depth, keys_out, keys_in, key_cap, cands_out,
+              cands_in, cand_cap):
+        for a in (rgb, depth, ht, lt, keys_out, keys_in, cands_out, cands_in):
+            if a is not None and (not _is_torch_cuda(a) or not a.is_contiguous()):
+                raise ValueError("shard graph frames take contiguous device tensors")
+        H, W = int(depth.shape[0]), int(depth.shape[1])
+        fr = _lib.Frame(W, H, _ptr(rgb), _ptr(depth), _ptr(ht), _ptr(lt), TSDF_MEM_DEVICE)
+        Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        self._eng._wait_torch(depth, keys_out, cands_out)
+        _lib.check(_lib.load().tsdf_graph_shard_begin(
+            self._g, C.byref(fr), C.byref(Kc), C.byref(cam_T_world._c()), max_depth, _ptr(keys_out),
+            _ptr(keys_in), key_cap, _ptr(cands_out), _ptr(cands_in), cand_cap), "tsdf_graph_shard_begin")
+        self._eng._signal_torch(depth, keys_out)
+
+    def update(self, keys_in=None, cands_out=None):
+        self._eng._wait_torch(keys_in)
+        _lib.check(_lib.load().tsdf_graph_shard_update(self._g), "tsdf_graph_shard_update")
+        self._eng._signal_torch(cands_out)
+
+    def end(self, cands_in=None):
+        self._eng._wait_torch(cands_in)
+        _lib.check(_lib.load().tsdf_graph_shard_end(self._g), "tsdf_graph_shard_end")
+        self._eng._signal_torch(cands_in)
+
+    def close(self):
+        if getattr(self, "_g", None):
+            _lib.load().tsdf_graph_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Engine:
     """One MI355X TSDF volume (one GPU shard). Thin owner of a tsdf_engine* handle."""
 
@@ -343,6 +392,10 @@ class Engine:
         a render camera) as one hipGraph launch per frame."""
         return FrameGraph(self, width, height, render_width, render_height)
 
+    def shard_frame_graph(self, width: int, height: int, slice_index: int = 0, slice_count: int = 1):
+        """A shard's graph-captured sharded frame (tsdf_graph_create_shard)."""
+        return ShardFrameGraph(self, width, height, slice_index, slice_count)
+
     # ---- stream ordering with torch (ADVICE r1: device tensors on torch's current stream) ----
     def _torch_stream(self, tensors):
         """torch's current stream when it differs from the engine stream and a device tensor is
@@ -463,6 +516,57 @@ class Engine:
                                             _ptr(normal), TSDF_MEM_HOST), "tsdf_raycast")
         return rgba, normal
 
+    def raycast_rows(self, K, width, height, cam_T_world: SE3, max_depth: float, row0: int, nrows: int,
+                     rgba=None, normal=None):
+        """Rows [row0, row0 + nrows) of raycast(K, width, height, ...) (tsdf_raycast_rows): numpy
+        (nrows, width, 4) u8 images, or into the given device tensors."""
+        Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        if rgba is not None and _is_torch_cuda(rgba):
+            self._wait_torch(rgba, normal)
+            _lib.check(_lib.load().tsdf_raycast_rows(self._h, C.byref(Kc), width, height,
+                                                     C.byref(cam_T_world._c()), max_depth, row0, nrows,
+                                                     _ptr(rgba), _ptr(normal), TSDF_MEM_DEVICE), "tsdf_raycast_rows")
+            self._signal_torch(rgba, normal)
+            return rgba, normal
+        rgba = np.zeros((nrows, width, 4), np.uint8)
+        normal = np.zeros((nrows, width, 4), np.uint8)
+        _lib.check(_lib.load().tsdf_raycast_rows(self._h, C.byref(Kc), width, height, C.byref(cam_T_world._c()),
+                                                 max_depth, row0, nrows, _ptr(rgba), _ptr(normal), TSDF_MEM_HOST),
+                   "tsdf_raycast_rows")
+        return rgba, normal
+
+    def _grouped(self, fn, args, ngroups, device):
+        """Two-call grouped records (tsdf_render_bands / tsdf_pack_halo) -> (counts, records)."""
+        counts = np.zeros(ngroups, np.int64)
+        _lib.check(fn(*args, None, 0, _ptr(counts), TSDF_MEM_HOST), fn.__name__)
+        n = int(counts.sum())
+        if device:
+            import torch
+            out = torch.empty((n, BLOCK_RECORD_BYTES), dtype=torch.uint8, device=f"cuda:{self.device}")
+        else:
+            out = np.empty((n, BLOCK_RECORD_BYTES), np.uint8)
+        if n:
+            self._wait_torch(out)
+            _lib.check(fn(*args, _ptr(out), n, _ptr(counts), TSDF_MEM_DEVICE if device else TSDF_MEM_HOST),
+                       fn.__name__)
+            self._signal_torch(out)
+        return counts, out
+
+    def render_bands(self, K, width, height, cam_T_world: SE3, max_depth: float, rows, device=False):
+        """(counts per band, records grouped by band) of this shard's blocks the rays of rows
+        [rows[b], rows[b + 1]) can read (tsdf_render_bands)."""
+        Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        r = np.ascontiguousarray(rows, dtype=np.int32)
+        self._rows_keep = r
+        L = _lib.load()
+        return self._grouped(L.tsdf_render_bands, (self._h, C.byref(Kc), width, height, C.byref(cam_T_world._c()),
+                                                   max_depth, r.shape[0] - 1, _ptr(r)), r.shape[0] - 1, device)
+
+    def pack_halo(self, device=False):
+        """(counts per destination shard, records grouped by destination) of this shard's blocks that
+        other shards' marching cubes read (tsdf_pack_halo)."""
+        return self._grouped(_lib.load().tsdf_pack_halo, (self._h,), self.shard_count, device)
+
     def render_blocks(self, K, width, height, cam_T_world: SE3, max_depth: float, device=False):
         """Records (n, TSDF_BLOCK_RECORD_BYTES) uint8 of the blocks a raycast of this camera can read
         (tsdf_render_blocks): a numpy array, or a torch tensor on this engine's GPU when device."""
@@ -528,26 +632,27 @@ class Engine:
         _lib.check(_lib.load().tsdf_reset(self._h), "tsdf_reset")
 
     def extract_mesh(self, bounds=None, missing_tsdf: float = 0.99, min_weight: int = 0,
-                     out=None) -> np.ndarray:
+                     out=None, owner=None) -> np.ndarray:
         """Marching-cubes triangles (n, 3, 3) float32 of the selected blocks (tsdf_extract_mesh).
-        out: optional device tensor of >= 9 n floats to receive them on the GPU instead."""
+        out: optional device tensor of >= 9 n floats to receive them on the GPU instead.
+        owner: (shard_index, shard_count) -- only the blocks of that shard emit
+        (tsdf_extract_mesh_owned; the others are read as neighbours)."""
         L = _lib.load()
         b = None if bounds is None else np.ascontiguousarray(
             bounds.as_array() if isinstance(bounds, BoundingCube) else bounds, dtype=np.float32)
+        oi, oc = owner if owner is not None else (0, 1)
+        fn = lambda ptr, cap, n, kind: L.tsdf_extract_mesh_owned(self._h, _ptr(b), missing_tsdf, min_weight,
+                                                                 oi, oc, ptr, cap, C.byref(n), kind)
         n = C.c_int64()
-        _lib.check(L.tsdf_extract_mesh(self._h, _ptr(b), missing_tsdf, min_weight, None, 0,
-                                       C.byref(n), TSDF_MEM_HOST), "tsdf_extract_mesh")
+        _lib.check(fn(None, 0, n, TSDF_MEM_HOST), "tsdf_extract_mesh")
         if out is not None:
             self._wait_torch(out)
-            _lib.check(L.tsdf_extract_mesh(self._h, _ptr(b), missing_tsdf, min_weight, _ptr(out),
-                                           out.numel() // 9, C.byref(n), TSDF_MEM_DEVICE),
-                       "tsdf_extract_mesh")
+            _lib.check(fn(_ptr(out), out.numel() // 9, n, TSDF_MEM_DEVICE), "tsdf_extract_mesh")
             self._signal_torch(out)
             return out[:9 * n.value].view(-1, 3, 3)
         tris = np.zeros((n.value, 3, 3), np.float32)
         if n.value:
-            _lib.check(L.tsdf_extract_mesh(self._h, _ptr(b), missing_tsdf, min_weight, _ptr(tris),
-                                           n.value, C.byref(n), TSDF_MEM_HOST), "tsdf_extract_mesh")
+            _lib.check(fn(_ptr(tris), n.value, n, TSDF_MEM_HOST), "tsdf_extract_mesh")
         return tris
 
     def query(self, bounds=None) -> np.ndarray:
@@ -673,9 +778,10 @@ class ShardGroup:
 
     def __init__(self, shard_count: int, voxel_size=0.005, truncation=0.03, max_width=1920,
                  max_height=1080, num_block_bits=18, device=0, key_cap=16384, cand_cap=16384,
-                 split=True, stream=None):
+                 split=True, stream=None, graph=None):
         import torch
         self.G = shard_count
+        self.graph_size = graph  # (width, height): frames through each shard's captured graph
         self.split = split
         self.key_cap, self.cand_cap = key_cap, cand_cap
         # all shards on ONE stream (torch's current one unless given), so the phases and the slot
@@ -689,6 +795,12 @@ class ShardGroup:
         self._cands = torch.zeros((shard_count, Engine.shard_slot_bytes(cand_cap)), dtype=torch.uint8, device=dev)
         self.keys_exchanged = 0   # key records that went through the exchange (all frames)
         self.cands_exchanged = 0  # carve-candidate records likewise
+        self.cands_by_shard = [0] * shard_count  # ... by the shard that sent them
+        self.graphs = None
+        if graph is not None:
+            w, h = graph
+            self.graphs = [e.shard_frame_graph(w, h, i if split else 0, shard_count if split else 1)
+                           for i, e in enumerate(self.engines)]
 
     def integrate(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float, count=False):
         try:
@@ -700,6 +812,16 @@ class ShardGroup:
 
     def _integrate(self, rgb, depth, ht, lt, K, cam_T_world, max_depth, count):
         G = self.G
+        if self.graphs is not None:
+            for i, g in enumerate(self.graphs):
+                g.begin(rgb, depth, ht, lt, K, cam_T_world, max_depth, self._keys[i], self._keys, self.key_cap,
+                        self._cands[i], self._cands, self.cand_cap)
+            for g in self.graphs:
+                g.update()
+            for g in self.graphs:
+                g.end()
+            self._count(count)
+            return
         for i, e in enumerate(self.engines):
             if self.split:
                 e.integrate_shard_begin(rgb, depth, ht, lt, K, cam_T_world, max_depth, i, G, self._keys[i],
@@ -711,6 +833,13 @@ class ShardGroup:
             e.integrate_shard_update(keys_in, self.key_cap, self._cands[i], self.cand_cap)
         for e in self.engines:
             e.integrate_shard_end(self._cands, self.cand_cap)
+        self._count(count)
+
+    def _count(self, count):
+        if count:  # per-shard candidate counts (slot headers), a host sync
+            import torch
+            per = self._cands[:, 8:12].contiguous().view(torch.int32).view(-1).tolist()
+            self.cands_by_shard = [a + b for a, b in zip(self.cands_by_shard, per)]
         if count:  # slot headers (record 0's count word), a host sync
             import torch
             hdr = lambda t: int(t[:, 8:12].contiguous().view(torch.int32).sum())
@@ -726,6 +855,8 @@ class ShardGroup:
         return [e.stats() for e in self.engines]
 
     def close(self):
+        for g in self.graphs or []:
+            g.close()
         for e in self.engines:
             e.close()
 

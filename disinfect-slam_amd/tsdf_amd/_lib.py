@@ -106,6 +106,8 @@ EXPORTS = [
     "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame", "tsdf_graph_destroy",
     "tsdf_snapshot_bytes", "tsdf_snapshot_save", "tsdf_snapshot_load",
     "tsdf_render_blocks", "tsdf_import_blocks", "tsdf_reset", "tsdf_pack_blocks",
+    "tsdf_raycast_rows", "tsdf_render_bands", "tsdf_pack_halo", "tsdf_extract_mesh_owned",
+    "tsdf_graph_create_shard", "tsdf_graph_shard_begin", "tsdf_graph_shard_update", "tsdf_graph_shard_end",
 ]
 
 _lib = None
@@ -144,12 +146,22 @@ def load(path: str | None = None):
     L.tsdf_graph_frame.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f,
                                    C.POINTER(Intrinsics), C.POINTER(Pose), P, P]
     L.tsdf_graph_destroy.argtypes = [P]
+    L.tsdf_graph_create_shard.argtypes = [P, i, i, i, i, C.POINTER(P)]
+    L.tsdf_graph_shard_begin.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f,
+                                         P, P, C.c_int32, P, P, C.c_int32]
+    L.tsdf_graph_shard_update.argtypes = [P]
+    L.tsdf_graph_shard_end.argtypes = [P]
     L.tsdf_snapshot_bytes.argtypes = [P, C.POINTER(i64)]
     L.tsdf_snapshot_save.argtypes = [P, P, i64]
     L.tsdf_snapshot_load.argtypes = [P, P, i64]
     L.tsdf_render_blocks.argtypes = [P, C.POINTER(Intrinsics), i, i, C.POINTER(Pose), f, P, i64,
                                      C.POINTER(i64), i]
     L.tsdf_import_blocks.argtypes = [P, P, i64, i, i]
+    L.tsdf_raycast_rows.argtypes = [P, C.POINTER(Intrinsics), i, i, C.POINTER(Pose), f, i, i, P, P, i]
+    L.tsdf_render_bands.argtypes = [P, C.POINTER(Intrinsics), i, i, C.POINTER(Pose), f, i, P, P, i64,
+                                    P, i]
+    L.tsdf_pack_halo.argtypes = [P, P, i64, P, i]
+    L.tsdf_extract_mesh_owned.argtypes = [P, P, f, i, i, i, P, i64, C.POINTER(i64), i]
     L.tsdf_reset.argtypes = [P]
     L.tsdf_pack_blocks.argtypes = [P, P, P, i64, C.POINTER(i64), i]
     L.tsdf_query.argtypes = [P, P, P, i64, C.POINTER(i64)]
@@ -186,7 +198,10 @@ def load(path: str | None = None):
                  "tsdf_integrate_shard_abort", "tsdf_stream_wait", "tsdf_stream_signal", "tsdf_get_stream",
                  "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame",
                  "tsdf_graph_destroy", "tsdf_snapshot_bytes", "tsdf_snapshot_save", "tsdf_snapshot_load",
-                 "tsdf_extract_mesh",
+                 "tsdf_extract_mesh", "tsdf_raycast_rows", "tsdf_render_bands", "tsdf_pack_halo",
+                 "tsdf_extract_mesh_owned", "tsdf_render_blocks", "tsdf_import_blocks", "tsdf_reset",
+                 "tsdf_pack_blocks", "tsdf_graph_create_shard", "tsdf_graph_shard_begin",
+                 "tsdf_graph_shard_update", "tsdf_graph_shard_end",
                  "tsdf_get_stats", "tsdf_synchronize", "tsdf_profile_begin", "tsdf_profile_end",
                  "tsdf_debug_dump", "tsdf_debug_stamps", "tsdf_hash_allocate", "tsdf_hash_delete",
                  "tsdf_hash_retrieve",

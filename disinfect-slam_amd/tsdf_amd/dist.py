@@ -60,16 +60,28 @@ class ShardBuffers:
         self.cands_in = torch.zeros((world, cb), dtype=torch.uint8, device=dev)
 
 
-def integrate_sharded(engine, bufs, rgb, depth, ht, lt, K, cam_T_world, max_depth, split=True):
+def integrate_sharded(engine, bufs, rgb, depth, ht, lt, K, cam_T_world, max_depth, split=True, graph=None):
     """One frame of a spatially sharded volume on this rank (tsdf_integrate_shard_*):
     begin (DDA over this rank's band of tile rows when split) -> all-gather of the key slots ->
-    update -> all-gather of the carve-candidate slots -> end. Asynchronous on the current stream."""
+    update -> all-gather of the carve-candidate slots -> end. Asynchronous on the current stream.
+    graph: the engine's ShardFrameGraph (Engine.shard_frame_graph): the three phases as its captured
+    segments, the all-gathers between them as here (RCCL calls cannot be recorded into the engine's
+    graphs across the C ABI)."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():
         rank, world = dist.get_rank(), dist.get_world_size()
     else:
         rank, world = 0, 1
     try:
+        if graph is not None:
+            graph.begin(rgb, depth, ht, lt, K, cam_T_world, max_depth, bufs.keys_out, bufs.keys_in, bufs.key_cap,
+                        bufs.cands_out, bufs.cands_in, bufs.cand_cap)
+            if graph.split:
+                all_gather_slots(bufs.keys_out, bufs.keys_in)
+            graph.update(bufs.keys_in, bufs.cands_out)
+            all_gather_slots(bufs.cands_out, bufs.cands_in)
+            graph.end(bufs.cands_in)
+            return
         _integrate_sharded(engine, bufs, rgb, depth, ht, lt, K, cam_T_world, max_depth, split, rank, world)
     except Exception:
         # a failed exchange (e.g. a collective timeout) must not leave the engine mid-frame
@@ -185,28 +197,118 @@ def gather_rows(rows, device=None):
     return torch.cat([allrows[r * cap:r * cap + counts[r]] for r in range(world)])
 
 
+def band_rows(height: int, world: int):
+    """Row boundaries of a sharded render's image bands: rank r renders rows [rows[r], rows[r + 1])."""
+    return [height * r // world for r in range(world + 1)]
+
+
+def exchange_groups(counts, recs):
+    """All-to-all-v of grouped rows (tsdf_render_bands / tsdf_pack_halo output): the counts[d] rows
+    of group d go to rank d. Returns (the rows this rank received, concatenated in source-rank order;
+    the received counts per source). RCCL on the GPU box (device tensors), gloo through the host.
+    Without a process group the rows are this rank's own group 0."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    t = recs if isinstance(recs, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(recs))
+    counts = [int(c) for c in counts]
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return t[:counts[0]], [counts[0]]
+    world = dist.get_world_size()
+    host = t.is_cuda and dist.get_backend() == "gloo"
+    cdev = torch.device("cpu") if (host or not t.is_cuda) else t.device
+    send_n = torch.tensor(counts, dtype=torch.int64, device=cdev)
+    recv_n = torch.empty(world, dtype=torch.int64, device=cdev)
+    dist.all_to_all_single(recv_n, send_n)
+    rcounts = [int(c) for c in recv_n.tolist()]
+    row = int(t[0].numel()) if t.dim() > 1 else 1
+    src = t.cpu() if host else t
+    out = torch.empty((sum(rcounts),) + tuple(t.shape[1:]), dtype=t.dtype, device=src.device)
+    dist.all_to_all_single(out.view(-1), src.contiguous().view(-1), [c * row for c in rcounts],
+                           [c * row for c in counts])
+    return (out.to(t.device) if host else out), rcounts
+
+
+# bytes this rank moved in the last sharded render / mesh (the bench reports them per frame)
+last_exchange = {}
+
+
 def render_sharded(engine, replica, K, width, height, cam_T_world, max_depth, device=True,
                    rgba=None, normal=None):
-    """Raycast of a spatially sharded volume (SURVEY.md 8e raycast composite): every
-    rank packs the blocks of its shard that this camera's rays can read (tsdf_render_blocks), the
-    records are all-gathered (RCCL over xGMI on the GPU box), and `replica` -- a scratch engine of
-    the same voxel size / truncation with room for them -- imports the union and renders it with
-    the unchanged raycast kernel. Every rank gets the image the unsharded volume renders.
-    Returns (rgba, normal) as numpy (H, W, 4) uint8, or the given device tensors rgba / normal."""
-    recs = engine.render_blocks(K, width, height, cam_T_world, max_depth, device=device)
-    allrecs = gather_rows(recs)
-    replica.import_blocks(allrecs if device else allrecs.numpy(), replace=True)
-    return replica.raycast(K, width, height, cam_T_world, max_depth, rgba=rgba, normal=normal)
+    """Raycast of a spatially sharded volume that divides the work: rank r renders the
+    image rows of band r. Every rank packs, per band, the blocks of its shard that the band's rays
+    can read (tsdf_render_bands) and sends band b's records to rank b (an all-to-all over xGMI on the
+    GPU box); rank r imports what it received into `replica` (a scratch engine of the same voxel
+    size / truncation) and renders its rows with the unchanged raycast kernel (tsdf_raycast_rows),
+    then the bands are all-gathered. Every rank gets the image the unsharded volume renders, bit for
+    bit. Returns (rgba, normal): numpy (H, W, 4) u8, or the given device tensors filled."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    rank, world = ((dist.get_rank(), dist.get_world_size())
+                   if dist.is_available() and dist.is_initialized() else (0, 1))
+    rows = band_rows(height, world)
+    counts, recs = engine.render_bands(K, width, height, cam_T_world, max_depth, rows, device=device)
+    mine, _ = exchange_groups(counts, recs)
+    replica.import_blocks(mine if device else mine.numpy(), replace=True)
+    r0, nr = rows[rank], rows[rank + 1] - rows[rank]
+    maxr = max(rows[i + 1] - rows[i] for i in range(world))
+    dev = torch.device("cuda", torch.cuda.current_device())
+    band = torch.zeros((2, maxr, width, 4), dtype=torch.uint8, device=dev)
+    replica.raycast_rows(K, width, height, cam_T_world, max_depth, r0, nr, rgba=band[0], normal=band[1])
+    if world > 1:
+        allb = torch.empty((world,) + tuple(band.shape), dtype=torch.uint8, device=dev)
+        if dist.get_backend() == "gloo":
+            hb = torch.empty(allb.shape, dtype=torch.uint8)
+            dist.all_gather_into_tensor(hb.view(-1), band.cpu().view(-1))
+            allb.copy_(hb)
+        else:
+            dist.all_gather_into_tensor(allb.view(-1), band.view(-1))
+    else:
+        allb = band[None]
+    img = torch.cat([allb[i, :, :rows[i + 1] - rows[i]] for i in range(world)], dim=1)  # (2, H, W, 4)
+    last_exchange.update(render_records_sent=int(recs.shape[0]), render_records_received=int(mine.shape[0]),
+                         render_bytes_sent=int(recs.shape[0]) * 6160, render_bytes_received=int(mine.shape[0]) * 6160,
+                         render_band_bytes=int(band.numel()), render_rows=nr)
+    if rgba is not None:
+        rgba.copy_(img[0])
+        if normal is not None:
+            normal.copy_(img[1])
+        return rgba, normal
+    out = img.cpu().numpy()
+    return np.ascontiguousarray(out[0]), np.ascontiguousarray(out[1])
 
 
 def mesh_sharded(engine, replica, bounds=None, missing_tsdf=0.99, min_weight=0, device=True,
                  out=None):
-    """Marching cubes of a spatially sharded volume: a shard's own extraction misses the cells that
-    straddle another owner's blocks, so every rank packs all its live blocks (tsdf_pack_blocks),
-    the records are all-gathered, `replica` imports the union -- the whole unsharded volume -- and
-    extracts there (tsdf_extract_mesh with bounds). Same triangles as the unsharded mesh, in the
-    replica's entry order."""
-    recs = engine.pack_blocks(None, device=device)
-    allrecs = gather_rows(recs)
-    replica.import_blocks(allrecs if device else allrecs.numpy(), replace=True)
-    return replica.extract_mesh(bounds, missing_tsdf, min_weight, out=out)
+    """Marching cubes of a spatially sharded volume that divides the work: each rank meshes the
+    cells of its own blocks. Its cells read one sample into every neighbouring block, so every rank
+    sends each of its blocks to the owners of the block's 26 neighbours (tsdf_pack_halo, an
+    all-to-all); rank r imports its own blocks plus the halo it received into `replica` and extracts
+    the triangles of its own blocks there (tsdf_extract_mesh_owned). The triangles are all-gathered:
+    the same set as the unsharded mesh (rank by rank, each in its replica's entry order). Returns an
+    (n, 3, 3) float32 numpy array, or a device tensor view when `out` is given."""
+    import torch
+    import torch.distributed as dist
+    rank, world = ((dist.get_rank(), dist.get_world_size())
+                   if dist.is_available() and dist.is_initialized() else (0, 1))
+    own = engine.pack_blocks(None, device=device)
+    if world > 1:
+        counts, halo = engine.pack_halo(device=device)
+        got, _ = exchange_groups(counts, halo)
+        sent = int(halo.shape[0])
+    else:
+        got, sent = own[:0], 0
+    recs = torch.cat([torch.as_tensor(own), torch.as_tensor(got).to(torch.as_tensor(own).device)])
+    replica.import_blocks(recs if device else recs.numpy(), replace=True)
+    tris = replica.extract_mesh(bounds, missing_tsdf, min_weight, out=out,
+                                owner=(rank, world) if world > 1 else None)
+    last_exchange.update(mesh_halo_records_sent=sent, mesh_halo_records_received=int(got.shape[0]),
+                         mesh_own_records=int(own.shape[0]))
+    rows = tris.reshape(-1, 9)
+    allrows = gather_rows(rows, device=rows.device if isinstance(rows, torch.Tensor) else None)
+    if out is not None:
+        n = int(allrows.shape[0])
+        out.view(-1)[:9 * n].copy_(allrows.reshape(-1).to(out.device))
+        return out.view(-1)[:9 * n].view(-1, 3, 3)
+    return allrows.cpu().numpy().reshape(-1, 3, 3) if isinstance(allrows, torch.Tensor) else allrows

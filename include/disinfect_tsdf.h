@@ -205,6 +205,25 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* frame, const tsdf_intrinsi
                      const tsdf_pose* cam_T_world, float max_depth, const tsdf_intrinsics* render_K,
                      const tsdf_pose* render_cam_T_world, uint8_t* rgba, uint8_t* normal);
 int tsdf_graph_destroy(tsdf_graph* g);
+/* A shard's graph frames (BASELINE config C5 on a sharded volume): the sharded frame of
+ * tsdf_integrate_shard_* as three captured segments around the caller's two exchanges --
+ *   tsdf_graph_shard_begin: the DDA of slice slice_index of slice_count (keys into keys_out; with
+ *     slice_count 1 every shard runs the whole DDA and keys_out / keys_in are unused);
+ *   (the caller all-gathers the key slots into keys_in) tsdf_graph_shard_update: merge, allocate,
+ *     update this shard's blocks (raw frame), carve candidates into cands_out;
+ *   (the caller all-gathers the candidate slots into cands_in) tsdf_graph_shard_end: the deletes.
+ * Every buffer is named at _begin (device memory, valid until _end has run). The exchanges are not
+ * recorded into the engine's graphs: stream-ordered collectives of another library (RCCL through
+ * torch.distributed) cannot be captured into a graph this library owns. Same results as
+ * tsdf_integrate_shard_*. */
+int tsdf_graph_create_shard(tsdf_engine* e, int width, int height, int slice_index, int slice_count,
+                            tsdf_graph** out);
+int tsdf_graph_shard_begin(tsdf_graph* g, const tsdf_frame* frame, const tsdf_intrinsics* K,
+                           const tsdf_pose* cam_T_world, float max_depth, void* keys_out,
+                           const void* keys_in, int32_t key_cap, void* cands_out, const void* cands_in,
+                           int32_t cand_cap);
+int tsdf_graph_shard_update(tsdf_graph* g);
+int tsdf_graph_shard_end(tsdf_graph* g);
 
 /* TSDFGrid::RayCast (voxel_tsdf.cu:490-506; ray_cast_kernel :232-307). rgba / normal are
  * height x width x 4 u8 (either may be NULL), host or device memory per mem_kind. */
@@ -243,6 +262,32 @@ int tsdf_reset(tsdf_engine* e);
  * its tsdf_extract_mesh equals the unsharded mesh (as a set of triangles). */
 int tsdf_pack_blocks(tsdf_engine* e, const float* bounds, void* out, int64_t capacity,
                      int64_t* count, int mem_kind);
+
+/* Sharded extraction that divides the work (no reference counterpart):
+ * - tsdf_raycast_rows: rows [row0, row0 + nrows) of the W x H raycast of tsdf_raycast, bit for bit the
+ *   same pixels, into rgba / normal of nrows x width x 4 u8 (ray_cast_kernel, voxel_tsdf.cu:232-307).
+ * - tsdf_render_bands: the shard's own blocks a raycast of rows [rows[b], rows[b + 1]) can read, for
+ *   each band b < nbands (<= 64): the records of tsdf_render_blocks, grouped band by band, counts[b]
+ *   per band (a block may be in several bands). Two-call: out == NULL returns the counts. Each rank of
+ *   a sharded render sends band b's records to the rank that renders band b (an all-to-all), imports
+ *   what it receives into a replica and renders its band with tsdf_raycast_rows.
+ * - tsdf_pack_halo: a shard's own blocks that another shard's marching cubes read -- the blocks with a
+ *   neighbour (of 26) owned by shard d go to group d (counts[shard_count]); the caller routes group d
+ *   to shard d. A replica holding a shard's own blocks (tsdf_pack_blocks) plus the halo it received
+ *   meshes that shard's part of the volume with tsdf_extract_mesh_owned.
+ * - tsdf_extract_mesh_owned: tsdf_extract_mesh of the blocks whose brick owner
+ *   (tsdf_block_owner(., shard_count)) is shard_index; the other selected blocks are read as
+ *   neighbours only. The shards' parts together are the volume's mesh (as a set of triangles). */
+int tsdf_raycast_rows(tsdf_engine* e, const tsdf_intrinsics* K, int width, int height,
+                      const tsdf_pose* cam_T_world, float max_depth, int row0, int nrows, uint8_t* rgba,
+                      uint8_t* normal, int mem_kind);
+int tsdf_render_bands(tsdf_engine* e, const tsdf_intrinsics* K, int width, int height,
+                      const tsdf_pose* cam_T_world, float max_depth, int nbands, const int32_t* rows,
+                      void* out, int64_t capacity, int64_t* counts, int mem_kind);
+int tsdf_pack_halo(tsdf_engine* e, void* out, int64_t capacity, int64_t* counts, int mem_kind);
+int tsdf_extract_mesh_owned(tsdf_engine* e, const float* bounds, float missing_tsdf, int min_weight,
+                            int shard_index, int shard_count, float* triangles, int64_t capacity,
+                            int64_t* num_triangles, int mem_kind);
 
 /* Marching-cubes mesh of the volume (GPU; replaces Query + KrisLibrary
  * SparseTSDFReconstruction::ExtractMesh in examples/ros_camera_driver/ros_offline.cc:258-318).

@@ -58,6 +58,18 @@ def _worker(rank, world, port):
         tdist.all_gather_slots(slot, out)
         for src in range(world):
             assert bool((out[src] == src + 7).all()), (rank, src, out[src][:4])
+        # banded render / mesh halo (tsdf_amd.dist.exchange_groups): all-to-all-v of grouped rows --
+        # rank r's group d (d + 1 + r rows tagged (r, d)) arrives at rank d, in source-rank order
+        counts = [d + 1 + rank for d in range(world)]
+        recs = torch.cat([torch.full((counts[d], 16), 16 * rank + d, dtype=torch.uint8) for d in range(world)])
+        got, rc = tdist.exchange_groups(counts, recs)
+        assert rc == [rank + 1 + src for src in range(world)], rc
+        off = 0
+        for src in range(world):
+            assert bool((got[off:off + rc[src]] == 16 * src + rank).all())
+            off += rc[src]
+        assert off == got.shape[0]
+        assert tdist.band_rows(480, world)[-1] == 480
         # render replicas (tsdf_amd.dist.render_sharded): all-gather-v of ragged record rows, rank order
         rows = np.full((rank + 1, 6160), rank + 1, np.uint8)
         rows[:, 0] = np.arange(rank + 1)

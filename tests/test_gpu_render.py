@@ -313,3 +313,112 @@ def test_render_sharded_two_ranks():
     mp.start_processes(_render_worker, args=(2, port, q), nprocs=2, join=True, start_method="spawn")
     res = dict(q.get(timeout=5) for _ in range(2))
     assert res == {0: "ok", 1: "ok"}, res
+
+
+def _banded_render(shards, replica, K, w, h, pose, rows):
+    """The sharded render of tsdf_amd.dist.render_sharded with the all-to-all done in-process:
+    band b's replica imports band b's records of every shard and renders band b's rows."""
+    import torch
+    G = len(shards)
+    parts = [e.render_bands(K, w, h, pose, 4.0, rows, device=True) for e in shards]
+    rgba = np.zeros((h, w, 4), np.uint8)
+    normal = np.zeros((h, w, 4), np.uint8)
+    received = []
+    for b in range(G):
+        recs = []
+        for counts, r in parts:
+            off = int(counts[:b].sum())
+            recs.append(r[off:off + int(counts[b])])
+        recs = torch.cat(recs)
+        received.append(int(recs.shape[0]))
+        replica.import_blocks(recs, replace=True)
+        got = replica.raycast_rows(K, w, h, pose, 4.0, rows[b], rows[b + 1] - rows[b])
+        rgba[rows[b]:rows[b + 1]] = got[0]
+        normal[rows[b]:rows[b + 1]] = got[1]
+    return rgba, normal, received
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_banded_sharded_render_equals_unsharded(G):
+    """Sharded render that splits the image: band b of the rows is rendered from the
+    blocks every shard selects for that band's sub-pyramid (tsdf_render_bands) -- bit-identical to
+    the unsharded raycast, and tsdf_raycast_rows equals the rows of a whole raycast."""
+    from tsdf_amd import dist as tdist
+    from tsdf_amd import synth
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    full, group, replica = _engines(G)
+    try:
+        _integrate([full, group], cam, 6)
+        for K, pose in _views(cam):
+            exp = full.raycast(K, W, H, pose, 4.0)
+            r0, n = 17, 23
+            part = full.raycast_rows(K, W, H, pose, 4.0, r0, n)
+            np.testing.assert_array_equal(part[0], exp[0][r0:r0 + n])
+            np.testing.assert_array_equal(part[1], exp[1][r0:r0 + n])
+            got = _banded_render(group.engines, replica, K, W, H, pose, tdist.band_rows(H, G))
+            np.testing.assert_array_equal(got[0], exp[0])
+            np.testing.assert_array_equal(got[1], exp[1])
+    finally:
+        _close(full, replica, group)
+
+
+def test_banded_sharded_render_bench_scale():
+    """C3 / C5 geometry, 8 shards: the banded render equals the unsharded raycast bit for bit, and a
+    band's replica holds a fraction of the view's blocks (the render work and the records each rank
+    receives shrink with the shard count)."""
+    import tsdf_amd
+    from tsdf_amd import dist as tdist
+    from tsdf_amd import synth
+    w, h, G = 640, 480, 8
+    cam = synth.camera(w, h, synth.TUM_FR1)
+    full, group, replica = _engines(G, nb_bits=16, w=w, h=h, voxel=0.005, trunc=0.03)
+    try:
+        _integrate([full, group], cam, 12, stride=3)
+        fr = synth.render(cam, 20)
+        pose = tsdf_amd.SE3(fr["q"], fr["t"])
+        exp = full.raycast(cam.K, w, h, pose, 4.0)
+        got = _banded_render(group.engines, replica, cam.K, w, h, pose, tdist.band_rows(h, G))
+        assert (exp[0][..., 3] == 255).sum() > 0.5 * w * h
+        np.testing.assert_array_equal(got[0], exp[0])
+        np.testing.assert_array_equal(got[1], exp[1])
+        view = full.render_blocks(cam.K, w, h, pose, 4.0).shape[0]
+        received = got[2]
+        assert max(received) < 0.5 * view, (received, view)
+        assert sum(received) < 2.0 * view, (received, view)
+    finally:
+        _close(full, replica, group)
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_halo_sharded_mesh_equals_unsharded(G):
+    """Sharded marching cubes that splits the work: shard s meshes only its own blocks, in a replica
+    holding them plus the halo of neighbouring blocks the other shards send it (tsdf_pack_halo) --
+    the union of the shards' triangles is the unsharded mesh, and the halo is smaller than the
+    volume."""
+    import torch
+
+    from tsdf_amd import synth
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    full, group, replica = _engines(G)
+    shards = group.engines
+    try:
+        _integrate([full, group], cam, 6)
+        xyz = full.query(None).view(np.float32).reshape(-1, 4)[:, :3]
+        lo, hi = np.percentile(xyz, 20, axis=0), np.percentile(xyz, 80, axis=0)
+        box = np.array([lo[0], hi[0], lo[1], hi[1], lo[2], hi[2]], np.float32)
+        halos = [e.pack_halo(device=True) for e in shards]
+        active = full.stats()["active_blocks"]
+        for bounds in (None, box):
+            tris = []
+            for s, e in enumerate(shards):
+                own = e.pack_blocks(None, device=True)
+                got = [r[int(c[:s].sum()):int(c[:s + 1].sum())] for c, r in halos]
+                halo = torch.cat(got)
+                assert halo.shape[0] < active - own.shape[0]
+                replica.import_blocks(torch.cat([own, halo]), replace=True)
+                tris.append(replica.extract_mesh(bounds, owner=(s, G)))
+            exp = full.extract_mesh(bounds)
+            assert exp.shape[0] > 100
+            np.testing.assert_array_equal(_tri_set(np.concatenate(tris)), _tri_set(exp))
+    finally:
+        _close(full, replica, group)

@@ -22,13 +22,15 @@ MAXD = 4.0
 
 
 def _run(G, W, H, voxel, trunc, frames, nb_bits, shard_bits, split=True, stride=1, intrinsics=None,
-         oracle_shards=True, semantic=True):
+         oracle_shards=True, semantic=True, graph=False):
+    import torch
+
     import tsdf_amd
     from tsdf_amd import synth
     from _oracle import OracleGrid, lib
     cam = synth.camera(W, H, intrinsics or synth.TUM_FR1)
     group = tsdf_amd.ShardGroup(G, voxel, trunc, max_width=W, max_height=H, num_block_bits=shard_bits,
-                                split=split)
+                                split=split, graph=(W, H) if graph else None)
     full = OracleGrid(voxel, trunc, nb_bits)
     oshards = []
     if oracle_shards:
@@ -42,8 +44,14 @@ def _run(G, W, H, voxel, trunc, frames, nb_bits, shard_bits, split=True, stride=
             fr = synth.render(cam, stride * f)
             ht, lt = (fr["ht"], fr["lt"]) if semantic else (None, None)
             fr = dict(fr, ht=ht, lt=lt)
-            group.integrate(fr["rgb"], fr["depth"], ht, lt, cam.K, tsdf_amd.SE3(fr["q"], fr["t"]), MAXD,
-                            count=True)
+            if graph:  # graph frames take device frames
+                dv = {k: None if fr[k] is None else torch.from_numpy(np.ascontiguousarray(fr[k])).cuda()
+                      for k in ("rgb", "depth", "ht", "lt")}
+                group.integrate(dv["rgb"], dv["depth"], dv["ht"], dv["lt"], cam.K, tsdf_amd.SE3(fr["q"], fr["t"]),
+                                MAXD, count=True)
+            else:
+                group.integrate(fr["rgb"], fr["depth"], ht, lt, cam.K, tsdf_amd.SE3(fr["q"], fr["t"]), MAXD,
+                                count=True)
             full.integrate(fr["rgb"], fr["depth"], ht, lt, MAXD, cam.K, fr["q"], fr["t"])
             if oshards:
                 oracle_shard_frame(oshards, fr, cam, MAXD, split=split)
@@ -92,12 +100,28 @@ def test_sharded_replicated_dda_union_equals_unsharded():
 
 
 def test_sharded_c4_l515_union_equals_unsharded():
-    """C4 shape: 1280x720 L515 intrinsics, 8 shards, 4 frames, depth-only."""
+    """C4 as configured: 1280x720 L515 intrinsics, depth + ht / lt, 8 routed shards (DDA split by
+    tile rows, keys and candidates exchanged), 10 frames: the union equals the unsharded oracle and
+    every shard its oracle shard."""
     from tsdf_amd import synth
-    nblk, cross, group = _run(8, 1280, 720, 0.005, 0.03, 4, nb_bits=16, shard_bits=14,
-                              intrinsics=synth.L515_FULL, oracle_shards=False, semantic=False)
+    nblk, cross, group = _run(8, 1280, 720, 0.005, 0.03, 10, nb_bits=17, shard_bits=14,
+                              intrinsics=synth.L515_FULL, oracle_shards=True, semantic=True)
     try:
         assert nblk > 5000
+        assert cross > 0
+    finally:
+        group.close()
+
+
+def test_sharded_routed_heavy_carving():
+    """Routed exchange (split DDA) under heavy carving: 8 shards, 2 cm voxels, 20 frames of a fast
+    orbit -- carve candidates of several shards are deleted from every shard's index each frame; the
+    union stays the unsharded oracle volume and every shard its oracle shard."""
+    nblk, cross, group = _run(8, 160, 120, 0.02, 0.06, 20, nb_bits=14, shard_bits=12, split=True, stride=3)
+    try:
+        assert nblk > 200
+        assert group.cands_exchanged > 100, group.cands_exchanged
+        assert sum(1 for c in group.cands_by_shard if c > 0) >= 4, group.cands_by_shard
     finally:
         group.close()
 
@@ -327,3 +351,15 @@ def test_shard_abort_returns_engine_between_frames():
         assert e.stats()["status"] == 0 and e.stats()["active_blocks"] > 0
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("split", [True, False])
+def test_sharded_graph_frames_equal_oracle(split):
+    """C5 on a sharded volume: every shard's frame as its three captured graph segments
+    (tsdf_graph_create_shard) around the exchanges -- each shard still equals the oracle's shard and
+    the union the unsharded oracle volume."""
+    nblk, cross, group = _run(3, 160, 120, 0.005, 0.03, 6, nb_bits=15, shard_bits=14, split=split, graph=True)
+    try:
+        assert nblk > 500
+    finally:
+        group.close()
