@@ -115,7 +115,16 @@ __global__ void k_init_heap(int32_t* heap, int n);
 __global__ void k_init_logodds(uint8_t* pool, int nb);
 // last-arriver counters (tsdf_resolve.h arrive_last), one 128-B line each: lines [0, 9) k_ingest_dda,
 // [16, 25) k_integrate, line 32 k_integrate's start stamp
-constexpr int kArrIngest = 0, kArrIntegrate = 16 * 16, kArrStart = 32 * 16, kArriveWords = 33 * 16;
+// first-level arrival counters per kernel (workgroup b arrives at counter b % kArrGroups: a multiple
+// of 8, so every counter's workgroups share an XCD), then one top counter
+#ifndef TSDF_ARRIVE_GROUPS
+#define TSDF_ARRIVE_GROUPS 8
+#endif
+constexpr int kArrGroups = TSDF_ARRIVE_GROUPS;
+static_assert(kArrGroups % 8 == 0 && kArrGroups <= 128, "arrival counters");
+constexpr int kArrStride = (kArrGroups + 1) * 16;  // u64 words of one kernel's counter lines
+constexpr int kArrIngest = 0, kArrIntegrate = kArrStride, kArrStart = 2 * kArrStride,
+              kArriveWords = 2 * kArrStride + 16;
 // per frame (2 launches; the resolvers run in the last workgroup of each)
 constexpr int kVisWorkgroups = kOccWords / 256;  // visibility-sweep workgroups of k_ingest_dda
 template <int TS>  // LDS key-set slots per tile (tsdf_alloc.hip): 1024 for maxs <= 3, else 2048

@@ -66,13 +66,14 @@ __device__ __forceinline__ bool arrive_last(unsigned long long* words, unsigned 
   if (drain) __builtin_amdgcn_s_waitcnt(0);
   lds_barrier();
   if (threadIdx.x == 0) {
-    const uint32_t g = blockIdx.x & 7u, ngrp = gridDim.x < 8u ? gridDim.x : 8u;
-    const uint32_t expect = (gridDim.x - g + 7u) / 8u;
+    constexpr uint32_t NG = (uint32_t)kArrGroups;
+    const uint32_t g = blockIdx.x % NG, ngrp = gridDim.x < NG ? gridDim.x : NG;
+    const uint32_t expect = (gridDim.x - g + NG - 1u) / NG;
     const unsigned long long old = __hip_atomic_fetch_add(&words[g * kArrLine], (1ull << 40) | payload,
                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int last = 0;
     if ((uint32_t)(old >> 40) + 1u == expect) {
-      const unsigned long long top = __hip_atomic_fetch_add(&words[8 * kArrLine], 1ull, __ATOMIC_RELAXED,
+      const unsigned long long top = __hip_atomic_fetch_add(&words[NG * kArrLine], 1ull, __ATOMIC_RELAXED,
                                                             __HIP_MEMORY_SCOPE_AGENT);
       last = (uint32_t)top + 1u == ngrp;
     }
@@ -83,16 +84,13 @@ __device__ __forceinline__ bool arrive_last(unsigned long long* words, unsigned 
 }
 // the last arriver, thread 0: the counters zeroed for the next launch (stores only)
 __device__ __forceinline__ void arrive_reset(unsigned long long* words) {
-#pragma unroll
-  for (int g = 0; g < 9; ++g) st_co(&words[g * kArrLine], 0ull);
+  for (int g = 0; g <= kArrGroups; ++g) st_co(&words[g * kArrLine], 0ull);
 }
 // the last arriver, thread 0: the sum of the payloads; the counters are zeroed for the next launch
 __device__ __forceinline__ unsigned long long arrive_collect(unsigned long long* words) {
   unsigned long long sum = 0ull;
-#pragma unroll
-  for (int g = 0; g < 8; ++g) sum += ld_co(&words[g * kArrLine]) & ((1ull << 40) - 1ull);
-#pragma unroll
-  for (int g = 0; g < 9; ++g) st_co(&words[g * kArrLine], 0ull);
+  for (int g = 0; g < kArrGroups; ++g) sum += ld_co(&words[g * kArrLine]) & ((1ull << 40) - 1ull);
+  for (int g = 0; g <= kArrGroups; ++g) st_co(&words[g * kArrLine], 0ull);
   return sum;
 }
 
