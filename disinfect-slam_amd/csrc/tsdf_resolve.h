@@ -58,6 +58,11 @@ __device__ __forceinline__ void st_co(T* p, T v) {
 // arriver to a top counter. The high 24 bits of a counter count arrivals, the low 40 accumulate
 // `payload` (k_integrate: its updated-voxel count). Each thread drains its own memory operations
 // first, so everything it published (st_co) is complete before its workgroup arrives.
+// Memory-model note: the ordering rests on the raw s_waitcnt vmcnt(0) + barrier before
+// the relaxed arrival, with the publications as agent-scope (sc1) stores, which gfx950 counts in
+// vmcnt -- not on an agent-scope release, whose gfx950 lowering (buffer_wbl2 sc1: a write-back of
+// the L2) in every workgroup would cost the frame. tests/test_isa.py pins that codegen in the built
+// library (every arrival after a drained barrier, no store sunk past it; sc1 publications).
 // ---------------------------------------------------------------------------------------------
 constexpr int kArrLine = 16;  // u64 per 128-B line
 // drain: this wave published data (wave-uniform); other waves' outstanding stores stay in flight

@@ -1,0 +1,88 @@
+"""Codegen pins of the in-kernel hand-offs: the last-arriver pattern
+(csrc/tsdf_resolve.h arrive_last) orders a workgroup's published records before its arrival with a
+raw s_waitcnt vmcnt(0) and a workgroup barrier, relying on the agent-scope (sc1) stores being counted
+in vmcnt -- not on a release fence, whose gfx950 form (buffer_wbl2 sc1: an L2 writeback per
+workgroup) costs the frame. These checks read the gfx950 code object of the built library and assert
+that every arrival atomic of the frame kernels is preceded by a barrier with no global store between
+the two, and that a vmcnt(0) wait precedes that barrier; and that the publishing stores and the last
+arriver's loads carry the agent-scope bit (sc1). CPU only (llvm-objdump on the built .so)."""
+import os
+import re
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "disinfect-slam_amd", "libdisinfect_tsdf.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _disassemble():
+    if not os.path.exists(LIB) or not os.path.exists(os.path.join(LLVM, "llvm-objdump")):
+        pytest.skip("library or llvm tools absent")
+    tmp = tempfile.mkdtemp()
+    try:
+        fb = os.path.join(tmp, "fatbin")
+        subprocess.check_call([os.path.join(LLVM, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fb}", LIB,
+                               os.path.join(tmp, "copy.so")])
+        data = open(fb, "rb").read()
+        starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)]
+        text = []
+        for i, st in enumerate(starts):
+            part = os.path.join(tmp, f"b{i}")
+            with open(part, "wb") as f:
+                f.write(data[st:starts[i + 1] if i + 1 < len(starts) else len(data)])
+            co = part + ".co"
+            subprocess.check_call([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o",
+                                   f"--input={part}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                                   f"--output={co}"])
+            text.append(subprocess.check_output([os.path.join(LLVM, "llvm-objdump"), "-d", co], text=True))
+        return "\n".join(text)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def _functions(asm):
+    funcs, name = {}, None
+    for line in asm.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(\S+)>:$", line)
+        if m:
+            name = m.group(1)
+            funcs[name] = []
+        elif name and line.startswith("\t"):
+            funcs[name].append(line.strip())
+    return funcs
+
+
+def test_arrivals_follow_a_drained_barrier():
+    funcs = _functions(_disassemble())
+    frame = {n: body for n, body in funcs.items() if "k_ingest_dda" in n or "k_integrate_t" in n}
+    assert len(frame) >= 8, sorted(funcs)[:20]
+    checked = 0
+    for name, body in frame.items():
+        for i, ins in enumerate(body):
+            # the arrivals: returning 64-bit adds on the counters (first level, then the top counter)
+            if not (ins.startswith("global_atomic_add_x2") and ins.split("//")[0].rstrip().endswith("sc0")):
+                continue
+            j = max(k for k in range(i) if body[k].startswith("s_barrier"))
+            between = body[j + 1:i]
+            assert not any(b.startswith(("global_store", "flat_store", "buffer_store")) for b in between), \
+                (name, between)
+            window = body[max(0, j - 60):j]
+            assert any(re.match(r"s_waitcnt\b.*vmcnt\(0\)", w) for w in window), (name, window[-10:])
+            checked += 1
+    assert checked >= 16
+
+
+def test_publication_is_agent_scope():
+    """st_co / ld_co: the new-key list, the candidate records and the arrival counters' readers use
+    sc1 (agent scope) so the last arriver on another XCD reads them from the coherent level."""
+    funcs = _functions(_disassemble())
+    ing = next(b for n, b in funcs.items() if n.startswith("_ZN4tsdf12k_ingest_ddaILi1024"))
+    integ = next(b for n, b in funcs.items() if n.startswith("_ZN4tsdf13k_integrate_tILb0ELb0"))
+    assert any(i.startswith("global_store_dwordx2") and "sc1" in i for i in ing)   # nk_list entries
+    assert any(i.startswith("global_load_dwordx2") and "sc1" in i for i in ing)    # resolver prologue
+    assert any(i.startswith("global_store_dwordx2") and "sc1" in i for i in integ)  # candidate records
