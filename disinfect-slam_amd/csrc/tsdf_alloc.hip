@@ -413,13 +413,16 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
   }
   if (!arrive_last(D.arrive + kArrIngest, 0ull, &S.last)) return;
   const unsigned long long tend = __builtin_amdgcn_s_memrealtime();
+  TSDF_STAMP(D, 6, 0);
   if (threadIdx.x == 0) arrive_reset(D.arrive + kArrIngest);  // (no loads: the resolver starts at once)
   if (P.tail == kTailPack)
     pack_keys_wg(D, P.slot, P.slot_cap);
   else
     resolve_alloc_wg(D, P, (uint32_t)P.W * (uint32_t)P.H * (uint32_t)P.maxs, 1, S.u.res);
   // the ingest's device span (start -> last arrival), accounted after the resolver, off its path
+  TSDF_STAMP(D, 6, 1);
   if (threadIdx.x == 0) D.ctr->ingest_ticks += tend - ld_co(&D.arrive[kArrStart + 8]);
+  TSDF_STAMP(D, 6, 2);
 }
 template <int TS>
 __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,

@@ -610,6 +610,10 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
     }
     rank_sort<RB>(L.batch, L.u.tmp, m);
     TSDF_STAMP(D, 1, 2);
+#if defined(TSDF_EXP) && (TSDF_EXP & 16)  // experiment: the same sort again, instruction cache warm
+    rank_sort<RB>(L.batch, L.u.tmp, m);
+    TSDF_STAMP(D, 1, 7);
+#endif
     if (t == 0) L.base = 0;
     lds_barrier();
     while (L.base < m) {

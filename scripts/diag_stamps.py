@@ -17,8 +17,11 @@ KERNELS = {0: ("ingest", ["lds_init", "pix_write", "dda", "barrier", "sweep"]),
            1: ("resolve_alloc", ["prepare", "sort", "claim", "dirty", "commit", "rest"]),
            2: ("vis (in ingest)", ["all"]),
            3: ("integrate", ["all"]),
-           4: ("resolve_delete", ["sum+prepare", "rounds"])}
+           4: ("resolve_delete", ["sum+prepare", "rounds"]),
+           6: ("ingest_tail", ["resolve", "ticks"]),
+           5: ("integrate_tail", ["carve", "stats"])}
 NK, NWG, NS = 8, 4096, 8
+ORDER = [2, 0, 1, 6, 3, 4, 5]  # dispatch / execution order of the stamped phases
 
 
 def main():
@@ -58,7 +61,7 @@ def main():
         S = buf.reshape(NK, NWG, NS).astype(np.int64)
         t0 = None
         bounds = []
-        for k, (name, phases) in sorted(KERNELS.items(), key=lambda kv: (kv[0] != 2, kv[0])):
+        for k, (name, phases) in sorted(KERNELS.items(), key=lambda kv: ORDER.index(kv[0])):
             s = S[k]
             valid = s[:, 0] > 0
             if not valid.any():
@@ -88,6 +91,9 @@ def main():
                 dur = (s[:, j + 1] - s[:, j]) * 10e-3
                 d[p].append(np.median(dur))
                 d[p + "_max"].append(dur.max())
+        if S[1, 0, 7] > 0:  # TSDF_EXP & 16 diag build: the resolver's sort repeated (warm)
+            acc.setdefault("resolve_alloc sort repeated", {}).setdefault("sort2", []).append(
+                (S[1, 0, 7] - S[1, 0, 2]) * 10e-3)
         for (n1, _, e1), (n2, s2, _) in zip(bounds, bounds[1:]):
             acc.setdefault("gaps", {}).setdefault(f"{n1}->{n2}", []).append((s2 - e1) * 10e-3)
         acc.setdefault("frame", {}).setdefault("first_start_to_last_end", []).append(
