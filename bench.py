@@ -46,6 +46,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BLOCK_READ_BYTES = 512 * 12 + 12  # voxel state + metadata of one visible block
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_integrate_r2.json")
+# SQ counters of k_raycast (rocprofv3 --pmc passes of `bench.py --loop c5`, scripts/profile_kernel_sq.sh)
+RAYCAST_SQ_FILE = os.path.join(ROOT, "profiles", "r3_raycast_sq.json")
+VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each
 
 
 def parse():
@@ -209,6 +212,24 @@ class Run:
         self.host_enqueue_ms = (t_enq - t0) / a.steps * 1e3
         return tdist.max_over_ranks(t1 - t0, device=self.dev), prof
 
+    def raycast_timing(self, reps=50):
+        """k_raycast's C5 work alone: `reps` back-to-back raycasts of the last timed frame's camera
+        into the final volume, bracketed by events on the engine stream (the whole tsdf_raycast call:
+        view grid + bitmaps + k_raycast). Returns microseconds per call."""
+        import torch
+        a = self.a
+        pose = self.poses[a.warmup + a.steps - 1]
+        for _ in range(3):
+            self.eng.raycast(self.K, a.width, a.height, pose, a.max_depth, rgba=self.rgba, normal=self.normal)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            self.eng.raycast(self.K, a.width, a.height, pose, a.max_depth, rgba=self.rgba, normal=self.normal)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / reps
+
     def close(self):
         if self.graph is not None:
             self.graph.close()
@@ -232,6 +253,31 @@ def kernel_roofline(a, prof, n_frames):
         kind = "HIP events bound to the k_integrate dispatch (hipExtLaunchKernel), engine stream"
     achieved = alg / t / 1e9 if t > 0 else 0.0
     return alg, t, achieved, kind
+
+
+def raycast_roofline(a, us_call):
+    """C5's raycast beside the line: rays/s of the whole call, and -- from the k_raycast SQ counters
+    committed under profiles/ for this image size -- its VALU issue rate against the chip's wave64
+    VALU issue peak (the kernel is bound by each wave's chain of dependent lookups; the
+    VALU fraction shows how much issue bandwidth that chain leaves idle). The rate is taken over the
+    whole call (view grid + bitmaps + k_raycast), so it is a lower bound for the kernel's own."""
+    rays = a.width * a.height
+    out = {"kernel": "k_raycast", "bound": "latency (each wave's chain of dependent view-grid lookups and "
+                                           "voxel reads; VALU second)",
+           "us_per_call": round(us_call, 3), "rays_per_s": round(rays / (us_call * 1e-6), 1),
+           "timing": "events around 50 back-to-back tsdf_raycast calls of the last timed camera, after the loop"}
+    try:
+        sq = json.load(open(RAYCAST_SQ_FILE))
+    except (OSError, ValueError):
+        return out
+    if sq.get("width") == a.width and sq.get("height") == a.height:
+        valu = sq["SQ_INSTS_VALU_per_wave"] * sq["SQ_WAVES"]
+        achieved = valu / (us_call * 1e-6)
+        out.update({"valu_instr_per_wave": sq["SQ_INSTS_VALU_per_wave"], "salu_instr_per_wave": sq["SQ_INSTS_SALU_per_wave"],
+                    "waves": sq["SQ_WAVES"], "achieved": round(achieved / 1e12, 4), "peak": round(VALU_PEAK_WAVE_INSTR / 1e12, 4),
+                    "unit": "T wave64 VALU instr/s", "frac": round(achieved / VALU_PEAK_WAVE_INSTR, 4),
+                    "counters_source": os.path.relpath(RAYCAST_SQ_FILE, ROOT)})
+    return out
 
 
 def pmc_traffic(a, mode, world, prof):
@@ -334,6 +380,9 @@ def main():
     frame_frac_read = b_read * steps_per_s / (world * HBM_PEAK_GBS * 1e9)
     frame_frac_rw = (b_read + b_write) * steps_per_s / (world * HBM_PEAK_GBS * 1e9)
     mesh_tris = run.mesh_tris[-1] if run.mesh_tris else None
+    ray = None
+    if a.loop == "c5" and not run.sharded:
+        ray = raycast_roofline(a, run.raycast_timing())
     host_enq = run.host_enqueue_ms
     exch = None
     if run.sharded:  # bytes this rank moved per frame (rank 0's view)
@@ -434,6 +483,8 @@ def main():
             "mesh_triangles": mesh_tris,
             "status": st["status"],
         }
+        if ray is not None:
+            out["raycast"] = ray
         if world > 1:
             out["frames_per_s_per_stream"] = round(fps_stream, 2)
         if bcast is not None:

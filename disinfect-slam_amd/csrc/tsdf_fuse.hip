@@ -415,6 +415,17 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
     }
   }
   TSDF_STAMP(D, 3, 1);
+#ifdef TSDF_DIAG_STAMPS
+  if (threadIdx.x == 0 && D.dbg && blockIdx.x < (unsigned)kDiagMaxWg) {  // placement + work of the WG
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    unsigned long long* q = D.dbg + ((size_t)3 * kDiagMaxWg + blockIdx.x) * kDiagStamps;
+    q[4] = hw;
+    q[5] = xcc;
+    q[6] = (unsigned long long)((p_hi - (p_lo + (int)(blockIdx.x >> 3)) + ngrp - 1) / ngrp);  // pairs
+  }
+#endif
   // waves that published drain their stores before the workgroup arrives (wave 0: the buffer;
   // the even waves' lane 0: overflow records)
   const bool drain = (wave == 0 && nc > 0) || (s_ovf && (wave & 1) == 0);

@@ -94,6 +94,37 @@ def main():
         if S[1, 0, 7] > 0:  # TSDF_EXP & 16 diag build: the resolver's sort repeated (warm)
             acc.setdefault("resolve_alloc sort repeated", {}).setdefault("sort2", []).append(
                 (S[1, 0, 7] - S[1, 0, 2]) * 10e-3)
+        # k_integrate placement (diag build): per CU (xcc, se, cu) the pairs of its workgroups and
+        # the latest end; per pair count the workgroups' end times
+        s3 = S[3]
+        ok3 = s3[:, 0] > 0
+        if ok3.any() and (s3[ok3, 5] >= 0).all():
+            t3 = s3[ok3, 0].min()
+            hw = s3[ok3, 4].astype(np.int64)
+            cu = (s3[ok3, 5] << 9) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15)
+            pairs = np.maximum(s3[ok3, 6], 0)
+            end = (s3[ok3, 1] - t3) * 10e-3
+            d = acc.setdefault("integrate per CU", {})
+            ucu = np.unique(cu)
+            per_pairs = np.array([pairs[cu == c].sum() for c in ucu])
+            per_end = np.array([end[cu == c].max() for c in ucu])
+            per_nwg = np.array([(cu == c).sum() for c in ucu])
+            d.setdefault("n_cu", []).append(len(ucu))
+            d.setdefault("wg_per_cu_min", []).append(per_nwg.min())
+            d.setdefault("wg_per_cu_max", []).append(per_nwg.max())
+            d.setdefault("pairs_per_cu_min", []).append(per_pairs.min())
+            d.setdefault("pairs_per_cu_mean", []).append(per_pairs.mean())
+            d.setdefault("pairs_per_cu_max", []).append(per_pairs.max())
+            d.setdefault("cu_end_min", []).append(per_end.min())
+            d.setdefault("cu_end_p50", []).append(np.median(per_end))
+            d.setdefault("cu_end_max", []).append(per_end.max())
+            d.setdefault("corr_pairs_end", []).append(np.corrcoef(per_pairs, per_end)[0, 1] if per_pairs.std() > 0 else 0)
+            for npair in (0, 1, 2, 3):
+                m = pairs == npair
+                if m.any():
+                    d.setdefault(f"wg_end_p50_{npair}pairs", []).append(np.median(end[m]))
+                    d.setdefault(f"wg_end_max_{npair}pairs", []).append(end[m].max())
+                    d.setdefault(f"n_wg_{npair}pairs", []).append(m.sum())
         for (n1, _, e1), (n2, s2, _) in zip(bounds, bounds[1:]):
             acc.setdefault("gaps", {}).setdefault(f"{n1}->{n2}", []).append((s2 - e1) * 10e-3)
         acc.setdefault("frame", {}).setdefault("first_start_to_last_end", []).append(
