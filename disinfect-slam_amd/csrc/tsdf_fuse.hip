@@ -108,12 +108,12 @@ __global__ __launch_bounds__(256) void k_shard_abort(EngineDev D) {
 __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FrameParams& P, DeleteLds& L) {
   const int t = threadIdx.x;
   const unsigned long long tend = __builtin_amdgcn_s_memrealtime();  // the update's span ends here
-  TSDF_STAMP(D, 5, 0);
+  TSDF_STAMP(D, 7, 0);
   if (P.tail == kTailPack)
     pack_cands_wg(D, P.slot, P.slot_cap);
   else
     resolve_delete_wg(D, D.cand, &D.ctr->n_cand, 0, L);
-  TSDF_STAMP(D, 5, 1);
+  TSDF_STAMP(D, 7, 1);
   lds_barrier();  // (L.scan is reused below)
   const int bc = t < kBands ? D.band[t * kBandStride] : 0;
   int nband;
@@ -125,7 +125,7 @@ __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FramePa
     D.ctr->n_vis = nband + D.ctr->n_fresh;
   }
   if (P.tail != kTailPack) frame_end(D);
-  TSDF_STAMP(D, 5, 2);
+  TSDF_STAMP(D, 7, 2);
 }
 
 // 64 VGPRs: 8 waves per SIMD (65 without the bound: 7). Graph: the graph-captured form reads its

@@ -51,6 +51,27 @@ def main():
         print(f"frame {i}: waves {waves} hits {q[6]} / {rays}")
         print(f"  per ray : iterations {q[0] / rays:7.1f}  block lookups {q[1] / rays:6.1f}  voxel reads {q[2] / rays:6.1f}")
         print(f"  per wave: iterations {q[3] / waves:7.1f}  with a lookup {q[4] / waves:6.1f}  with a read {q[5] / waves:6.1f}")
+        # per-wave lifetimes (kernel 6 stamps: wave w of workgroup wg at 2w / 2w + 1)
+        S6 = buf.reshape(NK, NWG, NS)[6].astype(np.int64)
+        nwg = 40 * 30
+        st, en = S6[:nwg, 0::2], S6[:nwg, 1::2]
+        ok = (st > 0) & (en > 0)
+        if ok.any():
+            t0 = st[ok].min()
+            dur = (en - st)[ok] * 10e-3
+            endt = (en[ok] - t0) * 10e-3
+            stt = (st[ok] - t0) * 10e-3
+            print(f"  wave lifetime us: p10 {np.percentile(dur, 10):6.1f} p50 {np.median(dur):6.1f} "
+                  f"p90 {np.percentile(dur, 90):6.1f} max {dur.max():6.1f}; start p50 {np.median(stt):5.1f} "
+                  f"max {stt.max():5.1f}; end p50 {np.median(endt):6.1f} p90 {np.percentile(endt, 90):6.1f} max {endt.max():6.1f}")
+            # where the slowest waves are: their tiles' rows / columns (XCD-aware tile map of k_raycast)
+            wg = np.repeat(np.arange(nwg)[:, None], 4, axis=1)[ok]
+            g = wg & 7
+            tile = g * (nwg >> 3) + np.minimum(g, nwg & 7) + (wg >> 3)
+            ty, tx = tile // 40, tile % 40
+            slow = dur >= np.percentile(dur, 95)
+            print(f"  slowest 5% of waves: tile rows {np.bincount(ty[slow], minlength=30).tolist()}")
+            print(f"                       tile cols {np.bincount(tx[slow], minlength=40).tolist()}")
     eng.close()
 
 
