@@ -191,6 +191,7 @@ class Run:
         a = self.a
         for i in range(a.warmup):
             self.step(i)
+        self.eng.flush()
         torch.cuda.synchronize()
         if self.dist:
             self.dist.barrier()
@@ -203,6 +204,8 @@ class Run:
         t0 = time.perf_counter()
         for i in range(a.warmup, a.warmup + a.steps):
             self.step(i)
+        # pipelined frames: the last frame's update is enqueued here, inside the timed region
+        self.eng.flush()
         t_enq = time.perf_counter()
         torch.cuda.synchronize()
         t1 = time.perf_counter()

@@ -8,98 +8,9 @@
 #include "tsdf_block.h"
 #include "tsdf_kernels.h"
 #include "tsdf_resolve.h"
+#include "tsdf_ingest.h"
 
 namespace tsdf {
-
-// ---------------------------------------------------------------------------------------------
-// per-frame new-key set: open addressing on 64-bit packed keys, min candidate order per key
-// ---------------------------------------------------------------------------------------------
-__device__ void keyset_insert(unsigned long long* keys, uint32_t* orders, NkEnt* list,
-                              int32_t* count, uint32_t* status, uint64_t key, uint32_t order) {
-  uint32_t h = (uint32_t)mix64(key) & (kNewKeyCap - 1);
-  for (int p = 0; p < 256; ++p) {
-    // the CAS itself reads the slot (measured equal to a plain read first)
-    const unsigned long long cur = atomicCAS(&keys[h], 0ull, (unsigned long long)key);
-    if (cur == 0ull) {
-      const int s = atomicAdd(count, 1);
-      // the list entry carries the key (the resolver's prologue needs no second load for it),
-      // published for the workgroup that resolves at the end of this launch
-      st_co(&list[s].key, (unsigned long long)key);
-      st_co(&list[s].slot, (unsigned long long)h);
-      atomicMin(&orders[h], order);
-      return;
-    }
-    if (cur == key) {
-      atomicMin(&orders[h], order);
-      return;
-    }
-    h = (h + 1) & (kNewKeyCap - 1);
-  }
-  atomicOr(status, 2u);  // TSDF_STATUS_NEWKEY_OVERFLOW
-}
-__device__ void nk_insert(const EngineDev& D, uint64_t key, uint32_t order) {
-  keyset_insert(D.nk_key, D.nk_order, D.nk_list, &D.ctr->nk_count, &D.ctr->status, key, order);
-}
-
-// ---------------------------------------------------------------------------------------------
-// k_ingest_dda: 16x16 pixel tile per workgroup.
-//  1. pack the frame into per-pixel records the integrate kernel gathers:
-//       pixA = {depth, range = |K^-1 [x y 1]|, w_new = (1 - d / max_depth) * 4, rgb}
-//       pixB = log2 ht - log2 lt
-//     (exactly the values tsdf_integrate_kernel recomputes per voxel, voxel_tsdf.cu:174-201)
-//  2. DDA of [p - trunc dir, p + trunc dir] (voxel_tsdf.cu:116-146); block keys deduplicated in
-//     an LDS hash set with their smallest candidate order (y*W + x)*maxs + i
-//  3. each unique key once: all-8-corners visibility (is_block_visible<true>), table probe;
-//     missing keys go to the global new-key set.
-// The launch covers tiles [P.tile_lo, P.tile_hi): every tile of the frame, or a sharded frame's
-// pixel slice. Step 1 runs only when P.pack_pixels (one volume); a shard's k_integrate gathers the
-// raw frame, so a shard runs the DDA of its slice and nothing else per pixel. A shard probes its
-// copy of the whole hash index, so its keys are exactly the ones one volume's DDA finds in those
-// tiles, whichever shard owns them.
-// ---------------------------------------------------------------------------------------------
-// LDS key-set slots per 16x16 tile: TS > 256 pixels x maxs. 1024 for maxs <= 3 (the reference's
-// 6x truncation / voxel ratio: 2-3 samples per pixel) keeps the workgroup at 16.5 KiB of LDS, so 9
-// workgroups fit a CU and the whole 640x480 grid is resident at once; 2048 up to maxs = 6.
-constexpr int kVisChunk = 1024;   // visibility sweep: 16 occupancy words x 64 entries per wave
-static_assert(kBands == 16, "ResolveLds band arrays");
-
-// LDS key-set slot of a block key: multiplicative hash of the two key words, top log2(TS) bits
-// (a few VALU per DDA sample instead of a 64-bit mixer; placement only, the set is exact)
-template <int TS>
-__device__ __forceinline__ uint32_t tile_slot(uint64_t key) {
-  const uint32_t h = (uint32_t)key * 0x9E3779B1u + (uint32_t)(key >> 32) * 0x85EBCA77u;
-  return h >> (32 - __builtin_ctz(TS));
-}
-
-// The allocation resolver runs in rounds of kIngestRB keys: kRT, one key per thread (the frame's
-// ~50-80 new keys fit one round either way). Measured against 2 kRT: the resolver 6.65 vs 7.15 us per
-// frame (fewer registers and LDS reads per thread), 19.25k vs 19.09k frames/s; its LDS falls under the
-// sweep's, so the union is 16.5 KiB instead of 24.6. (Forcing 7 or 8 resident workgroups per CU with
-// that LDS, by capping the registers at 72 / 64, measured equal / slower: the ingest is not
-// dispatch-bound.)
-#ifndef TSDF_INGEST_RB
-#define TSDF_INGEST_RB 256
-#endif
-constexpr int kIngestRB = TSDF_INGEST_RB;
-
-// the two roles of k_ingest_dda share one LDS allocation
-template <int TS>
-struct IngestLds {
-  union {
-    struct {
-      unsigned long long key[TS];
-      uint32_t ord[TS];
-      uint16_t vis[4][TS / 4];
-    } tile;
-    struct {
-      uint32_t list[4][kVisChunk];
-      int cnt[kBands], base[kBands];
-      int npass;
-    } sweep;
-    AllocLdsT<kIngestRB> res;  // the last-arriving workgroup's allocation resolve
-  } u;
-  int last;
-};
 
 // ---------------------------------------------------------------------------------------------
 // Visibility sweep (check_visibility_kernel + GatherVisible, voxel_tsdf.cu:82-93,388-397) over
@@ -197,170 +108,6 @@ __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, Inge
   }
 }
 
-// grid: kVisWorkgroups sweep workgroups first (dispatched first, they overlap the tiles), then
-// one workgroup per 16x16 pixel tile (tiles_x per row, `tiles` in all)
-template <int TS>
-__device__ __forceinline__ void ingest_tile(EngineDev& D, const FrameParams& P,
-                                            const float* __restrict__ depth,
-                                            const uint8_t* __restrict__ rgb,
-                                            const float* __restrict__ ht,
-                                            const float* __restrict__ lt, int tiles_x, int tile,
-                                            IngestLds<TS>& S) {
-  unsigned long long* s_key = S.u.tile.key;
-  uint32_t* s_ord = S.u.tile.ord;
-  TSDF_STAMP(D, 0, 0);
-  for (int i = threadIdx.x; i < TS; i += 256) {
-    s_key[i] = 0ull;
-    s_ord[i] = 0xFFFFFFFFu;
-  }
-  __syncthreads();
-  TSDF_STAMP(D, 0, 1);
-  const int x = (tile % tiles_x) * 16 + (threadIdx.x & 15);
-  const int y = (tile / tiles_x) * 16 + (threadIdx.x >> 4);
-  // DDA state of this lane's ray (valid: a pixel of this slice with 0 < d <= max_depth)
-  bool ray = false;
-  int nsamp = 0;
-  f3 pos{}, st{};
-  uint32_t order0 = 0;
-  if (x < P.W && y < P.H) {
-    const int i = y * P.W + x;
-    const float d = depth[i];
-    const f3 pc = pixel_ray(P, x, y);
-    const float range = sqrtf(dot3(pc, pc));  // img_depth_to_range (voxel_tsdf.cu:120)
-    if (P.pack_pixels) {  // (a shard's k_integrate reads the raw frame instead)
-      const uint32_t c = (uint32_t)rgb[3 * i] | ((uint32_t)rgb[3 * i + 1] << 8) |
-                         ((uint32_t)rgb[3 * i + 2] << 16);
-      const float h = ht ? ht[i] : 1.0f;
-      const float l = lt ? lt[i] : 1.0f;
-      D.pixA[i] = make_float4(d, range, pixel_w_new(P, d), __uint_as_float(c));
-      D.pixB[i] = pixel_logodds(h, l);
-    }
-    TSDF_STAMP(D, 0, 2);
-    if (!(d == 0 || d > P.max_depth)) {
-      const f3 pcd = {pc.x * d, pc.y * d, pc.z * d};
-      const f3 pw = se3_apply(P.wq, P.wt, pcd);
-      // pc / range (IEEE quotients; pc.z = 1): the Newton-refined pair division, exact in range
-      const float rr = __builtin_amdgcn_rcpf(range);
-      const v2f dxy = div_pair(v2(pc.x, pc.y), v2(range, range), v2(rr, rr), true, true);
-      const v2f dz1 = div_pair(v2(pc.z, pc.z), v2(range, range), v2(rr, rr), true, false);
-      const f3 dc = {dxy.x, dxy.y, dz1.x};
-      const f3 dw = qrot(P.wq, dc);
-      const f3 sw = {pw.x - dw.x * P.trunc, pw.y - dw.y * P.trunc, pw.z - dw.z * P.trunc};
-      const f3 dg = {quot_const(dw.x, P.voxel, P.inv_voxel), quot_const(dw.y, P.voxel, P.inv_voxel),
-                     quot_const(dw.z, P.voxel, P.inv_voxel)};
-      const f3 sg = {quot_const(sw.x, P.voxel, P.inv_voxel), quot_const(sw.y, P.voxel, P.inv_voxel),
-                     quot_const(sw.z, P.voxel, P.inv_voxel)};
-      const float two_trunc = 2 * P.trunc;
-      const f3 rg = {two_trunc * dg.x, two_trunc * dg.y, two_trunc * dg.z};
-      const int step_grid =
-          f2i(ceilf(fmaxf(fmaxf(fabsf(rg.x), fabsf(rg.y)), fabsf(rg.z)) / kBlockLen));
-      const float div = fmaxf((float)step_grid, 1.0f);
-      // ray / max(step_grid, 1): step_grid is 1 or 2 at the reference's 6x truncation / voxel
-      // ratio, where the quotient is exact as a product; larger counts take the IEEE divide
-      if (__builtin_expect(div <= 2.0f, 1)) {
-        const float m = div == 2.0f ? 0.5f : 1.0f;
-        st = {rg.x * m, rg.y * m, rg.z * m};
-      } else {
-        st = {rg.x / div, rg.y / div, rg.z / div};
-      }
-      pos = sg;
-      ray = true;
-      nsamp = step_grid + 1;
-      if (nsamp > P.maxs) {
-        atomicOr(&D.ctr->status, 4u);  // TSDF_STATUS_DDA_OVERFLOW
-        nsamp = P.maxs;
-      }
-      order0 = (uint32_t)i * (uint32_t)P.maxs;
-    }
-  }
-  // Samples s = 0 .. step_grid of every ray (voxel_tsdf.cu:141-146) into the tile's LDS key set
-  // with their smallest candidate order. Neighbouring pixels mostly hit the same blocks, so a sample
-  // whose key equals the key of the same step at the pixel to its left or above (a lane 1 or 16
-  // lower: the wave's 16x4 pixels are in raster order), or of the previous step at this pixel, is
-  // left out -- that sample has a smaller candidate order, and by induction some sample with the
-  // key and an order no larger is inserted. That removes most same-key LDS atomics (the serialised
-  // bank conflicts of r2's profile: 1.3 conflict cycles per LDS instruction cycle).
-  unsigned long long prev_key = 0ull;
-  for (int s = 0; s < P.maxs; ++s) {
-    const bool on = ray && s < nsamp;  // (uniform loop; the shuffles need every lane)
-    unsigned long long key = 0ull;
-    if (on) {
-      const int16_t kx = (int16_t)(round_s16(pos.x) >> kBlockLenBits);
-      const int16_t ky = (int16_t)(round_s16(pos.y) >> kBlockLenBits);
-      const int16_t kz = (int16_t)(round_s16(pos.z) >> kBlockLenBits);
-      pos.x += st.x;
-      pos.y += st.y;
-      pos.z += st.z;
-      key = pack_key(kx, ky, kz);
-    }
-    const int lane = lane_id();
-    const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
-    const uint32_t llo = __shfl_up(lo, 1, 64), lhi = __shfl_up(hi, 1, 64);
-    const uint32_t ulo = __shfl_up(lo, 16, 64), uhi = __shfl_up(hi, 16, 64);
-    const unsigned long long left = (lane & 15) ? (((unsigned long long)lhi << 32) | llo) : 0ull;
-    const unsigned long long up = lane >= 16 ? (((unsigned long long)uhi << 32) | ulo) : 0ull;
-    if (on && key != left && key != up && key != prev_key) {
-      const uint32_t order = order0 + (uint32_t)s;
-      uint32_t hs = tile_slot<TS>(key);
-      for (int p = 0; p < TS; ++p) {
-        const unsigned long long prev = atomicCAS(&s_key[hs], 0ull, key);
-        if (prev == 0ull || prev == key) {
-          atomicMin(&s_ord[hs], order);
-          break;
-        }
-        hs = (hs + 1) & (TS - 1);
-      }
-    }
-    prev_key = key;
-  }
-  TSDF_STAMP(D, 0, 3);
-  __syncthreads();
-  TSDF_STAMP(D, 0, 4);
-  // Each wave sweeps its 64-slot strips; the few occupied slots of a strip (ballot) are tested
-  // 8 at a time with 8 lanes per key, one block corner per lane (is_block_visible<true>), and the
-  // fully visible ones are listed in LDS. The table probes and new-key inserts then run one key
-  // per lane over that list, so the wave pays their memory latency once, not once per 8 keys.
-  uint16_t(*s_vis)[TS / 4] = S.u.tile.vis;
-  const int lane = lane_id(), wave = threadIdx.x >> 6;
-  const int grp = lane >> 3, corner = lane & 7;
-  int nv = 0;
-  for (int strip = wave; strip < TS / 64; strip += 4) {
-    const unsigned long long skey = s_key[strip * 64 + lane];
-    const unsigned long long occ = __ballot(skey != 0ull);
-    const int n = __popcll(occ);
-    for (int base = 0; base < n; base += 8) {
-      const int want = base + grp;  // rank of the occupied slot this 8-lane group handles
-      int src = 0;                  // lane holding that slot: binary search on prefix popcounts
-#pragma unroll
-      for (int step = 32; step > 0; step >>= 1)
-        if (src + step < 64 && __popcll(occ & ((1ull << (src + step)) - 1ull)) <= want) src += step;
-      const unsigned long long key = __shfl(skey, src, 64);
-      bool vis = false;
-      if (want < n) {
-        int16_t kx, ky, kz;
-        unpack_key(key, kx, ky, kz);
-        vis = voxel_visible(P, (int16_t)((int16_t)(kx << kBlockLenBits) + ((corner >> 0) & 1) * (kBlockLen - 1)),
-                            (int16_t)((int16_t)(ky << kBlockLenBits) + ((corner >> 1) & 1) * (kBlockLen - 1)),
-                            (int16_t)((int16_t)(kz << kBlockLenBits) + ((corner >> 2) & 1) * (kBlockLen - 1)));
-      }
-      const unsigned long long bal = __ballot(vis);
-      const bool lead = want < n && corner == 0 && ((bal >> (lane & ~7)) & 0xFFull) == 0xFFull;
-      const unsigned long long leads = __ballot(lead);
-      if (lead) s_vis[wave][nv + __popcll(leads & ((1ull << lane) - 1ull))] = (uint16_t)(strip * 64 + src);
-      nv += __popcll(leads);
-    }
-  }
-  for (int i = lane; i < nv; i += 64) {
-    const int slot = s_vis[wave][i];
-    const unsigned long long key = s_key[slot];
-    int16_t kx, ky, kz;
-    unpack_key(key, kx, ky, kz);
-    if (find_entry(D.table, kx, ky, kz) >= 0) continue;
-    nk_insert(D, key, s_ord[slot]);
-  }
-  TSDF_STAMP(D, 0, 5);
-}
-
 // a shard's split frame: the new-key set (this slice's keys) into the exchange slot, drained for
 // the merge of every shard's slots (k_resolve_alloc after the all-gather)
 __device__ void pack_keys_wg(const EngineDev& D, ShardRec* __restrict__ out, int cap) {
@@ -409,7 +156,11 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
     vis_sweep(D, P, blockIdx.x, S);
     TSDF_STAMP(D, 2, 1);
   } else if ((int)blockIdx.x - kVisWorkgroups < tiles) {  // tiles [P.tile_lo, P.tile_lo + tiles)
-    ingest_tile<TS>(D, P, depth, rgb, ht, lt, tiles_x, P.tile_lo + (int)blockIdx.x - kVisWorkgroups, S);
+    const int tile = P.tile_lo + (int)blockIdx.x - kVisWorkgroups;
+    if (P.prepared)
+      ingest_tile<TS, kTileProbe>(D, P, depth, rgb, ht, lt, tiles_x, tile, S);
+    else
+      ingest_tile<TS, kTileFull>(D, P, depth, rgb, ht, lt, tiles_x, tile, S);
   }
   if (!arrive_last(D.arrive + kArrIngest, 0ull, &S.last)) return;
   const unsigned long long tend = __builtin_amdgcn_s_memrealtime();
@@ -424,8 +175,10 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
   if (threadIdx.x == 0) D.ctr->ingest_ticks += tend - ld_co(&D.arrive[kArrStart + 8]);
   TSDF_STAMP(D, 6, 2);
 }
+// at least 6 waves per SIMD (<= 80 VGPRs): the whole 640x480 grid (1456 workgroups) resident at once;
+// the resolver tail alone would raise the kernel to 81 VGPRs (5 waves: 1280 workgroups, +2 us span)
 template <int TS>
-__global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TS <= 1024 ? 6 : 5))) void k_ingest_dda(EngineDev D, FrameParams P,
                                                     const float* __restrict__ depth,
                                                     const uint8_t* __restrict__ rgb,
                                                     const float* __restrict__ ht,
@@ -434,7 +187,7 @@ __global__ __launch_bounds__(256) void k_ingest_dda(EngineDev D, FrameParams P,
   ingest_dda<TS>(D, P, depth, rgb, ht, lt, tiles_x, tiles);
 }
 template <int TS>
-__global__ __launch_bounds__(256) void k_ingest_dda_g(EngineDev D, const FrameArgs* __restrict__ A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TS <= 1024 ? 6 : 5))) void k_ingest_dda_g(EngineDev D, const FrameArgs* __restrict__ A) {
   const FrameParams P = A->P;
   ingest_dda<TS>(D, P, A->depth, A->rgb, A->ht, A->lt, A->tiles_x, A->tiles);
 }

@@ -158,6 +158,13 @@ struct tsdf_engine {
   bool shard_keys_packed = false;  // _begin wrote a key slot (split DDA): _update merges an inbox
   FrameParams shard_P{};
   std::array<hipEvent_t, 5>* shard_ev = nullptr;
+  // pipelined frames (tsdf_integrate on one volume): the update of the last integrated frame is
+  // deferred to the next engine call, where it runs in one launch with the next frame's pixel-tile
+  // preparation (k_integrate_pre); every other entry point first enqueues it (flush_pending)
+  bool pipeline = false;  // (default set in tsdf_create)
+  bool pend = false;
+  FrameParams pend_P{};
+  std::array<hipEvent_t, 5>* pend_ev = nullptr;
   // feed_rgbd_frame staging: raw full-size inputs (host frames) and the half-size outputs
   uint8_t* fe_rgb = nullptr;
   uint16_t* fe_depth = nullptr;
@@ -175,7 +182,7 @@ void free_all(tsdf_engine* e) {
   void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.occ,
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs, D.fresh,
                   e->fe_rgb, e->fe_depth, e->fe_mask, e->fe_out_rgb, e->fe_out_depth,
-                  D.vis,     D.band,    D.cand,     D.arrive, D.fresh_vis, D.pend, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
+                  D.vis,     D.band,    D.cand,     D.arrive, D.fresh_vis, D.pend, D.pixA,     D.pixB,    D.tkeys, D.tcount, D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
                   e->vg_cell, e->vg_flags, e->vg_bits, e->g_visbits, e->g_wgcnt, e->g_sel, e->g_count,
                   e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
@@ -236,6 +243,9 @@ FrameParams make_params(const tsdf_engine* e, const tsdf_intrinsics* K, int W, i
   P.rgb = nullptr;
   P.ht = nullptr;
   P.lt = nullptr;
+  P.pixA = e->D.pixA;  // pixel-record buffer 0 (a pipelined frame may take buffer 1)
+  P.pixB = e->D.pixB;
+  P.prepared = 0;
   return P;
 }
 
@@ -292,8 +302,19 @@ int join_render(tsdf_engine* e) {
     if (_rc) return _rc;            \
   } while (0)
 
+int flush_pending(tsdf_engine* e);
+// every entry point that reads or writes the volume (or orders against it) first enqueues a deferred
+// update (pipelined frames) and joins the render stream
+#define ENTER(e)                       \
+  do {                                 \
+    int _rc = flush_pending(e);        \
+    if (_rc) return _rc;               \
+    _rc = join_render(e);              \
+    if (_rc) return _rc;               \
+  } while (0)
+
 int read_counters(tsdf_engine* e) {
-  JOIN_RENDER(e);
+  ENTER(e);
   HIP_OK(hipMemcpyAsync(e->h_ctr, e->D.ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
   return TSDF_OK;
@@ -472,8 +493,14 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
     if (const char* v = std::getenv("TSDF_INTEGRATE_WG_PER_CU")) per_cu = std::min(per_cu, std::atoi(v));  // tuning
     D.integrate_grid = std::max(8, std::min(kIntegrateGrid, (per_cu * ncu) & ~7));
   }
-  ALLOC(D.pixA, e->max_pixels);
-  ALLOC(D.pixB, e->max_pixels);
+  ALLOC(D.pixA, 2 * e->max_pixels);  // two buffers: a pipelined frame's and the next one's
+  ALLOC(D.pixB, 2 * e->max_pixels);
+  {
+    const int64_t tiles_max = (int64_t)((cfg.max_width + 15) / 16) * ((cfg.max_height + 15) / 16);
+    ALLOC(D.tkeys, tiles_max * kTileKeyCap);
+    ALLOC(D.tcount, tiles_max);
+  }
+  if (const char* v = std::getenv("TSDF_PIPELINE")) e->pipeline = v[0] == '1';
   ALLOC(D.visbits, kOccWords);
   ALLOC(D.wgcnt, kOccWords / 256);
   ALLOC(D.dbg, (size_t)kDiagKernels * kDiagMaxWg * kDiagStamps);
@@ -530,7 +557,7 @@ int tsdf_destroy(tsdf_engine* e) {
 
 int tsdf_synchronize(tsdf_engine* e) {
   if (!e) return TSDF_ERR_INVALID_ARG;
-  JOIN_RENDER(e);
+  ENTER(e);
   HIP_OK(hipStreamSynchronize(e->stream));
   return TSDF_OK;
 }
@@ -540,9 +567,14 @@ namespace {
 // Phase 1 of a frame: stage host inputs, then k_ingest_dda (pixel records for the whole frame, the
 // DDA over tiles of slice `slice_index` of `slice_count` -- contiguous bands of tile rows --, the
 // visibility of the existing blocks). *P / *ev carry the frame to the later phases.
+int frame_update(tsdf_engine* e, FrameParams P, std::array<hipEvent_t, 5>* ev, void* cands_out = nullptr,
+                 int cand_cap = 0, const FrameParams* Pn = nullptr, int tiles_x = 0, int tiles = 0);
+// pipelined: the pending frame's update is launched here with this frame's pixel-tile preparation
+// (k_integrate_pre), and this frame's ingest only probes the prepared keys
 int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, const tsdf_pose* pose,
                  float max_depth, int slice_index, int slice_count, FrameParams* P,
-                 std::array<hipEvent_t, 5>** ev_out, void* keys_out = nullptr, int key_cap = 0) {
+                 std::array<hipEvent_t, 5>** ev_out, void* keys_out = nullptr, int key_cap = 0,
+                 bool pipelined = false) {
   if (!e || !f || !K || !pose || !f->depth || !f->rgb || f->width <= 0 || f->height <= 0 ||
       (int64_t)f->width * f->height > e->max_pixels || f->width > e->cfg.max_width ||
       f->height > e->cfg.max_height || (f->ht == nullptr) != (f->lt == nullptr) ||
@@ -604,6 +636,16 @@ int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, 
     ev = &e->events[e->ev_used++];
   }
   *ev_out = ev;
+  if (pipelined && e->pend) {
+    // this frame's pixel records go to the buffer the pending frame does not read
+    const bool b0 = e->pend_P.pixA == e->D.pixA;
+    P->pixA = e->D.pixA + (b0 ? e->max_pixels : 0);
+    P->pixB = e->D.pixB + (b0 ? e->max_pixels : 0);
+    e->pend = false;
+    int rc = frame_update(e, e->pend_P, e->pend_ev, nullptr, 0, P, tiles_x, tiles);
+    if (rc) return rc;
+    P->prepared = 1;
+  }
   if (ev && e->prof_mode == TSDF_PROFILE_PHASES) HIP_OK(hipEventRecord((*ev)[0], s));
   // ---- allocate (voxel_tsdf.cu:377-386) + visibility (:388-397) ----
   // k_ingest_dda sweeps the blocks that already exist for visibility beside the DDA; its last
@@ -623,8 +665,8 @@ int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, 
 // the existing blocks beside the allocation resolver, on a second stream or as a dispatch without
 // the AQL barrier bit: the resolver's chain of dependent HBM round trips slows ~2.5x under the
 // update's memory load.)
-int frame_update(tsdf_engine* e, FrameParams P, std::array<hipEvent_t, 5>* ev, void* cands_out = nullptr,
-                 int cand_cap = 0) {
+int frame_update(tsdf_engine* e, FrameParams P, std::array<hipEvent_t, 5>* ev, void* cands_out, int cand_cap,
+                 const FrameParams* Pn, int tiles_x, int tiles) {
   hipStream_t s = e->stream;
   JOIN_RENDER(e);  // the update writes the pool a raycast on the render stream may still read
   const bool all_ev = ev && e->prof_mode == TSDF_PROFILE_PHASES;
@@ -634,7 +676,17 @@ int frame_update(tsdf_engine* e, FrameParams P, std::array<hipEvent_t, 5>* ev, v
   P.slot_cap = cand_cap;
   // ---- update (voxel_tsdf.cu:474-481) + space carving (:483-488) ----
   auto kfn = P.pack_pixels ? k_integrate_t<false, false> : k_integrate_t<false, true>;
-  if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
+  if (Pn) {  // + the next frame's pixel tiles (pipelined frames)
+    const dim3 grid(e->D.integrate_grid + tiles);
+    if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
+      hipExtLaunchKernelGGL(k_integrate_pre, grid, dim3(kIntegrateThreads), 0, s, (*ev)[2], (*ev)[3], 0, e->D, P,
+                            *Pn, tiles_x);
+    } else {
+      if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
+      hipLaunchKernelGGL(k_integrate_pre, grid, dim3(kIntegrateThreads), 0, s, e->D, P, *Pn, tiles_x);
+      if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
+    }
+  } else if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
     // the two events are bound to the kernel's own dispatch packet (its begin / end timestamps,
     // the interval rocprofv3's kernel trace reports): no marker packets enter the stream
     hipExtLaunchKernelGGL(kfn, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
@@ -652,8 +704,20 @@ int frame_update(tsdf_engine* e, FrameParams P, std::array<hipEvent_t, 5>* ev, v
 
 bool sharded(const tsdf_engine* e) { return e->cfg.shard_count > 1; }
 
+// the deferred update of the last pipelined frame, enqueued on its own
+int flush_pending(tsdf_engine* e) {
+  if (!e->pend) return TSDF_OK;
+  e->pend = false;
+  return frame_update(e, e->pend_P, e->pend_ev);
+}
+
 }  // namespace
 
+// One frame (TSDFGrid::Integrate). Pipelined (one volume, <= 3 DDA samples per pixel): the frame's
+// ingest is launched now and its update is deferred -- the next tsdf_integrate launches it together
+// with the next frame's pixel-tile preparation (k_integrate_pre), any other entry point (and
+// tsdf_flush / tsdf_synchronize) launches it alone. Stream order keeps every result identical to
+// the unpipelined two launches per frame.
 int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
                    const tsdf_pose* pose, float max_depth) {
   TraceRange trace_("tsdf_integrate");
@@ -661,11 +725,27 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
     set_error("tsdf_integrate: a shard of a sharded volume integrates through tsdf_integrate_shard_*");
     return TSDF_ERR_INVALID_ARG;
   }
+  if (e && (!e->pipeline || e->maxs > 3)) {
+    int rc = flush_pending(e);
+    if (rc) return rc;
+  }
+  const bool pipe = e && e->pipeline && e->maxs <= 3;
   FrameParams P;
   std::array<hipEvent_t, 5>* ev = nullptr;
-  int rc = frame_ingest(e, f, K, pose, max_depth, 0, 1, &P, &ev);
+  int rc = frame_ingest(e, f, K, pose, max_depth, 0, 1, &P, &ev, nullptr, 0, pipe);
   if (rc) return rc;
-  return frame_update(e, P, ev);
+  if (!pipe) return frame_update(e, P, ev);
+  e->pend = true;
+  e->pend_P = P;
+  e->pend_ev = ev;
+  return TSDF_OK;
+}
+
+int tsdf_flush(tsdf_engine* e) {
+  if (!e) return TSDF_ERR_INVALID_ARG;
+  HIP_OK(hipSetDevice(e->device));
+  ENTER(e);
+  return TSDF_OK;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -687,7 +767,7 @@ int tsdf_integrate_shard_begin(tsdf_engine* e, const tsdf_frame* f, const tsdf_i
               "slot unless slice_count == 1)");
     return TSDF_ERR_INVALID_ARG;
   }
-  JOIN_RENDER(e);
+  ENTER(e);
   FrameParams P;
   std::array<hipEvent_t, 5>* ev = nullptr;
   // split DDA: the last workgroup packs this slice's keys into keys_out; whole-frame DDA (no key
@@ -714,7 +794,7 @@ int tsdf_integrate_shard_update(tsdf_engine* e, const void* keys_in, int32_t key
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   if (keys_in) {  // merge every shard's keys, then the ordered allocation (one workgroup)
     const FrameParams& P = e->shard_P;
     hipLaunchKernelGGL(k_resolve_alloc, dim3(1), dim3(kRT), 0, e->stream, e->D, P,
@@ -736,7 +816,7 @@ int tsdf_integrate_shard_end(tsdf_engine* e, const void* cands_in, int32_t cand_
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kRT), 0, e->stream, e->D, (const VisRec*)e->D.cand,
                      (const int32_t*)&e->D.ctr->n_cand, 0, reinterpret_cast<const ShardRec*>(cands_in),
                      cand_cap, e->cfg.shard_count);
@@ -755,7 +835,7 @@ int tsdf_integrate_shard_abort(tsdf_engine* e) {
   }
   if (e->shard_phase == 0) return TSDF_OK;  // nothing pending
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   e->shard_phase = 0;
   e->shard_ev = nullptr;
   hipLaunchKernelGGL(k_shard_abort, dim3(1), dim3(256), 0, e->stream, e->D);
@@ -898,7 +978,7 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   auto* g = new tsdf_graph();
   g->e = e;
   g->W = width;
@@ -963,7 +1043,7 @@ int tsdf_graph_create_shard(tsdf_engine* e, int width, int height, int slice_ind
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   auto* g = new tsdf_graph();
   g->e = e;
   g->W = width;
@@ -1034,7 +1114,7 @@ int tsdf_graph_shard_begin(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrin
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   const int k = g->next;
   g->next = (k + 1) % tsdf_graph::kSlots;
   if (g->used[k]) HIP_OK(hipEventSynchronize(g->done[k]));  // slot k's upload has run
@@ -1100,7 +1180,7 @@ int tsdf_graph_shard_end(tsdf_graph* g) {
   }
   tsdf_engine* e = g->e;
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   HIP_OK(hipGraphLaunch(g->exec[g->cur][2], e->stream));
   g->cur = -1;
   e->shard_phase = 0;
@@ -1123,7 +1203,7 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   const int k = g->next;
   g->next = (k + 1) % tsdf_graph::kSlots;
   if (g->used[k]) HIP_OK(hipEventSynchronize(g->done[k]));  // slot k's upload has run
@@ -1276,7 +1356,7 @@ int raycast_impl(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const t
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   FrameParams P = make_params(e, K, W, H, pose, max_depth);
   P.row0 = row0;
   P.nrows = nrows;
@@ -1310,7 +1390,7 @@ int raycast_impl(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const t
     e->render_pending = true;
   }
   if (mem_kind == TSDF_MEM_HOST) {
-    JOIN_RENDER(e);
+    ENTER(e);
     const size_t bytes = (size_t)W * nrows * 4;
     if (rgba) HIP_OK(hipMemcpyAsync(rgba, e->rc_rgba, bytes, hipMemcpyDeviceToHost, e->stream));
     if (normal) HIP_OK(hipMemcpyAsync(normal, e->rc_norm, bytes, hipMemcpyDeviceToHost, e->stream));
@@ -1337,7 +1417,7 @@ int tsdf_query(tsdf_engine* e, const float* bounds, tsdf_voxel* out, int64_t cap
   TraceRange trace_("tsdf_query");
   if (!e || !count) return TSDF_ERR_INVALID_ARG;
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   short4 lo = make_short4(0, 0, 0, 0), hi = make_short4(0, 0, 0, 0);
   if (bounds) {  // BoundingCube::Scale<short>(1. / voxel_size_) (voxel_tsdf.cuh:21-26, :429)
     const float scale = (float)(1. / (double)e->cfg.voxel_size);
@@ -1409,7 +1489,7 @@ int tsdf_reset(tsdf_engine* e) {
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   if (!init_state(e)) {
     set_error("tsdf_reset: initialisation failed");
     return TSDF_ERR_HIP;
@@ -1452,7 +1532,7 @@ int tsdf_render_blocks(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H,
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   const FrameParams P = make_params(e, K, W, H, pose, max_depth);
   const RenderCull C = render_cull(e, P, W, 0, H);
   hipStream_t s = e->stream;
@@ -1559,7 +1639,7 @@ int tsdf_render_bands(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, co
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   const FrameParams P = make_params(e, K, W, H, pose, max_depth);
   GroupSel S{};
   S.mode = kGroupBands;
@@ -1586,7 +1666,7 @@ int tsdf_pack_halo(tsdf_engine* e, void* out, int64_t capacity, int64_t* counts,
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   FrameParams P{};
   P.shard_index = e->cfg.shard_index;
   P.shard_count = e->cfg.shard_count;
@@ -1604,7 +1684,7 @@ int tsdf_pack_blocks(tsdf_engine* e, const float* bounds, void* out, int64_t cap
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   short4 lo = make_short4(0, 0, 0, 0), hi = make_short4(0, 0, 0, 0);
   if (bounds) {  // the Query block selection (voxel_tsdf.cuh:21-26, voxel_tsdf.cu:429)
     const float scale = (float)(1. / (double)e->cfg.voxel_size);
@@ -1641,7 +1721,7 @@ int tsdf_import_blocks(tsdf_engine* e, const void* records, int64_t n, int mem_k
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   if (replace && !init_state(e, false)) {
     set_error("tsdf_import_blocks: clearing the volume failed");
     return TSDF_ERR_HIP;
@@ -1710,7 +1790,7 @@ int extract_mesh_impl(tsdf_engine* e, const float* bounds, float missing_tsdf, i
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   short4 lo = make_short4(0, 0, 0, 0), hi = make_short4(0, 0, 0, 0);
   if (bounds) {  // the Query block selection (voxel_tsdf.cuh:21-26, voxel_tsdf.cu:429)
     const float scale = (float)(1. / (double)e->cfg.voxel_size);
@@ -1783,7 +1863,7 @@ int tsdf_extract_mesh_owned(tsdf_engine* e, const float* bounds, float missing_t
 int tsdf_get_stats(tsdf_engine* e, tsdf_stats* o, int clear_status) {
   if (!e || !o) return TSDF_ERR_INVALID_ARG;
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   int rc = read_counters(e);
   if (rc) return rc;
   const DevCounters& c = *e->h_ctr;
@@ -1858,7 +1938,7 @@ int tsdf_profile_end(tsdf_engine* e, tsdf_profile* o) {
 int tsdf_debug_stamps(tsdf_engine* e, uint64_t* out, int64_t capacity, int* enabled) {
   if (!e) return TSDF_ERR_INVALID_ARG;
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
 #ifdef TSDF_DIAG_STAMPS
   if (enabled) *enabled = 1;
 #else
@@ -1971,7 +2051,7 @@ int tsdf_snapshot_save(tsdf_engine* e, void* out, int64_t capacity) {
     return TSDF_ERR_CAPACITY;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   hipStream_t s = e->stream;
   uint8_t* p = static_cast<uint8_t*>(out);
   SnapshotHeader h{};
@@ -2016,7 +2096,7 @@ int tsdf_snapshot_load(tsdf_engine* e, const void* in, int64_t size) {
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   hipStream_t s = e->stream;
   const uint8_t* p = static_cast<const uint8_t*>(in) + sizeof(h);
   HIP_OK(hipMemcpyAsync(e->D.ctr, p, sizeof(DevCounters), hipMemcpyHostToDevice, s));
@@ -2038,7 +2118,7 @@ int tsdf_debug_dump(tsdf_engine* e, int16_t* pos_off, int32_t* idx, int32_t* hea
                     int32_t* free_count, float* tsdf_out, float* prob, uint8_t* rgbw) {
   if (!e) return TSDF_ERR_INVALID_ARG;
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   hipStream_t s = e->stream;
   if (pos_off || idx) {
     short4* dpos = nullptr;
@@ -2097,7 +2177,7 @@ int tsdf_hash_allocate(tsdf_engine* e, const int16_t* keys, int n) {
   if (!e || n < 0 || (n > 0 && !keys) || n > (int)kNewKeyCap) return TSDF_ERR_INVALID_ARG;
   if (n == 0) return TSDF_OK;
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   int rc = ensure_test_cap(e, n);
   if (rc) return rc;
   HIP_OK(hipMemcpyAsync(e->t_keys, keys, sizeof(int16_t) * 3 * n, hipMemcpyHostToDevice, e->stream));
@@ -2114,7 +2194,7 @@ int tsdf_hash_delete(tsdf_engine* e, const int16_t* keys, int n) {
   if (!e || n < 0 || (n > 0 && !keys)) return TSDF_ERR_INVALID_ARG;
   if (n == 0) return TSDF_OK;
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   int rc = ensure_test_cap(e, n);
   if (rc) return rc;
   std::vector<VisRec> recs(n);
@@ -2140,7 +2220,7 @@ int tsdf_hash_retrieve(tsdf_engine* e, const int16_t* pts, int n, uint8_t* rgbw,
   if (!e || n < 0 || (n > 0 && !pts)) return TSDF_ERR_INVALID_ARG;
   if (n == 0) return TSDF_OK;
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   int rc = ensure_test_cap(e, n);
   if (rc) return rc;
   hipStream_t s = e->stream;
@@ -2162,7 +2242,7 @@ int tsdf_hash_assign(tsdf_engine* e, const int16_t* pts, int n, const uint8_t* r
   if (missing) *missing = 0;
   if (n == 0) return TSDF_OK;
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  ENTER(e);
   int rc = ensure_test_cap(e, n);
   if (rc) return rc;
   hipStream_t s = e->stream;
@@ -2189,7 +2269,7 @@ int tsdf_num_active_blocks(tsdf_engine* e, int32_t* out) {
 
 int tsdf_pool_acquire(tsdf_engine* e, int n, int32_t* idx_out) {
   if (!e || n < 0 || (n > 0 && !idx_out)) return TSDF_ERR_INVALID_ARG;
-  JOIN_RENDER(e);
+  ENTER(e);
   if (n == 0) return TSDF_OK;
   int rc = ensure_test_cap(e, n);
   if (rc) return rc;
@@ -2202,7 +2282,7 @@ int tsdf_pool_acquire(tsdf_engine* e, int n, int32_t* idx_out) {
 
 int tsdf_pool_release(tsdf_engine* e, const int32_t* idx, int n) {
   if (!e || n < 0 || (n > 0 && !idx)) return TSDF_ERR_INVALID_ARG;
-  JOIN_RENDER(e);
+  ENTER(e);
   if (n == 0) return TSDF_OK;
   int rc = ensure_test_cap(e, n);
   if (rc) return rc;
@@ -2215,7 +2295,7 @@ int tsdf_pool_release(tsdf_engine* e, const int32_t* idx, int n) {
 
 int tsdf_pool_set_weight(tsdf_engine* e, int32_t block, uint8_t w) {
   if (!e || block < 0 || block >= e->D.nblocks) return TSDF_ERR_INVALID_ARG;
-  JOIN_RENDER(e);
+  ENTER(e);
   hipLaunchKernelGGL(k_pool_weight, dim3(1), dim3(kBlockVolume), 0, e->stream, e->D, block, 1, w,
                      (uint8_t*)nullptr);
   LAUNCH_OK("k_pool_weight");
@@ -2225,7 +2305,7 @@ int tsdf_pool_set_weight(tsdf_engine* e, int32_t block, uint8_t w) {
 
 int tsdf_pool_get_weights(tsdf_engine* e, int32_t block, uint8_t* out) {
   if (!e || !out || block < 0 || block >= e->D.nblocks) return TSDF_ERR_INVALID_ARG;
-  JOIN_RENDER(e);
+  ENTER(e);
   int rc = ensure_test_cap(e, kBlockVolume);
   if (rc) return rc;
   uint8_t* d = reinterpret_cast<uint8_t*>(e->t_u32);

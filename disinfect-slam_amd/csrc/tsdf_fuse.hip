@@ -2,6 +2,7 @@
 #include "tsdf_block.h"
 #include "tsdf_kernels.h"
 #include "tsdf_resolve.h"
+#include "tsdf_ingest.h"
 
 namespace tsdf {
 
@@ -135,9 +136,14 @@ __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FramePa
 // Raw: a shard's frame -- the pixel terms come from the raw frame (depth, rgb, ht, lt gathers) and
 // are computed per voxel with the ingest's operations (pixel_w_new, pixel_logodds, the range of
 // pixel_ray), instead of from pixel records packed for the whole frame.
+#ifndef TSDF_INTEGRATE_WAVES
+#define TSDF_INTEGRATE_WAVES 8
+#endif
+// nint: the update's workgroups (blocks [0, nint) of the launch; k_integrate_pre appends the next
+// frame's pixel-tile workgroups after them). L: the LDS of the last arriver's carving resolve.
 template <bool Graph, bool Raw>
-__global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_integrate_t(
-    EngineDev D, FrameParams Pv, const FrameArgs* __restrict__ A) {
+__device__ __forceinline__ void integrate_body(const EngineDev& D, const FrameParams& Pv,
+                                               const FrameArgs* __restrict__ A, int nint, DeleteLds& L) {
   FrameParams P = Graph ? A->P : Pv;
   if (Graph && A->cands_out) {  // a shard's graph frame: the tail packs the carve candidates
     P.tail = kTailPack;
@@ -151,7 +157,6 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
   __shared__ int s_last;
   __shared__ int s_ncand, s_ovf;
   __shared__ VisRec s_cand[kIntegrateCandBuf];  // this workgroup's carve candidates
-  __shared__ DeleteLds L;  // the last-arriving workgroup's carving resolve
   const int lane = lane_id();
   // wave-uniform (scalar) loop state: the band search, the list record and the fresh flag are
   // SALU / scalar loads instead of per-lane selects
@@ -167,7 +172,7 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
   }
   const int nband = nvis;
   nvis += D.ctr->n_fresh;
-  const int g = blockIdx.x & 7, ngrp = gridDim.x >> 3;
+  const int g = blockIdx.x & 7, ngrp = nint >> 3;
   const int rx0 = (lane & 1) * 4, ry = (lane >> 1) & 7, rz = (lane >> 4) + 4 * hf;
   const int off = (hf * 256 + lane * 4) * 4;
   const float neg_trunc = -P.trunc;
@@ -284,8 +289,8 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
             px[j] = make_float4(P.depth[img], __int_as_float(uu[e]), __int_as_float(vv[e]), __uint_as_float(c));
             lg[j] = P.ht ? pixel_logodds(P.ht[img], P.lt[img]) : 0.0f;
           } else {
-            px[j] = D.pixA[img];
-            lg[j] = D.pixB[img];
+            px[j] = P.pixA[img];
+            lg[j] = P.pixB[img];
           }
 #endif
         }
@@ -429,7 +434,36 @@ __global__ __launch_bounds__(kIntegrateThreads) __attribute__((amdgpu_waves_per_
   // waves that published drain their stores before the workgroup arrives (wave 0: the buffer;
   // the even waves' lane 0: overflow records)
   const bool drain = (wave == 0 && nc > 0) || (s_ovf && (wave & 1) == 0);
-  if (arrive_last(D.arrive + kArrIntegrate, wg_upd, &s_last, drain)) integrate_tail(D, P, L);
+  if (arrive_last(D.arrive + kArrIntegrate, wg_upd, &s_last, drain, (uint32_t)nint)) integrate_tail(D, P, L);
+}
+
+template <bool Graph, bool Raw>
+__global__ __launch_bounds__(kIntegrateThreads)
+__attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES))) void k_integrate_t(
+    EngineDev D, FrameParams Pv, const FrameArgs* __restrict__ A) {
+  __shared__ DeleteLds L;  // the last-arriving workgroup's carving resolve
+  integrate_body<Graph, Raw>(D, Pv, A, (int)gridDim.x, L);
+}
+
+// A pipelined frame's second launch: the update of frame n (workgroups [0, D.integrate_grid), its
+// last arriver carves) and, after them, one workgroup per pixel tile of frame n + 1 preparing its
+// pixel records (Pn.pixA / pixB, the other buffer) and its DDA keys (kTilePrepass). The tile
+// workgroups read only frame n + 1 and the camera, write only their own buffers, and take no part
+// in the arrival: they fill the CUs the update's workgroups leave as they finish, and frame n + 1's
+// k_ingest_dda probes their keys after this launch (and so after frame n's carving).
+__global__ __launch_bounds__(kIntegrateThreads)
+__attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES))) void k_integrate_pre(
+    EngineDev D, FrameParams P, FrameParams Pn, int tiles_x) {
+  __shared__ union {
+    DeleteLds del;
+    IngestLds<1024> ing;
+  } U;
+  const int nint = D.integrate_grid;
+  if ((int)blockIdx.x >= nint) {
+    ingest_tile<1024, kTilePrepass>(D, Pn, Pn.depth, Pn.rgb, Pn.ht, Pn.lt, tiles_x, (int)blockIdx.x - nint, U.ing);
+    return;
+  }
+  integrate_body<false, false>(D, P, nullptr, nint, U.del);
 }
 template __global__ void k_integrate_t<false, false>(EngineDev, FrameParams, const FrameArgs*);
 template __global__ void k_integrate_t<true, false>(EngineDev, FrameParams, const FrameArgs*);

@@ -24,6 +24,14 @@ __device__ __forceinline__ int block_band(const FrameParams& P, int16_t bx, int1
   return pc.z > 0.f && bandf > 0.f ? min(kBands - 1, f2i(bandf)) : 0;
 }
 
+// one prepared DDA key of a pixel tile: the block key and its smallest candidate order in the tile
+struct alignas(16) TileKey {
+  unsigned long long key;
+  uint32_t order;
+  uint32_t pad;
+};
+constexpr int kTileKeyCap = 1024;  // distinct keys a 16x16 tile can hold (the LDS key set, maxs <= 3)
+
 // device pointers of one engine (passed by value to every kernel)
 struct EngineDev {
   int4* table;                  // kNumEntry hash entries
@@ -49,9 +57,13 @@ struct EngineDev {
   VisRec* fresh_vis;            // kNewKeyCap blocks created this frame (k_resolve_alloc frame mode)
   VisRec* pend;                 // kNewKeyCap: a shard's owned entries its exhausted pool left without
                                 // voxels this frame (ctr->n_pend); carved in the same frame
-  // packed frame
+  // packed frame: two buffers of max_pixels records each (FrameParams.pixA / pixB select one)
   float4* pixA;                 // {depth, range, w_new, rgb}
   float* pixB;                  // log2 ht - log2 lt (base-2 log-odds of the pixel)
+  // pipelined frames: the DDA keys each pixel tile of the next frame prepared (k_integrate_pre),
+  // kTileKeyCap records per tile, probed by that frame's k_ingest_dda
+  struct TileKey* tkeys;
+  int32_t* tcount;
   // query scratch
   unsigned long long* visbits;  // kOccWords
   int32_t* wgcnt;               // kOccWords / 256
@@ -139,6 +151,8 @@ __global__ void k_resolve_alloc_g(EngineDev D, const FrameArgs* A);
 __global__ void k_resolve_delete_g(EngineDev D, const FrameArgs* A);
 template <bool Graph, bool Raw>
 __global__ void k_integrate_t(EngineDev D, FrameParams P, const FrameArgs* A);
+// pipelined frames: the update of P's frame + the pixel-tile preparation of the next frame Pn
+__global__ void k_integrate_pre(EngineDev D, FrameParams P, FrameParams Pn, int tiles_x);
 // graph-captured forms of the frame kernels: identical bodies, arguments from FrameArgs
 template <int TS>
 __global__ void k_ingest_dda_g(EngineDev D, const FrameArgs* A);

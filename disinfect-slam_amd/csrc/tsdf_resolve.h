@@ -66,14 +66,16 @@ __device__ __forceinline__ void st_co(T* p, T v) {
 // ---------------------------------------------------------------------------------------------
 constexpr int kArrLine = 16;  // u64 per 128-B line
 // drain: this wave published data (wave-uniform); other waves' outstanding stores stay in flight
+// nwg: the arriving workgroups, blocks [0, nwg) of the launch (0: the whole grid)
 __device__ __forceinline__ bool arrive_last(unsigned long long* words, unsigned long long payload,
-                                            int* s_flag, bool drain = true) {
+                                            int* s_flag, bool drain = true, uint32_t nwg = 0u) {
   if (drain) __builtin_amdgcn_s_waitcnt(0);
   lds_barrier();
   if (threadIdx.x == 0) {
     constexpr uint32_t NG = (uint32_t)kArrGroups;
-    const uint32_t g = blockIdx.x % NG, ngrp = gridDim.x < NG ? gridDim.x : NG;
-    const uint32_t expect = (gridDim.x - g + NG - 1u) / NG;
+    const uint32_t nw = nwg ? nwg : gridDim.x;
+    const uint32_t g = blockIdx.x % NG, ngrp = nw < NG ? nw : NG;
+    const uint32_t expect = (nw - g + NG - 1u) / NG;
     const unsigned long long old = __hip_atomic_fetch_add(&words[g * kArrLine], (1ull << 40) | payload,
                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int last = 0;
@@ -515,6 +517,108 @@ __device__ void resolve_alloc_wave(const EngineDev& D, const FrameParams& P, int
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Commit-all fast path of the allocation resolver (a frame stream's steady state: tens of new keys
+// per frame in a table ~1 % full). When every key's bucket has an empty slot (the SLOT case of
+// voxel_hash.cu:79-91), no two keys share a bucket and the pool holds a block for every key this
+// engine owns, the canonical linearisation commits every key: each locks only its own bucket, so
+// no lock is lost and no key writes another key's bucket, and AquireBlock's pops go to the owned
+// keys in candidate order. Then there is no round, no sort and no claim table: one key per thread,
+// the distinct-bucket test in the LDS lock set, each key's pop rank by a broadcast scan of the
+// candidate orders. Any other launch returns false before anything global is written, and the
+// ordered resolver below handles it. Results are identical either way (the oracle decides:
+// tests/test_gpu_*.py run both paths).
+// ---------------------------------------------------------------------------------------------
+#ifdef TSDF_NO_FAST_RESOLVE
+__device__ constexpr bool resolve_fast_off() { return true; }
+#else
+__device__ constexpr bool resolve_fast_off() { return false; }
+#endif
+constexpr int kFastLockSlots = 1024;
+
+template <int RB>
+__device__ bool resolve_alloc_fast(const EngineDev& D, const FrameParams& P, int frame_mode, int n, int free0,
+                                   uint32_t epoch, unsigned long long key, int32_t slot, AllocLdsT<RB>& L,
+                                   unsigned long long tick0) {
+  static_assert(AllocLdsT<RB>::kLock >= kFastLockSlots && 2 * (RB + 2) >= kRT && RB >= kRT, "fast-path LDS");
+  const int t = threadIdx.x, wave = t >> 6;
+  const bool have = t < n;
+  for (int i = t; i < kFastLockSlots; i += kRT) L.lock[i] = 0u;
+  int16_t x = 0, y = 0, z = 0;
+  uint32_t B = 0, ord = 0xFFFFFFFFu;
+  bool e0 = false, e1 = false;
+  if (have) {
+    unpack_key(key, x, y, z);
+    B = hash_block(x, y, z);
+    ord = ld_co(&D.nk_order[slot]);
+    const Ent s0 = load_ent(D.table, 2 * B), s1 = load_ent(D.table, 2 * B + 1);
+    e0 = s0.idx < 0;
+    e1 = s1.idx < 0;
+  }
+  const int32_t htop = t < min(n, max(free0, 0)) ? D.heap[free0 - 1 - t] : 0;
+  const bool owned = have && (P.shard_count <= 1 ||
+                              brick_owner(x, y, z, (uint32_t)P.shard_count) == (uint32_t)P.shard_index);
+  lds_barrier();  // the lock set is zero
+  // a key whose bucket an earlier key of the launch already holds would be dropped: not this path
+  const bool bad = have && (!(e0 || e1) || !lock_take2<kFastLockSlots>(L.lock, B));
+  uint32_t* ordv = reinterpret_cast<uint32_t*>(L.batch);
+  ordv[t] = owned ? ord : 0xFFFFFFFFu;  // (threads >= n pad the scan with "never smaller")
+  L.heap_top[t] = htop;
+  const unsigned long long bo = __ballot(owned), bb = __ballot(bad);
+  if (lane_id() == 0) {
+    L.scan[wave] = __popcll(bo);
+    L.scan[4 + wave] = __popcll(bb);
+  }
+  lds_barrier();
+  const int nowned = L.scan[0] + L.scan[1] + L.scan[2] + L.scan[3];
+  if (L.scan[4] + L.scan[5] + L.scan[6] + L.scan[7] != 0 || nowned > free0) return false;
+  if (have) {
+    // pop rank: owned keys earlier in candidate order (orders are unique per key)
+    int prank = 0;
+    if (owned) {
+      const uint4* v4 = reinterpret_cast<const uint4*>(ordv);
+      const int nq = (n + 3) >> 2;
+      for (int j = 0; j < nq; ++j) {
+        const uint4 v = v4[j];
+        prank += (v.x < ord) + (v.y < ord) + (v.z < ord) + (v.w < ord);
+      }
+    }
+    const int32_t idx = owned ? L.heap_top[prank] : kForeignIdx;
+    const uint32_t e = 2 * B + (e0 ? 0u : 1u);
+    store_ent(D.table, e, x, y, z, 0, idx);
+    if (owned) {
+      atomicOr(&D.occ[e >> 6], 1ull << (e & 63));
+      if (frame_mode) {
+        VisRec vr;
+        vr.x = x;
+        vr.y = y;
+        vr.z = z;
+        vr.pad = 1;
+        vr.idx = idx;
+        vr.entry = (int32_t)e;
+        D.fresh_vis[prank] = vr;
+      } else {
+        D.fresh[prank] = idx;
+      }
+    }
+    D.nk_key[slot] = 0ull;
+    D.nk_order[slot] = 0xFFFFFFFFu;
+  }
+  if (t == 0) {
+    D.ctr->lock_epoch = epoch;
+    D.ctr->resolve_alloc_ticks += __builtin_amdgcn_s_memrealtime() - tick0;
+    D.ctr->free_count = free0 - nowned;
+    D.ctr->n_fresh = nowned;
+    D.ctr->nk_count = 0;
+    if (frame_mode) {
+      D.ctr->last_alloc = nowned;
+      D.ctr->last_new_keys = n;
+      D.ctr->total_alloc += (unsigned long long)nowned;
+    }
+  }
+  return true;
+}
+
 // frame_mode 1: new blocks this engine holds are listed in D.fresh_vis (flagged fresh, visible this
 // frame); 0 (hash-level test path): their pool indices in D.fresh for k_fresh_init.
 template <int RB>
@@ -534,6 +638,10 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
   const bool single = n <= RB;
   const bool lds_locks = n <= AllocLdsT<RB>::kLockKeys;
   const uint32_t epoch = epoch0 + 1u;
+  if (n <= kRT && !resolve_fast_off()) {
+    if (resolve_alloc_fast<RB>(D, P, frame_mode, n, free0, epoch, k0, h0, L, tick0)) return;
+    lds_barrier();  // fallback: the ordered rounds below reuse the LDS the fast path used
+  }
   if (n <= kWaveKeys && !resolve_wave_off()) {  // one-wave fast path; the other waves are done
     static_assert(AllocLdsT<RB>::kLock >= kWaveLockSlots, "lock set");
     if (t == 0) D.ctr->lock_epoch = epoch;
@@ -831,6 +939,74 @@ struct DeleteLds {
 };
 constexpr uint32_t kHintSlot0 = 1u << 9;  // (with kHintValid) slot 0 holds the key
 
+// Commit-all fast path of the carving resolver: when every candidate sits in slot 0 of its own
+// bucket (voxel_hash.cu:126-135: the lock-free delete), the deletes touch distinct entries, take no
+// lock and read nothing another delete writes, so the entry-ordered linearisation commits them all;
+// only ReleaseBlock's pushes are ordered (by hash entry). Any other launch returns false before
+// anything global is written and the ordered rounds below handle it.
+__device__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32_t epoch, int direct,
+                                    const unsigned long long (&a)[2], const unsigned long long (&b)[2],
+                                    DeleteLds& L, unsigned long long tick0) {
+  const int t = threadIdx.x, wave = t >> 6;
+  int16_t x[2] = {0, 0}, y[2] = {0, 0}, z[2] = {0, 0};
+  uint32_t A[2] = {0u, 0u}, entry[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+  int32_t idx[2] = {-1, -1};
+  bool bad = false, rel[2] = {false, false};
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (t + r * kRT >= n) continue;
+    x[r] = (int16_t)(a[r] & 0xFFFF);
+    y[r] = (int16_t)((a[r] >> 16) & 0xFFFF);
+    z[r] = (int16_t)((a[r] >> 32) & 0xFFFF);
+    entry[r] = (uint32_t)(b[r] >> 32);
+    A[r] = hash_block(x[r], y[r], z[r]);
+    const Ent s0 = load_ent(D.table, 2 * A[r]);
+    const bool in0 = s0.x == x[r] && s0.y == y[r] && s0.z == z[r] && s0.idx >= 0;
+    bad |= !in0;
+    idx[r] = s0.idx;
+    rel[r] = in0 && local_idx(s0.idx);
+  }
+  uint32_t* ev = reinterpret_cast<uint32_t*>(L.batch);  // entries of the released candidates
+  ev[t] = rel[0] ? entry[0] : 0xFFFFFFFFu;
+  ev[t + kRT] = rel[1] ? entry[1] : 0xFFFFFFFFu;
+  const unsigned long long bb = __ballot(bad);
+  const unsigned long long br = __ballot(rel[0]), br1 = __ballot(rel[1]);
+  if (lane_id() == 0) {
+    L.scan[wave] = __popcll(bb);
+    L.scan[4 + wave] = __popcll(br) + __popcll(br1);
+  }
+  lds_barrier();
+  if (L.scan[0] + L.scan[1] + L.scan[2] + L.scan[3] != 0) return false;
+  const int nrel = L.scan[4] + L.scan[5] + L.scan[6] + L.scan[7];
+  const int nq = (min(n, kRB) + 3) >> 2;
+  const uint4* v4 = reinterpret_cast<const uint4*>(ev);
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (t + r * kRT >= n) continue;
+    const uint32_t cur = 2 * A[r];
+    store_off_idx(D.table, cur, 0, -1);
+    atomicAnd(&D.occ[cur >> 6], ~(1ull << (cur & 63)));
+    if (rel[r]) {  // ReleaseBlock in entry order among the released blocks (entries are unique)
+      int rank = 0;
+      for (int j = 0; j < nq; ++j) {
+        const uint4 v = v4[j];
+        rank += (v.x < entry[r]) + (v.y < entry[r]) + (v.z < entry[r]) + (v.w < entry[r]);
+      }
+      D.heap[free0 + rank] = idx[r];
+    }
+  }
+  if (t == 0) {
+    D.ctr->lock_epoch = epoch;
+    D.ctr->free_count = free0 + nrel;
+    D.ctr->resolve_delete_ticks += __builtin_amdgcn_s_memrealtime() - tick0;
+    if (!direct) {
+      D.ctr->last_deleted = nrel;
+      D.ctr->total_deleted += (unsigned long long)nrel;
+    }
+  }
+  return true;
+}
+
 // Carve candidates recs[0..*count) (VisRec: key and hash entry; any order). direct: the hash-level
 // test path -- the candidates in list order, one per round (VoxelHashTable::Delete's launch of
 // voxel_hash_test.cu).
@@ -851,6 +1027,11 @@ __device__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__
     b0 = ld_co(&rq[2 * t + 1]);
     a1 = ld_co(&rq[2 * (t + kRT)]);
     b1 = ld_co(&rq[2 * (t + kRT) + 1]);
+    if (!resolve_fast_off()) {
+      const unsigned long long a[2] = {a0, a1}, b[2] = {b0, b1};
+      if (resolve_delete_fast(D, n, free0, epoch, direct, a, b, L, tick0)) return;
+      lds_barrier();  // fallback: the ordered rounds below reuse the LDS the fast path used
+    }
   }
   if (lds_locks)
     for (int i = t; i < kRLockD; i += kRT) L.lock[i] = 0u;

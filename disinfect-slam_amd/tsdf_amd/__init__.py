@@ -499,6 +499,12 @@ class Engine:
     def synchronize(self):
         _lib.check(_lib.load().tsdf_synchronize(self._h), "tsdf_synchronize")
 
+    def flush(self):
+        """Enqueue the deferred update of the last integrated frame (pipelined frames) on the engine
+        stream without waiting: a device synchronisation (torch.cuda.synchronize) afterwards covers
+        every frame integrated so far."""
+        _lib.check(_lib.load().tsdf_flush(self._h), "tsdf_flush")
+
     # ---- extraction ----
     def raycast(self, K, width, height, cam_T_world: SE3, max_depth: float, rgba=None, normal=None):
         Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])

@@ -96,7 +96,7 @@ class Profile(C.Structure):
 
 EXPORTS = [
     "tsdf_config_default", "tsdf_create", "tsdf_destroy", "tsdf_integrate", "tsdf_raycast",
-    "tsdf_query", "tsdf_extract_mesh", "tsdf_get_stats", "tsdf_synchronize", "tsdf_profile_begin", "tsdf_profile_end",
+    "tsdf_query", "tsdf_extract_mesh", "tsdf_get_stats", "tsdf_synchronize", "tsdf_flush", "tsdf_profile_begin", "tsdf_profile_end",
     "tsdf_debug_dump", "tsdf_debug_stamps", "tsdf_num_entries", "tsdf_num_blocks", "tsdf_hash_allocate",
     "tsdf_hash_delete", "tsdf_hash_retrieve", "tsdf_hash_assign", "tsdf_num_active_blocks",
     "tsdf_pool_acquire", "tsdf_pool_release", "tsdf_pool_set_weight", "tsdf_pool_get_weights",
@@ -168,6 +168,7 @@ def load(path: str | None = None):
     L.tsdf_extract_mesh.argtypes = [P, P, f, i, P, i64, C.POINTER(i64), i]
     L.tsdf_get_stats.argtypes = [P, C.POINTER(Stats), i]
     L.tsdf_synchronize.argtypes = [P]
+    L.tsdf_flush.argtypes = [P]
     L.tsdf_profile_begin.argtypes = [P, i, i]
     L.tsdf_profile_end.argtypes = [P, C.POINTER(Profile)]
     L.tsdf_debug_dump.argtypes = [P, P, P, P, P, P, P, P]
@@ -202,7 +203,7 @@ def load(path: str | None = None):
                  "tsdf_extract_mesh_owned", "tsdf_render_blocks", "tsdf_import_blocks", "tsdf_reset",
                  "tsdf_pack_blocks", "tsdf_graph_create_shard", "tsdf_graph_shard_begin",
                  "tsdf_graph_shard_update", "tsdf_graph_shard_end",
-                 "tsdf_get_stats", "tsdf_synchronize", "tsdf_profile_begin", "tsdf_profile_end",
+                 "tsdf_get_stats", "tsdf_synchronize", "tsdf_flush", "tsdf_profile_begin", "tsdf_profile_end",
                  "tsdf_debug_dump", "tsdf_debug_stamps", "tsdf_hash_allocate", "tsdf_hash_delete",
                  "tsdf_hash_retrieve",
                  "tsdf_hash_assign", "tsdf_num_active_blocks", "tsdf_pool_acquire",

@@ -123,9 +123,19 @@ int tsdf_destroy(tsdf_engine* e);
 
 /* TSDFGrid::Integrate (voxel_tsdf.cu:347-375): allocate -> visibility -> update -> carve.
  * Asynchronous on the engine stream when the frame is TSDF_MEM_DEVICE (inputs must stay valid
- * until the next engine call or tsdf_synchronize); host frames are copied before returning. */
+ * until the next engine call or tsdf_synchronize); host frames are copied before returning.
+ * Pipelined frames (one volume, truncation / voxel <= 6 -- at most 3 DDA samples per pixel): the
+ * frame's allocation is enqueued at once and its update / carving is deferred; the next
+ * tsdf_integrate enqueues it in one launch with the next frame's pixel work, and every other entry
+ * point that reads or writes the volume (raycast, query, stats, snapshots, mesh, ..., tsdf_flush,
+ * tsdf_synchronize) enqueues it first, so every observable result is that of the frames in order.
+ * tsdf_stream_wait / tsdf_stream_signal do not enqueue it (they order the frame's inputs, which the
+ * deferred part no longer reads). TSDF_PIPELINE=0 in the environment disables the deferral. */
 int tsdf_integrate(tsdf_engine* e, const tsdf_frame* frame, const tsdf_intrinsics* K,
                    const tsdf_pose* cam_T_world, float max_depth);
+/* Enqueue a deferred update (pipelined frames) on the engine stream without waiting for it: after
+ * tsdf_flush, a synchronisation of the engine stream covers every frame integrated so far. */
+int tsdf_flush(tsdf_engine* e);
 
 /* Sharded volume (no reference counterpart: TSDFGrid is single-GPU). An engine
  * created with shard_count > 1 is shard `shard_index` of one volume: it keeps the whole hash index
