@@ -45,7 +45,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BLOCK_READ_BYTES = 512 * 12 + 12  # voxel state + metadata of one visible block
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_integrate_r2.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_integrate_r3.json")
 # SQ counters of k_raycast (rocprofv3 --pmc passes of `bench.py --loop c5`, scripts/profile_kernel_sq.sh)
 RAYCAST_SQ_FILE = os.path.join(ROOT, "profiles", "r3_raycast_sq.json")
 VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each
@@ -243,11 +243,22 @@ class Run:
         self.eng.close()
 
 
+PIX_RECORD_BYTES = 20  # pixA {depth, range, w_new, rgb} + pixB log-odds, written once per pixel
+
+
+def pipe_fraction(prof):
+    """Share of the update launches that also prepared the next frame's pixel tiles (pipelined
+    frames: k_integrate_pre)."""
+    return prof.get("pipelined", 0) / max(prof.get("calls", 0), 1)
+
+
 def kernel_roofline(a, prof, n_frames):
-    """k_integrate: algorithmic bytes per launch / average launch duration (this rank)."""
+    """k_integrate: algorithmic bytes per launch / average launch duration (this rank). A pipelined
+    launch (k_integrate_pre) also reads the next frame and writes its pixel records."""
     W, H = a.width, a.height
     img_bytes = (12 if a.depth_only else 15) * W * H
     alg = (prof["sum_visible"] * BLOCK_READ_BYTES + prof["sum_updated"] * 12) / n_frames + img_bytes
+    alg += pipe_fraction(prof) * (img_bytes + PIX_RECORD_BYTES * W * H)
     if a.graph or a.no_events or prof["frames"] == 0:  # no (or one) dispatch event: the device clock
         t = prof["ms_integrate_device"] / n_frames / 1e3
         kind = "in-kernel device clock (first-workgroup start -> last arrival)"
@@ -290,7 +301,7 @@ def pmc_traffic(a, mode, world, prof):
     try:
         runs = json.load(open(PMC_FILE))["runs"]
     except (OSError, ValueError, KeyError):
-        return None, "no PMC file (profiles/pmc_integrate_r2.json)"
+        return None, "no PMC file (profiles/pmc_integrate_r3.json)"
     for r in runs:
         if r.get("key") != key:
             continue
@@ -298,14 +309,14 @@ def pmc_traffic(a, mode, world, prof):
             return None, (f"PMC pass of this command saw N_vis/N_upd sums {r.get('sum_visible')}/"
                           f"{r.get('sum_updated')}, this run {prof['sum_visible']}/{prof['sum_updated']}: rejected")
         return r, "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes of this command, timed-window launches"
-    return None, "no PMC pass of this command in profiles/pmc_integrate_r2.json"
+    return None, "no PMC pass of this command in profiles/pmc_integrate_r3.json"
 
 
 def pmc_key(a, mode, world):
     return {"width": a.width, "height": a.height, "voxel": a.voxel, "trunc": a.trunc,
             "max_depth": a.max_depth, "depth_only": bool(a.depth_only), "block_bits": a.block_bits,
             "steps": a.steps, "warmup": a.warmup, "mode": mode, "n_gpus": world, "loop": a.loop,
-            "graph": bool(a.graph)}
+            "graph": bool(a.graph), "pipelined": os.environ.get("TSDF_PIPELINE", "1") != "0"}
 
 
 def device_spans(prof, n):
@@ -428,8 +439,12 @@ def main():
             parallelism += " (gloo rehearsal, ranks sharing GPUs: not a performance number)"
         if a.graph:
             parallelism += ", one hipGraph launch per frame"
+        pf = pipe_fraction(prof)
         roof = {
-            "kernel": "k_integrate",
+            "kernel": "k_integrate" if pf == 0 else
+                      "k_integrate_pre (frame n's update + carving, and frame n+1's pixel tiles: "
+                      "pixel records, DDA, key dedupe; pipelined frames)",
+            "pipelined_fraction": round(pf, 4),
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
@@ -440,7 +455,7 @@ def main():
             "traffic_write": None if pmc is None else int(pmc["write_bytes_per_launch"]),
             "traffic_source": pmc_src,
             "alg_bytes_per_launch": int(alg),
-            "alg_read_bytes_per_launch": int(prof["sum_visible"] * BLOCK_READ_BYTES / a.steps + img_bytes),
+            "alg_read_bytes_per_launch": int(prof["sum_visible"] * BLOCK_READ_BYTES / a.steps + img_bytes * (1 + pf)),
             "us_per_launch": round(t_int * 1e6, 3),
             "event_timed_launches": prof["frames"],
             "event_kind": ev_kind,

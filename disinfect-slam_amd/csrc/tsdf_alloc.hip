@@ -12,102 +12,6 @@
 
 namespace tsdf {
 
-// ---------------------------------------------------------------------------------------------
-// Visibility sweep (check_visibility_kernel + GatherVisible, voxel_tsdf.cu:82-93,388-397) over
-// the 512 KiB occupancy bitmap instead of the 48 MiB table: every allocated block with any corner
-// in view (no depth test) is appended to the list of the image band its centre projects into
-// (LDS counts, one global atomic per band per pass). Workgroup `wg` covers occupancy words
-// [256 wg, 256 wg + 256), 64 per wave, one per lane; each wave compacts the live entries of its
-// words into LDS so the corner tests run 8 lanes per block on dense work, in passes of at most
-// kVisChunk entries (one pass at the bench's ~1 % table occupancy; each pass costs three dependent
-// global round trips). It runs inside k_ingest_dda, before allocation: it sees the
-// blocks that existed after the previous frame's carving, and k_resolve_alloc appends the
-// blocks it creates. Order within a list is irrelevant to the update; the carving resolver
-// restores the reference's entry order for the deletes.
-// ---------------------------------------------------------------------------------------------
-template <int TS>
-__device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, IngestLds<TS>& S) {
-  const int lane = lane_id(), wave = threadIdx.x >> 6;
-  uint32_t* L = S.u.sweep.list[wave];
-  int* s_cnt = S.u.sweep.cnt;
-  int* s_base = S.u.sweep.base;
-  const int grp = lane >> 3, corner = lane & 7;
-  const int w = wg * 256 + wave * 64 + lane;
-  const unsigned long long occ_all = D.occ[w];
-  const int cw = __popcll(occ_all);
-  const int incl = wave_incl_scan(cw);
-  const int excl = incl - cw;
-  const int wave_total = __shfl(incl, 63, 64);
-  if (threadIdx.x == 0) S.u.sweep.npass = 0;
-  __syncthreads();
-  if (lane == 0) atomicMax(&S.u.sweep.npass, (wave_total + kVisChunk - 1) / kVisChunk);
-  __syncthreads();
-  const int npass = S.u.sweep.npass;
-  for (int pass = 0; pass < npass; ++pass) {
-    if (threadIdx.x < kBands) s_cnt[threadIdx.x] = 0;
-    // this pass lists the wave's live entries of rank [lo, lo + kVisChunk)
-    const int lo = pass * kVisChunk;
-    const int total = min(max(wave_total - lo, 0), kVisChunk);
-    if (excl < lo + kVisChunk && incl > lo) {
-      unsigned long long occ = occ_all;
-      for (int r = excl; occ; ++r) {
-        const int b = __ffsll((long long)occ) - 1;
-        occ &= occ - 1;
-        if (r >= lo && r < lo + kVisChunk) L[r - lo] = (uint32_t)(w * 64 + b);
-      }
-    }
-    __syncthreads();
-    // any-corner visibility (is_block_visible<false>), 8 lanes per block, one corner each; the
-    // visible ones are packed in place as entry | band << 24
-    int nvis = 0;
-    for (int base = 0; base < total; base += 8) {
-      const int i = base + grp;
-      bool v = false;
-      uint32_t e = 0;
-      Ent en{};
-      if (i < total) {
-        e = L[i];
-        en = load_ent(D.table, e);
-        v = voxel_visible(P, (int16_t)((int16_t)(en.x << kBlockLenBits) + ((corner >> 0) & 1) * (kBlockLen - 1)),
-                          (int16_t)((int16_t)(en.y << kBlockLenBits) + ((corner >> 1) & 1) * (kBlockLen - 1)),
-                          (int16_t)((int16_t)(en.z << kBlockLenBits) + ((corner >> 2) & 1) * (kBlockLen - 1)));
-      }
-      const unsigned long long bal = __ballot(v);
-      const bool lead = corner == 0 && i < total && ((bal >> (lane & ~7)) & 0xFFull) != 0;
-      const unsigned long long leads = __ballot(lead);
-      if (lead) {  // rank among this round's visible blocks; slots < base + 8 were all read above
-        const int band = block_band(P, en.x, en.y, en.z);
-        L[nvis + __popcll(leads & ((1ull << lane) - 1ull))] = e | ((uint32_t)band << 24);
-        atomicAdd(&s_cnt[band], 1);
-      }
-      nvis += __popcll(leads);
-    }
-    __syncthreads();
-    if (threadIdx.x < kBands) {  // one global atomic per non-empty band per pass
-      const int cnt = s_cnt[threadIdx.x];
-      s_base[threadIdx.x] = cnt ? atomicAdd(&D.band[threadIdx.x * kBandStride], cnt) : 0;
-      s_cnt[threadIdx.x] = 0;
-    }
-    __syncthreads();
-    for (int k = lane; k < nvis; k += 64) {
-      const uint32_t pk = L[k];
-      const uint32_t e = pk & 0xFFFFFFu;
-      const int band = (int)(pk >> 24);
-      const int pos = s_base[band] + atomicAdd(&s_cnt[band], 1);
-      const Ent en = load_ent(D.table, e);
-      VisRec r;
-      r.x = en.x;
-      r.y = en.y;
-      r.z = en.z;
-      r.pad = 0;  // existed before this frame (not fresh)
-      r.idx = en.idx;
-      r.entry = (int32_t)e;
-      D.vis[(size_t)band * D.nblocks + pos] = r;
-    }
-    __syncthreads();  // L and the band counts are reused by the next pass
-  }
-}
-
 // a shard's split frame: the new-key set (this slice's keys) into the exchange slot, drained for
 // the merge of every shard's slots (k_resolve_alloc after the all-gather)
 __device__ void pack_keys_wg(const EngineDev& D, ShardRec* __restrict__ out, int cap) {
@@ -177,8 +81,18 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
 }
 // at least 6 waves per SIMD (<= 80 VGPRs): the whole 640x480 grid (1456 workgroups) resident at once;
 // the resolver tail alone would raise the kernel to 81 VGPRs (5 waves: 1280 workgroups, +2 us span)
+#ifndef TSDF_INGEST_WAVES_ATTR
+#define TSDF_INGEST_WAVES_ATTR 1
+#endif
+#if TSDF_INGEST_WAVES_ATTR == 1
+#define INGEST_WAVES(TS) __attribute__((amdgpu_waves_per_eu(TS <= 1024 ? 6 : 5)))
+#elif TSDF_INGEST_WAVES_ATTR == 2
+#define INGEST_WAVES(TS) __attribute__((amdgpu_waves_per_eu(TS <= 1024 ? 6 : 5, TS <= 1024 ? 6 : 5)))
+#else
+#define INGEST_WAVES(TS)
+#endif
 template <int TS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TS <= 1024 ? 6 : 5))) void k_ingest_dda(EngineDev D, FrameParams P,
+__global__ __launch_bounds__(256) INGEST_WAVES(TS) void k_ingest_dda(EngineDev D, FrameParams P,
                                                     const float* __restrict__ depth,
                                                     const uint8_t* __restrict__ rgb,
                                                     const float* __restrict__ ht,
@@ -187,7 +101,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TS <= 1024 
   ingest_dda<TS>(D, P, depth, rgb, ht, lt, tiles_x, tiles);
 }
 template <int TS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TS <= 1024 ? 6 : 5))) void k_ingest_dda_g(EngineDev D, const FrameArgs* __restrict__ A) {
+__global__ __launch_bounds__(256) INGEST_WAVES(TS) void k_ingest_dda_g(EngineDev D, const FrameArgs* __restrict__ A) {
   const FrameParams P = A->P;
   ingest_dda<TS>(D, P, A->depth, A->rgb, A->ht, A->lt, A->tiles_x, A->tiles);
 }

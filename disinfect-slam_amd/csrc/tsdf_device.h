@@ -82,8 +82,8 @@ struct FrameParams {
   const float* ht;           // NULL: ones (tsdf_module.cc:29-33)
   const float* lt;
   int row0, nrows;           // raycast: the rows [row0, row0 + nrows) of the W x H camera it renders
-  float4* pixA;              // this frame's pixel records (one of the engine's two buffers: a
-  float* pixB;               //   pipelined frame's are written while the previous frame reads its own)
+  int pix_off;               // this frame's pixel records: D.pixA / pixB + pix_off (one of the two
+                             //   buffers: a pipelined frame's are written while the previous frame reads its own)
   int prepared;              // k_ingest_dda: the tiles' DDA keys were prepared by the previous
                              //   frame's k_integrate_pre (pipelined frames): the tiles only probe them
 };

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <string>
+#include <deque>
 #include <vector>
 
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -149,7 +150,9 @@ struct tsdf_engine {
   int prof_mode = TSDF_PROFILE_PHASES;
   int prof_every = 1;        // event-time every n-th integrate call
   int64_t prof_calls = 0;    // integrate calls since profile_begin
-  std::vector<std::array<hipEvent_t, 5>> events;
+  int64_t prof_pipelined = 0;  // update launches with the next frame's pixel tiles since profile_begin
+  // a deque: a deferred frame (pipelined, sharded) keeps a pointer to its events across later calls
+  std::deque<std::array<hipEvent_t, 5>> events;
   size_t ev_used = 0;
   unsigned long long prof_vis0 = 0, prof_upd0 = 0, prof_ticks0 = 0, prof_ing0 = 0, prof_ra0 = 0, prof_rd0 = 0;
   // sharded frame (tsdf_integrate_shard_*): 0 idle, 1 after _begin, 2 after _update
@@ -161,7 +164,7 @@ struct tsdf_engine {
   // pipelined frames (tsdf_integrate on one volume): the update of the last integrated frame is
   // deferred to the next engine call, where it runs in one launch with the next frame's pixel-tile
   // preparation (k_integrate_pre); every other entry point first enqueues it (flush_pending)
-  bool pipeline = false;  // (default set in tsdf_create)
+  bool pipeline = true;
   bool pend = false;
   FrameParams pend_P{};
   std::array<hipEvent_t, 5>* pend_ev = nullptr;
@@ -243,8 +246,7 @@ FrameParams make_params(const tsdf_engine* e, const tsdf_intrinsics* K, int W, i
   P.rgb = nullptr;
   P.ht = nullptr;
   P.lt = nullptr;
-  P.pixA = e->D.pixA;  // pixel-record buffer 0 (a pipelined frame may take buffer 1)
-  P.pixB = e->D.pixB;
+  P.pix_off = 0;  // pixel-record buffer 0 (a pipelined frame may take buffer 1)
   P.prepared = 0;
   return P;
 }
@@ -492,6 +494,12 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
       return fail(TSDF_ERR_HIP);
     if (const char* v = std::getenv("TSDF_INTEGRATE_WG_PER_CU")) per_cu = std::min(per_cu, std::atoi(v));  // tuning
     D.integrate_grid = std::max(8, std::min(kIntegrateGrid, (per_cu * ncu) & ~7));
+    int per_cu_pre = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_pre, reinterpret_cast<const void*>(k_integrate_pre),
+                                                     kIntegrateThreads, 0) != hipSuccess)
+      return fail(TSDF_ERR_HIP);
+    if (const char* v = std::getenv("TSDF_INTEGRATE_WG_PER_CU")) per_cu_pre = std::min(per_cu_pre, std::atoi(v));
+    D.integrate_grid_pre = std::max(8, std::min(kIntegrateGrid, (per_cu_pre * ncu) & ~7));
   }
   ALLOC(D.pixA, 2 * e->max_pixels);  // two buffers: a pipelined frame's and the next one's
   ALLOC(D.pixB, 2 * e->max_pixels);
@@ -500,7 +508,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
     ALLOC(D.tkeys, tiles_max * kTileKeyCap);
     ALLOC(D.tcount, tiles_max);
   }
-  if (const char* v = std::getenv("TSDF_PIPELINE")) e->pipeline = v[0] == '1';
+  if (const char* v = std::getenv("TSDF_PIPELINE")) e->pipeline = v[0] != '0';
   ALLOC(D.visbits, kOccWords);
   ALLOC(D.wgcnt, kOccWords / 256);
   ALLOC(D.dbg, (size_t)kDiagKernels * kDiagMaxWg * kDiagStamps);
@@ -638,9 +646,7 @@ int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, 
   *ev_out = ev;
   if (pipelined && e->pend) {
     // this frame's pixel records go to the buffer the pending frame does not read
-    const bool b0 = e->pend_P.pixA == e->D.pixA;
-    P->pixA = e->D.pixA + (b0 ? e->max_pixels : 0);
-    P->pixB = e->D.pixB + (b0 ? e->max_pixels : 0);
+    P->pix_off = e->pend_P.pix_off ? 0 : (int)e->max_pixels;
     e->pend = false;
     int rc = frame_update(e, e->pend_P, e->pend_ev, nullptr, 0, P, tiles_x, tiles);
     if (rc) return rc;
@@ -676,25 +682,27 @@ int frame_update(tsdf_engine* e, FrameParams P, std::array<hipEvent_t, 5>* ev, v
   P.slot_cap = cand_cap;
   // ---- update (voxel_tsdf.cu:474-481) + space carving (:483-488) ----
   auto kfn = P.pack_pixels ? k_integrate_t<false, false> : k_integrate_t<false, true>;
+  const EngineDev& Df = e->D;
   if (Pn) {  // + the next frame's pixel tiles (pipelined frames)
-    const dim3 grid(e->D.integrate_grid + tiles);
+    if (e->profiling) ++e->prof_pipelined;
+    const dim3 grid(e->D.integrate_grid_pre + tiles);
     if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
-      hipExtLaunchKernelGGL(k_integrate_pre, grid, dim3(kIntegrateThreads), 0, s, (*ev)[2], (*ev)[3], 0, e->D, P,
+      hipExtLaunchKernelGGL(k_integrate_pre, grid, dim3(kIntegrateThreads), 0, s, (*ev)[2], (*ev)[3], 0, Df, P,
                             *Pn, tiles_x);
     } else {
       if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
-      hipLaunchKernelGGL(k_integrate_pre, grid, dim3(kIntegrateThreads), 0, s, e->D, P, *Pn, tiles_x);
+      hipLaunchKernelGGL(k_integrate_pre, grid, dim3(kIntegrateThreads), 0, s, Df, P, *Pn, tiles_x);
       if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
     }
   } else if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
     // the two events are bound to the kernel's own dispatch packet (its begin / end timestamps,
     // the interval rocprofv3's kernel trace reports): no marker packets enter the stream
     hipExtLaunchKernelGGL(kfn, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
-                          (*ev)[2], (*ev)[3], 0, e->D, P, (const FrameArgs*)nullptr);
+                          (*ev)[2], (*ev)[3], 0, Df, P, (const FrameArgs*)nullptr);
   } else {
     if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
     hipLaunchKernelGGL(kfn, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
-                       e->D, P, (const FrameArgs*)nullptr);
+                       Df, P, (const FrameArgs*)nullptr);
     if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
   }
   LAUNCH_OK("k_integrate");
@@ -1895,6 +1903,7 @@ int tsdf_profile_begin(tsdf_engine* e, int mode, int every) {
   e->prof_mode = mode;
   e->prof_every = every;
   e->prof_calls = 0;
+  e->prof_pipelined = 0;
   int rc = read_counters(e);
   if (rc) return rc;
   e->prof_vis0 = e->h_ctr->total_visible;
@@ -1916,6 +1925,7 @@ int tsdf_profile_end(tsdf_engine* e, tsdf_profile* o) {
   std::memset(o, 0, sizeof(*o));
   o->frames = (int64_t)e->ev_used;
   o->calls = e->prof_calls;
+  o->pipelined = e->prof_pipelined;
   for (size_t i = 0; i < e->ev_used; ++i) {
     float ms[4] = {0.f, 0.f, 0.f, 0.f};
     for (int k = 0; k < 4; ++k)

@@ -137,7 +137,7 @@ __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FramePa
 // are computed per voxel with the ingest's operations (pixel_w_new, pixel_logodds, the range of
 // pixel_ray), instead of from pixel records packed for the whole frame.
 #ifndef TSDF_INTEGRATE_WAVES
-#define TSDF_INTEGRATE_WAVES 8
+#define TSDF_INTEGRATE_WAVES 7
 #endif
 // nint: the update's workgroups (blocks [0, nint) of the launch; k_integrate_pre appends the next
 // frame's pixel-tile workgroups after them). L: the LDS of the last arriver's carving resolve.
@@ -289,8 +289,8 @@ __device__ __forceinline__ void integrate_body(const EngineDev& D, const FramePa
             px[j] = make_float4(P.depth[img], __int_as_float(uu[e]), __int_as_float(vv[e]), __uint_as_float(c));
             lg[j] = P.ht ? pixel_logodds(P.ht[img], P.lt[img]) : 0.0f;
           } else {
-            px[j] = P.pixA[img];
-            lg[j] = P.pixB[img];
+            px[j] = D.pixA[P.pix_off + img];
+            lg[j] = D.pixB[P.pix_off + img];
           }
 #endif
         }
@@ -445,20 +445,26 @@ __attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES)))
   integrate_body<Graph, Raw>(D, Pv, A, (int)gridDim.x, L);
 }
 
-// A pipelined frame's second launch: the update of frame n (workgroups [0, D.integrate_grid), its
+// A pipelined frame's second launch: the update of frame n (workgroups [0, D.integrate_grid_pre), its
 // last arriver carves) and, after them, one workgroup per pixel tile of frame n + 1 preparing its
-// pixel records (Pn.pixA / pixB, the other buffer) and its DDA keys (kTilePrepass). The tile
-// workgroups read only frame n + 1 and the camera, write only their own buffers, and take no part
-// in the arrival: they fill the CUs the update's workgroups leave as they finish, and frame n + 1's
+// pixel records (the other record buffer, Pn.pix_off) and its DDA keys (kTilePrepass). The tile
+// workgroups read only frame n + 1 and its camera, write only their own buffers, and take no part in
+// the arrival: they fill the CUs the update's workgroups leave as they finish, and frame n + 1's
 // k_ingest_dda probes their keys after this launch (and so after frame n's carving).
+// (Measured and not kept, round 3: frame n + 1's visibility sweep here too, with the update of frame
+// n + 1 skipping listed blocks the carving deleted -- the ingest 8.1 -> 5.3 us, but this launch
+// 31.3 -> 34.6 us: 21.5k vs 21.8k frames/s.)
+#ifndef TSDF_PRE_WAVES
+#define TSDF_PRE_WAVES TSDF_INTEGRATE_WAVES
+#endif
 __global__ __launch_bounds__(kIntegrateThreads)
-__attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES))) void k_integrate_pre(
+__attribute__((amdgpu_waves_per_eu(TSDF_PRE_WAVES, TSDF_PRE_WAVES))) void k_integrate_pre(
     EngineDev D, FrameParams P, FrameParams Pn, int tiles_x) {
   __shared__ union {
     DeleteLds del;
     IngestLds<1024> ing;
   } U;
-  const int nint = D.integrate_grid;
+  const int nint = D.integrate_grid_pre;
   if ((int)blockIdx.x >= nint) {
     ingest_tile<1024, kTilePrepass>(D, Pn, Pn.depth, Pn.rgb, Pn.ht, Pn.lt, tiles_x, (int)blockIdx.x - nint, U.ing);
     return;

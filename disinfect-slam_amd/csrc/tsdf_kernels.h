@@ -42,6 +42,7 @@ struct EngineDev {
   DevCounters* ctr;
   int32_t nblocks;
   int32_t integrate_grid;       // k_integrate workgroups (resident capacity, multiple of 8)
+  int32_t integrate_grid_pre;   // k_integrate_pre's update workgroups (its resident capacity)
   // per-frame allocation scratch
   unsigned long long* nk_key;   // kNewKeyCap new-key set
   uint32_t* nk_order;           // kNewKeyCap smallest candidate order per key

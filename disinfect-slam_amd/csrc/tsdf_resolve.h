@@ -536,8 +536,13 @@ __device__ constexpr bool resolve_fast_off() { return false; }
 #endif
 constexpr int kFastLockSlots = 1024;
 
+#ifdef TSDF_FAST_NOINLINE
+#define FAST_INLINE __attribute__((noinline))
+#else
+#define FAST_INLINE
+#endif
 template <int RB>
-__device__ bool resolve_alloc_fast(const EngineDev& D, const FrameParams& P, int frame_mode, int n, int free0,
+__device__ FAST_INLINE bool resolve_alloc_fast(const EngineDev& D, const FrameParams& P, int frame_mode, int n, int free0,
                                    uint32_t epoch, unsigned long long key, int32_t slot, AllocLdsT<RB>& L,
                                    unsigned long long tick0) {
   static_assert(AllocLdsT<RB>::kLock >= kFastLockSlots && 2 * (RB + 2) >= kRT && RB >= kRT, "fast-path LDS");
@@ -578,6 +583,7 @@ __device__ bool resolve_alloc_fast(const EngineDev& D, const FrameParams& P, int
     if (owned) {
       const uint4* v4 = reinterpret_cast<const uint4*>(ordv);
       const int nq = (n + 3) >> 2;
+#pragma unroll 2
       for (int j = 0; j < nq; ++j) {
         const uint4 v = v4[j];
         prank += (v.x < ord) + (v.y < ord) + (v.z < ord) + (v.w < ord);
@@ -940,10 +946,12 @@ struct DeleteLds {
 constexpr uint32_t kHintSlot0 = 1u << 9;  // (with kHintValid) slot 0 holds the key
 
 // Commit-all fast path of the carving resolver: when every candidate sits in slot 0 of its own
-// bucket (voxel_hash.cu:126-135: the lock-free delete), the deletes touch distinct entries, take no
-// lock and read nothing another delete writes, so the entry-ordered linearisation commits them all;
-// only ReleaseBlock's pushes are ordered (by hash entry). Any other launch returns false before
-// anything global is written and the ordered rounds below handle it.
+// bucket (voxel_hash.cu:126-135: the lock-free delete) or is its bucket's list head with no list
+// behind it (:137-152 with offset 0: the head "moves onto itself", i.e. is cleared; it locks the
+// bucket, and a bucket has one head), the deletes touch distinct entries, win every lock and read
+// nothing another delete writes, so the entry-ordered linearisation commits them all; only
+// ReleaseBlock's pushes are ordered (by hash entry). Any other launch returns false before anything
+// global is written and the ordered rounds below handle it.
 __device__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32_t epoch, int direct,
                                     const unsigned long long (&a)[2], const unsigned long long (&b)[2],
                                     DeleteLds& L, unsigned long long tick0) {
@@ -960,11 +968,13 @@ __device__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32
     z[r] = (int16_t)((a[r] >> 32) & 0xFFFF);
     entry[r] = (uint32_t)(b[r] >> 32);
     A[r] = hash_block(x[r], y[r], z[r]);
-    const Ent s0 = load_ent(D.table, 2 * A[r]);
+    const Ent s0 = load_ent(D.table, 2 * A[r]), s1 = load_ent(D.table, 2 * A[r] + 1);
     const bool in0 = s0.x == x[r] && s0.y == y[r] && s0.z == z[r] && s0.idx >= 0;
-    bad |= !in0;
-    idx[r] = s0.idx;
-    rel[r] = in0 && local_idx(s0.idx);
+    const bool head = !in0 && s1.x == x[r] && s1.y == y[r] && s1.z == z[r] && s1.idx >= 0 && s1.off == 0;
+    bad |= !(in0 || head);
+    if (head) A[r] |= 0x80000000u;  // (the entry is 2 A + 1)
+    idx[r] = in0 ? s0.idx : s1.idx;
+    rel[r] = (in0 || head) && local_idx(idx[r]);
   }
   uint32_t* ev = reinterpret_cast<uint32_t*>(L.batch);  // entries of the released candidates
   ev[t] = rel[0] ? entry[0] : 0xFFFFFFFFu;
@@ -983,11 +993,12 @@ __device__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     if (t + r * kRT >= n) continue;
-    const uint32_t cur = 2 * A[r];
+    const uint32_t cur = 2 * (A[r] & 0x7FFFFFFFu) + (A[r] >> 31);
     store_off_idx(D.table, cur, 0, -1);
     atomicAnd(&D.occ[cur >> 6], ~(1ull << (cur & 63)));
     if (rel[r]) {  // ReleaseBlock in entry order among the released blocks (entries are unique)
       int rank = 0;
+#pragma unroll 2
       for (int j = 0; j < nq; ++j) {
         const uint4 v = v4[j];
         rank += (v.x < entry[r]) + (v.y < entry[r]) + (v.z < entry[r]) + (v.w < entry[r]);

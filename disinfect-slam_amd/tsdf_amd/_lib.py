@@ -91,6 +91,7 @@ class Profile(C.Structure):
         ("ms_ingest_device", C.c_double),
         ("ms_resolve_alloc_device", C.c_double),
         ("ms_resolve_delete_device", C.c_double),
+        ("pipelined", C.c_int64),
     ]
 
 

@@ -115,6 +115,8 @@ typedef struct tsdf_profile { /* device time of the integrate phases between beg
   double ms_ingest_device;          /* k_ingest_dda start -> its last workgroup's arrival */
   double ms_resolve_alloc_device;   /* ordered allocation resolve (VoxelHashTable::Allocate) */
   double ms_resolve_delete_device;  /* ordered carving resolve (VoxelHashTable::Delete) */
+  int64_t pipelined;   /* update launches that also prepared the next frame's pixel tiles
+                          (k_integrate_pre; their events / device clock include that work) */
 } tsdf_profile;
 
 /* ---- engine lifetime: TSDFGrid::TSDFGrid / ~TSDFGrid (voxel_tsdf.cu:309-345) ---- */
@@ -130,7 +132,7 @@ int tsdf_destroy(tsdf_engine* e);
  * point that reads or writes the volume (raycast, query, stats, snapshots, mesh, ..., tsdf_flush,
  * tsdf_synchronize) enqueues it first, so every observable result is that of the frames in order.
  * tsdf_stream_wait / tsdf_stream_signal do not enqueue it (they order the frame's inputs, which the
- * deferred part no longer reads). TSDF_PIPELINE=0 in the environment disables the deferral. */
+ * deferred part no longer reads). TSDF_PIPELINE=0 in the environment disables the deferral (on by default). */
 int tsdf_integrate(tsdf_engine* e, const tsdf_frame* frame, const tsdf_intrinsics* K,
                    const tsdf_pose* cam_T_world, float max_depth);
 /* Enqueue a deferred update (pipelined frames) on the engine stream without waiting for it: after

@@ -44,10 +44,14 @@ def kname(full):
     return re.sub(r"k_integrate_t<true(, false)?>", "k_integrate_graph", n)
 
 
-def window(rows, b):
-    """rows (dispatch id, value) of one kernel -> the bench's timed-window launches."""
+def window(rows, b, name=""):
+    """rows (dispatch id, value) of one kernel -> the bench's timed-window launches. Pipelined frames
+    (k_integrate_pre): the timed window's steps - 1 fused launches are that kernel's last ones (the
+    bench flushes after the warmup; nothing after the timed loop launches it)."""
     rows = sorted(rows)
     w, k = b["warmup"], b["steps"]
+    if name == "k_integrate_pre":
+        return [v for _, v in rows[-(k - 1):]]
     return [v for _, v in rows[w:w + k]]
 
 
@@ -74,9 +78,9 @@ def main(out):
                 (int(r["Dispatch_Id"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
         res["timed_window"] = {}
         for name, rows in per.items():
-            if not name.startswith("k_") or len(rows) < b0["warmup"] + b0["steps"]:
+            if not name.startswith("k_") or len(rows) < b0["steps"] - 1:
                 continue
-            win = window(rows, b0)
+            win = window(rows, b0, name)
             res["timed_window"][name] = {"launches": len(win), "avg_us": statistics.mean(win) / 1e3,
                                          "min_us": min(win) / 1e3, "max_us": max(win) / 1e3}
         res["bench_event_us_per_launch"] = b0["roofline"]["us_per_launch"]
@@ -95,13 +99,15 @@ def main(out):
             per.setdefault(kname(kn), []).append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
         corr = 2.0 if c == "FETCH_SIZE" else 1.0
         for name, rows in per.items():
-            win = window(rows, b) if len(rows) >= b["warmup"] + b["steps"] else [v for _, v in sorted(rows)]
+            full = len(rows) >= b["warmup"] + b["steps"] or (name == "k_integrate_pre" and len(rows) >= b["steps"] - 1)
+            win = window(rows, b, name) if full else [v for _, v in sorted(rows)]
             res["pmc"].setdefault(name, {})[c] = {
                 "bytes_per_launch": statistics.mean(win) * 1024 * corr, "dispatches": len(win),
-                "timed_window": len(rows) >= b["warmup"] + b["steps"]}
+                "timed_window": full}
     if b0:
         res["bench"] = b0
-    ki = res["pmc"].get("k_integrate", {})
+    # the update launch of the line: k_integrate_pre for pipelined frames, else k_integrate
+    ki = res["pmc"].get("k_integrate_pre") or res["pmc"].get("k_integrate", {})
     if "FETCH_SIZE" in ki and "WRITE_SIZE" in ki:
         bf, bw = pmc_lines["FETCH_SIZE"], pmc_lines["WRITE_SIZE"]
         same = (bf["sum_visible"], bf["sum_updated"]) == (bw["sum_visible"], bw["sum_updated"])
