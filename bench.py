@@ -90,7 +90,7 @@ def parse():
                         "(a rehearsal of the multi-rank code path; ranks may share a GPU, exchanges staged "
                         "through the host -- not a performance number)")
     p.add_argument("--block-bits", type=int, default=18)
-    p.add_argument("--event-every", type=int, default=8,
+    p.add_argument("--event-every", type=int, default=16,
                    help="HIP-event-time k_integrate on every n-th timed frame (a dispatch with bound "
                         "events runs ~1 us slower, so the loop samples)")
     p.add_argument("--no-events", action="store_true",
@@ -254,7 +254,8 @@ def pipe_fraction(prof):
 
 def kernel_roofline(a, prof, n_frames):
     """k_integrate: algorithmic bytes per launch / average launch duration (this rank). A pipelined
-    launch (k_integrate_pre) also reads the next frame and writes its pixel records."""
+    launch (k_integrate_pre) also reads the next frame and writes its pixel records (the next frame's
+    table probes and inserts are not counted: a lower bound)."""
     W, H = a.width, a.height
     img_bytes = (12 if a.depth_only else 15) * W * H
     alg = (prof["sum_visible"] * BLOCK_READ_BYTES + prof["sum_updated"] * 12) / n_frames + img_bytes
@@ -442,8 +443,9 @@ def main():
         pf = pipe_fraction(prof)
         roof = {
             "kernel": "k_integrate" if pf == 0 else
-                      "k_integrate_pre (frame n's update + carving, and frame n+1's pixel tiles: "
-                      "pixel records, DDA, key dedupe; pipelined frames)",
+                      "k_integrate_pre (the whole pipelined frame in one launch: frame n's update + "
+                      "carving, then frame n+1's pixel records, DDA, key dedupe, visibility sweep, probe, "
+                      "insert and allocation resolver)",
             "pipelined_fraction": round(pf, 4),
             "bound": "hbm",
             "achieved": round(achieved, 1),

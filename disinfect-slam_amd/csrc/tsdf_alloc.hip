@@ -60,11 +60,7 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
     vis_sweep(D, P, blockIdx.x, S);
     TSDF_STAMP(D, 2, 1);
   } else if ((int)blockIdx.x - kVisWorkgroups < tiles) {  // tiles [P.tile_lo, P.tile_lo + tiles)
-    const int tile = P.tile_lo + (int)blockIdx.x - kVisWorkgroups;
-    if (P.prepared)
-      ingest_tile<TS, kTileProbe>(D, P, depth, rgb, ht, lt, tiles_x, tile, S);
-    else
-      ingest_tile<TS, kTileFull>(D, P, depth, rgb, ht, lt, tiles_x, tile, S);
+    ingest_tile<TS, kTileFull>(D, P, depth, rgb, ht, lt, tiles_x, P.tile_lo + (int)blockIdx.x - kVisWorkgroups, S);
   }
   if (!arrive_last(D.arrive + kArrIngest, 0ull, &S.last)) return;
   const unsigned long long tend = __builtin_amdgcn_s_memrealtime();

@@ -84,8 +84,6 @@ struct FrameParams {
   int row0, nrows;           // raycast: the rows [row0, row0 + nrows) of the W x H camera it renders
   int pix_off;               // this frame's pixel records: D.pixA / pixB + pix_off (one of the two
                              //   buffers: a pipelined frame's are written while the previous frame reads its own)
-  int prepared;              // k_ingest_dda: the tiles' DDA keys were prepared by the previous
-                             //   frame's k_integrate_pre (pipelined frames): the tiles only probe them
 };
 // the last-arriving workgroup of k_ingest_dda / k_integrate: resolve (allocation / carving) or, in a
 // shard's frame with an exchange after the kernel, pack the keys / candidates into the slot
@@ -144,6 +142,11 @@ struct DevCounters {
   unsigned long long ingest_ticks;          // k_ingest_dda start -> last arrival (100 MHz clock)
   unsigned long long resolve_alloc_ticks;   // resolve_alloc_wg durations
   unsigned long long resolve_delete_ticks;  // resolve_delete_wg durations
+  // pipelined frames (k_integrate_pre): the tag of the last frame whose carving was published, and
+  // the next frame's sweep / tile workgroups that finished
+  uint32_t carved;
+  int32_t pre_done;
+  unsigned long long dbg_start_max, dbg_prewait_max;  // (TSDF_CHAIN_DIAG builds only)
 };
 
 // ------------------------------------------------------------------------------------------

@@ -166,6 +166,7 @@ struct tsdf_engine {
   // preparation (k_integrate_pre); every other entry point first enqueues it (flush_pending)
   bool pipeline = true;
   bool pend = false;
+  uint32_t pipe_tag = 0;  // one per pipelined launch: k_integrate_pre's carving-published flag value
   FrameParams pend_P{};
   std::array<hipEvent_t, 5>* pend_ev = nullptr;
   // feed_rgbd_frame staging: raw full-size inputs (host frames) and the half-size outputs
@@ -185,7 +186,7 @@ void free_all(tsdf_engine* e) {
   void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.occ,
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs, D.fresh,
                   e->fe_rgb, e->fe_depth, e->fe_mask, e->fe_out_rgb, e->fe_out_depth,
-                  D.vis,     D.band,    D.cand,     D.arrive, D.fresh_vis, D.pend, D.pixA,     D.pixB,    D.tkeys, D.tcount, D.visbits,    D.wgcnt, D.dbg,
+                  D.vis,     D.band,    D.cand,     D.arrive, D.fresh_vis, D.pend, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
                   e->vg_cell, e->vg_flags, e->vg_bits, e->g_visbits, e->g_wgcnt, e->g_sel, e->g_count,
                   e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
@@ -247,7 +248,6 @@ FrameParams make_params(const tsdf_engine* e, const tsdf_intrinsics* K, int W, i
   P.ht = nullptr;
   P.lt = nullptr;
   P.pix_off = 0;  // pixel-record buffer 0 (a pipelined frame may take buffer 1)
-  P.prepared = 0;
   return P;
 }
 
@@ -503,11 +503,6 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   }
   ALLOC(D.pixA, 2 * e->max_pixels);  // two buffers: a pipelined frame's and the next one's
   ALLOC(D.pixB, 2 * e->max_pixels);
-  {
-    const int64_t tiles_max = (int64_t)((cfg.max_width + 15) / 16) * ((cfg.max_height + 15) / 16);
-    ALLOC(D.tkeys, tiles_max * kTileKeyCap);
-    ALLOC(D.tcount, tiles_max);
-  }
   if (const char* v = std::getenv("TSDF_PIPELINE")) e->pipeline = v[0] != '0';
   ALLOC(D.visbits, kOccWords);
   ALLOC(D.wgcnt, kOccWords / 256);
@@ -577,8 +572,8 @@ namespace {
 // visibility of the existing blocks). *P / *ev carry the frame to the later phases.
 int frame_update(tsdf_engine* e, FrameParams P, std::array<hipEvent_t, 5>* ev, void* cands_out = nullptr,
                  int cand_cap = 0, const FrameParams* Pn = nullptr, int tiles_x = 0, int tiles = 0);
-// pipelined: the pending frame's update is launched here with this frame's pixel-tile preparation
-// (k_integrate_pre), and this frame's ingest only probes the prepared keys
+// pipelined: the pending frame's update and this frame's whole ingest (sweep, tiles, allocation) are
+// one launch (k_integrate_pre); there is no k_ingest_dda launch
 int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, const tsdf_pose* pose,
                  float max_depth, int slice_index, int slice_count, FrameParams* P,
                  std::array<hipEvent_t, 5>** ev_out, void* keys_out = nullptr, int key_cap = 0,
@@ -648,9 +643,9 @@ int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, 
     // this frame's pixel records go to the buffer the pending frame does not read
     P->pix_off = e->pend_P.pix_off ? 0 : (int)e->max_pixels;
     e->pend = false;
-    int rc = frame_update(e, e->pend_P, e->pend_ev, nullptr, 0, P, tiles_x, tiles);
-    if (rc) return rc;
-    P->prepared = 1;
+    // (phase events: this frame's ingest starts with the launch that runs it)
+    if (ev && e->prof_mode == TSDF_PROFILE_PHASES) HIP_OK(hipEventRecord((*ev)[0], s));
+    return frame_update(e, e->pend_P, e->pend_ev, nullptr, 0, P, tiles_x, tiles);
   }
   if (ev && e->prof_mode == TSDF_PROFILE_PHASES) HIP_OK(hipEventRecord((*ev)[0], s));
   // ---- allocate (voxel_tsdf.cu:377-386) + visibility (:388-397) ----
@@ -685,13 +680,14 @@ int frame_update(tsdf_engine* e, FrameParams P, std::array<hipEvent_t, 5>* ev, v
   const EngineDev& Df = e->D;
   if (Pn) {  // + the next frame's pixel tiles (pipelined frames)
     if (e->profiling) ++e->prof_pipelined;
-    const dim3 grid(e->D.integrate_grid_pre + tiles);
+    const dim3 grid(e->D.integrate_grid_pre + kVisWorkgroups + tiles);
+    const uint32_t tag = ++e->pipe_tag ? e->pipe_tag : ++e->pipe_tag;  // (0 is the initial flag)
     if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
       hipExtLaunchKernelGGL(k_integrate_pre, grid, dim3(kIntegrateThreads), 0, s, (*ev)[2], (*ev)[3], 0, Df, P,
-                            *Pn, tiles_x);
+                            *Pn, tiles_x, tiles, tag);
     } else {
       if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
-      hipLaunchKernelGGL(k_integrate_pre, grid, dim3(kIntegrateThreads), 0, s, Df, P, *Pn, tiles_x);
+      hipLaunchKernelGGL(k_integrate_pre, grid, dim3(kIntegrateThreads), 0, s, Df, P, *Pn, tiles_x, tiles, tag);
       if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
     }
   } else if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
@@ -2110,6 +2106,9 @@ int tsdf_snapshot_load(tsdf_engine* e, const void* in, int64_t size) {
   hipStream_t s = e->stream;
   const uint8_t* p = static_cast<const uint8_t*>(in) + sizeof(h);
   HIP_OK(hipMemcpyAsync(e->D.ctr, p, sizeof(DevCounters), hipMemcpyHostToDevice, s));
+  // the pipelining flags are this engine's, not the snapshot's (a stale carved tag could match a
+  // later launch of this engine)
+  HIP_OK(hipMemsetAsync(&e->D.ctr->carved, 0, sizeof(uint32_t) + sizeof(int32_t), s));
   p += sizeof(DevCounters);
   HIP_OK(hipMemcpyAsync(e->D.table, p, (size_t)kNumEntry * 16, hipMemcpyHostToDevice, s));
   p += (size_t)kNumEntry * 16;

@@ -39,7 +39,7 @@ __device__ void frame_end(const EngineDev& D) {
     D.ctr->n_cand = 0;  // the next frame's lists start empty (its sweep runs before allocation)
     D.ctr->n_pend = 0;
   }
-  if (threadIdx.x < kBands) D.band[threadIdx.x * kBandStride] = 0;
+  if (threadIdx.x < kBands) st_co(&D.band[threadIdx.x * kBandStride], 0);  // (written through: see k_integrate_pre)
 }
 
 // a shard's frame: its carve candidates into the exchange slot, then the owned entries its
@@ -141,8 +141,9 @@ __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FramePa
 #endif
 // nint: the update's workgroups (blocks [0, nint) of the launch; k_integrate_pre appends the next
 // frame's pixel-tile workgroups after them). L: the LDS of the last arriver's carving resolve.
+// returns true in the workgroup that arrived last (and ran the carving tail)
 template <bool Graph, bool Raw>
-__device__ __forceinline__ void integrate_body(const EngineDev& D, const FrameParams& Pv,
+__device__ __forceinline__ bool integrate_body(const EngineDev& D, const FrameParams& Pv,
                                                const FrameArgs* __restrict__ A, int nint, DeleteLds& L) {
   FrameParams P = Graph ? A->P : Pv;
   if (Graph && A->cands_out) {  // a shard's graph frame: the tail packs the carve candidates
@@ -434,7 +435,9 @@ __device__ __forceinline__ void integrate_body(const EngineDev& D, const FramePa
   // waves that published drain their stores before the workgroup arrives (wave 0: the buffer;
   // the even waves' lane 0: overflow records)
   const bool drain = (wave == 0 && nc > 0) || (s_ovf && (wave & 1) == 0);
-  if (arrive_last(D.arrive + kArrIntegrate, wg_upd, &s_last, drain, (uint32_t)nint)) integrate_tail(D, P, L);
+  if (!arrive_last(D.arrive + kArrIntegrate, wg_upd, &s_last, drain, (uint32_t)nint)) return false;
+  integrate_tail(D, P, L);
+  return true;
 }
 
 template <bool Graph, bool Raw>
@@ -445,31 +448,95 @@ __attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES)))
   integrate_body<Graph, Raw>(D, Pv, A, (int)gridDim.x, L);
 }
 
-// A pipelined frame's second launch: the update of frame n (workgroups [0, D.integrate_grid_pre), its
-// last arriver carves) and, after them, one workgroup per pixel tile of frame n + 1 preparing its
-// pixel records (the other record buffer, Pn.pix_off) and its DDA keys (kTilePrepass). The tile
-// workgroups read only frame n + 1 and its camera, write only their own buffers, and take no part in
-// the arrival: they fill the CUs the update's workgroups leave as they finish, and frame n + 1's
-// k_ingest_dda probes their keys after this launch (and so after frame n's carving).
-// (Measured and not kept, round 3: frame n + 1's visibility sweep here too, with the update of frame
-// n + 1 skipping listed blocks the carving deleted -- the ingest 8.1 -> 5.3 us, but this launch
-// 31.3 -> 34.6 us: 21.5k vs 21.8k frames/s.)
+// A pipelined frame: ONE launch does frame n's update and carving and frame n + 1's ingest.
+//  * workgroups [0, nint): frame n's update (D.integrate_grid_pre: one resident wave of them, all
+//    dispatched before any of the workgroups below); the last to arrive carves frame n, publishes
+//    the carving (agent-scope release, then D.ctr->carved = tag), waits for every workgroup below
+//    and then runs frame n + 1's allocation resolver -- k_ingest_dda's tail;
+//  * kVisWorkgroups workgroups: frame n + 1's visibility sweep, once the carving is published;
+//  * one workgroup per pixel tile of frame n + 1 (kTileChained): pixel records into the other record
+//    buffer, the DDA, the key dedupe and the all-corners test while frame n is updated, then, once
+//    the carving is published, the table probe and the new-key insert.
+// The sweep and the probes read the table frame n's carving left and the allocation reads the keys
+// they inserted: the same operations in the same order as the two-launch frame, so the same results.
+// The waits cannot deadlock: the update's workgroups are all dispatched before the waiting ones and
+// wait for nothing; the last of them waits only for workgroups that wait for nothing it has not
+// already published. Every wait is bounded (TSDF_STATUS_PIPELINE_TIMEOUT).
 #ifndef TSDF_PRE_WAVES
 #define TSDF_PRE_WAVES TSDF_INTEGRATE_WAVES
 #endif
 __global__ __launch_bounds__(kIntegrateThreads)
 __attribute__((amdgpu_waves_per_eu(TSDF_PRE_WAVES, TSDF_PRE_WAVES))) void k_integrate_pre(
-    EngineDev D, FrameParams P, FrameParams Pn, int tiles_x) {
+    EngineDev D, FrameParams P, FrameParams Pn, int tiles_x, int tiles, uint32_t tag) {
   __shared__ union {
     DeleteLds del;
     IngestLds<1024> ing;
   } U;
   const int nint = D.integrate_grid_pre;
-  if ((int)blockIdx.x >= nint) {
-    ingest_tile<1024, kTilePrepass>(D, Pn, Pn.depth, Pn.rgb, Pn.ht, Pn.lt, tiles_x, (int)blockIdx.x - nint, U.ing);
+  const int w = (int)blockIdx.x - nint;
+  if (w >= 0) {
+#ifdef TSDF_CHAIN_DIAG
+    if (threadIdx.x == 0) atomicMax(&D.ctr->dbg_start_max, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
+    // the sweep workgroups first (resident early, they start the moment the carving is published;
+    // measured: 22.85k frames/s against 22.3k with the tiles first), then the tiles
+    if (w < kVisWorkgroups) {
+      wait_tag(D.arrive + kArrCarved + (blockIdx.x & 7) * 16, tag, &D.ctr->status);
+      vis_sweep<1024, kChainCoherentLoads>(D, Pn, w, U.ing);
+    } else {
+      ingest_tile<1024, kTileChained>(D, Pn, Pn.depth, Pn.rgb, Pn.ht, Pn.lt, tiles_x, w - kVisWorkgroups, U.ing, tag);
+    }
+    // done: this workgroup's band counts / new keys are published (atomics that returned, sc1 list
+    // stores drained), then it counts itself for the allocation
+    __builtin_amdgcn_s_waitcnt(0);
+    lds_barrier();
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add(D.arrive + kArrChained + (blockIdx.x & 7) * 16, 1ull, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
-  integrate_body<false, false>(D, P, nullptr, nint, U.del);
+  if (!integrate_body<false, false>(D, P, nullptr, nint, U.del)) return;
+  const unsigned long long t_pub = __builtin_amdgcn_s_memrealtime();
+  // the carving tail has run (frame_end reset the band counts the sweep appends to); its table and
+  // band stores were written through (sc1) and its occupancy updates are atomics: drained, they are
+  // visible to agent-scope reads on every XCD, so publish (no L2 write-back of the update's lines)
+  __builtin_amdgcn_s_waitcnt(0);
+  lds_barrier();
+  const int t = threadIdx.x;
+  if (t < 8) st_co(D.arrive + kArrCarved + t * 16, (unsigned long long)tag);
+  if (t == 0) {
+    const unsigned long long want = (unsigned long long)(kVisWorkgroups + tiles);
+    uint32_t n = 0;
+    for (;;) {
+      unsigned long long done = 0ull;
+      for (int g = 0; g < 8; ++g)
+        done += __hip_atomic_fetch_add(D.arrive + kArrChained + g * 16, 0ull, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+      if (done >= want) break;
+      __builtin_amdgcn_s_sleep(2);
+      if (++n > (1u << 23)) {
+        atomicOr(&D.ctr->status, 64u);  // TSDF_STATUS_PIPELINE_TIMEOUT
+        break;
+      }
+    }
+    for (int g = 0; g < 8; ++g) st_co(D.arrive + kArrChained + g * 16, 0ull);  // (for the next launch)
+#ifdef TSDF_CHAIN_DIAG  // ingest span <- last chained start - publish; allocation <- last pre-wait end - publish
+    {
+      const unsigned long long s0 = __hip_atomic_fetch_or(&D.ctr->dbg_start_max, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long s1 = __hip_atomic_fetch_or(&D.ctr->dbg_prewait_max, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      D.ctr->ingest_ticks += s0 > t_pub ? s0 - t_pub : 0ull;
+      D.ctr->resolve_alloc_ticks += s1 > t_pub ? s1 - t_pub : 0ull;
+      D.ctr->resolve_alloc_ticks -= 0ull;
+    }
+#else
+    // chained frames have no k_ingest_dda: its span counter holds carving published -> every chained
+    // workgroup done (the sweep and the probes after the carving)
+    D.ctr->ingest_ticks += __builtin_amdgcn_s_memrealtime() - t_pub;
+#endif
+  }
+  __syncthreads();
+  // frame n + 1's allocation (k_ingest_dda's tail)
+  resolve_alloc_wg(D, Pn, (uint32_t)Pn.W * (uint32_t)Pn.H * (uint32_t)Pn.maxs, 1, U.ing.u.res);
 }
 template __global__ void k_integrate_t<false, false>(EngineDev, FrameParams, const FrameArgs*);
 template __global__ void k_integrate_t<true, false>(EngineDev, FrameParams, const FrameArgs*);

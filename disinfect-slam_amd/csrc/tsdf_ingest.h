@@ -99,8 +99,63 @@ struct IngestLds {
     AllocLdsT<kIngestRB> res;  // the last-arriving workgroup's allocation resolve
   } u;
   int last;
-  int tcnt;  // kTilePrepass: the tile's stored keys
 };
+
+// the workgroup waits until *flag == tag (thread 0 polls; bounded: a flag that never comes sets
+// TSDF_STATUS_PIPELINE_TIMEOUT and the frame goes on, wrong but without a hung GPU)
+#ifndef TSDF_PIPE_SLEEP
+#define TSDF_PIPE_SLEEP 16
+#endif
+__device__ __forceinline__ void wait_tag(const unsigned long long* flag, uint32_t tag, uint32_t* status) {
+  if (threadIdx.x == 0) {
+    uint32_t n = 0;
+    // polled with an atomic (performed past the L2): a plain or agent-scope load can keep hitting
+    // this XCD's L2 copy of the line from the first poll, long after the tail wrote the tag
+    while ((uint32_t)__hip_atomic_fetch_or(const_cast<unsigned long long*>(flag), 0ull, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT) != tag) {
+      __builtin_amdgcn_s_sleep(TSDF_PIPE_SLEEP);
+      if (++n > (1u << 22)) {
+        atomicOr(status, 64u);  // TSDF_STATUS_PIPELINE_TIMEOUT
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// hash entry read at agent scope (two 8-byte atomic loads: the table is not being written while a
+// chained tile or sweep reads it, so the halves are consistent)
+__device__ __forceinline__ Ent load_ent_co(const int4* table, uint32_t e) {
+  const unsigned long long* q = reinterpret_cast<const unsigned long long*>(table + e);
+  const unsigned long long a = ld_co(q), b = ld_co(q + 1);
+  Ent r;
+  r.x = (int16_t)(a & 0xFFFF);
+  r.y = (int16_t)((a >> 16) & 0xFFFF);
+  r.z = (int16_t)((a >> 32) & 0xFFFF);
+  r.off = (int16_t)((a >> 48) & 0xFFFF);
+  r.idx = (int32_t)(uint32_t)b;
+  return r;
+}
+template <bool Co>
+__device__ __forceinline__ Ent load_ent_t(const int4* table, uint32_t e) {
+  return Co ? load_ent_co(table, e) : load_ent(table, e);
+}
+// find_entry (tsdf_device.h) with the entry loads of load_ent_t<Co>
+template <bool Co>
+__device__ __forceinline__ int32_t find_entry_t(const int4* __restrict__ table, int16_t x, int16_t y, int16_t z) {
+  const uint32_t e0 = hash_block(x, y, z) << 1;
+  const Ent a = load_ent_t<Co>(table, e0);
+  if (a.x == x && a.y == y && a.z == z && a.idx >= 0) return (int32_t)e0;
+  Ent b = load_ent_t<Co>(table, e0 + 1);
+  if (b.x == x && b.y == y && b.z == z && b.idx >= 0) return (int32_t)(e0 + 1);
+  uint32_t last = e0 + 1;
+  while (b.off) {
+    last = (uint32_t)(last + (int32_t)b.off) & kEntryMask;
+    b = load_ent_t<Co>(table, last);
+    if (b.x == x && b.y == y && b.z == z && b.idx >= 0) return (int32_t)last;
+  }
+  return -1;
+}
 
 // ---------------------------------------------------------------------------------------------
 // Visibility sweep (check_visibility_kernel + GatherVisible, voxel_tsdf.cu:82-93,388-397) over
@@ -115,7 +170,9 @@ struct IngestLds {
 // blocks it creates. Order within a list is irrelevant to the update; the carving resolver
 // restores the reference's entry order for the deletes.
 // ---------------------------------------------------------------------------------------------
-template <int TS>
+// Co: the sweep of a chained frame (k_integrate_pre, after frame n's carving was published): the
+// occupancy words and entries are read at agent scope
+template <int TS, bool Co = false>
 __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, IngestLds<TS>& S) {
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   uint32_t* L = S.u.sweep.list[wave];
@@ -123,7 +180,7 @@ __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, Inge
   int* s_base = S.u.sweep.base;
   const int grp = lane >> 3, corner = lane & 7;
   const int w = wg * 256 + wave * 64 + lane;
-  const unsigned long long occ_all = D.occ[w];
+  const unsigned long long occ_all = Co ? ld_co(&D.occ[w]) : D.occ[w];
   const int cw = __popcll(occ_all);
   const int incl = wave_incl_scan(cw);
   const int excl = incl - cw;
@@ -157,7 +214,7 @@ __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, Inge
       Ent en{};
       if (i < total) {
         e = L[i];
-        en = load_ent(D.table, e);
+        en = load_ent_t<Co>(D.table, e);
         v = voxel_visible(P, (int16_t)((int16_t)(en.x << kBlockLenBits) + ((corner >> 0) & 1) * (kBlockLen - 1)),
                           (int16_t)((int16_t)(en.y << kBlockLenBits) + ((corner >> 1) & 1) * (kBlockLen - 1)),
                           (int16_t)((int16_t)(en.z << kBlockLenBits) + ((corner >> 2) & 1) * (kBlockLen - 1)));
@@ -184,7 +241,7 @@ __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, Inge
       const uint32_t e = pk & 0xFFFFFFu;
       const int band = (int)(pk >> 24);
       const int pos = s_base[band] + atomicAdd(&s_cnt[band], 1);
-      const Ent en = load_ent(D.table, e);
+      const Ent en = load_ent_t<Co>(D.table, e);
       VisRec r;
       r.x = en.x;
       r.y = en.y;
@@ -198,32 +255,26 @@ __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, Inge
   }
 }
 
-// One 16x16 pixel tile. kTileFull: everything below in one workgroup (k_ingest_dda). A pipelined
-// frame splits it: kTilePrepass (inside the previous frame's k_integrate_pre) packs the pixel records
-// and runs the DDA, the LDS dedupe and the all-corners test, and stores the tile's visible keys with
-// their smallest candidate orders (D.tkeys / D.tcount); kTileProbe (this frame's k_ingest_dda, after
-// the previous frame's carving) probes the table for those keys and inserts the missing ones --
-// the same keys and orders reach the new-key set, so the allocation is identical.
-constexpr int kTileFull = 0, kTilePrepass = 1, kTileProbe = 2;
+// One 16x16 pixel tile. kTileFull: k_ingest_dda's tile -- pixel records, the DDA, the LDS key dedupe,
+// the all-corners test, then the table probe and the new-key insert. kTileChained: the same tile of
+// frame n + 1 inside frame n's k_integrate_pre (pipelined frames): everything that reads only the
+// frame and its camera runs while frame n's blocks are updated; the probe and insert wait until frame
+// n's carving has been published (D.ctr->carved == tag) and read the table coherently (the carving
+// ran on another XCD), so they see exactly the table the unpipelined frame's ingest would.
+constexpr int kTileFull = 0, kTileChained = 1;
+#ifdef TSDF_CHAIN_PLAIN
+constexpr bool kChainCoherentLoads = false;
+#else
+constexpr bool kChainCoherentLoads = true;
+#endif
+
 template <int TS, int Mode = kTileFull>
 __device__ __forceinline__ void ingest_tile(const EngineDev& D, const FrameParams& P,
                                             const float* __restrict__ depth,
                                             const uint8_t* __restrict__ rgb,
                                             const float* __restrict__ ht,
                                             const float* __restrict__ lt, int tiles_x, int tile,
-                                            IngestLds<TS>& S) {
-  if (Mode == kTileProbe) {  // the keys kTilePrepass stored for this tile
-    const int n = D.tcount[tile];
-    const TileKey* tk = D.tkeys + (size_t)tile * kTileKeyCap;
-    for (int i = threadIdx.x; i < n; i += 256) {
-      const TileKey k = tk[i];
-      int16_t kx, ky, kz;
-      unpack_key(k.key, kx, ky, kz);
-      if (find_entry(D.table, kx, ky, kz) >= 0) continue;
-      nk_insert(D, k.key, k.order);
-    }
-    return;
-  }
+                                            IngestLds<TS>& S, uint32_t tag = 0u) {
   unsigned long long* s_key = S.u.tile.key;
   uint32_t* s_ord = S.u.tile.ord;
   TSDF_STAMP(D, 0, 0);
@@ -231,7 +282,6 @@ __device__ __forceinline__ void ingest_tile(const EngineDev& D, const FrameParam
     s_key[i] = 0ull;
     s_ord[i] = 0xFFFFFFFFu;
   }
-  if (Mode == kTilePrepass && threadIdx.x == 0) S.tcnt = 0;
   __syncthreads();
   TSDF_STAMP(D, 0, 1);
   const int x = (tile % tiles_x) * 16 + (threadIdx.x & 15);
@@ -369,29 +419,18 @@ __device__ __forceinline__ void ingest_tile(const EngineDev& D, const FrameParam
       nv += __popcll(leads);
     }
   }
-  if (Mode == kTilePrepass) {  // the tile's visible keys for the next k_ingest_dda (kTileProbe)
-    int base = 0;
-    if (lane == 0) base = atomicAdd(&S.tcnt, nv);
-    base = __shfl(base, 0, 64);
-    TileKey* tk = D.tkeys + (size_t)tile * kTileKeyCap + base;
-    for (int i = lane; i < nv; i += 64) {
-      const int slot = s_vis[wave][i];
-      TileKey k;
-      k.key = s_key[slot];
-      k.order = s_ord[slot];
-      k.pad = 0u;
-      tk[i] = k;
-    }
-    lds_barrier();
-    if (threadIdx.x == 0) D.tcount[tile] = S.tcnt;
-    return;
-  }
+#ifdef TSDF_CHAIN_DIAG
+  if (Mode == kTileChained && threadIdx.x == 0)
+    atomicMax(&D.ctr->dbg_prewait_max, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
+  if (Mode == kTileChained)  // frame n's carving is done (this XCD's copy of the flag)
+    wait_tag(D.arrive + kArrCarved + (blockIdx.x & 7) * 16, tag, &D.ctr->status);
   for (int i = lane; i < nv; i += 64) {
     const int slot = s_vis[wave][i];
     const unsigned long long key = s_key[slot];
     int16_t kx, ky, kz;
     unpack_key(key, kx, ky, kz);
-    if (find_entry(D.table, kx, ky, kz) >= 0) continue;
+    if (find_entry_t<Mode == kTileChained && kChainCoherentLoads>(D.table, kx, ky, kz) >= 0) continue;
     nk_insert(D, key, s_ord[slot]);
   }
   TSDF_STAMP(D, 0, 5);

@@ -24,14 +24,6 @@ __device__ __forceinline__ int block_band(const FrameParams& P, int16_t bx, int1
   return pc.z > 0.f && bandf > 0.f ? min(kBands - 1, f2i(bandf)) : 0;
 }
 
-// one prepared DDA key of a pixel tile: the block key and its smallest candidate order in the tile
-struct alignas(16) TileKey {
-  unsigned long long key;
-  uint32_t order;
-  uint32_t pad;
-};
-constexpr int kTileKeyCap = 1024;  // distinct keys a 16x16 tile can hold (the LDS key set, maxs <= 3)
-
 // device pointers of one engine (passed by value to every kernel)
 struct EngineDev {
   int4* table;                  // kNumEntry hash entries
@@ -61,10 +53,6 @@ struct EngineDev {
   // packed frame: two buffers of max_pixels records each (FrameParams.pixA / pixB select one)
   float4* pixA;                 // {depth, range, w_new, rgb}
   float* pixB;                  // log2 ht - log2 lt (base-2 log-odds of the pixel)
-  // pipelined frames: the DDA keys each pixel tile of the next frame prepared (k_integrate_pre),
-  // kTileKeyCap records per tile, probed by that frame's k_ingest_dda
-  struct TileKey* tkeys;
-  int32_t* tcount;
   // query scratch
   unsigned long long* visbits;  // kOccWords
   int32_t* wgcnt;               // kOccWords / 256
@@ -136,8 +124,12 @@ __global__ void k_init_logodds(uint8_t* pool, int nb);
 constexpr int kArrGroups = TSDF_ARRIVE_GROUPS;
 static_assert(kArrGroups % 8 == 0 && kArrGroups <= 128, "arrival counters");
 constexpr int kArrStride = (kArrGroups + 1) * 16;  // u64 words of one kernel's counter lines
+// pipelined frames: kArrCarved + 16 x: XCD x's copy of the carving-published flag (a line each, so
+// the waiting workgroups of one XCD poll their own line); kArrChained + 16 x: the chained workgroups
+// of XCD x that finished (one counter per XCD: ~1,500 atomics on one word serialise for ~15 us)
 constexpr int kArrIngest = 0, kArrIntegrate = kArrStride, kArrStart = 2 * kArrStride,
-              kArriveWords = 2 * kArrStride + 16;
+              kArrCarved = 2 * kArrStride + 16, kArrChained = kArrCarved + 8 * 16,
+              kArriveWords = kArrChained + 8 * 16;
 // per frame (2 launches; the resolvers run in the last workgroup of each)
 constexpr int kVisWorkgroups = kOccWords / 256;  // visibility-sweep workgroups of k_ingest_dda
 template <int TS>  // LDS key-set slots per tile (tsdf_alloc.hip): 1024 for maxs <= 3, else 2048
@@ -153,7 +145,7 @@ __global__ void k_resolve_delete_g(EngineDev D, const FrameArgs* A);
 template <bool Graph, bool Raw>
 __global__ void k_integrate_t(EngineDev D, FrameParams P, const FrameArgs* A);
 // pipelined frames: the update of P's frame + the pixel-tile preparation of the next frame Pn
-__global__ void k_integrate_pre(EngineDev D, FrameParams P, FrameParams Pn, int tiles_x);
+__global__ void k_integrate_pre(EngineDev D, FrameParams P, FrameParams Pn, int tiles_x, int tiles, uint32_t tag);
 // graph-captured forms of the frame kernels: identical bodies, arguments from FrameArgs
 template <int TS>
 __global__ void k_ingest_dda_g(EngineDev D, const FrameArgs* A);

@@ -51,6 +51,26 @@ __device__ __forceinline__ void st_co(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Table stores of the carving resolver, written through at agent scope (32-bit sc1 stores; the
+// 16-bit offset by read-modify-write of its dword -- nothing else writes the table meanwhile): a
+// pipelined frame's chained sweep and probes on other XCDs read the carved table right after the
+// carving is published, with no L2 write-back in between (tsdf_fuse.hip k_integrate_pre).
+__device__ __forceinline__ void store_ent_co(int4* table, uint32_t e, int16_t x, int16_t y, int16_t z, int16_t off,
+                                             int32_t idx) {
+  uint32_t* p = reinterpret_cast<uint32_t*>(&table[e]);
+  st_co(&p[0], (uint32_t)(uint16_t)x | ((uint32_t)(uint16_t)y << 16));
+  st_co(&p[1], (uint32_t)(uint16_t)z | ((uint32_t)(uint16_t)off << 16));
+  st_co(&p[2], (uint32_t)idx);
+}
+__device__ __forceinline__ void store_off_co(int4* table, uint32_t e, int16_t off) {
+  uint32_t* p = reinterpret_cast<uint32_t*>(&table[e]) + 1;
+  st_co(p, (ld_co(p) & 0xFFFFu) | ((uint32_t)(uint16_t)off << 16));
+}
+__device__ __forceinline__ void store_off_idx_co(int4* table, uint32_t e, int16_t off, int32_t idx) {
+  store_off_co(table, e, off);
+  st_co(reinterpret_cast<uint32_t*>(&table[e]) + 2, (uint32_t)idx);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Last-arriver detection: every workgroup of the launch arrives once at its end; the function
 // returns true (in all threads) in the workgroup that arrives last. Arrivals go to 8 counters by
@@ -994,7 +1014,7 @@ __device__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32
   for (int r = 0; r < 2; ++r) {
     if (t + r * kRT >= n) continue;
     const uint32_t cur = 2 * (A[r] & 0x7FFFFFFFu) + (A[r] >> 31);
-    store_off_idx(D.table, cur, 0, -1);
+    store_off_idx_co(D.table, cur, 0, -1);
     atomicAnd(&D.occ[cur >> 6], ~(1ull << (cur & 63)));
     if (rel[r]) {  // ReleaseBlock in entry order among the released blocks (entries are unique)
       int rank = 0;
@@ -1176,12 +1196,12 @@ __device__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__
       if (ok) {
         if (kind == 1) {  // voxel_hash.cu:126-135
           released = ecur.idx;
-          store_off_idx(D.table, cur, 0, -1);
+          store_off_idx_co(D.table, cur, 0, -1);
         } else if (kind == 2) {  // :137-152 (cur aliases the head when the list is empty)
           released = eprev.idx;
           const int16_t noff = ecur.off ? (int16_t)(eprev.off + ecur.off) : (int16_t)0;
-          store_ent(D.table, prev, ecur.x, ecur.y, ecur.z, noff, ecur.idx);
-          store_off_idx(D.table, cur, 0, -1);
+          store_ent_co(D.table, prev, ecur.x, ecur.y, ecur.z, noff, ecur.idx);
+          store_off_idx_co(D.table, cur, 0, -1);
           // the next list element moved into the head entry: its occupancy bit moves with it
           // (a shard lists only its own blocks; one volume's head bit simply stays set)
           if (prev != cur) {
@@ -1193,8 +1213,8 @@ __device__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__
         } else {  // :154-170
           released = ecur.idx;
           const int16_t noff = ecur.off ? (int16_t)(eprev.off + ecur.off) : (int16_t)0;
-          store_off(D.table, prev, noff);
-          store_off_idx(D.table, cur, 0, -1);
+          store_off_co(D.table, prev, noff);
+          store_off_idx_co(D.table, cur, 0, -1);
         }
         atomicAnd(&D.occ[cur >> 6], ~(1ull << (cur & 63)));
         L.changed = 1;

@@ -38,6 +38,7 @@ extern "C" {
 #define TSDF_STATUS_RESOLVE_ABORT 8u   /* allocation resolver made no progress (internal error) */
 #define TSDF_STATUS_SHARD_OVERFLOW 16u /* a sharded frame had more keys / candidates than a slot holds */
 #define TSDF_STATUS_SHARD_ABORTED 32u  /* a pending sharded frame was aborted (the shards may differ) */
+#define TSDF_STATUS_PIPELINE_TIMEOUT 64u /* a pipelined frame's in-kernel wait timed out (internal error) */
 
 typedef struct tsdf_engine tsdf_engine;
 typedef struct tsdf_graph tsdf_graph;
