@@ -326,7 +326,10 @@ def device_spans(prof, n):
             "integrate": us("ms_integrate_device"), "resolve_delete": us("ms_resolve_delete_device"),
             "note": "in-kernel 100 MHz clock, mean per timed frame: ingest = k_ingest_dda start -> "
                     "last workgroup arrival; resolve_* = the resolvers in the last-arriving workgroups "
-                    "of k_ingest_dda / k_integrate; integrate = k_integrate start -> last arrival"}
+                    "of k_ingest_dda / k_integrate; integrate = k_integrate start -> last arrival. "
+                    "Pipelined frames (one k_integrate_pre per frame): integrate = the update's start -> "
+                    "its last arrival, ingest = the carving published -> the next frame's last chained "
+                    "workgroup counted"}
 
 
 def main():
