@@ -142,11 +142,6 @@ struct DevCounters {
   unsigned long long ingest_ticks;          // k_ingest_dda start -> last arrival (100 MHz clock)
   unsigned long long resolve_alloc_ticks;   // resolve_alloc_wg durations
   unsigned long long resolve_delete_ticks;  // resolve_delete_wg durations
-  // pipelined frames (k_integrate_pre): the tag of the last frame whose carving was published, and
-  // the next frame's sweep / tile workgroups that finished
-  uint32_t carved;
-  int32_t pre_done;
-  unsigned long long dbg_start_max, dbg_prewait_max;  // (TSDF_CHAIN_DIAG builds only)
 };
 
 // ------------------------------------------------------------------------------------------

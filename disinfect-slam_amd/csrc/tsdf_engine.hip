@@ -186,7 +186,7 @@ void free_all(tsdf_engine* e) {
   void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.occ,
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs, D.fresh,
                   e->fe_rgb, e->fe_depth, e->fe_mask, e->fe_out_rgb, e->fe_out_depth,
-                  D.vis,     D.band,    D.cand,     D.arrive, D.fresh_vis, D.pend, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
+                  D.vis,     D.band,    D.cand,     D.arrive, D.swdirty, D.fresh_vis, D.pend, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
                   e->vg_cell, e->vg_flags, e->vg_bits, e->g_visbits, e->g_wgcnt, e->g_sel, e->g_count,
                   e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
@@ -397,6 +397,7 @@ bool init_state(tsdf_engine* e, bool with_pool = true) {
   ok &= hipMemsetAsync(D.band, 0, sizeof(int32_t) * kBands * kBandStride, s) == hipSuccess;
   ok &= hipMemsetAsync(D.visbits, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
   ok &= hipMemsetAsync(D.arrive, 0, sizeof(unsigned long long) * kArriveWords, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.swdirty, 0, sizeof(unsigned long long) * (kOccWords / 64), s) == hipSuccess;
   DevCounters c0{};
   c0.free_count = nb;
   ok &= hipMemcpyAsync(D.ctr, &c0, sizeof(c0), hipMemcpyHostToDevice, s) == hipSuccess;
@@ -482,6 +483,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   if (const char* v = std::getenv("TSDF_CAND_CAP")) D.cand_cap = std::min(D.cand_cap, std::max(1024, std::atoi(v)));
   ALLOC(D.cand, D.cand_cap);
   ALLOC(D.arrive, kArriveWords);
+  ALLOC(D.swdirty, kOccWords / 64);
   ALLOC(D.fresh_vis, kNewKeyCap);
   ALLOC(D.pend, kNewKeyCap);
   {  // one resident wave of k_integrate workgroups: no second-round stragglers
@@ -2106,9 +2108,6 @@ int tsdf_snapshot_load(tsdf_engine* e, const void* in, int64_t size) {
   hipStream_t s = e->stream;
   const uint8_t* p = static_cast<const uint8_t*>(in) + sizeof(h);
   HIP_OK(hipMemcpyAsync(e->D.ctr, p, sizeof(DevCounters), hipMemcpyHostToDevice, s));
-  // the pipelining flags are this engine's, not the snapshot's (a stale carved tag could match a
-  // later launch of this engine)
-  HIP_OK(hipMemsetAsync(&e->D.ctr->carved, 0, sizeof(uint32_t) + sizeof(int32_t), s));
   p += sizeof(DevCounters);
   HIP_OK(hipMemcpyAsync(e->D.table, p, (size_t)kNumEntry * 16, hipMemcpyHostToDevice, s));
   p += (size_t)kNumEntry * 16;

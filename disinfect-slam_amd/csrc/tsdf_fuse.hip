@@ -106,15 +106,51 @@ __global__ __launch_bounds__(256) void k_shard_abort(EngineDev D) {
 // space carving of the candidates (voxel_tsdf.cu:483-488, kTailResolve) or, in a shard's frame,
 // the packing of its candidates for the exchange (kTailPack; k_resolve_delete follows it).
 // The statistics (their loads) come after the carving, off its path.
+// Pre (k_integrate_pre): only the carving and the band-count reset the next frame's chained sweep
+// waits for; the statistics follow once the carving is published (integrate_stats), off the frame's
+// path. The band counts are read before the carving (they are final since the previous launch).
+__device__ __forceinline__ void integrate_stats(const EngineDev& D, DeleteLds& L) {
+  const int t = threadIdx.x;
+  lds_barrier();
+  const int bc = t < kBands ? L.bcnt[t] : 0;
+  int nband;
+  (void)wg_excl_scan(bc, L.scan, &nband);
+  if (t == 0) {
+    const unsigned long long upd = arrive_collect(D.arrive + kArrIntegrate);
+    const int nvis = nband + D.ctr->n_fresh;
+    D.ctr->last_updated = upd;
+    D.ctr->integrate_ticks += L.tend - ld_co(&D.arrive[kArrStart]);
+    D.ctr->n_vis = nvis;
+    D.ctr->total_visible += (unsigned long long)nvis;
+    D.ctr->total_updated += upd;
+    D.ctr->frames += 1ull;
+  }
+}
+
+template <bool Pre = false>
 __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FrameParams& P, DeleteLds& L) {
   const int t = threadIdx.x;
   const unsigned long long tend = __builtin_amdgcn_s_memrealtime();  // the update's span ends here
   TSDF_STAMP(D, 7, 0);
+  const int bc_pre = Pre && t < kBands ? D.band[t * kBandStride] : 0;
   if (P.tail == kTailPack)
     pack_cands_wg(D, P.slot, P.slot_cap);
   else
     resolve_delete_wg(D, D.cand, &D.ctr->n_cand, 0, L);
   TSDF_STAMP(D, 7, 1);
+  if (Pre) {
+    lds_barrier();
+    if (t < kBands) {
+      L.bcnt[t] = bc_pre;
+      st_co(&D.band[t * kBandStride], 0);  // (written through: see k_integrate_pre)
+    }
+    if (t == 0) {  // (written through: the allocation resolver later in this launch adds to n_pend)
+      L.tend = tend;
+      st_co(&D.ctr->n_cand, 0);
+      st_co(&D.ctr->n_pend, 0);
+    }
+    return;
+  }
   lds_barrier();  // (L.scan is reused below)
   const int bc = t < kBands ? D.band[t * kBandStride] : 0;
   int nband;
@@ -142,7 +178,7 @@ __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FramePa
 // nint: the update's workgroups (blocks [0, nint) of the launch; k_integrate_pre appends the next
 // frame's pixel-tile workgroups after them). L: the LDS of the last arriver's carving resolve.
 // returns true in the workgroup that arrived last (and ran the carving tail)
-template <bool Graph, bool Raw>
+template <bool Graph, bool Raw, bool Pre = false>
 __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FrameParams& Pv,
                                                const FrameArgs* __restrict__ A, int nint, DeleteLds& L) {
   FrameParams P = Graph ? A->P : Pv;
@@ -436,7 +472,7 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
   // the even waves' lane 0: overflow records)
   const bool drain = (wave == 0 && nc > 0) || (s_ovf && (wave & 1) == 0);
   if (!arrive_last(D.arrive + kArrIntegrate, wg_upd, &s_last, drain, (uint32_t)nint)) return false;
-  integrate_tail(D, P, L);
+  integrate_tail<Pre>(D, P, L);
   return true;
 }
 
@@ -451,8 +487,9 @@ __attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES)))
 // A pipelined frame: ONE launch does frame n's update and carving and frame n + 1's ingest.
 //  * workgroups [0, nint): frame n's update (D.integrate_grid_pre: one resident wave of them, all
 //    dispatched before any of the workgroups below); the last to arrive carves frame n, publishes
-//    the carving (agent-scope release, then D.ctr->carved = tag), waits for every workgroup below
-//    and then runs frame n + 1's allocation resolver -- k_ingest_dda's tail;
+//    the carving (write-through stores drained, then one flag per XCD = tag), waits until every
+//    workgroup below has counted itself (per-XCD counters) and then runs frame n + 1's allocation
+//    resolver -- k_ingest_dda's tail;
 //  * kVisWorkgroups workgroups: frame n + 1's visibility sweep, once the carving is published;
 //  * one workgroup per pixel tile of frame n + 1 (kTileChained): pixel records into the other record
 //    buffer, the DDA, the key dedupe and the all-corners test while frame n is updated, then, once
@@ -475,35 +512,50 @@ __attribute__((amdgpu_waves_per_eu(TSDF_PRE_WAVES, TSDF_PRE_WAVES))) void k_inte
   const int nint = D.integrate_grid_pre;
   const int w = (int)blockIdx.x - nint;
   if (w >= 0) {
-#ifdef TSDF_CHAIN_DIAG
-    if (threadIdx.x == 0) atomicMax(&D.ctr->dbg_start_max, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-#endif
+    TSDF_STAMP_WG(D, 5, w, 0);
     // the sweep workgroups first (resident early, they start the moment the carving is published;
     // measured: 22.85k frames/s against 22.3k with the tiles first), then the tiles
+#ifdef TSDF_PRE_TILES_FIRST  // (experiment)
+    if (w >= tiles) {
+      vis_sweep_chained<1024>(D, Pn, w - tiles, U.ing, D.arrive + kArrCarved + (blockIdx.x & 7) * 16, tag);
+    } else {
+      ingest_tile<1024, kTileChained>(D, Pn, Pn.depth, Pn.rgb, Pn.ht, Pn.lt, tiles_x, w, U.ing, tag);
+    }
+#else
     if (w < kVisWorkgroups) {
+#ifdef TSDF_SWEEP_AFTER_WAIT  // (experiment: the whole sweep after the carving)
       wait_tag(D.arrive + kArrCarved + (blockIdx.x & 7) * 16, tag, &D.ctr->status);
-      vis_sweep<1024, kChainCoherentLoads>(D, Pn, w, U.ing);
+      vis_sweep<1024, true>(D, Pn, w, U.ing);
+#else
+      vis_sweep_chained<1024>(D, Pn, w, U.ing, D.arrive + kArrCarved + (blockIdx.x & 7) * 16, tag);
+#endif
     } else {
       ingest_tile<1024, kTileChained>(D, Pn, Pn.depth, Pn.rgb, Pn.ht, Pn.lt, tiles_x, w - kVisWorkgroups, U.ing, tag);
     }
+#endif
     // done: this workgroup's band counts / new keys are published (atomics that returned, sc1 list
     // stores drained), then it counts itself for the allocation
     __builtin_amdgcn_s_waitcnt(0);
     lds_barrier();
+    TSDF_STAMP_WG(D, 5, w, 3);
     if (threadIdx.x == 0)
       __hip_atomic_fetch_add(D.arrive + kArrChained + (blockIdx.x & 7) * 16, 1ull, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
-  if (!integrate_body<false, false>(D, P, nullptr, nint, U.del)) return;
+  if (!integrate_body<false, false, true>(D, P, nullptr, nint, U.del)) return;
   const unsigned long long t_pub = __builtin_amdgcn_s_memrealtime();
-  // the carving tail has run (frame_end reset the band counts the sweep appends to); its table and
+  TSDF_STAMP_WG(D, 5, kDiagMaxWg - 1, 0);
+  // the carving tail has run (it reset the band counts the sweep appends to); its table and
   // band stores were written through (sc1) and its occupancy updates are atomics: drained, they are
   // visible to agent-scope reads on every XCD, so publish (no L2 write-back of the update's lines)
   __builtin_amdgcn_s_waitcnt(0);
   lds_barrier();
   const int t = threadIdx.x;
   if (t < 8) st_co(D.arrive + kArrCarved + t * 16, (unsigned long long)tag);
+  TSDF_STAMP_WG(D, 5, kDiagMaxWg - 1, 1);
+  integrate_stats(D, U.del);  // frame n's statistics, while the chained workgroups run
+  unsigned long long t_done = 0ull;
   if (t == 0) {
     const unsigned long long want = (unsigned long long)(kVisWorkgroups + tiles);
     uint32_t n = 0;
@@ -520,23 +572,16 @@ __attribute__((amdgpu_waves_per_eu(TSDF_PRE_WAVES, TSDF_PRE_WAVES))) void k_inte
       }
     }
     for (int g = 0; g < 8; ++g) st_co(D.arrive + kArrChained + g * 16, 0ull);  // (for the next launch)
-#ifdef TSDF_CHAIN_DIAG  // ingest span <- last chained start - publish; allocation <- last pre-wait end - publish
-    {
-      const unsigned long long s0 = __hip_atomic_fetch_or(&D.ctr->dbg_start_max, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long s1 = __hip_atomic_fetch_or(&D.ctr->dbg_prewait_max, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      D.ctr->ingest_ticks += s0 > t_pub ? s0 - t_pub : 0ull;
-      D.ctr->resolve_alloc_ticks += s1 > t_pub ? s1 - t_pub : 0ull;
-      D.ctr->resolve_alloc_ticks -= 0ull;
-    }
-#else
-    // chained frames have no k_ingest_dda: its span counter holds carving published -> every chained
-    // workgroup done (the sweep and the probes after the carving)
-    D.ctr->ingest_ticks += __builtin_amdgcn_s_memrealtime() - t_pub;
-#endif
+    t_done = __builtin_amdgcn_s_memrealtime();
   }
+  TSDF_STAMP_WG(D, 5, kDiagMaxWg - 1, 2);
   __syncthreads();
   // frame n + 1's allocation (k_ingest_dda's tail)
   resolve_alloc_wg(D, Pn, (uint32_t)Pn.W * (uint32_t)Pn.H * (uint32_t)Pn.maxs, 1, U.ing.u.res);
+  TSDF_STAMP_WG(D, 5, kDiagMaxWg - 1, 3);
+  // chained frames have no k_ingest_dda: its span counter holds carving published -> every chained
+  // workgroup counted (the sweep and the probes after the carving)
+  if (t == 0) D.ctr->ingest_ticks += t_done - t_pub;
 }
 template __global__ void k_integrate_t<false, false>(EngineDev, FrameParams, const FrameArgs*);
 template __global__ void k_integrate_t<true, false>(EngineDev, FrameParams, const FrameArgs*);

@@ -95,6 +95,7 @@ struct IngestLds {
       uint32_t list[4][kVisChunk];
       int cnt[kBands], base[kBands];
       int npass;
+      unsigned long long dm[4];  // (vis_sweep_chained) the carving's marks of each wave's 64 words
     } sweep;
     AllocLdsT<kIngestRB> res;  // the last-arriving workgroup's allocation resolve
   } u;
@@ -252,6 +253,196 @@ __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, Inge
       D.vis[(size_t)band * D.nblocks + pos] = r;
     }
     __syncthreads();  // L and the band counts are reused by the next pass
+  }
+}
+
+// The chained sweep of a pipelined frame (k_integrate_pre, frame n + 1's sweep inside frame n's
+// launch). Frame n's carving only clears entries and moves a list element into its head entry, and it
+// marks every occupancy word it changes (D.swdirty, tsdf_resolve.h mark_swept_dirty); nothing else
+// writes the table in the launch. So the listing and the visibility tests run BEFORE the carving is
+// published (possibly while it runs), keeping each wave's visible blocks in LDS (entry | band << 24 in
+// list[0, kPreMax), the record's x, y, z, idx in the 3 words per block after it); after the wait the
+// workgroup takes its marks (and clears them), drops the blocks of marked words, re-lists and re-tests
+// those words, and appends their visible blocks to the band lists directly. The result is the lists
+// vis_sweep<TS, true> would build after the wait (order within a list is irrelevant). Every read of
+// the occupancy and the table here is an atomic (performed past the L2 and not kept in it): a plain
+// or agent-scope load would leave this XCD's L2 a pre-carving copy of the line, which the chained
+// tiles' agent-scope probes after the wait would then read. A wave with more than kPreMax live
+// entries (far above the bench's ~1 % occupancy) makes the workgroup wait and run the agent-scope
+// sweep instead.
+constexpr int kPreMax = 256;
+__device__ __forceinline__ Ent load_ent_rmw(int4* table, uint32_t e) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(table + e);
+  const unsigned long long a = __hip_atomic_fetch_or(q, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long b = __hip_atomic_fetch_or(q + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  Ent r;
+  r.x = (int16_t)(a & 0xFFFF);
+  r.y = (int16_t)((a >> 16) & 0xFFFF);
+  r.z = (int16_t)((a >> 32) & 0xFFFF);
+  r.off = (int16_t)((a >> 48) & 0xFFFF);
+  r.idx = (int32_t)(uint32_t)b;
+  return r;
+}
+template <int TS>
+__device__ void vis_sweep_chained(const EngineDev& D, const FrameParams& P, int wg, IngestLds<TS>& S,
+                                  const unsigned long long* flag, uint32_t tag) {
+  static_assert(kVisChunk >= 4 * kPreMax, "list + records of kPreMax blocks per wave");
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  uint32_t* L = S.u.sweep.list[wave];
+  uint32_t* R = L + kPreMax;
+  int* s_cnt = S.u.sweep.cnt;
+  int* s_base = S.u.sweep.base;
+  const int grp = lane >> 3, corner = lane & 7;
+  const int w = wg * 256 + wave * 64 + lane;
+  const unsigned long long occ_all = __hip_atomic_fetch_or(&D.occ[w], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int cw = __popcll(occ_all);
+  const int incl = wave_incl_scan(cw);
+  const int excl = incl - cw;
+  const int total = __shfl(incl, 63, 64);
+  if (threadIdx.x == 0) S.u.sweep.npass = 0;
+  __syncthreads();
+  if (lane == 0) atomicMax(&S.u.sweep.npass, total);
+  __syncthreads();
+  if (S.u.sweep.npass > kPreMax) {  // (uniform) before any table read of this workgroup
+    wait_tag(flag, tag, &D.ctr->status);
+    if (threadIdx.x < 4)
+      __hip_atomic_store(&D.swdirty[wg * 4 + threadIdx.x], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    vis_sweep<TS, true>(D, P, wg, S);
+    return;
+  }
+  {
+    unsigned long long occ = occ_all;
+    for (int r = excl; occ; ++r) {
+      const int b = __ffsll((long long)occ) - 1;
+      occ &= occ - 1;
+      L[r] = (uint32_t)(w * 64 + b);
+    }
+  }
+  if (threadIdx.x < kBands) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  int nvis = 0;
+  for (int base = 0; base < total; base += 8) {  // vis_sweep's any-corner test, 8 lanes per block
+    const int i = base + grp;
+    bool v = false;
+    uint32_t e = 0;
+    Ent en{};
+    unsigned long long qa = 0ull, qb = 0ull;
+    if (i < total) {
+      e = L[i];
+      if (corner == 0) {  // one lane of the 8 reads the entry (two 8-byte atomics), then broadcasts
+        unsigned long long* q = reinterpret_cast<unsigned long long*>(D.table + e);
+        qa = __hip_atomic_fetch_or(q, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        qb = __hip_atomic_fetch_or(q + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    const int src = lane & ~7;
+    const uint32_t a0 = __shfl((uint32_t)qa, src, 64), a1 = __shfl((uint32_t)(qa >> 32), src, 64);
+    const uint32_t b0 = __shfl((uint32_t)qb, src, 64);
+    if (i < total) {
+      en.x = (int16_t)(a0 & 0xFFFFu);
+      en.y = (int16_t)(a0 >> 16);
+      en.z = (int16_t)(a1 & 0xFFFFu);
+      en.idx = (int32_t)b0;
+      v = voxel_visible(P, (int16_t)((int16_t)(en.x << kBlockLenBits) + ((corner >> 0) & 1) * (kBlockLen - 1)),
+                        (int16_t)((int16_t)(en.y << kBlockLenBits) + ((corner >> 1) & 1) * (kBlockLen - 1)),
+                        (int16_t)((int16_t)(en.z << kBlockLenBits) + ((corner >> 2) & 1) * (kBlockLen - 1)));
+    }
+    const unsigned long long bal = __ballot(v);
+    const bool lead = corner == 0 && i < total && ((bal >> (lane & ~7)) & 0xFFull) != 0;
+    const unsigned long long leads = __ballot(lead);
+    if (lead) {  // slots < base + 8 were all read above
+      const int k = nvis + __popcll(leads & ((1ull << lane) - 1ull));
+      L[k] = e | ((uint32_t)block_band(P, en.x, en.y, en.z) << 24);
+      R[3 * k] = (uint32_t)(uint16_t)en.x | ((uint32_t)(uint16_t)en.y << 16);
+      R[3 * k + 1] = (uint32_t)(uint16_t)en.z;
+      R[3 * k + 2] = (uint32_t)en.idx;
+    }
+    nvis += __popcll(leads);
+  }
+  // ---- frame n's carving published ----
+  TSDF_STAMP_WG(D, 5, (int)blockIdx.x - D.integrate_grid_pre, 1);
+  wait_tag(flag, tag, &D.ctr->status);
+  TSDF_STAMP_WG(D, 5, (int)blockIdx.x - D.integrate_grid_pre, 2);
+  if (threadIdx.x < 4)
+    S.u.sweep.dm[threadIdx.x] = __hip_atomic_fetch_and(&D.swdirty[wg * 4 + threadIdx.x], 0ull, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const unsigned long long dm = S.u.sweep.dm[wave];  // bit j: word wg * 256 + wave * 64 + j
+  if (dm) {  // (wave-uniform) drop the blocks of marked words, in place
+    int keep = 0;
+    for (int b0 = 0; b0 < nvis; b0 += 64) {
+      const int k = b0 + lane;
+      uint32_t pk = 0, r0 = 0, r1 = 0, r2 = 0;
+      bool kp = false;
+      if (k < nvis) {
+        pk = L[k];
+        r0 = R[3 * k];
+        r1 = R[3 * k + 1];
+        r2 = R[3 * k + 2];
+        kp = !((dm >> (((pk & 0xFFFFFFu) >> 6) & 63)) & 1ull);
+      }
+      const unsigned long long kb = __ballot(kp);  // (every lane has read its slot)
+      if (kp) {
+        const int d = keep + __popcll(kb & ((1ull << lane) - 1ull));
+        L[d] = pk;
+        R[3 * d] = r0;
+        R[3 * d + 1] = r1;
+        R[3 * d + 2] = r2;
+      }
+      keep += __popcll(kb);
+    }
+    nvis = keep;
+  }
+  for (int k = lane; k < nvis; k += 64) atomicAdd(&s_cnt[L[k] >> 24], 1);
+  __syncthreads();
+  int gbase = 0;
+  if (threadIdx.x < kBands) {  // one global atomic per non-empty band (its result waited for below)
+    const int cnt = s_cnt[threadIdx.x];
+    gbase = cnt ? atomicAdd(&D.band[threadIdx.x * kBandStride], cnt) : 0;
+  }
+  if ((dm >> lane) & 1ull) {  // this lane's word was changed: re-list and re-test it (any corner)
+    unsigned long long occ = __hip_atomic_fetch_or(&D.occ[w], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (occ) {
+      const int b = __ffsll((long long)occ) - 1;
+      occ &= occ - 1;
+      const uint32_t e = (uint32_t)(w * 64 + b);
+      const Ent en = load_ent_rmw(D.table, e);
+      bool v = false;
+      for (int c = 0; c < 8; ++c)
+        v |= voxel_visible(P, (int16_t)((int16_t)(en.x << kBlockLenBits) + ((c >> 0) & 1) * (kBlockLen - 1)),
+                           (int16_t)((int16_t)(en.y << kBlockLenBits) + ((c >> 1) & 1) * (kBlockLen - 1)),
+                           (int16_t)((int16_t)(en.z << kBlockLenBits) + ((c >> 2) & 1) * (kBlockLen - 1)));
+      if (v) {
+        const int band = block_band(P, en.x, en.y, en.z);
+        const int pos = atomicAdd(&D.band[band * kBandStride], 1);
+        VisRec r;
+        r.x = en.x;
+        r.y = en.y;
+        r.z = en.z;
+        r.pad = 0;
+        r.idx = en.idx;
+        r.entry = (int32_t)e;
+        D.vis[(size_t)band * D.nblocks + pos] = r;
+      }
+    }
+  }
+  if (threadIdx.x < kBands) {
+    s_base[threadIdx.x] = gbase;
+    s_cnt[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  for (int k = lane; k < nvis; k += 64) {
+    const uint32_t pk = L[k];
+    const int band = (int)(pk >> 24);
+    const int pos = s_base[band] + atomicAdd(&s_cnt[band], 1);
+    VisRec r;
+    r.x = (int16_t)(R[3 * k] & 0xFFFFu);
+    r.y = (int16_t)(R[3 * k] >> 16);
+    r.z = (int16_t)(R[3 * k + 1] & 0xFFFFu);
+    r.pad = 0;  // existed before this frame (not fresh)
+    r.idx = (int32_t)R[3 * k + 2];
+    r.entry = (int32_t)(pk & 0xFFFFFFu);
+    D.vis[(size_t)band * D.nblocks + pos] = r;
   }
 }
 
@@ -419,12 +610,11 @@ __device__ __forceinline__ void ingest_tile(const EngineDev& D, const FrameParam
       nv += __popcll(leads);
     }
   }
-#ifdef TSDF_CHAIN_DIAG
-  if (Mode == kTileChained && threadIdx.x == 0)
-    atomicMax(&D.ctr->dbg_prewait_max, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-#endif
-  if (Mode == kTileChained)  // frame n's carving is done (this XCD's copy of the flag)
+  if (Mode == kTileChained) {  // frame n's carving is done (this XCD's copy of the flag)
+    TSDF_STAMP_WG(D, 5, (int)blockIdx.x - D.integrate_grid_pre, 1);
     wait_tag(D.arrive + kArrCarved + (blockIdx.x & 7) * 16, tag, &D.ctr->status);
+    TSDF_STAMP_WG(D, 5, (int)blockIdx.x - D.integrate_grid_pre, 2);
+  }
   for (int i = lane; i < nv; i += 64) {
     const int slot = s_vis[wave][i];
     const unsigned long long key = s_key[slot];

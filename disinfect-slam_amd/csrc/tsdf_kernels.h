@@ -47,6 +47,7 @@ struct EngineDev {
   VisRec* cand;                 // cand_cap carve candidates (any order; sorted by entry)
   int32_t cand_cap;             // records D.cand holds (<= the D.pairs scratch, >= 1024)
   unsigned long long* arrive;   // kArriveWords: last-arriver counters of the frame kernels
+  unsigned long long* swdirty;  // kOccWords / 64: occupancy words the carving changed (tsdf_resolve.h)
   VisRec* fresh_vis;            // kNewKeyCap blocks created this frame (k_resolve_alloc frame mode)
   VisRec* pend;                 // kNewKeyCap: a shard's owned entries its exhausted pool left without
                                 // voxels this frame (ctr->n_pend); carved in the same frame

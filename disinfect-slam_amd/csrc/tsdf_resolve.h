@@ -71,6 +71,14 @@ __device__ __forceinline__ void store_off_idx_co(int4* table, uint32_t e, int16_
   st_co(reinterpret_cast<uint32_t*>(&table[e]) + 2, (uint32_t)idx);
 }
 
+// Entries the carving changed, by occupancy word (bit (e >> 6) & 63 of D.swdirty[e >> 12]): a
+// pipelined frame's chained sweep tests visibility before the carving is published and re-tests
+// only the words marked here (tsdf_ingest.h vis_sweep_chained). Conservative: a mark left by a
+// carving no chained sweep followed only costs a re-test.
+__device__ __forceinline__ void mark_swept_dirty(const EngineDev& D, uint32_t e) {
+  atomicOr(&D.swdirty[e >> 12], 1ull << ((e >> 6) & 63));
+}
+
 // ---------------------------------------------------------------------------------------------
 // Last-arriver detection: every workgroup of the launch arrives once at its end; the function
 // returns true (in all threads) in the workgroup that arrives last. Arrivals go to 8 counters by
@@ -962,6 +970,8 @@ struct DeleteLds {
   uint32_t lock[kRLockD];
   int scan[8];
   int sfree, ndel, changed, m;
+  int bcnt[kBands];                // (k_integrate_pre) the frame's band counts, for integrate_stats
+  unsigned long long tend;         // (k_integrate_pre) the update's end, for integrate_stats
 };
 constexpr uint32_t kHintSlot0 = 1u << 9;  // (with kHintValid) slot 0 holds the key
 
@@ -1016,6 +1026,7 @@ __device__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32
     const uint32_t cur = 2 * (A[r] & 0x7FFFFFFFu) + (A[r] >> 31);
     store_off_idx_co(D.table, cur, 0, -1);
     atomicAnd(&D.occ[cur >> 6], ~(1ull << (cur & 63)));
+    mark_swept_dirty(D, cur);
     if (rel[r]) {  // ReleaseBlock in entry order among the released blocks (entries are unique)
       int rank = 0;
 #pragma unroll 2
@@ -1217,6 +1228,8 @@ __device__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__
           store_off_idx_co(D.table, cur, 0, -1);
         }
         atomicAnd(&D.occ[cur >> 6], ~(1ull << (cur & 63)));
+        mark_swept_dirty(D, cur);
+        if (kind == 2) mark_swept_dirty(D, prev);  // (the next element's content moved into prev)
         L.changed = 1;
       }
       // ReleaseBlock (voxel_mem.cu:54-59) of the blocks this engine holds (a shard deletes every
