@@ -490,11 +490,14 @@ __attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES)))
 //    the carving (write-through stores drained, then one flag per XCD = tag), waits until every
 //    workgroup below has counted itself (per-XCD counters) and then runs frame n + 1's allocation
 //    resolver -- k_ingest_dda's tail;
-//  * kVisWorkgroups workgroups: frame n + 1's visibility sweep, once the carving is published;
+//  * kVisWorkgroups workgroups: frame n + 1's visibility sweep (vis_sweep_chained: listed and tested
+//    while frame n is updated, the words the carving marks re-tested once it is published, then the
+//    band lists appended);
 //  * one workgroup per pixel tile of frame n + 1 (kTileChained): pixel records into the other record
 //    buffer, the DDA, the key dedupe and the all-corners test while frame n is updated, then, once
 //    the carving is published, the table probe and the new-key insert.
-// The sweep and the probes read the table frame n's carving left and the allocation reads the keys
+// The tail publishes the carving, then computes frame n's statistics (integrate_stats) while the
+// chained workgroups run. The sweep and the probes see the table frame n's carving left and the allocation reads the keys
 // they inserted: the same operations in the same order as the two-launch frame, so the same results.
 // The waits cannot deadlock: the update's workgroups are all dispatched before the waiting ones and
 // wait for nothing; the last of them waits only for workgroups that wait for nothing it has not
