@@ -270,7 +270,10 @@ __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, Inge
 // tiles' agent-scope probes after the wait would then read. A wave with more than kPreMax live
 // entries (far above the bench's ~1 % occupancy) makes the workgroup wait and run the agent-scope
 // sweep instead.
-constexpr int kPreMax = 256;
+#ifndef TSDF_PRE_MAX  // (a test build lowers it to run the fallback: scripts/gpu_r3_premax.sh)
+#define TSDF_PRE_MAX 256
+#endif
+constexpr int kPreMax = TSDF_PRE_MAX;
 __device__ __forceinline__ Ent load_ent_rmw(int4* table, uint32_t e) {
   unsigned long long* q = reinterpret_cast<unsigned long long*>(table + e);
   const unsigned long long a = __hip_atomic_fetch_or(q, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -286,7 +289,7 @@ __device__ __forceinline__ Ent load_ent_rmw(int4* table, uint32_t e) {
 template <int TS>
 __device__ void vis_sweep_chained(const EngineDev& D, const FrameParams& P, int wg, IngestLds<TS>& S,
                                   const unsigned long long* flag, uint32_t tag) {
-  static_assert(kVisChunk >= 4 * kPreMax, "list + records of kPreMax blocks per wave");
+  static_assert(kVisChunk >= 4 * kPreMax && kPreMax <= 256, "list + records of kPreMax blocks per wave");
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   uint32_t* L = S.u.sweep.list[wave];
   uint32_t* R = L + kPreMax;
