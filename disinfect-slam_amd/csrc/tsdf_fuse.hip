@@ -542,7 +542,7 @@ __attribute__((amdgpu_waves_per_eu(TSDF_PRE_WAVES, TSDF_PRE_WAVES))) void k_inte
     lds_barrier();
     TSDF_STAMP_WG(D, 5, w, 3);
     if (threadIdx.x == 0)
-      __hip_atomic_fetch_add(D.arrive + kArrChained + (blockIdx.x & 7) * 16, 1ull, __ATOMIC_RELAXED,
+      __hip_atomic_fetch_add(D.arrive + kArrChained + (blockIdx.x % kChainCounters) * 16, 1ull, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
@@ -559,22 +559,24 @@ __attribute__((amdgpu_waves_per_eu(TSDF_PRE_WAVES, TSDF_PRE_WAVES))) void k_inte
   TSDF_STAMP_WG(D, 5, kDiagMaxWg - 1, 1);
   integrate_stats(D, U.del);  // frame n's statistics, while the chained workgroups run
   unsigned long long t_done = 0ull;
-  if (t == 0) {
+  if (t < 64) {  // wave 0 polls the completion counters, one per lane (spread: no hot word)
     const unsigned long long want = (unsigned long long)(kVisWorkgroups + tiles);
+    unsigned long long* ctr = D.arrive + kArrChained + (t % kChainCounters) * 16;
+    const bool mine = t < kChainCounters;
     uint32_t n = 0;
     for (;;) {
-      unsigned long long done = 0ull;
-      for (int g = 0; g < 8; ++g)
-        done += __hip_atomic_fetch_add(D.arrive + kArrChained + g * 16, 0ull, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-      if (done >= want) break;
+      unsigned long long done =
+          mine ? __hip_atomic_fetch_add(ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) done += __shfl_xor(done, o, 64);
+      if (done >= want) break;  // (wave-uniform)
       __builtin_amdgcn_s_sleep(2);
       if (++n > (1u << 23)) {
-        atomicOr(&D.ctr->status, 64u);  // TSDF_STATUS_PIPELINE_TIMEOUT
+        if (t == 0) atomicOr(&D.ctr->status, 64u);  // TSDF_STATUS_PIPELINE_TIMEOUT
         break;
       }
     }
-    for (int g = 0; g < 8; ++g) st_co(D.arrive + kArrChained + g * 16, 0ull);  // (for the next launch)
+    if (mine) st_co(ctr, 0ull);  // (for the next launch)
     t_done = __builtin_amdgcn_s_memrealtime();
   }
   TSDF_STAMP_WG(D, 5, kDiagMaxWg - 1, 2);
