@@ -520,17 +520,17 @@ __attribute__((amdgpu_waves_per_eu(TSDF_PRE_WAVES, TSDF_PRE_WAVES))) void k_inte
     // measured: 22.85k frames/s against 22.3k with the tiles first), then the tiles
 #ifdef TSDF_PRE_TILES_FIRST  // (experiment)
     if (w >= tiles) {
-      vis_sweep_chained<1024>(D, Pn, w - tiles, U.ing, D.arrive + kArrCarved + (blockIdx.x & 7) * 16, tag);
+      vis_sweep_chained<1024>(D, Pn, w - tiles, U.ing, D.arrive + kArrCarved + (blockIdx.x % kCarvedFlags) * 16, tag);
     } else {
       ingest_tile<1024, kTileChained>(D, Pn, Pn.depth, Pn.rgb, Pn.ht, Pn.lt, tiles_x, w, U.ing, tag);
     }
 #else
     if (w < kVisWorkgroups) {
 #ifdef TSDF_SWEEP_AFTER_WAIT  // (experiment: the whole sweep after the carving)
-      wait_tag(D.arrive + kArrCarved + (blockIdx.x & 7) * 16, tag, &D.ctr->status);
+      wait_tag(D.arrive + kArrCarved + (blockIdx.x % kCarvedFlags) * 16, tag, &D.ctr->status);
       vis_sweep<1024, true>(D, Pn, w, U.ing);
 #else
-      vis_sweep_chained<1024>(D, Pn, w, U.ing, D.arrive + kArrCarved + (blockIdx.x & 7) * 16, tag);
+      vis_sweep_chained<1024>(D, Pn, w, U.ing, D.arrive + kArrCarved + (blockIdx.x % kCarvedFlags) * 16, tag);
 #endif
     } else {
       ingest_tile<1024, kTileChained>(D, Pn, Pn.depth, Pn.rgb, Pn.ht, Pn.lt, tiles_x, w - kVisWorkgroups, U.ing, tag);
@@ -555,7 +555,7 @@ __attribute__((amdgpu_waves_per_eu(TSDF_PRE_WAVES, TSDF_PRE_WAVES))) void k_inte
   __builtin_amdgcn_s_waitcnt(0);
   lds_barrier();
   const int t = threadIdx.x;
-  if (t < 8) st_co(D.arrive + kArrCarved + t * 16, (unsigned long long)tag);
+  if (t < kCarvedFlags) st_co(D.arrive + kArrCarved + t * 16, (unsigned long long)tag);
   TSDF_STAMP_WG(D, 5, kDiagMaxWg - 1, 1);
   integrate_stats(D, U.del);  // frame n's statistics, while the chained workgroups run
   unsigned long long t_done = 0ull;

@@ -615,7 +615,7 @@ __device__ __forceinline__ void ingest_tile(const EngineDev& D, const FrameParam
   }
   if (Mode == kTileChained) {  // frame n's carving is done (this XCD's copy of the flag)
     TSDF_STAMP_WG(D, 5, (int)blockIdx.x - D.integrate_grid_pre, 1);
-    wait_tag(D.arrive + kArrCarved + (blockIdx.x & 7) * 16, tag, &D.ctr->status);
+    wait_tag(D.arrive + kArrCarved + (blockIdx.x % kCarvedFlags) * 16, tag, &D.ctr->status);
     TSDF_STAMP_WG(D, 5, (int)blockIdx.x - D.integrate_grid_pre, 2);
   }
   for (int i = lane; i < nv; i += 64) {
