@@ -516,9 +516,12 @@ __attribute__((amdgpu_waves_per_eu(TSDF_PRE_WAVES, TSDF_PRE_WAVES))) void k_inte
   const int w = (int)blockIdx.x - nint;
   if (w >= 0) {
     TSDF_STAMP_WG(D, 5, w, 0);
-    // the sweep workgroups first (resident early, they start the moment the carving is published;
-    // measured: 22.85k frames/s against 22.3k with the tiles first), then the tiles
-#ifdef TSDF_PRE_TILES_FIRST  // (experiment)
+    // the tiles first, then the sweep workgroups. Measured: with the sweep after the wait, sweep
+    // first was faster (22.85k vs 22.3k frames/s); since the sweep tests before the carving is
+    // published, tiles first ends the chained work 0.3-0.5 us earlier (23.77k / 23.95k vs 23.65k /
+    // 23.82k, scripts/gpu_r3_last.sh): the tiles' DDA, dispatched as the update retires, is the
+    // longer pre-carving part
+#ifndef TSDF_PRE_SWEEP_FIRST
     if (w >= tiles) {
       vis_sweep_chained<1024>(D, Pn, w - tiles, U.ing, D.arrive + kArrCarved + (blockIdx.x % kCarvedFlags) * 16, tag);
     } else {

@@ -3,8 +3,9 @@
 
 k_integrate_pre stamps (kernel slot 5): per chained workgroup w -- start, before its wait, after its
 wait, done -- and in slot kDiagMaxWg - 1 the tail: carving published (t_pub), flags stored, every
-chained workgroup counted, allocation resolver done. All times in us relative to t_pub; the sweep
-workgroups (w < 256) and the tiles reported apart. Frames are integrated in pairs (the second is a
+chained workgroup counted, allocation resolver done. All times in us relative to t_pub; the tiles
+(w < tiles: the shipped order, tiles first) and the sweep workgroups reported apart (--sweep-first
+for a TSDF_PRE_SWEEP_FIRST build). Frames are integrated in pairs (the second is a
 pipelined launch) and the stamps read after each pair (the read flushes the pending update).
 Usage: make -C disinfect-slam_amd diag && \
     TSDF_AMD_LIB=disinfect-slam_amd/libdisinfect_tsdf_diag.so python scripts/diag_chain.py
@@ -69,7 +70,11 @@ def main():
         put("tail: flags stored", rel(tail[1]))
         put("tail: all chained counted", rel(tail[2]))
         put("tail: allocation done", rel(tail[3]))
-        for name, rows in (("sweep", S[:NVIS]), ("tiles", S[NVIS:NVIS + tiles])):
+        sweep_first = "--sweep-first" in sys.argv
+        groups = ((("sweep", slice(0, NVIS)), ("tiles", slice(NVIS, NVIS + tiles))) if sweep_first else
+                  (("tiles", slice(0, tiles)), ("sweep", slice(tiles, tiles + NVIS))))
+        for name, sl in groups:
+            rows = S[sl]
             rows = rows[rows[:, 0] > 0]
             for j, ph in enumerate(("start", "pre-wait", "wait end", "done")):
                 r = rel(rows[:, j])

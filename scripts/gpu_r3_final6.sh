@@ -3,7 +3,7 @@
 # counters of k_integrate_pre, default line with the CPU baseline, unpipelined line, C5, C4 unsharded,
 # 8-shard C4 rehearsal, chained-phase stamps (diagnostic library)
 set -uo pipefail
-OUT=gpurun_out/r3final5; mkdir -p $OUT
+OUT=gpurun_out/r3final6; mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_all.log 2>&1 || { grep -E "^E |FAILED" $OUT/pytest_all.log | head -30; exit 1; }
 tail -1 $OUT/pytest_all.log
