@@ -45,7 +45,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BLOCK_READ_BYTES = 512 * 12 + 12  # voxel state + metadata of one visible block
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_integrate_r3.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_integrate_r4.json")
 # SQ counters of k_raycast (rocprofv3 --pmc passes of `bench.py --loop c5`, scripts/profile_kernel_sq.sh)
 RAYCAST_SQ_FILE = os.path.join(ROOT, "profiles", "r3_raycast_sq.json")
 VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each
@@ -90,9 +90,10 @@ def parse():
                         "(a rehearsal of the multi-rank code path; ranks may share a GPU, exchanges staged "
                         "through the host -- not a performance number)")
     p.add_argument("--block-bits", type=int, default=18)
-    p.add_argument("--event-every", type=int, default=16,
-                   help="HIP-event-time k_integrate on every n-th timed frame (a dispatch with bound "
-                        "events runs ~1 us slower, so the loop samples)")
+    p.add_argument("--event-every", type=int, default=0,
+                   help="HIP-event-time the frame kernel on every n-th timed frame (a dispatch with bound "
+                        "events runs ~1 us slower, so the loop samples); 0 = steps // 5 clamped to [1, 16] "
+                        "(at least 5 timed launches)")
     p.add_argument("--no-events", action="store_true",
                    help="diagnostic: no HIP events in the timed loop (kernel roofline then from the "
                         "device clock)")
@@ -198,7 +199,8 @@ class Run:
         # start/stop events bound to every event_every-th k_integrate dispatch (hipExtLaunchKernel):
         # the kernel's own begin/end timestamps, nothing added to the stream; the device-clock spans
         # and the N_vis / N_upd sums cover every timed frame
-        self.eng.profile_begin(integrate_only=True, every=(1 << 30) if a.no_events else a.event_every,
+        every = a.event_every or max(1, min(16, a.steps // 5))
+        self.eng.profile_begin(integrate_only=True, every=(1 << 30) if a.no_events else every,
                                kernel_events=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -253,21 +255,34 @@ def pipe_fraction(prof):
 
 
 def kernel_roofline(a, prof, n_frames):
-    """k_integrate: algorithmic bytes per launch / average launch duration (this rank). A pipelined
-    launch (k_integrate_pre) also reads the next frame and writes its pixel records (the next frame's
-    table probes and inserts are not counted: a lower bound)."""
+    """The frame launch: SURVEY.md 8(d) algorithmic bytes of ONE frame (every launch of the timed
+    window processes one frame's update, carving, allocation and ingest) / its average launch
+    duration (this rank):  N_vis * 6156 + N_upd * 12 + 15 W H  (12 W H depth-only). What the launch
+    moves beyond that -- the pixel records written by the ingest and gathered by the update, the next
+    frame's image, table probes, the occupancy bitmap -- is implementation traffic: it shows up in
+    roofline.traffic (rocprofv3 PMC), not here."""
     W, H = a.width, a.height
     img_bytes = (12 if a.depth_only else 15) * W * H
     alg = (prof["sum_visible"] * BLOCK_READ_BYTES + prof["sum_updated"] * 12) / n_frames + img_bytes
-    alg += pipe_fraction(prof) * (img_bytes + PIX_RECORD_BYTES * W * H)
-    if a.graph or a.no_events or prof["frames"] == 0:  # no (or one) dispatch event: the device clock
+    if a.graph or a.no_events or prof["frames"] == 0:  # no dispatch event: the device clock
         t = prof["ms_integrate_device"] / n_frames / 1e3
         kind = "in-kernel device clock (first-workgroup start -> last arrival)"
     else:
         t = prof["ms_integrate"] / prof["frames"] / 1e3
-        kind = "HIP events bound to the k_integrate dispatch (hipExtLaunchKernel), engine stream"
+        kind = "HIP events bound to the frame kernel's dispatch (hipExtLaunchKernel), engine stream"
     achieved = alg / t / 1e9 if t > 0 else 0.0
     return alg, t, achieved, kind
+
+
+def implementation_bytes(a, prof):
+    """Bytes per frame launch that SURVEY 8(d) does not count (a lower bound, by construction): the
+    20 B pixel records the ingest writes and the update gathers back (each once), and -- pipelined --
+    nothing else by design (the launch reads the next frame's image instead of this frame's; counted
+    once in the algorithmic bytes)."""
+    W, H = a.width, a.height
+    return {"pixel_records_written": PIX_RECORD_BYTES * W * H,
+            "pixel_records_read": PIX_RECORD_BYTES * W * H,
+            "occupancy_bitmap_read": 512 * 1024}
 
 
 def raycast_roofline(a, us_call):
@@ -302,7 +317,7 @@ def pmc_traffic(a, mode, world, prof):
     try:
         runs = json.load(open(PMC_FILE))["runs"]
     except (OSError, ValueError, KeyError):
-        return None, "no PMC file (profiles/pmc_integrate_r3.json)"
+        return None, "no PMC file (" + os.path.relpath(PMC_FILE, ROOT) + ")"
     for r in runs:
         if r.get("key") != key:
             continue
@@ -310,7 +325,7 @@ def pmc_traffic(a, mode, world, prof):
             return None, (f"PMC pass of this command saw N_vis/N_upd sums {r.get('sum_visible')}/"
                           f"{r.get('sum_updated')}, this run {prof['sum_visible']}/{prof['sum_updated']}: rejected")
         return r, "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes of this command, timed-window launches"
-    return None, "no PMC pass of this command in profiles/pmc_integrate_r3.json"
+    return None, "no PMC pass of this command in " + os.path.relpath(PMC_FILE, ROOT)
 
 
 def pmc_key(a, mode, world):
@@ -434,7 +449,8 @@ def main():
         cpu = cpu_baseline(a, cam, fr_host)
 
     if rank == 0:
-        metric = "TSDF integrate frames/s (640x480 depth+label, 5mm voxel)"
+        metric = (f"TSDF integrate frames/s ({W}x{H} depth{'' if a.depth_only else '+label'}, "
+                  f"{a.voxel * 1000:g}mm voxel)")
         if a.loop == "c5":
             metric = ("C5 frame loop frames/s (integrate + raycast every frame, marching cubes every 30 "
                       "frames)")
@@ -460,7 +476,10 @@ def main():
             "traffic_write": None if pmc is None else int(pmc["write_bytes_per_launch"]),
             "traffic_source": pmc_src,
             "alg_bytes_per_launch": int(alg),
-            "alg_read_bytes_per_launch": int(prof["sum_visible"] * BLOCK_READ_BYTES / a.steps + img_bytes * (1 + pf)),
+            "alg_read_bytes_per_launch": int(prof["sum_visible"] * BLOCK_READ_BYTES / a.steps + img_bytes),
+            "alg_def": "SURVEY 8(d) per frame launch: N_vis * 6156 + N_upd * 12 + 15 W H (N_vis, N_upd counted on "
+                       "device over the timed frames)",
+            "implementation_bytes_per_launch": implementation_bytes(a, prof),
             "us_per_launch": round(t_int * 1e6, 3),
             "event_timed_launches": prof["frames"],
             "event_kind": ev_kind,

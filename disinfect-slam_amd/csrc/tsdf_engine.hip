@@ -161,14 +161,18 @@ struct tsdf_engine {
   bool shard_keys_packed = false;  // _begin wrote a key slot (split DDA): _update merges an inbox
   FrameParams shard_P{};
   std::array<hipEvent_t, 5>* shard_ev = nullptr;
-  // pipelined frames (tsdf_integrate on one volume): the update of the last integrated frame is
-  // deferred to the next engine call, where it runs in one launch with the next frame's pixel-tile
-  // preparation (k_integrate_pre); every other entry point first enqueues it (flush_pending)
+  // pipelined frames (tsdf_integrate on one volume, k_frame): what the next launch
+  // continues. kPipeNone: nothing pending. kPipeU: frame p_fid's ingest and allocation ran
+  // (k_ingest_dda), its update is pending. kPipeCAU: frame p_carve's carving and frame p_fid's
+  // allocation and update are pending (p_fid's tiles probed and inserted its keys, its sweep listed
+  // its blocks). Every other entry point first completes them (flush_pending).
   bool pipeline = true;
-  bool pend = false;
-  uint32_t pipe_tag = 0;  // one per pipelined launch: k_integrate_pre's carving-published flag value
-  FrameParams pend_P{};
-  std::array<hipEvent_t, 5>* pend_ev = nullptr;
+  static constexpr int kPipeNone = 0, kPipeU = 1, kPipeCAU = 2;
+  int ps = kPipeNone;
+  uint32_t fid_next = 1;  // engine-wide frame ids (views, tags; never 0)
+  uint32_t p_carve = 0, p_fid = 0;
+  FrameParams p_P{};      // frame p_fid's camera / frame / pixel-record buffer
+  uint32_t pipe_tag = 0;  // one per k_frame launch: its flags' value
   // feed_rgbd_frame staging: raw full-size inputs (host frames) and the half-size outputs
   uint8_t* fe_rgb = nullptr;
   uint16_t* fe_depth = nullptr;
@@ -183,7 +187,8 @@ namespace {
 
 void free_all(tsdf_engine* e) {
   EngineDev& D = e->D;
-  void* ptrs[] = {D.table,   D.lock_tag, D.heap,     D.pool,    D.occ,
+  void* ptrs[] = {D.pipe,    D.ctag,     D.rtag,     D.fo,
+                  D.table,   D.lock_tag, D.heap,     D.pool,    D.occ,
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs, D.fresh,
                   e->fe_rgb, e->fe_depth, e->fe_mask, e->fe_out_rgb, e->fe_out_depth,
                   D.vis,     D.band,    D.cand,     D.arrive, D.swdirty, D.fresh_vis, D.pend, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
@@ -368,6 +373,7 @@ const char* tsdf_error_string(int code) {
     case TSDF_ERR_HIP: return "HIP runtime error";
     case TSDF_ERR_CAPACITY: return "output buffer too small";
     case TSDF_ERR_NO_DEVICE: return "no HIP device";
+    case TSDF_ERR_PIPELINE: return "pipelined frame wait timed out";
     default: return "unknown error";
   }
 }
@@ -394,7 +400,11 @@ bool init_state(tsdf_engine* e, bool with_pool = true) {
   ok &= hipMemsetAsync(D.occ, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
   ok &= hipMemsetAsync(D.nk_key, 0, sizeof(unsigned long long) * kNewKeyCap, s) == hipSuccess;
   ok &= hipMemsetAsync(D.nk_order, 0xFF, sizeof(uint32_t) * kNewKeyCap, s) == hipSuccess;
-  ok &= hipMemsetAsync(D.band, 0, sizeof(int32_t) * kBands * kBandStride, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.band, 0, sizeof(int32_t) * 3 * kBands * kBandStride, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.pipe, 0, sizeof(unsigned long long) * kPipeWords, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.ctag, 0, sizeof(uint32_t) * 2 * (size_t)nb, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.rtag, 0, sizeof(uint32_t) * (size_t)nb, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.fo, 0xFF, sizeof(unsigned long long) * (size_t)nb, s) == hipSuccess;
   ok &= hipMemsetAsync(D.visbits, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
   ok &= hipMemsetAsync(D.arrive, 0, sizeof(unsigned long long) * kArriveWords, s) == hipSuccess;
   ok &= hipMemsetAsync(D.swdirty, 0, sizeof(unsigned long long) * (kOccWords / 64), s) == hipSuccess;
@@ -474,14 +484,19 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.nk_list, kNewKeyCap);
   ALLOC(D.pairs, std::max<size_t>(kNewKeyCap, (size_t)nb));
   ALLOC(D.fresh, kNewKeyCap);
-  ALLOC(D.vis, (size_t)kBands * nb);
-  ALLOC(D.band, kBands * kBandStride);
+  // two frames' visible lists, three frames' band counts (pipelined frames: frame_view)
+  ALLOC(D.vis, (size_t)2 * kBands * nb);
+  ALLOC(D.band, 3 * kBands * kBandStride);
+  ALLOC(D.pipe, kPipeWords);
+  ALLOC(D.ctag, (size_t)2 * nb);
+  ALLOC(D.rtag, nb);
+  ALLOC(D.fo, nb);
   // carve candidates of one frame: a shard's list takes every shard's (their visible blocks and the
   // entries exhausted pools left without voxels), so it is sized like the resolver's D.pairs scratch;
   // more are clamped with TSDF_STATUS_SHARD_OVERFLOW. TSDF_CAND_CAP (tests) sets a smaller list.
   D.cand_cap = (int32_t)std::max<size_t>(kNewKeyCap, (size_t)nb);
   if (const char* v = std::getenv("TSDF_CAND_CAP")) D.cand_cap = std::min(D.cand_cap, std::max(1024, std::atoi(v)));
-  ALLOC(D.cand, D.cand_cap);
+  ALLOC(D.cand, (size_t)2 * D.cand_cap);  // two frames' lists (frame_view)
   ALLOC(D.arrive, kArriveWords);
   ALLOC(D.swdirty, kOccWords / 64);
   ALLOC(D.fresh_vis, kNewKeyCap);
@@ -497,10 +512,10 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
     if (const char* v = std::getenv("TSDF_INTEGRATE_WG_PER_CU")) per_cu = std::min(per_cu, std::atoi(v));  // tuning
     D.integrate_grid = std::max(8, std::min(kIntegrateGrid, (per_cu * ncu) & ~7));
     int per_cu_pre = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_pre, reinterpret_cast<const void*>(k_integrate_pre),
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_pre, reinterpret_cast<const void*>(k_frame),
                                                      kIntegrateThreads, 0) != hipSuccess)
       return fail(TSDF_ERR_HIP);
-    if (const char* v = std::getenv("TSDF_INTEGRATE_WG_PER_CU")) per_cu_pre = std::min(per_cu_pre, std::atoi(v));
+    if (const char* v = std::getenv("TSDF_FRAME_WG_PER_CU")) per_cu_pre = std::min(per_cu_pre, std::atoi(v));
     D.integrate_grid_pre = std::max(8, std::min(kIntegrateGrid, (per_cu_pre * ncu) & ~7));
   }
   ALLOC(D.pixA, 2 * e->max_pixels);  // two buffers: a pipelined frame's and the next one's
@@ -528,6 +543,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(e->m_total, 1);
   ALLOC(e->t_count, 1);
 #undef ALLOC
+  D = frame_view(D, 0u);  // the base view (sharded / graph / hash-level paths): frame parity 0
   if (hipHostMalloc(reinterpret_cast<void**>(&e->h_ctr), sizeof(DevCounters)) != hipSuccess)
     return fail(TSDF_ERR_OUT_OF_MEMORY);
   if (cfg.use_stream) {  // the caller's stream; NULL is the legacy default stream (torch's default)
@@ -562,24 +578,30 @@ int tsdf_destroy(tsdf_engine* e) {
 
 int tsdf_synchronize(tsdf_engine* e) {
   if (!e) return TSDF_ERR_INVALID_ARG;
+  HIP_OK(hipSetDevice(e->device));
   ENTER(e);
   HIP_OK(hipStreamSynchronize(e->stream));
+  // a pipelined frame whose in-kernel wait timed out has wrong results: an error here, not only a
+  // status bit; the flags are per-launch tags, so later launches are not affected
+  uint32_t st = 0;
+  HIP_OK(hipMemcpy(&st, &e->D.ctr->status, sizeof(st), hipMemcpyDeviceToHost));
+  if (st & TSDF_STATUS_PIPELINE_TIMEOUT) {
+    set_error("tsdf_synchronize: a pipelined frame's in-kernel wait timed out (TSDF_STATUS_PIPELINE_TIMEOUT)");
+    return TSDF_ERR_PIPELINE;
+  }
   return TSDF_OK;
 }
 
 namespace {
 
-// Phase 1 of a frame: stage host inputs, then k_ingest_dda (pixel records for the whole frame, the
-// DDA over tiles of slice `slice_index` of `slice_count` -- contiguous bands of tile rows --, the
-// visibility of the existing blocks). *P / *ev carry the frame to the later phases.
-int frame_update(tsdf_engine* e, FrameParams P, std::array<hipEvent_t, 5>* ev, void* cands_out = nullptr,
-                 int cand_cap = 0, const FrameParams* Pn = nullptr, int tiles_x = 0, int tiles = 0);
-// pipelined: the pending frame's update and this frame's whole ingest (sweep, tiles, allocation) are
-// one launch (k_integrate_pre); there is no k_ingest_dda launch
-int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, const tsdf_pose* pose,
-                 float max_depth, int slice_index, int slice_count, FrameParams* P,
+// Phase 1 of a frame: stage host inputs, then (launch) k_ingest_dda on view Dv (the frame's lists,
+// counts and candidates: frame_view): pixel records for the whole frame, the DDA over tiles of slice
+// `slice_index` of `slice_count` -- contiguous bands of tile rows --, the visibility of the existing
+// blocks, and the allocation in its last workgroup. *P / *ev carry the frame to the later phases.
+int frame_ingest(tsdf_engine* e, const EngineDev& Dv, const tsdf_frame* f, const tsdf_intrinsics* K,
+                 const tsdf_pose* pose, float max_depth, int slice_index, int slice_count, FrameParams* P,
                  std::array<hipEvent_t, 5>** ev_out, void* keys_out = nullptr, int key_cap = 0,
-                 bool pipelined = false) {
+                 bool launch = true, int pix_buf = 0) {
   if (!e || !f || !K || !pose || !f->depth || !f->rgb || f->width <= 0 || f->height <= 0 ||
       (int64_t)f->width * f->height > e->max_pixels || f->width > e->cfg.max_width ||
       f->height > e->cfg.max_height || (f->ht == nullptr) != (f->lt == nullptr) ||
@@ -615,6 +637,7 @@ int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, 
   P->rgb = rgb;
   P->ht = ht;
   P->lt = lt;
+  P->pix_off = pix_buf ? (int)e->max_pixels : 0;  // which of the two pixel-record buffers
   // a shard's k_integrate reads the raw frame: no whole-frame pixel pass in its ingest
   P->pack_pixels = e->cfg.shard_count > 1 ? 0 : 1;
   const int tiles_x = (W + 15) / 16, tiles_y = (H + 15) / 16;
@@ -641,35 +664,28 @@ int frame_ingest(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, 
     ev = &e->events[e->ev_used++];
   }
   *ev_out = ev;
-  if (pipelined && e->pend) {
-    // this frame's pixel records go to the buffer the pending frame does not read
-    P->pix_off = e->pend_P.pix_off ? 0 : (int)e->max_pixels;
-    e->pend = false;
-    // (phase events: this frame's ingest starts with the launch that runs it)
-    if (ev && e->prof_mode == TSDF_PROFILE_PHASES) HIP_OK(hipEventRecord((*ev)[0], s));
-    return frame_update(e, e->pend_P, e->pend_ev, nullptr, 0, P, tiles_x, tiles);
-  }
+  if (!launch) return TSDF_OK;
   if (ev && e->prof_mode == TSDF_PROFILE_PHASES) HIP_OK(hipEventRecord((*ev)[0], s));
   // ---- allocate (voxel_tsdf.cu:377-386) + visibility (:388-397) ----
   // k_ingest_dda sweeps the blocks that already exist for visibility beside the DDA; its last
   // workgroup resolves the new keys and appends the blocks it creates to the visible lists
   if (e->maxs <= 3)
-    hipLaunchKernelGGL(k_ingest_dda<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, s, e->D, *P, depth,
+    hipLaunchKernelGGL(k_ingest_dda<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, s, Dv, *P, depth,
                        rgb, ht, lt, tiles_x, tiles);
   else
-    hipLaunchKernelGGL(k_ingest_dda<2048>, dim3(kVisWorkgroups + tiles), dim3(256), 0, s, e->D, *P, depth,
+    hipLaunchKernelGGL(k_ingest_dda<2048>, dim3(kVisWorkgroups + tiles), dim3(256), 0, s, Dv, *P, depth,
                        rgb, ht, lt, tiles_x, tiles);
   LAUNCH_OK("k_ingest_dda");
   return TSDF_OK;
 }
 
-// Phase 2: fused update (+ carve minimum); the last workgroup carves (kTailResolve) or packs a
-// shard's carve candidates into cands_out. (Measured and not kept in round 1: running the update of
-// the existing blocks beside the allocation resolver, on a second stream or as a dispatch without
-// the AQL barrier bit: the resolver's chain of dependent HBM round trips slows ~2.5x under the
-// update's memory load.)
-int frame_update(tsdf_engine* e, FrameParams P, std::array<hipEvent_t, 5>* ev, void* cands_out, int cand_cap,
-                 const FrameParams* Pn, int tiles_x, int tiles) {
+// Phase 2: fused update (+ carve minimum) on view Dv; the last workgroup carves (kTailResolve) or
+// packs a shard's carve candidates into cands_out. (Measured and not kept in round 1: running the
+// update of the existing blocks beside the allocation resolver, on a second stream or as a dispatch
+// without the AQL barrier bit: the resolver's chain of dependent HBM round trips slows ~2.5x under
+// the update's memory load.)
+int frame_update(tsdf_engine* e, const EngineDev& Dv, FrameParams P, std::array<hipEvent_t, 5>* ev,
+                 void* cands_out = nullptr, int cand_cap = 0) {
   hipStream_t s = e->stream;
   JOIN_RENDER(e);  // the update writes the pool a raycast on the render stream may still read
   const bool all_ev = ev && e->prof_mode == TSDF_PROFILE_PHASES;
@@ -679,28 +695,15 @@ int frame_update(tsdf_engine* e, FrameParams P, std::array<hipEvent_t, 5>* ev, v
   P.slot_cap = cand_cap;
   // ---- update (voxel_tsdf.cu:474-481) + space carving (:483-488) ----
   auto kfn = P.pack_pixels ? k_integrate_t<false, false> : k_integrate_t<false, true>;
-  const EngineDev& Df = e->D;
-  if (Pn) {  // + the next frame's pixel tiles (pipelined frames)
-    if (e->profiling) ++e->prof_pipelined;
-    const dim3 grid(e->D.integrate_grid_pre + kVisWorkgroups + tiles);
-    const uint32_t tag = ++e->pipe_tag ? e->pipe_tag : ++e->pipe_tag;  // (0 is the initial flag)
-    if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
-      hipExtLaunchKernelGGL(k_integrate_pre, grid, dim3(kIntegrateThreads), 0, s, (*ev)[2], (*ev)[3], 0, Df, P,
-                            *Pn, tiles_x, tiles, tag);
-    } else {
-      if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
-      hipLaunchKernelGGL(k_integrate_pre, grid, dim3(kIntegrateThreads), 0, s, Df, P, *Pn, tiles_x, tiles, tag);
-      if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
-    }
-  } else if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
+  if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
     // the two events are bound to the kernel's own dispatch packet (its begin / end timestamps,
     // the interval rocprofv3's kernel trace reports): no marker packets enter the stream
     hipExtLaunchKernelGGL(kfn, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
-                          (*ev)[2], (*ev)[3], 0, Df, P, (const FrameArgs*)nullptr);
+                          (*ev)[2], (*ev)[3], 0, Dv, P, (const FrameArgs*)nullptr);
   } else {
     if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
     hipLaunchKernelGGL(kfn, dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, s,
-                       Df, P, (const FrameArgs*)nullptr);
+                       Dv, P, (const FrameArgs*)nullptr);
     if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
   }
   LAUNCH_OK("k_integrate");
@@ -708,21 +711,68 @@ int frame_update(tsdf_engine* e, FrameParams P, std::array<hipEvent_t, 5>* ev, v
   return TSDF_OK;
 }
 
+// One k_frame launch (tsdf_fuse.hip): frame A.fid_carve's carving, frame A.fid_alloc's allocation and
+// update (camera / pixel records Pu), frame A.fid_new's ingest (Pn) -- the parts A enables.
+int launch_frame(tsdf_engine* e, PipeArgs A, const FrameParams& Pu, const FrameParams& Pn,
+                 std::array<hipEvent_t, 5>* ev) {
+  hipStream_t s = e->stream;
+  JOIN_RENDER(e);
+  A.tag = ++e->pipe_tag ? e->pipe_tag : ++e->pipe_tag;  // (0: the flags' initial value)
+  A.nint = e->D.integrate_grid_pre;
+  A.range = A.has_alloc ? (uint32_t)((size_t)Pu.W * Pu.H * e->maxs) : 0u;
+  if (!A.has_frame) A.tiles = A.tiles_x = 0;
+  const int nwg = kPipeHead + (A.has_update ? A.nint : 0) + (A.has_update && !A.fresh_ready ? kPipeFreshWG : 0) +
+                  (A.has_frame ? A.tiles + kVisWorkgroups : 0);
+  if (e->profiling) ++e->prof_pipelined;
+  if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
+    hipExtLaunchKernelGGL(k_frame, dim3(nwg), dim3(kIntegrateThreads), 0, s, (*ev)[2], (*ev)[3], 0, e->D, Pu, Pn, A);
+  } else {
+    // (phase events: the launch is the whole frame -- "integrate" spans it, the other phases are empty)
+    const bool all_ev = ev && e->prof_mode == TSDF_PROFILE_PHASES;
+    if (all_ev) HIP_OK(hipEventRecord((*ev)[0], s));
+    if (all_ev) HIP_OK(hipEventRecord((*ev)[1], s));
+    if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
+    hipLaunchKernelGGL(k_frame, dim3(nwg), dim3(kIntegrateThreads), 0, s, e->D, Pu, Pn, A);
+    if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
+    if (all_ev) HIP_OK(hipEventRecord((*ev)[4], s));
+  }
+  LAUNCH_OK("k_frame");
+  return TSDF_OK;
+}
+
 bool sharded(const tsdf_engine* e) { return e->cfg.shard_count > 1; }
 
-// the deferred update of the last pipelined frame, enqueued on its own
+// complete the pending frames (pipelined): kPipeU -- the frame's update with its carving in its last
+// workgroup (k_integrate); kPipeCAU -- one k_frame for the pending carving, allocation and update,
+// then one for that frame's own carving
 int flush_pending(tsdf_engine* e) {
-  if (!e->pend) return TSDF_OK;
-  e->pend = false;
-  return frame_update(e, e->pend_P, e->pend_ev);
+  if (e->ps == tsdf_engine::kPipeNone) return TSDF_OK;
+  HIP_OK(hipSetDevice(e->device));
+  const int ps = e->ps;
+  e->ps = tsdf_engine::kPipeNone;
+  if (ps == tsdf_engine::kPipeU) return frame_update(e, frame_view(e->D, e->p_fid), e->p_P, nullptr);
+  PipeArgs A{};
+  A.has_carve = 1;
+  A.fid_carve = e->p_carve;
+  A.has_alloc = 1;
+  A.has_update = 1;
+  A.fid_alloc = e->p_fid;
+  const FrameParams none{};
+  int rc = launch_frame(e, A, e->p_P, none, nullptr);
+  if (rc) return rc;
+  PipeArgs C{};
+  C.has_carve = 1;
+  C.fid_carve = e->p_fid;
+  return launch_frame(e, C, none, none, nullptr);
 }
 
 }  // namespace
 
-// One frame (TSDFGrid::Integrate). Pipelined (one volume, <= 3 DDA samples per pixel): the frame's
-// ingest is launched now and its update is deferred -- the next tsdf_integrate launches it together
-// with the next frame's pixel-tile preparation (k_integrate_pre), any other entry point (and
-// tsdf_flush / tsdf_synchronize) launches it alone. Stream order keeps every result identical to
+// One frame (TSDFGrid::Integrate). Pipelined (one volume, <= 3 DDA samples per pixel):
+// tsdf_integrate of frame c launches ONE k_frame that carves frame c - 2, allocates and updates frame
+// c - 1 and runs frame c's ingest; what remains (c - 1's carving, c's allocation and update) runs in
+// the next call's launch, or in flush_pending, which every other entry point (and tsdf_flush /
+// tsdf_synchronize) calls first. Stream order and the in-launch flags keep every result identical to
 // the unpipelined two launches per frame.
 int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
                    const tsdf_pose* pose, float max_depth) {
@@ -731,19 +781,47 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
     set_error("tsdf_integrate: a shard of a sharded volume integrates through tsdf_integrate_shard_*");
     return TSDF_ERR_INVALID_ARG;
   }
-  if (e && (!e->pipeline || e->maxs > 3)) {
+  if (!e) return TSDF_ERR_INVALID_ARG;
+  const bool pipe = e->pipeline && e->maxs <= 3;
+  if (!pipe) {
     int rc = flush_pending(e);
     if (rc) return rc;
   }
-  const bool pipe = e && e->pipeline && e->maxs <= 3;
+  uint32_t fid = e->fid_next++;
+  if (fid == 0u) fid = e->fid_next++;
+  const EngineDev Dv = frame_view(e->D, fid);
   FrameParams P;
   std::array<hipEvent_t, 5>* ev = nullptr;
-  int rc = frame_ingest(e, f, K, pose, max_depth, 0, 1, &P, &ev, nullptr, 0, pipe);
+  // the first frame after a flush runs k_ingest_dda (its ingest and allocation in one launch)
+  const bool ingest_alone = !pipe || e->ps == tsdf_engine::kPipeNone;
+  int rc = frame_ingest(e, Dv, f, K, pose, max_depth, 0, 1, &P, &ev, nullptr, 0, ingest_alone, (int)(fid & 1u));
   if (rc) return rc;
-  if (!pipe) return frame_update(e, P, ev);
-  e->pend = true;
-  e->pend_P = P;
-  e->pend_ev = ev;
+  if (!pipe) return frame_update(e, Dv, P, ev);
+  if (ingest_alone) {
+    if (ev) --e->ev_used;  // (no k_frame / k_integrate launch to time in this call)
+    e->ps = tsdf_engine::kPipeU;
+  } else {
+    PipeArgs A{};
+    A.has_update = 1;
+    A.fid_alloc = e->p_fid;
+    A.has_frame = 1;
+    A.fid_new = fid;
+    A.tiles_x = (P.W + 15) / 16;
+    A.tiles = A.tiles_x * ((P.H + 15) / 16);
+    if (e->ps == tsdf_engine::kPipeU) {
+      A.fresh_ready = 1;  // p_fid's new blocks were listed by its k_ingest_dda
+    } else {
+      A.has_carve = 1;
+      A.fid_carve = e->p_carve;
+      A.has_alloc = 1;
+    }
+    rc = launch_frame(e, A, e->p_P, P, ev);
+    if (rc) return rc;
+    e->p_carve = e->p_fid;
+    e->ps = tsdf_engine::kPipeCAU;
+  }
+  e->p_fid = fid;
+  e->p_P = P;
   return TSDF_OK;
 }
 
@@ -778,7 +856,7 @@ int tsdf_integrate_shard_begin(tsdf_engine* e, const tsdf_frame* f, const tsdf_i
   std::array<hipEvent_t, 5>* ev = nullptr;
   // split DDA: the last workgroup packs this slice's keys into keys_out; whole-frame DDA (no key
   // exchange): it resolves the allocation right away, like one volume
-  int rc = frame_ingest(e, f, K, pose, max_depth, slice_index, slice_count, &P, &ev, keys_out, key_cap);
+  int rc = frame_ingest(e, e->D, f, K, pose, max_depth, slice_index, slice_count, &P, &ev, keys_out, key_cap);
   if (rc) return rc;
   P.tail = kTailResolve;
   P.slot = nullptr;
@@ -808,7 +886,7 @@ int tsdf_integrate_shard_update(tsdf_engine* e, const void* keys_in, int32_t key
                        key_cap, e->cfg.shard_count);
     LAUNCH_OK("k_resolve_alloc");
   }
-  int rc = frame_update(e, e->shard_P, e->shard_ev, cands_out, cand_cap);
+  int rc = frame_update(e, e->D, e->shard_P, e->shard_ev, cands_out, cand_cap);
   if (rc) return rc;
   e->shard_phase = 2;
   return TSDF_OK;
@@ -824,7 +902,7 @@ int tsdf_integrate_shard_end(tsdf_engine* e, const void* cands_in, int32_t cand_
   HIP_OK(hipSetDevice(e->device));
   ENTER(e);
   hipLaunchKernelGGL(k_resolve_delete, dim3(1), dim3(kRT), 0, e->stream, e->D, (const VisRec*)e->D.cand,
-                     (const int32_t*)&e->D.ctr->n_cand, 0, reinterpret_cast<const ShardRec*>(cands_in),
+                     (const int32_t*)e->D.ncand, 0, reinterpret_cast<const ShardRec*>(cands_in),
                      cand_cap, e->cfg.shard_count);
   LAUNCH_OK("k_resolve_delete");
   e->shard_phase = 0;

@@ -36,17 +36,17 @@ __device__ void frame_end(const EngineDev& D) {
     D.ctr->total_visible += (unsigned long long)D.ctr->n_vis;
     D.ctr->total_updated += D.ctr->last_updated;
     D.ctr->frames += 1ull;
-    D.ctr->n_cand = 0;  // the next frame's lists start empty (its sweep runs before allocation)
+    *D.ncand = 0;  // the next frame's lists start empty (its sweep runs before allocation)
     D.ctr->n_pend = 0;
   }
-  if (threadIdx.x < kBands) st_co(&D.band[threadIdx.x * kBandStride], 0);  // (written through: see k_integrate_pre)
+  if (threadIdx.x < kBands) st_co(&D.band[threadIdx.x * kBandStride], 0);
 }
 
 // a shard's frame: its carve candidates into the exchange slot, then the owned entries its
 // exhausted pool left without voxels this frame (D.pend, written by the allocation resolver before
 // this launch)
 __device__ void pack_cands_wg(const EngineDev& D, ShardRec* __restrict__ out, int cap) {
-  const int nc = ld_co(&D.ctr->n_cand);
+  const int nc = ld_co(D.ncand);
   const int np = min(D.ctr->n_pend, (int)kNewKeyCap);
   const int n = nc + np;
   const unsigned long long* rq = reinterpret_cast<const unsigned long long*>(D.cand);
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void k_shard_abort(EngineDev D) {
   __syncthreads();
   if (threadIdx.x == 0) {
     D.ctr->nk_count = 0;
-    D.ctr->n_cand = 0;
+    *D.ncand = 0;
     D.ctr->n_fresh = 0;
     D.ctr->n_pend = 0;
     D.ctr->status |= 32u;  // TSDF_STATUS_SHARD_ABORTED
@@ -106,51 +106,15 @@ __global__ __launch_bounds__(256) void k_shard_abort(EngineDev D) {
 // space carving of the candidates (voxel_tsdf.cu:483-488, kTailResolve) or, in a shard's frame,
 // the packing of its candidates for the exchange (kTailPack; k_resolve_delete follows it).
 // The statistics (their loads) come after the carving, off its path.
-// Pre (k_integrate_pre): only the carving and the band-count reset the next frame's chained sweep
-// waits for; the statistics follow once the carving is published (integrate_stats), off the frame's
-// path. The band counts are read before the carving (they are final since the previous launch).
-__device__ __forceinline__ void integrate_stats(const EngineDev& D, DeleteLds& L) {
-  const int t = threadIdx.x;
-  lds_barrier();
-  const int bc = t < kBands ? L.bcnt[t] : 0;
-  int nband;
-  (void)wg_excl_scan(bc, L.scan, &nband);
-  if (t == 0) {
-    const unsigned long long upd = arrive_collect(D.arrive + kArrIntegrate);
-    const int nvis = nband + D.ctr->n_fresh;
-    D.ctr->last_updated = upd;
-    D.ctr->integrate_ticks += L.tend - ld_co(&D.arrive[kArrStart]);
-    D.ctr->n_vis = nvis;
-    D.ctr->total_visible += (unsigned long long)nvis;
-    D.ctr->total_updated += upd;
-    D.ctr->frames += 1ull;
-  }
-}
-
-template <bool Pre = false>
 __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FrameParams& P, DeleteLds& L) {
   const int t = threadIdx.x;
   const unsigned long long tend = __builtin_amdgcn_s_memrealtime();  // the update's span ends here
   TSDF_STAMP(D, 7, 0);
-  const int bc_pre = Pre && t < kBands ? D.band[t * kBandStride] : 0;
   if (P.tail == kTailPack)
     pack_cands_wg(D, P.slot, P.slot_cap);
   else
-    resolve_delete_wg(D, D.cand, &D.ctr->n_cand, 0, L);
+    resolve_delete_wg(D, D.cand, D.ncand, 0, L);
   TSDF_STAMP(D, 7, 1);
-  if (Pre) {
-    lds_barrier();
-    if (t < kBands) {
-      L.bcnt[t] = bc_pre;
-      st_co(&D.band[t * kBandStride], 0);  // (written through: see k_integrate_pre)
-    }
-    if (t == 0) {  // (written through: the allocation resolver later in this launch adds to n_pend)
-      L.tend = tend;
-      st_co(&D.ctr->n_cand, 0);
-      st_co(&D.ctr->n_pend, 0);
-    }
-    return;
-  }
   lds_barrier();  // (L.scan is reused below)
   const int bc = t < kBands ? D.band[t * kBandStride] : 0;
   int nband;
@@ -165,6 +129,186 @@ __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FramePa
   TSDF_STAMP(D, 7, 2);
 }
 
+// One visible block's update (tsdf_integrate_kernel, voxel_tsdf.cu:149-205) by one wave of the two
+// that share it (hf: which half of its 512 voxels; 4 voxels per lane). mn: the minimum |tsdf| of the
+// lane's voxels after the update (the carving test), my_upd: + the lane's updated voxels.
+template <bool Raw>
+__device__ __forceinline__ void update_block(const EngineDev& D, const FrameParams& P, const VisRec& r, int lane,
+                                             int hf, float& mn, int& my_upd) {
+  const int rx0 = (lane & 1) * 4, ry = (lane >> 1) & 7, rz = (lane >> 4) + 4 * hf;
+  const int off = (hf * 256 + lane * 4) * 4;
+  const float neg_trunc = -P.trunc;
+  const int32_t pidx = r.idx;
+  uint8_t* blk = D.pool + (size_t)pidx * kBlockBytes;
+#if defined(TSDF_EXP) && (TSDF_EXP & 2)  // experiment build: no pool state loads
+  float4 ts = make_float4(0.5f, 0.5f, 0.5f, 0.5f), pr = ts;
+  uint4 cw = make_uint4(0x05808080u, 0x05808080u, 0x05808080u, 0x05808080u);
+#else
+  float4 ts, pr;
+  uint4 cw;
+  const bool fresh = r.pad != 0;
+  if (fresh) {  // wave-uniform: a block created this frame loads nothing
+    ts = make_float4(-1.f, -1.f, -1.f, -1.f);
+    pr = make_float4(0.f, 0.f, 0.f, 0.f);  // log-odds of AquireBlock's p = 0.5
+    // weight 0; AquireBlock leaves rgb as it was (voxel_mem.cu:43-51): uninitialised memory
+    // or a previous block's colour, i.e. unspecified, visible only on weight-0 voxels. It is
+    // defined as 0 here and in the oracle (a sharded volume's pool indices differ).
+    cw = make_uint4(0u, 0u, 0u, 0u);
+  } else {
+    ts = pool_ld(blk + off);
+    pr = pool_ld(blk + kProbOffset + off);
+    cw = pool_ldu(blk + kRgbwOffset + off);
+  }
+#endif
+#if defined(TSDF_EXP) && (TSDF_EXP & 2)
+  fresh = r.pad != 0;
+#endif
+  const int16_t ax0 = (int16_t)(r.x << kBlockLenBits), ay = (int16_t)((r.y << kBlockLenBits) + ry),
+                az = (int16_t)((r.z << kBlockLenBits) + rz);
+  const float fy = (float)ay * P.voxel, fz = (float)az * P.voxel;
+  int upd_mask = 0;
+  // ---- pass 1: project the lane's 4 voxels (two packed pairs) and issue every pixel gather
+  // before any is consumed (predicated, so all 8 stay in flight together).
+  // cam_T_world * (x voxel, fy, fz) in QuaternionBase::_transformVector's exact order, with the
+  // parts that do not depend on x computed once per lane (identical operations, so identical
+  // results to se3_apply per voxel).
+  const float qx = P.cq.x, qy = P.cq.y, qz = P.cq.z, qw = P.cq.w;
+  const float qx_fz = qx * fz, qx_fy = qx * fy;
+  float uvx = qy * fz - qz * fy;
+  uvx += uvx;
+  const float w_uvx = qw * uvx, qz_uvx = qz * uvx, qy_uvx = qy * uvx;
+  v2f hzs[2];
+  float4 px[4];
+  float lg[4];
+  bool inb[4];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const v2f wx = v2((float)(int16_t)(ax0 + rx0 + 2 * k), (float)(int16_t)(ax0 + rx0 + 2 * k + 1)) * P.voxel;
+    v2f uvy = qz * wx - qx_fz;
+    v2f uvz = qx_fy - qy * wx;
+    uvy += uvy;
+    uvz += uvz;
+    const v2f cx = qy * uvz - qz * uvy;
+    const v2f cy = qz_uvx - qx * uvz;
+    const v2f cz = qx * uvy - qy_uvx;
+    const v2f pcx = ((wx + w_uvx) + cx) + P.ct.x;
+    const v2f pcy = ((fy + qw * uvy) + cy) + P.ct.y;
+    const v2f pcz = ((fz + qw * uvz) + cz) + P.ct.z;
+    const v2f hx = P.fx * pcx + P.cx * pcz;
+    const v2f hy = P.fy * pcy + P.cy * pcz;
+    const v2f rz = v2(__builtin_amdgcn_rcpf(pcz.x), __builtin_amdgcn_rcpf(pcz.y));
+    int u0, u1, v0, v1;
+    round_quot_i2(hx, pcz, rz, true, true, u0, u1);
+    round_quot_i2(hy, pcz, rz, true, true, v0, v1);
+    hzs[k] = pcz;
+    const int uu[2] = {u0, u1}, vv[2] = {v0, v1};
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int j = 2 * k + e;
+      inb[j] = uu[e] >= 0 && uu[e] < P.W && vv[e] >= 0 && vv[e] < P.H;
+#if defined(TSDF_EXP) && (TSDF_EXP & 1)  // experiment build: no pixel gathers
+      if (inb[j]) px[j] = make_float4(pcz[e] + 0.01f, 1.0f, 1.0f, __uint_as_float(0x00808080u));
+#else
+      // unconditional gathers at a clamped index (pixel 0 when out of the image): no exec-
+      // masked region around the loads, so all 8 stay in flight until pass 2
+      const int img = inb[j] ? vv[e] * P.W + uu[e] : 0;
+      if (Raw) {  // x: depth, y: pixel x, z: pixel y, w: rgb (range / w_new computed in pass 2)
+        const uint32_t c = (uint32_t)P.rgb[3 * img] | ((uint32_t)P.rgb[3 * img + 1] << 8) |
+                           ((uint32_t)P.rgb[3 * img + 2] << 16);
+        px[j] = make_float4(P.depth[img], __int_as_float(uu[e]), __int_as_float(vv[e]), __uint_as_float(c));
+        lg[j] = P.ht ? pixel_logodds(P.ht[img], P.lt[img]) : 0.0f;
+      } else {
+        px[j] = D.pixA[P.pix_off + img];
+        lg[j] = D.pixB[P.pix_off + img];
+      }
+#endif
+    }
+  }
+  // ---- pass 2: tsdf_integrate_kernel's update (voxel_tsdf.cu:174-203), branch-free on
+  // packed pairs; each voxel's result is kept only where it is updated (the reference's
+  // conditions: in image, 0 < d <= max_depth, sdf > -trunc).
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int j0 = 2 * k, j1 = 2 * k + 1;
+    const v2f d = v2(px[j0].x, px[j1].x);
+    v2f rng, w_new;
+    if (Raw) {  // the ingest's per-pixel terms (identical operations)
+      const f3 r0 = pixel_ray(P, __float_as_int(px[j0].y), __float_as_int(px[j0].z));
+      const f3 r1 = pixel_ray(P, __float_as_int(px[j1].y), __float_as_int(px[j1].z));
+      rng = v2(sqrtf(dot3(r0, r0)), sqrtf(dot3(r1, r1)));
+      w_new = v2(pixel_w_new(P, d.x), pixel_w_new(P, d.y));
+    } else {
+      rng = v2(px[j0].y, px[j1].y);
+      w_new = v2(px[j0].z, px[j1].z);
+    }
+    const uint32_t n0 = __float_as_uint(px[j0].w), n1 = __float_as_uint(px[j1].w);
+    const v2f sdf = rng * (d - hzs[k]);
+    const bool a0 = inb[j0] && !(d.x == 0 || d.x > P.max_depth) && sdf.x > neg_trunc;
+    const bool a1 = inb[j1] && !(d.y == 0 || d.y > P.max_depth) && sdf.y > neg_trunc;
+    if (a0 || a1) {
+      v2f tn = quot_const2(sdf, P.trunc, P.inv_trunc, a0, a1);
+      tn = v2(fminf(1.0f, tn.x), fminf(1.0f, tn.y));
+      const uint32_t o0 = compu(cw, j0), o1 = compu(cw, j1);
+      const v2f w_old = v2((float)(o0 >> 24), (float)(o1 >> 24));
+      const v2f wc = w_old + w_new;  // >= 0: both weights are
+      const v2f iwc = v2(__builtin_amdgcn_rcpf(wc.x), __builtin_amdgcn_rcpf(wc.y));
+      uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {  // rgb running average, numerators >= 0
+        const v2f num = v2((float)((o0 >> (8 * ch)) & 0xFF), (float)((o1 >> (8 * ch)) & 0xFF)) * w_old +
+                        v2((float)((n0 >> (8 * ch)) & 0xFF), (float)((n1 >> (8 * ch)) & 0xFF)) * w_new;
+        int32_t r0, r1;
+        round_quot_pos2(num, wc, iwc, a0, a1, r0, r1);
+        c0 |= (uint32_t)min(255, r0) << (8 * ch);
+        c1 |= (uint32_t)min(255, r1) << (8 * ch);
+      }
+      const v2f tnum = v2(comp(ts, j0), comp(ts, j1)) * w_old + tn * w_new;
+      const v2f tq = div_pair(tnum, wc, iwc, a0, a1);
+      const v2f wr = wc + v2(0x1.fffffep-2f, 0x1.fffffep-2f);
+      c0 |= weight_round_cap(wr.x, 40u) << 24;
+      c1 |= weight_round_cap(wr.y, 40u) << 24;
+      // semantic fusion (voxel_tsdf.cu:196-202): p' = P / (P + N) with
+      //   P = exp((w_old ln p + w_new ln ht) / wc), N = exp((w_old ln(1 - p) + w_new ln lt) / wc)
+      // is exactly the logistic of  L' = (w_old L + w_new log2(ht / lt)) / wc  in the base-2
+      // log-odds L = log2(p / (1 - p)) the pool stores (pixB holds log2 ht - log2 lt), so the
+      // update is two products and a sum; readers convert with prob_of_logodds (within 1e-4
+      // of the reference's float chain, and L stays exactly 0 -- p 0.5 -- when ht == lt)
+      const v2f pn = (w_old * v2(comp(pr, j0), comp(pr, j1)) + w_new * v2(lg[j0], lg[j1])) * iwc;
+      if (a0) {
+        setc(ts, j0, tq.x);
+        setc(pr, j0, pn.x);
+        setu(cw, j0, c0);
+      }
+      if (a1) {
+        setc(ts, j1, tq.y);
+        setc(pr, j1, pn.y);
+        setu(cw, j1, c1);
+      }
+      upd_mask |= (a0 ? 1 << j0 : 0) | (a1 ? 1 << j1 : 0);
+    }
+    mn = fminf(mn, fminf(fabsf(comp(ts, j0)), fabsf(comp(ts, j1))));
+  }
+#if defined(TSDF_EXP) && (TSDF_EXP & 4)  // experiment build: no pool state stores
+  if (upd_mask < 0) {
+#else
+  if (upd_mask == 0xF || fresh) {
+#endif
+    // all four voxels written (a fresh block's untouched voxels get AquireBlock's state)
+    pool_st(blk + off, ts);
+    pool_st(blk + kProbOffset + off, pr);
+    pool_stu(blk + kRgbwOffset + off, cw);
+  } else if (upd_mask) {  // only the updated voxels' words: writes stay N_upd x 12 B
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (upd_mask & (1 << j)) {
+        reinterpret_cast<float*>(blk + off)[j] = comp(ts, j);
+        reinterpret_cast<float*>(blk + kProbOffset + off)[j] = comp(pr, j);
+        reinterpret_cast<uint32_t*>(blk + kRgbwOffset + off)[j] = compu(cw, j);
+      }
+  }
+  my_upd += __popc(upd_mask);
+}
+
 // 64 VGPRs: 8 waves per SIMD (65 without the bound: 7). Graph: the graph-captured form reads its
 // camera from the FrameArgs block the graph's first node uploads.
 // The visible blocks are the sweep's band lists (blocks that existed before the frame) followed by
@@ -175,10 +319,9 @@ __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FramePa
 #ifndef TSDF_INTEGRATE_WAVES
 #define TSDF_INTEGRATE_WAVES 7
 #endif
-// nint: the update's workgroups (blocks [0, nint) of the launch; k_integrate_pre appends the next
-// frame's pixel-tile workgroups after them). L: the LDS of the last arriver's carving resolve.
+// nint: the update's workgroups (the whole grid). L: the LDS of the last arriver's carving resolve.
 // returns true in the workgroup that arrived last (and ran the carving tail)
-template <bool Graph, bool Raw, bool Pre = false>
+template <bool Graph, bool Raw>
 __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FrameParams& Pv,
                                                const FrameArgs* __restrict__ A, int nint, DeleteLds& L) {
   FrameParams P = Graph ? A->P : Pv;
@@ -210,9 +353,6 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
   const int nband = nvis;
   nvis += D.ctr->n_fresh;
   const int g = blockIdx.x & 7, ngrp = nint >> 3;
-  const int rx0 = (lane & 1) * 4, ry = (lane >> 1) & 7, rz = (lane >> 4) + 4 * hf;
-  const int off = (hf * 256 + lane * 4) * 4;
-  const float neg_trunc = -P.trunc;
   int my_upd = 0;
   if (threadIdx.x == 0) {  // (ordered before their first use by the pair loop's barrier)
     s_ncand = 0;
@@ -230,8 +370,6 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
   for (int pp = p_lo + (blockIdx.x >> 3); pp < p_hi; pp += ngrp) {
     const int b = 2 * pp + pair;
     float mn = __builtin_inff();
-    bool fresh = false;
-    int32_t pidx = 0;
     VisRec r{};
     if (b < nvis) {
       if (b >= nband) {
@@ -246,175 +384,7 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
           }
         r = D.vis[(size_t)bd * D.nblocks + __builtin_amdgcn_readfirstlane(ofs)];
       }
-      pidx = r.idx;
-      uint8_t* blk = D.pool + (size_t)pidx * kBlockBytes;
-#if defined(TSDF_EXP) && (TSDF_EXP & 2)  // experiment build: no pool state loads
-      float4 ts = make_float4(0.5f, 0.5f, 0.5f, 0.5f), pr = ts;
-      uint4 cw = make_uint4(0x05808080u, 0x05808080u, 0x05808080u, 0x05808080u);
-#else
-      float4 ts, pr;
-      uint4 cw;
-      fresh = r.pad != 0;
-      if (fresh) {  // wave-uniform: a block created this frame loads nothing
-        ts = make_float4(-1.f, -1.f, -1.f, -1.f);
-        pr = make_float4(0.f, 0.f, 0.f, 0.f);  // log-odds of AquireBlock's p = 0.5
-        // weight 0; AquireBlock leaves rgb as it was (voxel_mem.cu:43-51): uninitialised memory
-        // or a previous block's colour, i.e. unspecified, visible only on weight-0 voxels. It is
-        // defined as 0 here and in the oracle (a sharded volume's pool indices differ).
-        cw = make_uint4(0u, 0u, 0u, 0u);
-      } else {
-        ts = pool_ld(blk + off);
-        pr = pool_ld(blk + kProbOffset + off);
-        cw = pool_ldu(blk + kRgbwOffset + off);
-      }
-#endif
-#if defined(TSDF_EXP) && (TSDF_EXP & 2)
-      fresh = r.pad != 0;
-#endif
-      const int16_t ax0 = (int16_t)(r.x << kBlockLenBits), ay = (int16_t)((r.y << kBlockLenBits) + ry),
-                    az = (int16_t)((r.z << kBlockLenBits) + rz);
-      const float fy = (float)ay * P.voxel, fz = (float)az * P.voxel;
-      int upd_mask = 0;
-      // ---- pass 1: project the lane's 4 voxels (two packed pairs) and issue every pixel gather
-      // before any is consumed (predicated, so all 8 stay in flight together).
-      // cam_T_world * (x voxel, fy, fz) in QuaternionBase::_transformVector's exact order, with the
-      // parts that do not depend on x computed once per lane (identical operations, so identical
-      // results to se3_apply per voxel).
-      const float qx = P.cq.x, qy = P.cq.y, qz = P.cq.z, qw = P.cq.w;
-      const float qx_fz = qx * fz, qx_fy = qx * fy;
-      float uvx = qy * fz - qz * fy;
-      uvx += uvx;
-      const float w_uvx = qw * uvx, qz_uvx = qz * uvx, qy_uvx = qy * uvx;
-      v2f hzs[2];
-      float4 px[4];
-      float lg[4];
-      bool inb[4];
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const v2f wx = v2((float)(int16_t)(ax0 + rx0 + 2 * k), (float)(int16_t)(ax0 + rx0 + 2 * k + 1)) * P.voxel;
-        v2f uvy = qz * wx - qx_fz;
-        v2f uvz = qx_fy - qy * wx;
-        uvy += uvy;
-        uvz += uvz;
-        const v2f cx = qy * uvz - qz * uvy;
-        const v2f cy = qz_uvx - qx * uvz;
-        const v2f cz = qx * uvy - qy_uvx;
-        const v2f pcx = ((wx + w_uvx) + cx) + P.ct.x;
-        const v2f pcy = ((fy + qw * uvy) + cy) + P.ct.y;
-        const v2f pcz = ((fz + qw * uvz) + cz) + P.ct.z;
-        const v2f hx = P.fx * pcx + P.cx * pcz;
-        const v2f hy = P.fy * pcy + P.cy * pcz;
-        const v2f rz = v2(__builtin_amdgcn_rcpf(pcz.x), __builtin_amdgcn_rcpf(pcz.y));
-        int u0, u1, v0, v1;
-        round_quot_i2(hx, pcz, rz, true, true, u0, u1);
-        round_quot_i2(hy, pcz, rz, true, true, v0, v1);
-        hzs[k] = pcz;
-        const int uu[2] = {u0, u1}, vv[2] = {v0, v1};
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int j = 2 * k + e;
-          inb[j] = uu[e] >= 0 && uu[e] < P.W && vv[e] >= 0 && vv[e] < P.H;
-#if defined(TSDF_EXP) && (TSDF_EXP & 1)  // experiment build: no pixel gathers
-          if (inb[j]) px[j] = make_float4(pcz[e] + 0.01f, 1.0f, 1.0f, __uint_as_float(0x00808080u));
-#else
-          // unconditional gathers at a clamped index (pixel 0 when out of the image): no exec-
-          // masked region around the loads, so all 8 stay in flight until pass 2
-          const int img = inb[j] ? vv[e] * P.W + uu[e] : 0;
-          if (Raw) {  // x: depth, y: pixel x, z: pixel y, w: rgb (range / w_new computed in pass 2)
-            const uint32_t c = (uint32_t)P.rgb[3 * img] | ((uint32_t)P.rgb[3 * img + 1] << 8) |
-                               ((uint32_t)P.rgb[3 * img + 2] << 16);
-            px[j] = make_float4(P.depth[img], __int_as_float(uu[e]), __int_as_float(vv[e]), __uint_as_float(c));
-            lg[j] = P.ht ? pixel_logodds(P.ht[img], P.lt[img]) : 0.0f;
-          } else {
-            px[j] = D.pixA[P.pix_off + img];
-            lg[j] = D.pixB[P.pix_off + img];
-          }
-#endif
-        }
-      }
-      // ---- pass 2: tsdf_integrate_kernel's update (voxel_tsdf.cu:174-203), branch-free on
-      // packed pairs; each voxel's result is kept only where it is updated (the reference's
-      // conditions: in image, 0 < d <= max_depth, sdf > -trunc).
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int j0 = 2 * k, j1 = 2 * k + 1;
-        const v2f d = v2(px[j0].x, px[j1].x);
-        v2f rng, w_new;
-        if (Raw) {  // the ingest's per-pixel terms (identical operations)
-          const f3 r0 = pixel_ray(P, __float_as_int(px[j0].y), __float_as_int(px[j0].z));
-          const f3 r1 = pixel_ray(P, __float_as_int(px[j1].y), __float_as_int(px[j1].z));
-          rng = v2(sqrtf(dot3(r0, r0)), sqrtf(dot3(r1, r1)));
-          w_new = v2(pixel_w_new(P, d.x), pixel_w_new(P, d.y));
-        } else {
-          rng = v2(px[j0].y, px[j1].y);
-          w_new = v2(px[j0].z, px[j1].z);
-        }
-        const uint32_t n0 = __float_as_uint(px[j0].w), n1 = __float_as_uint(px[j1].w);
-        const v2f sdf = rng * (d - hzs[k]);
-        const bool a0 = inb[j0] && !(d.x == 0 || d.x > P.max_depth) && sdf.x > neg_trunc;
-        const bool a1 = inb[j1] && !(d.y == 0 || d.y > P.max_depth) && sdf.y > neg_trunc;
-        if (a0 || a1) {
-          v2f tn = quot_const2(sdf, P.trunc, P.inv_trunc, a0, a1);
-          tn = v2(fminf(1.0f, tn.x), fminf(1.0f, tn.y));
-          const uint32_t o0 = compu(cw, j0), o1 = compu(cw, j1);
-          const v2f w_old = v2((float)(o0 >> 24), (float)(o1 >> 24));
-          const v2f wc = w_old + w_new;  // >= 0: both weights are
-          const v2f iwc = v2(__builtin_amdgcn_rcpf(wc.x), __builtin_amdgcn_rcpf(wc.y));
-          uint32_t c0 = 0, c1 = 0;
-#pragma unroll
-          for (int ch = 0; ch < 3; ++ch) {  // rgb running average, numerators >= 0
-            const v2f num = v2((float)((o0 >> (8 * ch)) & 0xFF), (float)((o1 >> (8 * ch)) & 0xFF)) * w_old +
-                            v2((float)((n0 >> (8 * ch)) & 0xFF), (float)((n1 >> (8 * ch)) & 0xFF)) * w_new;
-            int32_t r0, r1;
-            round_quot_pos2(num, wc, iwc, a0, a1, r0, r1);
-            c0 |= (uint32_t)min(255, r0) << (8 * ch);
-            c1 |= (uint32_t)min(255, r1) << (8 * ch);
-          }
-          const v2f tnum = v2(comp(ts, j0), comp(ts, j1)) * w_old + tn * w_new;
-          const v2f tq = div_pair(tnum, wc, iwc, a0, a1);
-          const v2f wr = wc + v2(0x1.fffffep-2f, 0x1.fffffep-2f);
-          c0 |= weight_round_cap(wr.x, 40u) << 24;
-          c1 |= weight_round_cap(wr.y, 40u) << 24;
-          // semantic fusion (voxel_tsdf.cu:196-202): p' = P / (P + N) with
-          //   P = exp((w_old ln p + w_new ln ht) / wc), N = exp((w_old ln(1 - p) + w_new ln lt) / wc)
-          // is exactly the logistic of  L' = (w_old L + w_new log2(ht / lt)) / wc  in the base-2
-          // log-odds L = log2(p / (1 - p)) the pool stores (pixB holds log2 ht - log2 lt), so the
-          // update is two products and a sum; readers convert with prob_of_logodds (within 1e-4
-          // of the reference's float chain, and L stays exactly 0 -- p 0.5 -- when ht == lt)
-          const v2f pn = (w_old * v2(comp(pr, j0), comp(pr, j1)) + w_new * v2(lg[j0], lg[j1])) * iwc;
-          if (a0) {
-            setc(ts, j0, tq.x);
-            setc(pr, j0, pn.x);
-            setu(cw, j0, c0);
-          }
-          if (a1) {
-            setc(ts, j1, tq.y);
-            setc(pr, j1, pn.y);
-            setu(cw, j1, c1);
-          }
-          upd_mask |= (a0 ? 1 << j0 : 0) | (a1 ? 1 << j1 : 0);
-        }
-        mn = fminf(mn, fminf(fabsf(comp(ts, j0)), fabsf(comp(ts, j1))));
-      }
-#if defined(TSDF_EXP) && (TSDF_EXP & 4)  // experiment build: no pool state stores
-      if (upd_mask < 0) {
-#else
-      if (upd_mask == 0xF || fresh) {
-#endif
-        // all four voxels written (a fresh block's untouched voxels get AquireBlock's state)
-        pool_st(blk + off, ts);
-        pool_st(blk + kProbOffset + off, pr);
-        pool_stu(blk + kRgbwOffset + off, cw);
-      } else if (upd_mask) {  // only the updated voxels' words: writes stay N_upd x 12 B
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (upd_mask & (1 << j)) {
-            reinterpret_cast<float*>(blk + off)[j] = comp(ts, j);
-            reinterpret_cast<float*>(blk + kProbOffset + off)[j] = comp(pr, j);
-            reinterpret_cast<uint32_t*>(blk + kRgbwOffset + off)[j] = compu(cw, j);
-          }
-      }
-      my_upd += __popc(upd_mask);
+      update_block<Raw>(D, P, r, lane, hf, mn, my_upd);
     }
     mn = wave_min(mn);
     if (lane == 0) s_min[wave] = mn;
@@ -426,7 +396,7 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
         if (k < kIntegrateCandBuf) {
           s_cand[k] = r;
         } else {  // buffer full (heavy carving): publish this one now
-          const int kg = atomicAdd(&D.ctr->n_cand, 1);
+          const int kg = atomicAdd(D.ncand, 1);
           const unsigned long long* rv = reinterpret_cast<const unsigned long long*>(&r);
           unsigned long long* dst = reinterpret_cast<unsigned long long*>(&D.cand[kg]);
           st_co(&dst[0], rv[0]);
@@ -447,7 +417,7 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
   const int nc = min(s_ncand, kIntegrateCandBuf);
   if (wave == 0 && nc > 0) {
     int k0 = 0;
-    if (lane == 0) k0 = atomicAdd(&D.ctr->n_cand, nc);
+    if (lane == 0) k0 = atomicAdd(D.ncand, nc);
     k0 = __shfl(k0, 0, 64);
     if (lane < nc) {
       const unsigned long long* rv = reinterpret_cast<const unsigned long long*>(&s_cand[lane]);
@@ -472,7 +442,7 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
   // the even waves' lane 0: overflow records)
   const bool drain = (wave == 0 && nc > 0) || (s_ovf && (wave & 1) == 0);
   if (!arrive_last(D.arrive + kArrIntegrate, wg_upd, &s_last, drain, (uint32_t)nint)) return false;
-  integrate_tail<Pre>(D, P, L);
+  integrate_tail(D, P, L);
   return true;
 }
 
@@ -484,113 +454,297 @@ __attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES)))
   integrate_body<Graph, Raw>(D, Pv, A, (int)gridDim.x, L);
 }
 
-// A pipelined frame: ONE launch does frame n's update and carving and frame n + 1's ingest.
-//  * workgroups [0, nint): frame n's update (D.integrate_grid_pre: one resident wave of them, all
-//    dispatched before any of the workgroups below); the last to arrive carves frame n, publishes
-//    the carving (write-through stores drained, then one flag per XCD = tag), waits until every
-//    workgroup below has counted itself (per-XCD counters) and then runs frame n + 1's allocation
-//    resolver -- k_ingest_dda's tail;
-//  * kVisWorkgroups workgroups: frame n + 1's visibility sweep (vis_sweep_chained: listed and tested
-//    while frame n is updated, the words the carving marks re-tested once it is published, then the
-//    band lists appended);
-//  * one workgroup per pixel tile of frame n + 1 (kTileChained): pixel records into the other record
-//    buffer, the DDA, the key dedupe and the all-corners test while frame n is updated, then, once
-//    the carving is published, the table probe and the new-key insert.
-// The tail publishes the carving, then computes frame n's statistics (integrate_stats) while the
-// chained workgroups run. The sweep and the probes see the table frame n's carving left and the allocation reads the keys
-// they inserted: the same operations in the same order as the two-launch frame, so the same results.
-// The waits cannot deadlock: the update's workgroups are all dispatched before the waiting ones and
-// wait for nothing; the last of them waits only for workgroups that wait for nothing it has not
-// already published. Every wait is bounded (TSDF_STATUS_PIPELINE_TIMEOUT).
-#ifndef TSDF_PRE_WAVES
-#define TSDF_PRE_WAVES TSDF_INTEGRATE_WAVES
-#endif
-__global__ __launch_bounds__(kIntegrateThreads)
-__attribute__((amdgpu_waves_per_eu(TSDF_PRE_WAVES, TSDF_PRE_WAVES))) void k_integrate_pre(
-    EngineDev D, FrameParams P, FrameParams Pn, int tiles_x, int tiles, uint32_t tag) {
-  __shared__ union {
-    DeleteLds del;
-    IngestLds<1024> ing;
-  } U;
-  const int nint = D.integrate_grid_pre;
-  const int w = (int)blockIdx.x - nint;
-  if (w >= 0) {
-    TSDF_STAMP_WG(D, 5, w, 0);
-    // the tiles first, then the sweep workgroups. Measured: with the sweep after the wait, sweep
-    // first was faster (22.85k vs 22.3k frames/s); since the sweep tests before the carving is
-    // published, tiles first ends the chained work 0.3-0.5 us earlier (23.77k / 23.95k vs 23.65k /
-    // 23.82k, scripts/gpu_r3_last.sh): the tiles' DDA, dispatched as the update retires, is the
-    // longer pre-carving part
-#ifndef TSDF_PRE_SWEEP_FIRST
-    if (w >= tiles) {
-      vis_sweep_chained<1024>(D, Pn, w - tiles, U.ing, D.arrive + kArrCarved + (blockIdx.x % kCarvedFlags) * 16, tag);
-    } else {
-      ingest_tile<1024, kTileChained>(D, Pn, Pn.depth, Pn.rgb, Pn.ht, Pn.lt, tiles_x, w, U.ing, tag);
-    }
-#else
-    if (w < kVisWorkgroups) {
-#ifdef TSDF_SWEEP_AFTER_WAIT  // (experiment: the whole sweep after the carving)
-      wait_tag(D.arrive + kArrCarved + (blockIdx.x % kCarvedFlags) * 16, tag, &D.ctr->status);
-      vis_sweep<1024, true>(D, Pn, w, U.ing);
-#else
-      vis_sweep_chained<1024>(D, Pn, w, U.ing, D.arrive + kArrCarved + (blockIdx.x % kCarvedFlags) * 16, tag);
-#endif
-    } else {
-      ingest_tile<1024, kTileChained>(D, Pn, Pn.depth, Pn.rgb, Pn.ht, Pn.lt, tiles_x, w - kVisWorkgroups, U.ing, tag);
-    }
-#endif
-    // done: this workgroup's band counts / new keys are published (atomics that returned, sc1 list
-    // stores drained), then it counts itself for the allocation
-    __builtin_amdgcn_s_waitcnt(0);
-    lds_barrier();
-    TSDF_STAMP_WG(D, 5, w, 3);
-    if (threadIdx.x == 0)
-      __hip_atomic_fetch_add(D.arrive + kArrChained + (blockIdx.x % kChainCounters) * 16, 1ull, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-    return;
+// =============================================================================================
+// Pipelined frames (tsdf_integrate on one volume; DESIGN.md 4 "Pipelined frames"): k_frame.
+// TSDFGrid::Integrate (voxel_tsdf.cu:347-375) of frame b is allocation -> visibility -> update ->
+// carving, and frame b + 1 needs frame b's carving before its own allocation. The update of a block
+// reads only that block and the frame, and a carving only deletes blocks that were its own frame's
+// carve candidates, so the blocks frame b sees that were not frame b - 1's candidates can be updated
+// before frame b - 1's carving has run. One launch per frame in a stream does:
+//  * workgroup 0: frame b - 1's carving (its candidates, listed by last launch's update), then frame
+//    b's allocation (its new keys, inserted by last launch's tiles), each published with a flag;
+//  * frame b's update: the blocks of b's visible lists (last launch's sweep) right away, except frame
+//    b - 1's candidates (ctag), which wait for the carving flag and are updated if it kept them
+//    (rtag); the blocks b's allocation creates, once its flag is up (kPipeFreshWG workgroups);
+//  * frame c = b + 1's ingest: pixel records, DDA, tile dedupe and all-corners test, and the sweep's
+//    listing at once; after the allocation flag the tiles probe and insert (a found key records its
+//    order in D.fo: the next launch's carving re-inserts the keys it deletes) and the sweep re-tests
+//    the occupancy words the carving and the allocation changed (swdirty).
+// Every operation reads the data it would read in the unpipelined frame order, so the results are
+// identical (tests/test_gpu_pipeline.py). Frame f's lists, counts and candidates live in its view
+// (frame_view); nothing a launch reads is written by the same launch except through the two flags.
+// The waits cannot deadlock: workgroup 0 is dispatched first and waits for nothing. Every wait is
+// bounded (TSDF_STATUS_PIPELINE_TIMEOUT).
+// =============================================================================================
+
+// frame f's statistics from its update workgroups' counters (the update ran in an earlier launch),
+// zeroed for frame f + 2. Wave 0.
+__device__ void pipe_frame_stats(const EngineDev& D, uint32_t f) {
+  const int t = threadIdx.x;
+  if (t >= 64) return;
+  unsigned long long* base = D.pipe + kPipeStats + (size_t)(f & 1u) * (kPipeStatLines * 16);
+  const unsigned long long w = base[16 * t], te = base[16 * t + 1];
+  base[16 * t] = 0ull;
+  base[16 * t + 1] = 0ull;
+  unsigned long long vis = w >> 40, upd = w & ((1ull << 40) - 1ull), tmax = te;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    vis += __shfl_xor(vis, o, 64);
+    upd += __shfl_xor(upd, o, 64);
+    const unsigned long long m = __shfl_xor(tmax, o, 64);
+    tmax = m > tmax ? m : tmax;
   }
-  if (!integrate_body<false, false, true>(D, P, nullptr, nint, U.del)) return;
-  const unsigned long long t_pub = __builtin_amdgcn_s_memrealtime();
-  TSDF_STAMP_WG(D, 5, kDiagMaxWg - 1, 0);
-  // the carving tail has run (it reset the band counts the sweep appends to); its table and
-  // band stores were written through (sc1) and its occupancy updates are atomics: drained, they are
-  // visible to agent-scope reads on every XCD, so publish (no L2 write-back of the update's lines)
+  if (t == 0) {
+    const unsigned long long t0 = D.pipe[kPipeT0 + 16 * (f & 1u)];
+    D.ctr->n_vis = (int32_t)vis;
+    D.ctr->last_updated = upd;
+    D.ctr->total_visible += vis;
+    D.ctr->total_updated += upd;
+    D.ctr->frames += 1ull;
+    if (tmax > t0) D.ctr->integrate_ticks += tmax - t0;
+  }
+}
+
+// every store of the calling workgroup drained (each wave's vmcnt(0)), then a workgroup barrier: a
+// flag stored after this publishes them (sc1 stores + drained wait + flag, MI355X_MICROARCH.md)
+__device__ __forceinline__ void drain_barrier() {
   __builtin_amdgcn_s_waitcnt(0);
   lds_barrier();
+}
+// one copy of a launch flag per XCD (8 lines), set by an agent-scope atomic exchange: the only
+// global_atomic_swap_x2 in k_frame, so tests/test_isa.py can pin that a drained barrier precedes it
+__device__ __forceinline__ void publish_flags(unsigned long long* flags, uint32_t tag) {
+  if (threadIdx.x < 8)
+    (void)__hip_atomic_exchange(flags + 16 * threadIdx.x, (unsigned long long)tag, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+}
+
+union FrameLds {
+  DeleteLds del;
+  IngestLds<1024> ing;
+};
+
+// workgroup 0: frame fid_carve's carving, then frame fid_alloc's allocation, each published
+__device__ void pipe_head(const EngineDev& D, const FrameParams& Pu, const PipeArgs& A, FrameLds& U) {
   const int t = threadIdx.x;
-  if (t < kCarvedFlags) st_co(D.arrive + kArrCarved + t * 16, (unsigned long long)tag);
-  TSDF_STAMP_WG(D, 5, kDiagMaxWg - 1, 1);
-  integrate_stats(D, U.del);  // frame n's statistics, while the chained workgroups run
-  unsigned long long t_done = 0ull;
-  if (t < 64) {  // wave 0 polls the completion counters, one per lane (spread: no hot word)
-    const unsigned long long want = (unsigned long long)(kVisWorkgroups + tiles);
-    unsigned long long* ctr = D.arrive + kArrChained + (t % kChainCounters) * 16;
-    const bool mine = t < kChainCounters;
-    uint32_t n = 0;
-    for (;;) {
-      unsigned long long done =
-          mine ? __hip_atomic_fetch_add(ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+  if (A.has_carve) {
+    const EngineDev Dk = frame_view(D, A.fid_carve);
+    resolve_delete_wg(Dk, Dk.cand, Dk.ncand, 0, U.del, A.fid_carve, A.has_alloc ? A.fid_alloc : 0u);
+    lds_barrier();
+    // the carved frame's candidate count and band counts start empty for frame fid_carve + 2 / + 3
+    if (t < kBands) st_co(&Dk.band[t * kBandStride], 0);
+    if (t == 0) st_co(Dk.ncand, 0);
+  }
+  drain_barrier();
+  publish_flags(D.pipe + kPipeCarved, A.tag);
+  if (A.has_alloc) {
+    if (t == 0) {  // frame fid_alloc's ingest span (last launch): allocation flag -> last tile / sweep end
+      unsigned long long* ie = D.pipe + kPipeIngEnd + 16 * (A.fid_alloc & 1u);
+      const unsigned long long a0 = D.pipe[kPipeAPub + 16 * (A.fid_alloc & 1u)], a1 = *ie;
+      if (a1 > a0) D.ctr->ingest_ticks += a1 - a0;
+      *ie = 0ull;
+    }
+    resolve_alloc_wg(D, Pu, A.range, 1, U.ing.u.res);
+    drain_barrier();
+  }
+  const unsigned long long t_pub = __builtin_amdgcn_s_memrealtime();
+  publish_flags(D.pipe + kPipeAlloc, A.tag);
+  if (t == 0) D.pipe[kPipeAPub + 16 * (A.fid_new & 1u)] = t_pub;
+  if (A.has_carve) pipe_frame_stats(D, A.fid_carve);  // off the chain
+}
+
+// One update workgroup of frame b (Db = frame_view(D, b), b = A.fid_alloc). kind 0: b's listed blocks
+// (its band lists, then its fresh list when it was built by an earlier launch), XCD-split like
+// k_integrate; kind 1 (workgroup wi of kPipeFreshWG): the blocks this launch's allocation creates,
+// after its flag. Frame b - 1's carve candidates among the listed blocks (ctag) are deferred to the
+// end of the workgroup's work, after the carving flag, and updated unless the carving released them
+// (rtag); more than kPipeDefer of them: the workgroup waits for the carving at once.
+__device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const PipeArgs& A, int kind, int wi) {
+  __shared__ float s_min[4];
+  __shared__ int s_upd[4], s_vis[4];
+  __shared__ int s_ncand;
+  __shared__ VisRec s_cand[kIntegrateCandBuf];  // this workgroup's carve candidates
+  __shared__ VisRec s_def[kPipeDefer];          // deferred (candidate of frame b - 1) blocks
+  const int lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int pair = wave >> 1, hf = wave & 1;
+  const uint32_t fb = A.fid_alloc;
+  const unsigned long long* carved = Db.pipe + kPipeCarved + (blockIdx.x & 7) * 16;
+  if (threadIdx.x == 0) s_ncand = 0;  // (ordered before its first use by the loop's barriers)
+  if (kind == 0 && (int)blockIdx.x == kPipeHead && threadIdx.x == 0)  // the update's device-clock start
+    st_co(Db.pipe + kPipeT0 + 16 * (fb & 1u), (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  int bstart[kBands];
+  int nvis = 0, nband = 0, p, p_hi, pstep;
+  if (kind == 0) {
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) done += __shfl_xor(done, o, 64);
-      if (done >= want) break;  // (wave-uniform)
-      __builtin_amdgcn_s_sleep(2);
-      if (++n > (1u << 23)) {
-        if (t == 0) atomicOr(&D.ctr->status, 64u);  // TSDF_STATUS_PIPELINE_TIMEOUT
-        break;
+    for (int i = 0; i < kBands; ++i) {
+      bstart[i] = nvis;
+      nvis += Db.band[i * kBandStride];
+    }
+    nband = nvis;
+    if (A.fresh_ready) nvis += Db.ctr->n_fresh;
+    // group g = blockIdx % 8 (one XCD) takes the g-th contiguous eighth of the pairs in band order
+    const int g = blockIdx.x & 7, npairs = (nvis + 1) >> 1;
+    p = (int)(((long long)npairs * g) >> 3) + (((int)blockIdx.x - kPipeHead) >> 3);
+    p_hi = (int)(((long long)npairs * (g + 1)) >> 3);
+    pstep = A.nint >> 3;
+  } else {
+#pragma unroll
+    for (int i = 0; i < kBands; ++i) bstart[i] = 0;
+    wait_tag(Db.pipe + kPipeAlloc + (blockIdx.x & 7) * 16, A.tag, &Db.ctr->status);
+    nvis = ld_co(&Db.ctr->n_fresh);
+    p = wi;
+    p_hi = (nvis + 1) >> 1;
+    pstep = kPipeFreshWG;
+  }
+  const bool chk = A.has_carve && kind == 0;
+  const uint32_t* ct = Db.ctag + (size_t)(A.fid_carve & 1u) * Db.nblocks;
+  auto fetch = [&](int b) -> VisRec {
+    if (b >= nband) return kind ? ld_rec_co(&Db.fresh_vis[b - nband]) : Db.fresh_vis[b - nband];
+    int bd = 0, ofs = b;
+#pragma unroll
+    for (int i = 1; i < kBands; ++i)
+      if (b >= bstart[i]) {
+        bd = i;
+        ofs = b - bstart[i];
+      }
+    return Db.vis[(size_t)bd * Db.nblocks + __builtin_amdgcn_readfirstlane(ofs)];
+  };
+  // a candidate of frame b - 1 the carving has run for: kept unless released (one lane's atomic read:
+  // rtag was written through by workgroup 0 on another XCD)
+  auto kept = [&](const VisRec& r) -> bool {
+    uint32_t v = 0u;
+    if (lane == 0)
+      v = __hip_atomic_fetch_or(&Db.rtag[r.idx], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (uint32_t)__builtin_amdgcn_readfirstlane(v) != A.fid_carve;
+  };
+  int my_upd = 0, my_vis = 0, ndef = 0, dpos = 0;
+  bool phase1 = false, carved_known = false;
+  for (;;) {  // (all control flow below is workgroup-uniform)
+    VisRec r{};
+    bool have = false;
+    if (!phase1) {
+      if (p >= p_hi) {
+        if (ndef == 0) break;
+        if (!carved_known) wait_tag(carved, A.tag, &Db.ctr->status);  // (its barrier publishes s_def)
+        else lds_barrier();
+        carved_known = true;
+        phase1 = true;
+        continue;
+      }
+      const int b0 = 2 * p;
+      const VisRec r0 = b0 < nvis ? fetch(b0) : VisRec{}, r1 = b0 + 1 < nvis ? fetch(b0 + 1) : VisRec{};
+      const bool t0 = chk && b0 < nvis && r0.pad == 0 && ct[r0.idx] == A.fid_carve;
+      const bool t1 = chk && b0 + 1 < nvis && r1.pad == 0 && ct[r1.idx] == A.fid_carve;
+      r = pair ? r1 : r0;
+      const bool mine_t = pair ? t1 : t0;
+      have = b0 + pair < nvis;
+      if (t0 || t1) {
+        const int nt = (int)t0 + (int)t1;
+        if (!carved_known && ndef + nt <= kPipeDefer) {  // deferred to the end
+          if (threadIdx.x == 0) {
+            if (t0) s_def[ndef] = r0;
+            if (t1) s_def[ndef + (int)t0] = r1;
+          }
+          ndef += nt;
+          have = have && !mine_t;
+        } else {
+          if (!carved_known) wait_tag(carved, A.tag, &Db.ctr->status);
+          carved_known = true;
+          if (have && mine_t) have = kept(r);
+        }
+      }
+      p += pstep;
+    } else {
+      if (dpos >= ndef) break;
+      const int d = dpos + pair;
+      dpos += 2;
+      if (d < ndef) {
+        r = s_def[d];
+        have = kept(r);
       }
     }
-    if (mine) st_co(ctr, 0ull);  // (for the next launch)
-    t_done = __builtin_amdgcn_s_memrealtime();
+    float mn = __builtin_inff();
+    if (have) {
+      update_block<false>(Db, P, r, lane, hf, mn, my_upd);
+      my_vis += hf == 0 ? 1 : 0;
+    }
+    mn = wave_min(mn);
+    if (lane == 0) s_min[wave] = mn;
+    lds_barrier();  // (LDS only: this pair's pool stores stay in flight)
+    if (hf == 0 && lane == 0 && have) {
+      const float m2 = fminf(s_min[wave], s_min[wave + 1]);
+      if (m2 >= 0.9f) {  // space_carving_kernel threshold (voxel_tsdf.cu:227, :485)
+        Db.ctag[(size_t)(fb & 1u) * Db.nblocks + r.idx] = fb;  // (read by the next launch's update)
+        const int k = atomicAdd(&s_ncand, 1);
+        if (k < kIntegrateCandBuf) {
+          s_cand[k] = r;
+        } else {  // buffer full (heavy carving): this one now
+          const int kg = atomicAdd(Db.ncand, 1);
+          if (kg < Db.cand_cap) st_rec_co(&Db.cand[kg], r);
+          else atomicOr(&Db.ctr->status, 16u);  // (a list longer than the pool: internal error)
+        }
+      }
+    }
+    lds_barrier();
   }
-  TSDF_STAMP_WG(D, 5, kDiagMaxWg - 1, 2);
-  __syncthreads();
-  // frame n + 1's allocation (k_ingest_dda's tail)
-  resolve_alloc_wg(D, Pn, (uint32_t)Pn.W * (uint32_t)Pn.H * (uint32_t)Pn.maxs, 1, U.ing.u.res);
-  TSDF_STAMP_WG(D, 5, kDiagMaxWg - 1, 3);
-  // chained frames have no k_ingest_dda: its span counter holds carving published -> every chained
-  // workgroup counted (the sweep and the probes after the carving)
-  if (t == 0) D.ctr->ingest_ticks += t_done - t_pub;
+  // the workgroup's carve candidates (read by the next launch's carving) and statistics
+  const int tot = wave_sum(my_upd);
+  if (lane == 0) {
+    s_upd[wave] = tot;
+    s_vis[wave] = my_vis;
+  }
+  lds_barrier();
+  const int nc = min(s_ncand, kIntegrateCandBuf);
+  if (wave == 0 && nc > 0) {
+    int k0 = 0;
+    if (lane == 0) k0 = atomicAdd(Db.ncand, nc);
+    k0 = __shfl(k0, 0, 64);
+    if (lane < nc && k0 + lane < Db.cand_cap) st_rec_co(&Db.cand[k0 + lane], s_cand[lane]);
+  }
+  if (threadIdx.x == 0) {
+    const unsigned long long upd = (unsigned long long)(s_upd[0] + s_upd[1] + s_upd[2] + s_upd[3]);
+    const unsigned long long vis = (unsigned long long)(s_vis[0] + s_vis[1] + s_vis[2] + s_vis[3]);
+    unsigned long long* st = Db.pipe + kPipeStats + (size_t)(fb & 1u) * (kPipeStatLines * 16) +
+                             (blockIdx.x % kPipeStatLines) * 16;
+    if (vis | upd) atomicAdd(st, (vis << 40) | upd);
+    atomicMax(st + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
 }
+
+#ifndef TSDF_FRAME_WAVES
+#define TSDF_FRAME_WAVES TSDF_INTEGRATE_WAVES
+#endif
+// grid: kPipeHead head workgroups (0: carving + allocation), A.nint update workgroups (listed blocks),
+// kPipeFreshWG (this launch's new blocks), then frame c's A.tiles pixel tiles and kVisWorkgroups
+// sweep workgroups -- each part only when the launch has it
+__global__ __launch_bounds__(kIntegrateThreads)
+__attribute__((amdgpu_waves_per_eu(TSDF_FRAME_WAVES, TSDF_FRAME_WAVES))) void k_frame(
+    EngineDev D, FrameParams Pu, FrameParams Pn, PipeArgs A) {
+  __shared__ FrameLds U;
+  int w = (int)blockIdx.x;
+  if (w < kPipeHead) {
+    if (w == 0) pipe_head(D, Pu, A, U);
+    return;
+  }
+  w -= kPipeHead;
+  const int nold = A.has_update ? A.nint : 0;
+  const int nfr = A.has_update && !A.fresh_ready ? kPipeFreshWG : 0;
+  if (w < nold + nfr) {
+    pipe_update(frame_view(D, A.fid_alloc), Pu, A, w < nold ? 0 : 1, w - nold);
+    return;
+  }
+  w -= nold + nfr;
+  const unsigned long long* aflag = D.pipe + kPipeAlloc + (blockIdx.x & 7) * 16;
+  if (w < A.tiles)
+    ingest_tile<1024, kTileChained>(D, Pn, Pn.depth, Pn.rgb, Pn.ht, Pn.lt, A.tiles_x, w, U.ing, aflag, A.tag,
+                                    A.fid_new);
+  else
+    vis_sweep_chained<1024>(frame_view(D, A.fid_new), Pn, w - A.tiles, U.ing, aflag, A.tag);
+  if (threadIdx.x == 0)  // the ingest's span ends with its last workgroup
+    atomicMax(D.pipe + kPipeIngEnd + 16 * (A.fid_new & 1u), (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 template __global__ void k_integrate_t<false, false>(EngineDev, FrameParams, const FrameArgs*);
 template __global__ void k_integrate_t<true, false>(EngineDev, FrameParams, const FrameArgs*);
 template __global__ void k_integrate_t<false, true>(EngineDev, FrameParams, const FrameArgs*);
@@ -624,7 +778,7 @@ __device__ __forceinline__ void resolve_delete_merged(EngineDev D, const VisRec*
         run += n;
       }
       s_base[nshard] = run;
-      st_co(&D.ctr->n_cand, run);
+      st_co(D.ncand, run);
       if (ovf) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_SHARD_OVERFLOW
     }
     __syncthreads();
@@ -659,7 +813,7 @@ __global__ __launch_bounds__(kRT) void k_resolve_delete(EngineDev D, const VisRe
   resolve_delete_merged(D, recs, count, direct, cands_in, cap, nshard);
 }
 __global__ __launch_bounds__(kRT) void k_resolve_delete_g(EngineDev D, const FrameArgs* __restrict__ A) {
-  resolve_delete_merged(D, D.cand, &D.ctr->n_cand, 0, A->cands_in, A->cand_cap, A->nshard);
+  resolve_delete_merged(D, D.cand, D.ncand, 0, A->cands_in, A->cand_cap, A->nshard);
 }
 
 

@@ -12,36 +12,6 @@
 namespace tsdf {
 
 // ---------------------------------------------------------------------------------------------
-// per-frame new-key set: open addressing on 64-bit packed keys, min candidate order per key
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void keyset_insert(unsigned long long* keys, uint32_t* orders, NkEnt* list,
-                              int32_t* count, uint32_t* status, uint64_t key, uint32_t order) {
-  uint32_t h = (uint32_t)mix64(key) & (kNewKeyCap - 1);
-  for (int p = 0; p < 256; ++p) {
-    // the CAS itself reads the slot (measured equal to a plain read first)
-    const unsigned long long cur = atomicCAS(&keys[h], 0ull, (unsigned long long)key);
-    if (cur == 0ull) {
-      const int s = atomicAdd(count, 1);
-      // the list entry carries the key (the resolver's prologue needs no second load for it),
-      // published for the workgroup that resolves at the end of this launch
-      st_co(&list[s].key, (unsigned long long)key);
-      st_co(&list[s].slot, (unsigned long long)h);
-      atomicMin(&orders[h], order);
-      return;
-    }
-    if (cur == key) {
-      atomicMin(&orders[h], order);
-      return;
-    }
-    h = (h + 1) & (kNewKeyCap - 1);
-  }
-  atomicOr(status, 2u);  // TSDF_STATUS_NEWKEY_OVERFLOW
-}
-__device__ __forceinline__ void nk_insert(const EngineDev& D, uint64_t key, uint32_t order) {
-  keyset_insert(D.nk_key, D.nk_order, D.nk_list, &D.ctr->nk_count, &D.ctr->status, key, order);
-}
-
-// ---------------------------------------------------------------------------------------------
 // k_ingest_dda: 16x16 pixel tile per workgroup.
 //  1. pack the frame into per-pixel records the integrate kernel gathers:
 //       pixA = {depth, range = |K^-1 [x y 1]|, w_new = (1 - d / max_depth) * 4, rgb}
@@ -142,20 +112,27 @@ __device__ __forceinline__ Ent load_ent_t(const int4* table, uint32_t e) {
   return Co ? load_ent_co(table, e) : load_ent(table, e);
 }
 // find_entry (tsdf_device.h) with the entry loads of load_ent_t<Co>
+// (*idx: the entry's pool index when found)
 template <bool Co>
-__device__ __forceinline__ int32_t find_entry_t(const int4* __restrict__ table, int16_t x, int16_t y, int16_t z) {
+__device__ __forceinline__ int32_t find_entry_t(const int4* __restrict__ table, int16_t x, int16_t y, int16_t z,
+                                                int32_t* idx = nullptr) {
   const uint32_t e0 = hash_block(x, y, z) << 1;
   const Ent a = load_ent_t<Co>(table, e0);
-  if (a.x == x && a.y == y && a.z == z && a.idx >= 0) return (int32_t)e0;
+  if (a.x == x && a.y == y && a.z == z && a.idx >= 0) {
+    if (idx) *idx = a.idx;
+    return (int32_t)e0;
+  }
   Ent b = load_ent_t<Co>(table, e0 + 1);
-  if (b.x == x && b.y == y && b.z == z && b.idx >= 0) return (int32_t)(e0 + 1);
   uint32_t last = e0 + 1;
-  while (b.off) {
+  for (;;) {
+    if (b.x == x && b.y == y && b.z == z && b.idx >= 0) {
+      if (idx) *idx = b.idx;
+      return (int32_t)last;
+    }
+    if (!b.off) return -1;
     last = (uint32_t)(last + (int32_t)b.off) & kEntryMask;
     b = load_ent_t<Co>(table, last);
-    if (b.x == x && b.y == y && b.z == z && b.idx >= 0) return (int32_t)last;
   }
-  return -1;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -451,10 +428,13 @@ __device__ void vis_sweep_chained(const EngineDev& D, const FrameParams& P, int 
 
 // One 16x16 pixel tile. kTileFull: k_ingest_dda's tile -- pixel records, the DDA, the LDS key dedupe,
 // the all-corners test, then the table probe and the new-key insert. kTileChained: the same tile of
-// frame n + 1 inside frame n's k_integrate_pre (pipelined frames): everything that reads only the
-// frame and its camera runs while frame n's blocks are updated; the probe and insert wait until frame
-// n's carving has been published (D.ctr->carved == tag) and read the table coherently (the carving
-// ran on another XCD), so they see exactly the table the unpipelined frame's ingest would.
+// frame c inside a pipelined launch (k_frame): everything that reads only the frame and its camera runs
+// while frame c - 1's blocks are updated; the probe and insert wait until frame c - 1's allocation has
+// been published (*flag == tag) and read the table coherently (the allocation ran on another XCD). Frame
+// c - 2's carving has not run yet (it runs in the next launch), so a key found now may be missing after
+// it: a found key records its smallest candidate order in D.fo of its pool block, tagged ~fid, and the
+// carving re-inserts the keys of the blocks it releases (tsdf_resolve.h released_block). Missing keys
+// stay missing (a carving only deletes), so they go to the new-key set now.
 constexpr int kTileFull = 0, kTileChained = 1;
 #ifdef TSDF_CHAIN_PLAIN
 constexpr bool kChainCoherentLoads = false;
@@ -468,7 +448,8 @@ __device__ __forceinline__ void ingest_tile(const EngineDev& D, const FrameParam
                                             const uint8_t* __restrict__ rgb,
                                             const float* __restrict__ ht,
                                             const float* __restrict__ lt, int tiles_x, int tile,
-                                            IngestLds<TS>& S, uint32_t tag = 0u) {
+                                            IngestLds<TS>& S, const unsigned long long* flag = nullptr,
+                                            uint32_t tag = 0u, uint32_t fid = 0u) {
   unsigned long long* s_key = S.u.tile.key;
   uint32_t* s_ord = S.u.tile.ord;
   TSDF_STAMP(D, 0, 0);
@@ -613,17 +594,18 @@ __device__ __forceinline__ void ingest_tile(const EngineDev& D, const FrameParam
       nv += __popcll(leads);
     }
   }
-  if (Mode == kTileChained) {  // frame n's carving is done (this XCD's copy of the flag)
-    TSDF_STAMP_WG(D, 5, (int)blockIdx.x - D.integrate_grid_pre, 1);
-    wait_tag(D.arrive + kArrCarved + (blockIdx.x % kCarvedFlags) * 16, tag, &D.ctr->status);
-    TSDF_STAMP_WG(D, 5, (int)blockIdx.x - D.integrate_grid_pre, 2);
-  }
+  if (Mode == kTileChained) wait_tag(flag, tag, &D.ctr->status);  // the previous frame's allocation is published
   for (int i = lane; i < nv; i += 64) {
     const int slot = s_vis[wave][i];
     const unsigned long long key = s_key[slot];
     int16_t kx, ky, kz;
     unpack_key(key, kx, ky, kz);
-    if (find_entry_t<Mode == kTileChained && kChainCoherentLoads>(D.table, kx, ky, kz) >= 0) continue;
+    int32_t idx = -1;
+    if (find_entry_t<Mode == kTileChained && kChainCoherentLoads>(D.table, kx, ky, kz, &idx) >= 0) {
+      if (Mode == kTileChained && local_idx(idx))
+        atomicMin(&D.fo[idx], ((unsigned long long)~fid << 32) | s_ord[slot]);
+      continue;
+    }
     nk_insert(D, key, s_ord[slot]);
   }
   TSDF_STAMP(D, 0, 5);

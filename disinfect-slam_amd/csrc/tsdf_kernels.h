@@ -45,6 +45,7 @@ struct EngineDev {
   VisRec* vis;                  // kBands x nblocks visible blocks (band-major, any order within)
   int32_t* band;                // kBands x kBandStride: record count of each band list
   VisRec* cand;                 // cand_cap carve candidates (any order; sorted by entry)
+  int32_t* ncand;               // their count (frame views: one list + count per frame parity)
   int32_t cand_cap;             // records D.cand holds (<= the D.pairs scratch, >= 1024)
   unsigned long long* arrive;   // kArriveWords: last-arriver counters of the frame kernels
   unsigned long long* swdirty;  // kOccWords / 64: occupancy words the carving changed (tsdf_resolve.h)
@@ -54,6 +55,13 @@ struct EngineDev {
   // packed frame: two buffers of max_pixels records each (FrameParams.pixA / pixB select one)
   float4* pixA;                 // {depth, range, w_new, rgb}
   float* pixB;                  // log2 ht - log2 lt (base-2 log-odds of the pixel)
+  // pipelined frames (k_frame): flags, per-frame statistics and the per-pool-block tags
+  unsigned long long* pipe;     // kPipeWords (layout below)
+  uint32_t* ctag;               // 2 x nblocks: ctag[(f & 1) * nblocks + b] == f: block b was a carve
+                                //   candidate of frame f
+  uint32_t* rtag;               // nblocks: rtag[b] == f: frame f's carving released block b
+  unsigned long long* fo;       // nblocks: (~f << 32) | order: frame f's DDA found block b's key in
+                                //   the table, with this smallest candidate order
   // query scratch
   unsigned long long* visbits;  // kOccWords
   int32_t* wgcnt;               // kOccWords / 256
@@ -156,8 +164,48 @@ __global__ void k_resolve_alloc_g(EngineDev D, const FrameArgs* A);
 __global__ void k_resolve_delete_g(EngineDev D, const FrameArgs* A);
 template <bool Graph, bool Raw>
 __global__ void k_integrate_t(EngineDev D, FrameParams P, const FrameArgs* A);
-// pipelined frames: the update of P's frame + the pixel-tile preparation of the next frame Pn
-__global__ void k_integrate_pre(EngineDev D, FrameParams P, FrameParams Pn, int tiles_x, int tiles, uint32_t tag);
+// ---- pipelined frames (k_frame, tsdf_fuse.hip; DESIGN.md 4 "Pipelined frames") ----
+// A frame f in flight keeps its visible lists at vis + (f & 1) * kBands * nblocks, their counts at
+// band + (f % 3) * kBands * kBandStride (reset by f's carving, two launches after the sweep wrote
+// them), its carve candidates at cand + (f & 1) * cand_cap with the count in pipe[kPipeNCand + 16 (f & 1)].
+// D.pipe layout (u64 words; every hot word on its own 128-B line):
+constexpr int kPipeNCand = 0;                   // + 16 p: carve-candidate count of parity p (int32)
+constexpr int kPipeCarved = 32;                 // + 16 x: the carving-done flag, copy of XCD x (= tag)
+constexpr int kPipeAlloc = kPipeCarved + 128;   // + 16 x: the allocation-done flag (= tag)
+constexpr int kPipeT0 = kPipeAlloc + 128;       // + 16 p: first update workgroup's start (parity p)
+constexpr int kPipeIngEnd = kPipeT0 + 32;       // + 16 p: the latest sweep / tile workgroup end
+constexpr int kPipeAPub = kPipeIngEnd + 32;     // + 16 p: allocation published (the ingest span start)
+constexpr int kPipeStats = 512;                 // + 1024 p + 16 i: payload (blocks << 40 | voxels) and,
+constexpr int kPipeStatLines = 64;              //   at +1, the latest end stamp of update counter i
+constexpr int kPipeWords = kPipeStats + 2 * kPipeStatLines * 16;
+constexpr int kPipeHead = 8;                    // workgroups before the update's (0: carving + allocation)
+constexpr int kPipeFreshWG = 64;                // workgroups that update the blocks allocated in the launch
+constexpr int kPipeDefer = 32;                  // deferred (carve-pending) blocks one update workgroup holds
+// What one k_frame launch does. Frame ids f are engine-wide (1, 2, ...); frame b's update, frame
+// b - 1's carving and frame c = b + 1's ingest share the launch (any part may be absent).
+struct PipeArgs {
+  int has_carve;        // carve frame fid_carve (its candidates, listed by its update last launch)
+  int has_alloc;        // allocate frame fid_alloc (= b: its new keys, inserted by last launch's tiles)
+  int has_update;       // update frame b's blocks (its lists from last launch's sweep)
+  int fresh_ready;      // b's new blocks were listed by an earlier launch (no allocation in this one)
+  int has_frame;        // frame c's ingest: pixel records, DDA, probe / insert, visibility sweep
+  uint32_t fid_carve, fid_alloc, fid_new;
+  uint32_t tag;         // this launch's flag value
+  uint32_t range;       // candidate order space of frame b (W H maxs)
+  int tiles_x, tiles;   // frame c's pixel tiles
+  int nint;             // update workgroups (a multiple of 8)
+};
+// frame f's view of the engine: its visible lists, their counts, its carve candidates and count
+__device__ __host__ __forceinline__ EngineDev frame_view(const EngineDev& D, uint32_t f) {
+  EngineDev V = D;
+  V.vis = D.vis + (size_t)(f & 1u) * kBands * (size_t)D.nblocks;
+  V.band = D.band + (size_t)(f % 3u) * kBands * kBandStride;
+  V.cand = D.cand + (size_t)(f & 1u) * (size_t)D.cand_cap;
+  V.ncand = reinterpret_cast<int32_t*>(D.pipe + kPipeNCand + 16 * (f & 1u));
+  return V;
+}
+__global__ void k_frame(EngineDev D, FrameParams Pu, FrameParams Pn, PipeArgs A);
+// the update of one frame b with its carving in the same launch (unpipelined tail form): see k_integrate_t
 // graph-captured forms of the frame kernels: identical bodies, arguments from FrameArgs
 template <int TS>
 __global__ void k_ingest_dda_g(EngineDev D, const FrameArgs* A);

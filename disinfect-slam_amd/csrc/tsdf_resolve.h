@@ -51,6 +51,25 @@ __device__ __forceinline__ void st_co(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// a 16-B record written through / read at agent scope (two 8-byte halves)
+template <class R>
+__device__ __forceinline__ void st_rec_co(R* dst, const R& v) {
+  static_assert(sizeof(R) == 16, "16-B record");
+  const unsigned long long* q = reinterpret_cast<const unsigned long long*>(&v);
+  unsigned long long* d = reinterpret_cast<unsigned long long*>(dst);
+  st_co(&d[0], q[0]);
+  st_co(&d[1], q[1]);
+}
+template <class R>
+__device__ __forceinline__ R ld_rec_co(const R* src) {
+  static_assert(sizeof(R) == 16, "16-B record");
+  const unsigned long long* q = reinterpret_cast<const unsigned long long*>(src);
+  unsigned long long a[2] = {ld_co(&q[0]), ld_co(&q[1])};
+  R v;
+  __builtin_memcpy(&v, a, 16);
+  return v;
+}
+
 // Table stores of the carving resolver, written through at agent scope (32-bit sc1 stores; the
 // 16-bit offset by read-modify-write of its dword -- nothing else writes the table meanwhile): a
 // pipelined frame's chained sweep and probes on other XCDs read the carved table right after the
@@ -77,6 +96,36 @@ __device__ __forceinline__ void store_off_idx_co(int4* table, uint32_t e, int16_
 // carving no chained sweep followed only costs a re-test.
 __device__ __forceinline__ void mark_swept_dirty(const EngineDev& D, uint32_t e) {
   atomicOr(&D.swdirty[e >> 12], 1ull << ((e >> 6) & 63));
+}
+
+// ---------------------------------------------------------------------------------------------
+// per-frame new-key set: open addressing on 64-bit packed keys, min candidate order per key
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void keyset_insert(unsigned long long* keys, uint32_t* orders, NkEnt* list,
+                              int32_t* count, uint32_t* status, uint64_t key, uint32_t order) {
+  uint32_t h = (uint32_t)mix64(key) & (kNewKeyCap - 1);
+  for (int p = 0; p < 256; ++p) {
+    // the CAS itself reads the slot (measured equal to a plain read first)
+    const unsigned long long cur = atomicCAS(&keys[h], 0ull, (unsigned long long)key);
+    if (cur == 0ull) {
+      const int s = atomicAdd(count, 1);
+      // the list entry carries the key (the resolver's prologue needs no second load for it),
+      // published for the workgroup that resolves at the end of this launch
+      st_co(&list[s].key, (unsigned long long)key);
+      st_co(&list[s].slot, (unsigned long long)h);
+      atomicMin(&orders[h], order);
+      return;
+    }
+    if (cur == key) {
+      atomicMin(&orders[h], order);
+      return;
+    }
+    h = (h + 1) & (kNewKeyCap - 1);
+  }
+  atomicOr(status, 2u);  // TSDF_STATUS_NEWKEY_OVERFLOW
+}
+__device__ __forceinline__ void nk_insert(const EngineDev& D, uint64_t key, uint32_t order) {
+  keyset_insert(D.nk_key, D.nk_order, D.nk_list, &D.ctr->nk_count, &D.ctr->status, key, order);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -482,10 +531,11 @@ __device__ void resolve_alloc_wave(const EngineDev& D, const FrameParams& P, int
           e = 2 * B + (uint32_t)sl;
         } else {
           const uint32_t wrap = E > T ? 0u : kNumEntry;
-          store_off(D.table, T, (int16_t)(E + wrap - T));
+          store_off_co(D.table, T, (int16_t)(E + wrap - T));
           e = E;
         }
-        store_ent(D.table, e, x, y, z, 0, idx);
+        store_ent_co(D.table, e, x, y, z, 0, idx);
+        mark_swept_dirty(D, e);
         if (mine && idx == kForeignIdx) {  // voxel-less owned entry: carved this frame
           const int pk = atomicAdd(&D.ctr->n_pend, 1);
           if (pk < (int)kNewKeyCap) {
@@ -509,7 +559,7 @@ __device__ void resolve_alloc_wave(const EngineDev& D, const FrameParams& P, int
             vr.pad = 1;
             vr.idx = idx;
             vr.entry = (int32_t)e;
-            D.fresh_vis[nfresh + prank] = vr;
+            st_rec_co(&D.fresh_vis[nfresh + prank], vr);
           } else {
             D.fresh[nfresh + prank] = idx;
           }
@@ -517,8 +567,8 @@ __device__ void resolve_alloc_wave(const EngineDev& D, const FrameParams& P, int
       }
     }
     if (proc) {  // processed: the key-set slot is empty for the next frame
-      D.nk_key[slot] = 0ull;
-      D.nk_order[slot] = 0xFFFFFFFFu;
+      st_co(&D.nk_key[slot], 0ull);
+      st_co(&D.nk_order[slot], 0xFFFFFFFFu);
     }
     const int used = nmine < sfree ? nmine : (sfree > 0 ? sfree : 0);
     sfree -= used;
@@ -535,8 +585,8 @@ __device__ void resolve_alloc_wave(const EngineDev& D, const FrameParams& P, int
   if (l == 0) {
     D.ctr->resolve_alloc_ticks += __builtin_amdgcn_s_memrealtime() - tick0;
     D.ctr->free_count = sfree;
-    D.ctr->n_fresh = nfresh;
-    D.ctr->nk_count = 0;
+    st_co(&D.ctr->n_fresh, nfresh);
+    st_co(&D.ctr->nk_count, 0);
     if (frame_mode) {
       D.ctr->last_alloc = nfresh;
       D.ctr->last_new_keys = n;
@@ -619,7 +669,8 @@ __device__ FAST_INLINE bool resolve_alloc_fast(const EngineDev& D, const FramePa
     }
     const int32_t idx = owned ? L.heap_top[prank] : kForeignIdx;
     const uint32_t e = 2 * B + (e0 ? 0u : 1u);
-    store_ent(D.table, e, x, y, z, 0, idx);
+    store_ent_co(D.table, e, x, y, z, 0, idx);
+        mark_swept_dirty(D, e);
     if (owned) {
       atomicOr(&D.occ[e >> 6], 1ull << (e & 63));
       if (frame_mode) {
@@ -630,20 +681,20 @@ __device__ FAST_INLINE bool resolve_alloc_fast(const EngineDev& D, const FramePa
         vr.pad = 1;
         vr.idx = idx;
         vr.entry = (int32_t)e;
-        D.fresh_vis[prank] = vr;
+        st_rec_co(&D.fresh_vis[prank], vr);
       } else {
         D.fresh[prank] = idx;
       }
     }
-    D.nk_key[slot] = 0ull;
-    D.nk_order[slot] = 0xFFFFFFFFu;
+    st_co(&D.nk_key[slot], 0ull);
+    st_co(&D.nk_order[slot], 0xFFFFFFFFu);
   }
   if (t == 0) {
     D.ctr->lock_epoch = epoch;
     D.ctr->resolve_alloc_ticks += __builtin_amdgcn_s_memrealtime() - tick0;
     D.ctr->free_count = free0 - nowned;
-    D.ctr->n_fresh = nowned;
-    D.ctr->nk_count = 0;
+    st_co(&D.ctr->n_fresh, nowned);
+    st_co(&D.ctr->nk_count, 0);
     if (frame_mode) {
       D.ctr->last_alloc = nowned;
       D.ctr->last_new_keys = n;
@@ -879,10 +930,11 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
             } else {
               const uint32_t T = k[r].T, E = k[r].E;
               const uint32_t wrap = E > T ? 0u : kNumEntry;
-              store_off(D.table, T, (int16_t)(E + wrap - T));
+              store_off_co(D.table, T, (int16_t)(E + wrap - T));
               e = E;
             }
-            store_ent(D.table, e, k[r].x, k[r].y, k[r].z, 0, idx);
+            store_ent_co(D.table, e, k[r].x, k[r].y, k[r].z, 0, idx);
+            mark_swept_dirty(D, e);
             if (mine[r] && idx == kForeignIdx) {
               // a shard's owned entry without voxels (its pool is exhausted): listed for this
               // frame's carving, so no voxel-less owned entry outlives the frame and the key is
@@ -913,7 +965,7 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
                 vr.pad = 1;
                 vr.idx = idx;
                 vr.entry = (int32_t)e;
-                D.fresh_vis[L.nfresh + prank[r]] = vr;
+                st_rec_co(&D.fresh_vis[L.nfresh + prank[r]], vr);
               } else {
                 D.fresh[L.nfresh + prank[r]] = idx;
               }
@@ -921,8 +973,8 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
           }
         }
         if (t + r * kRT < first_dirty) {  // processed: the key-set slot is empty for the next frame
-          D.nk_key[L.bslot[k[r].p]] = 0ull;
-          D.nk_order[L.bslot[k[r].p]] = 0xFFFFFFFFu;
+          st_co(&D.nk_key[L.bslot[k[r].p]], 0ull);
+          st_co(&D.nk_order[L.bslot[k[r].p]], 0xFFFFFFFFu);
         }
       }
       // the table writes must be visible to the next round's loads; after the launch's last round
@@ -945,8 +997,8 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
   if (t == 0) {
     D.ctr->resolve_alloc_ticks += __builtin_amdgcn_s_memrealtime() - tick0;
     D.ctr->free_count = L.sfree;
-    D.ctr->n_fresh = L.nfresh;
-    D.ctr->nk_count = 0;
+    st_co(&D.ctr->n_fresh, L.nfresh);
+    st_co(&D.ctr->nk_count, 0);
     if (frame_mode) {
       D.ctr->last_alloc = L.nalloc;
       D.ctr->last_new_keys = n;
@@ -982,9 +1034,21 @@ constexpr uint32_t kHintSlot0 = 1u << 9;  // (with kHintValid) slot 0 holds the 
 // nothing another delete writes, so the entry-ordered linearisation commits them all; only
 // ReleaseBlock's pushes are ordered (by hash entry). Any other launch returns false before anything
 // global is written and the ordered rounds below handle it.
+// rel_fid != 0 (pipelined frames): ReleaseBlock also tags the block rtag = rel_fid, and when fo_fid
+// != 0 a released block whose key frame fo_fid's DDA found in the table (D.fo, tsdf_ingest.h) goes back
+// into the new-key set with that frame's smallest candidate order: its key is missing again.
+__device__ __forceinline__ void released_block(const EngineDev& D, int32_t idx, int16_t x, int16_t y, int16_t z,
+                                               uint32_t rel_fid, uint32_t fo_fid) {
+  if (!rel_fid) return;
+  st_co(&D.rtag[idx], rel_fid);
+  if (fo_fid) {
+    const unsigned long long w = D.fo[idx];
+    if ((uint32_t)(w >> 32) == ~fo_fid) nk_insert(D, pack_key(x, y, z), (uint32_t)w);
+  }
+}
 __device__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32_t epoch, int direct,
-                                    const unsigned long long (&a)[2], const unsigned long long (&b)[2],
-                                    DeleteLds& L, unsigned long long tick0) {
+                                    const unsigned long long (&a)[2], DeleteLds& L, unsigned long long tick0,
+                                    uint32_t rel_fid, uint32_t fo_fid) {
   const int t = threadIdx.x, wave = t >> 6;
   int16_t x[2] = {0, 0}, y[2] = {0, 0}, z[2] = {0, 0};
   uint32_t A[2] = {0u, 0u}, entry[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
@@ -996,12 +1060,13 @@ __device__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32
     x[r] = (int16_t)(a[r] & 0xFFFF);
     y[r] = (int16_t)((a[r] >> 16) & 0xFFFF);
     z[r] = (int16_t)((a[r] >> 32) & 0xFFFF);
-    entry[r] = (uint32_t)(b[r] >> 32);
     A[r] = hash_block(x[r], y[r], z[r]);
     const Ent s0 = load_ent(D.table, 2 * A[r]), s1 = load_ent(D.table, 2 * A[r] + 1);
     const bool in0 = s0.x == x[r] && s0.y == y[r] && s0.z == z[r] && s0.idx >= 0;
     const bool head = !in0 && s1.x == x[r] && s1.y == y[r] && s1.z == z[r] && s1.idx >= 0 && s1.off == 0;
     bad |= !(in0 || head);
+    // the entry as the table holds it now (a pipelined frame's record may predate an earlier carving)
+    entry[r] = 2 * A[r] + (head ? 1u : 0u);
     if (head) A[r] |= 0x80000000u;  // (the entry is 2 A + 1)
     idx[r] = in0 ? s0.idx : s1.idx;
     rel[r] = (in0 || head) && local_idx(idx[r]);
@@ -1035,6 +1100,7 @@ __device__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32
         rank += (v.x < entry[r]) + (v.y < entry[r]) + (v.z < entry[r]) + (v.w < entry[r]);
       }
       D.heap[free0 + rank] = idx[r];
+      released_block(D, idx[r], x[r], y[r], z[r], rel_fid, fo_fid);
     }
   }
   if (t == 0) {
@@ -1052,8 +1118,12 @@ __device__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32
 // Carve candidates recs[0..*count) (VisRec: key and hash entry; any order). direct: the hash-level
 // test path -- the candidates in list order, one per round (VoxelHashTable::Delete's launch of
 // voxel_hash_test.cu).
+// rel_fid / fo_fid: pipelined frames (released_block above). The deletes are ordered by the entry each
+// candidate holds in the table NOW (its record's entry may predate an earlier carving that moved a list
+// element into its bucket's head).
 __device__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__ recs,
-                                  const int32_t* __restrict__ count, int direct, DeleteLds& L) {
+                                  const int32_t* __restrict__ count, int direct, DeleteLds& L,
+                                  uint32_t rel_fid = 0u, uint32_t fo_fid = 0u) {
   const int t = threadIdx.x;
   TSDF_STAMP(D, 4, 0);
   const unsigned long long tick0 = __builtin_amdgcn_s_memrealtime();
@@ -1070,8 +1140,8 @@ __device__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__
     a1 = ld_co(&rq[2 * (t + kRT)]);
     b1 = ld_co(&rq[2 * (t + kRT) + 1]);
     if (!resolve_fast_off()) {
-      const unsigned long long a[2] = {a0, a1}, b[2] = {b0, b1};
-      if (resolve_delete_fast(D, n, free0, epoch, direct, a, b, L, tick0)) return;
+      const unsigned long long a[2] = {a0, a1};
+      if (resolve_delete_fast(D, n, free0, epoch, direct, a, L, tick0, rel_fid, fo_fid)) return;
       lds_barrier();  // fallback: the ordered rounds below reuse the LDS the fast path used
     }
   }
@@ -1091,17 +1161,23 @@ __device__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__
         const unsigned long long a = r ? a1 : a0, b = r ? b1 : b0;
         const int16_t x = (int16_t)(a & 0xFFFF), y = (int16_t)((a >> 16) & 0xFFFF),
                       z = (int16_t)((a >> 32) & 0xFFFF);
-        const uint32_t entry = (uint32_t)(b >> 32);
         const Ent s0 = load_ent(D.table, 2 * hash_block(x, y, z));
         const bool in0 = s0.x == x && s0.y == y && s0.z == z && s0.idx >= 0;
+        int32_t ce = in0 ? (int32_t)(2 * hash_block(x, y, z)) : find_entry(D.table, x, y, z);
+        const uint32_t entry = ce >= 0 ? (uint32_t)ce : (uint32_t)(b >> 32);
         L.bkey[p] = pack_key(x, y, z);
         L.bidx0[p] = s0.idx;
         L.batch[p] = ((unsigned long long)entry << 32) | (in0 ? kHintSlot0 : 0u) | kHintValid | (uint32_t)p;
       }
     }
   } else if (!direct) {
-    for (int i = t; i < n; i += kRT)
-      D.pairs[i] = ((unsigned long long)(uint32_t)ld_co(&recs[i].entry) << 32) | (uint32_t)i;
+    for (int i = t; i < n; i += kRT) {
+      const unsigned long long a = ld_co(&rq[2 * i]);
+      const int32_t ce = find_entry(D.table, (int16_t)(a & 0xFFFF), (int16_t)((a >> 16) & 0xFFFF),
+                                    (int16_t)((a >> 32) & 0xFFFF));
+      const uint32_t entry = ce >= 0 ? (uint32_t)ce : (uint32_t)ld_co(&recs[i].entry);
+      D.pairs[i] = ((unsigned long long)entry << 32) | (uint32_t)i;
+    }
   }
   if (single || direct) lds_barrier(); else __syncthreads();  // (D.pairs: global)
   TSDF_STAMP(D, 4, 1);
@@ -1149,11 +1225,11 @@ __device__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__
       int kind = 0;  // 1 slot 0, 2 list head, 3 list element
       uint32_t A = 0, prev = 0, cur = 0;
       Ent ecur = {}, eprev = {};
+      int16_t x = 0, y = 0, z = 0;
       if (have) {
         const unsigned long long v = L.batch[base + t];
         const uint32_t lw = (uint32_t)v;
         const int p = (int)(lw & 511u);
-        int16_t x, y, z;
         unpack_key(L.bkey[p], x, y, z);
         A = hash_block(x, y, z);
         if ((lw & kHintValid) && (lw & kHintSlot0) && !L.changed) {  // slot 0 as loaded
@@ -1237,7 +1313,10 @@ __device__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__
       const bool rel = ok && local_idx(released);
       int nrel;
       const int rank = wg_excl_scan(rel ? 1 : 0, L.scan, &nrel);
-      if (rel) D.heap[L.sfree + rank] = released;
+      if (rel) {
+        D.heap[L.sfree + rank] = released;
+        released_block(D, released, x, y, z, rel_fid, fo_fid);
+      }
       if (base + kRT < m || done + m < n) __syncthreads(); else lds_barrier();
       if (t == 0) {
         L.sfree += nrel;

@@ -19,7 +19,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import (SHARD_RECORD_BYTES, STATUS_DDA_OVERFLOW, STATUS_NEWKEY_OVERFLOW,
-                   STATUS_POOL_EXHAUSTED, STATUS_SHARD_ABORTED, STATUS_SHARD_OVERFLOW, TSDF_MEM_DEVICE,
+                   STATUS_PIPELINE_TIMEOUT, STATUS_POOL_EXHAUSTED, STATUS_SHARD_ABORTED, STATUS_SHARD_OVERFLOW, TSDF_MEM_DEVICE,
                    TSDF_MEM_HOST, TSDFError)
 
 NUM_ENTRY = 1 << 22
@@ -33,6 +33,7 @@ __all__ = [
     "CameraIntrinsics", "CameraParams", "SE3", "BoundingCube", "TSDFGrid", "Engine", "ShardGroup",
     "VOXEL_DTYPE", "TSDFError", "hash_block", "block_owner", "load_library", "FOREIGN_IDX",
     "STATUS_SHARD_ABORTED",
+    "STATUS_PIPELINE_TIMEOUT",
 ]
 FOREIGN_IDX = 0x7FFFFFFF  # a shard's index entry of a block another shard holds (kForeignIdx)
 
@@ -246,12 +247,14 @@ class ShardFrameGraph:
         _lib.check(_lib.load().tsdf_graph_shard_begin(
             self._g, C.byref(fr), C.byref(Kc), C.byref(cam_T_world._c()), max_depth, _ptr(keys_out),
             _ptr(keys_in), key_cap, _ptr(cands_out), _ptr(cands_in), cand_cap), "tsdf_graph_shard_begin")
-        self._eng._signal_torch(depth, keys_out)
+        self._eng._signal_torch(keys_out)
+        self._frame = (rgb, depth, ht, lt)  # read again by the update segment (see Engine.integrate_shard_begin)
 
     def update(self, keys_in=None, cands_out=None):
         self._eng._wait_torch(keys_in)
         _lib.check(_lib.load().tsdf_graph_shard_update(self._g), "tsdf_graph_shard_update")
-        self._eng._signal_torch(cands_out)
+        keep, self._frame = getattr(self, "_frame", None) or (), None
+        self._eng._signal_torch(cands_out, *keep)
 
     def end(self, cands_in=None):
         self._eng._wait_torch(cands_in)
@@ -445,8 +448,11 @@ class Engine:
                                                           C.byref(cam_T_world._c()), max_depth,
                                                           slice_index, slice_count, _ptr(keys_out),
                                                           key_cap), "tsdf_integrate_shard_begin")
-        self._signal_torch(depth, keys_out)
-        del keep
+        self._signal_torch(keys_out)
+        # the update (_update) gathers the raw device frame again: the tensors stay referenced here
+        # (a temporary such as depth.float() is not freed and reused by torch's allocator) and torch's
+        # stream is ordered after the engine for them only once _update is enqueued
+        self._shard_frame = keep if _is_torch_cuda(depth) else None
 
     def integrate_shard_update(self, keys_in, key_cap: int, cands_out, cand_cap: int):
         """Sharded frame, phase 2: merge the all-gathered key slots (None after a whole-frame DDA),
@@ -457,7 +463,14 @@ class Engine:
         self._wait_torch(keys_in, cands_out)
         _lib.check(_lib.load().tsdf_integrate_shard_update(self._h, _ptr(keys_in), key_cap, _ptr(cands_out),
                                                            cand_cap), "tsdf_integrate_shard_update")
-        self._signal_torch(keys_in, cands_out)
+        self._release_shard_frame(keys_in, cands_out)
+
+    def _release_shard_frame(self, *tensors):
+        """The engine no longer reads the sharded frame's raw tensors once its update is enqueued:
+        torch's stream waits for the engine, then the references go."""
+        keep = getattr(self, "_shard_frame", None) or ()
+        self._signal_torch(*tensors, *keep)
+        self._shard_frame = None
 
     def integrate_shard_end(self, cands_in, cand_cap: int):
         """Sharded frame, phase 3: delete the all-gathered carve candidates (every shard's)."""
@@ -470,7 +483,10 @@ class Engine:
     def integrate_shard_abort(self):
         """Abort a pending sharded frame (tsdf_integrate_shard_abort): the engine is between frames
         again; STATUS_SHARD_ABORTED is set because shards may have diverged (restore snapshots)."""
-        _lib.check(_lib.load().tsdf_integrate_shard_abort(self._h), "tsdf_integrate_shard_abort")
+        try:
+            _lib.check(_lib.load().tsdf_integrate_shard_abort(self._h), "tsdf_integrate_shard_abort")
+        finally:
+            self._release_shard_frame()
 
     def integrate(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float):
         dev = _is_torch_cuda(depth)
@@ -812,8 +828,13 @@ class ShardGroup:
         try:
             self._integrate(rgb, depth, ht, lt, K, cam_T_world, max_depth, count)
         except Exception:
-            for e in self.engines:  # no shard stays stuck mid-frame (the caller sees the error)
-                e.integrate_shard_abort()
+            # no shard stays stuck mid-frame; every shard is aborted even if one abort fails, and the
+            # caller sees the original error
+            for e in self.engines:
+                try:
+                    e.integrate_shard_abort()
+                except Exception:
+                    pass
             raise
 
     def _integrate(self, rgb, depth, ht, lt, K, cam_T_world, max_depth, count):

@@ -21,6 +21,7 @@ STATUS_DDA_OVERFLOW = 4
 STATUS_RESOLVE_ABORT = 8
 STATUS_SHARD_OVERFLOW = 16
 STATUS_SHARD_ABORTED = 32
+STATUS_PIPELINE_TIMEOUT = 64
 SHARD_RECORD_BYTES = 16
 
 

@@ -84,8 +84,12 @@ def integrate_sharded(engine, bufs, rgb, depth, ht, lt, K, cam_T_world, max_dept
             return
         _integrate_sharded(engine, bufs, rgb, depth, ht, lt, K, cam_T_world, max_depth, split, rank, world)
     except Exception:
-        # a failed exchange (e.g. a collective timeout) must not leave the engine mid-frame
-        engine.integrate_shard_abort()
+        # a failed exchange (e.g. a collective timeout) must not leave the engine mid-frame; the
+        # caller sees the original error even if the abort itself fails
+        try:
+            engine.integrate_shard_abort()
+        except Exception:
+            pass
         raise
 
 

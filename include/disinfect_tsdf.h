@@ -27,6 +27,7 @@ extern "C" {
 #define TSDF_ERR_HIP 3
 #define TSDF_ERR_CAPACITY 4 /* caller buffer too small (two-call pattern) */
 #define TSDF_ERR_NO_DEVICE 5
+#define TSDF_ERR_PIPELINE 6 /* tsdf_synchronize: TSDF_STATUS_PIPELINE_TIMEOUT is set (results wrong) */
 
 #define TSDF_MEM_HOST 0   /* pointer is host memory: engine copies it (pageable is fine) */
 #define TSDF_MEM_DEVICE 1 /* pointer is device memory on the engine's GPU */
@@ -149,10 +150,13 @@ int tsdf_flush(tsdf_engine* e);
  * volume, and the union of the shards equals the unsharded volume block for block and voxel for
  * voxel. TSDFGrid::Integrate (voxel_tsdf.cu:347-375) of a shard is three calls around two
  * exchanges, all asynchronous on the engine stream:
- *   1. tsdf_integrate_shard_begin: the frame's pixel records (every shard's blocks may project
- *      anywhere), the visibility of this shard's blocks, and the block_allocate_kernel DDA
- *      (voxel_tsdf.cu:104-147) over slice `slice_index` of `slice_count` (bands of 16-pixel tile
- *      rows). The keys it finds missing from the index go to keys_out: one slot of
+ *   1. tsdf_integrate_shard_begin: the visibility of this shard's blocks and the
+ *      block_allocate_kernel DDA (voxel_tsdf.cu:104-147) over slice `slice_index` of `slice_count`
+ *      (bands of 16-pixel tile rows). No pixel records are packed: the update in _update gathers
+ *      the raw frame again, so a DEVICE frame (depth, rgb, ht, lt) must stay allocated and
+ *      unmodified until _update has been enqueued and has run in stream order (a host frame is
+ *      staged by _begin and may be reused at once). The keys it finds missing from the index go to
+ *      keys_out: one slot of
  *      tsdf_shard_slot_bytes(key_cap) bytes (record 0 = count header, then 16-B records).
  *      slice_count == 1 with keys_out == NULL: every shard runs the whole DDA and finds the same
  *      keys itself, so no key exchange is needed (keys_in NULL below).

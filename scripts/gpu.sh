@@ -1,0 +1,66 @@
+#!/bin/bash
+# GPU-box evidence runs -- ONE parametrised script (run through gpurun from the repo root):
+#   scripts/gpu.sh <tag> <stage> [<stage> ...]        -> gpurun_out/<tag>/
+# Stages (each under its own time limit; the first failure ends the run):
+#   tests             the whole GPU suite (pytest -m gpu)
+#   tests:<file.py>   one GPU test file
+#   unpiped           tests/test_gpu_parity.py with TSDF_PIPELINE=0
+#   driver            the driver's bench command: bench.py --gpus 1 --steps 20 --warmup 5
+#   profile-driver    kernel trace + FETCH_SIZE / WRITE_SIZE PMC passes of the driver command
+#                     (scripts/profile_integrate.sh; summary + pmc_entry.json under <tag>/prof_driver)
+#   default           bench.py (300 timed frames, CPU baseline)
+#   c5 | c5graph | c4 | c2 | graph   bench.py --loop c5 [--graph] / 1280x720 / --depth-only / --graph
+#   shard8            bench.py --width 1280 --height 720 --shard 8 (single-GPU 8-shard rehearsal)
+#   sq:<kernel>       SQ counter passes of one kernel on the default command (profile_kernel_sq.sh)
+#   stamps            per-workgroup chain stamps (diagnostic library, scripts/diag_chain.py)
+#   ab:<lib1>,<lib2>  interleaved A/B of engine builds on the driver command (scripts/ab.sh)
+set -uo pipefail
+TAG=${1:?tag}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+DRIVER="--gpus 1 --steps 20 --warmup 5"
+PYT="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
+fail() { echo "stage $1 failed"; tail -20 "$2"; exit 1; }
+line() { python3 - "$1" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+r = d.get("roofline", {})
+print(sys.argv[1].split("/")[-1], d["value"], d.get("unit"), "ms/step", d.get("ms_per_step"),
+      "frac", r.get("frac"), "frame.frac_read", r.get("frame", {}).get("frac_read"), "traffic", r.get("traffic"))
+PY
+}
+for st in "$@"; do
+  case $st in
+    tests) timeout -k 10 900 $PYT tests -m gpu > $OUT/pytest.log 2>&1 || fail $st $OUT/pytest.log
+           tail -1 $OUT/pytest.log ;;
+    tests:*) f=${st#tests:}; timeout -k 10 600 $PYT tests/$f -m gpu -v > $OUT/pytest_${f%.py}.log 2>&1 || fail $st $OUT/pytest_${f%.py}.log
+           tail -1 $OUT/pytest_${f%.py}.log ;;
+    unpiped) TSDF_PIPELINE=0 timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_pipeline.py -m gpu > $OUT/pytest_unpiped.log 2>&1 || fail $st $OUT/pytest_unpiped.log
+           tail -1 $OUT/pytest_unpiped.log ;;
+    driver) timeout -k 10 300 python3 bench.py $DRIVER > $OUT/bench_driver.json 2> $OUT/bench_driver.err || fail $st $OUT/bench_driver.err
+           line $OUT/bench_driver.json ;;
+    profile-driver) bash scripts/profile_integrate.sh $OUT/prof_driver $DRIVER || fail $st $OUT/prof_driver/trace_bench.log
+           tail -14 $OUT/prof_driver/summary.txt ;;
+    default) timeout -k 10 300 python3 bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || fail $st $OUT/bench_default.err
+           line $OUT/bench_default.json ;;
+    c5) timeout -k 10 300 python3 bench.py --no-cpu --loop c5 > $OUT/bench_c5.json 2> $OUT/bench_c5.err || fail $st $OUT/bench_c5.err
+           line $OUT/bench_c5.json ;;
+    c5graph) timeout -k 10 300 python3 bench.py --no-cpu --loop c5 --graph > $OUT/bench_c5graph.json 2> $OUT/bench_c5graph.err || fail $st $OUT/bench_c5graph.err
+           line $OUT/bench_c5graph.json ;;
+    graph) timeout -k 10 300 python3 bench.py --no-cpu --graph > $OUT/bench_graph.json 2> $OUT/bench_graph.err || fail $st $OUT/bench_graph.err
+           line $OUT/bench_graph.json ;;
+    c4) timeout -k 10 300 python3 bench.py --no-cpu --width 1280 --height 720 > $OUT/bench_c4.json 2> $OUT/bench_c4.err || fail $st $OUT/bench_c4.err
+           line $OUT/bench_c4.json ;;
+    c2) timeout -k 10 300 python3 bench.py --no-cpu --depth-only > $OUT/bench_c2.json 2> $OUT/bench_c2.err || fail $st $OUT/bench_c2.err
+           line $OUT/bench_c2.json ;;
+    shard8) timeout -k 10 300 python3 bench.py --no-cpu --steps 100 --width 1280 --height 720 --shard 8 > $OUT/shard8_c4.json 2> $OUT/shard8_c4.err || fail $st $OUT/shard8_c4.err
+           line $OUT/shard8_c4.json ;;
+    sq:*) k=${st#sq:}; bash scripts/profile_kernel_sq.sh $OUT/sq_$k $k > $OUT/sq_$k.txt 2>&1 || fail $st $OUT/sq_$k.txt
+           tail -8 $OUT/sq_$k.txt ;;
+    stamps) TSDF_AMD_LIB=disinfect-slam_amd/libdisinfect_tsdf_diag.so timeout -k 10 120 python3 scripts/diag_chain.py > $OUT/chain_stamps.txt 2>&1 || fail $st $OUT/chain_stamps.txt
+           tail -20 $OUT/chain_stamps.txt ;;
+    ab:*) IFS=, read -ra LIBS <<< "${st#ab:}"; bash scripts/ab.sh 20 "${LIBS[@]}" || exit 1 ;;
+    *) echo "unknown stage $st"; exit 2 ;;
+  esac
+done

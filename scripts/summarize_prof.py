@@ -46,12 +46,14 @@ def kname(full):
 
 def window(rows, b, name=""):
     """rows (dispatch id, value) of one kernel -> the bench's timed-window launches. Pipelined frames
-    (k_integrate_pre): the timed window's steps - 1 fused launches are that kernel's last ones (the
-    bench flushes after the warmup; nothing after the timed loop launches it)."""
+    (k_frame): the timed window is one k_ingest_dda (the first frame after the warmup's flush), then
+    steps - 1 k_frame launches of one frame each, then the flush's two k_frame launches (the last
+    frame's allocation + update, then its carving alone): the window's per-frame launches are the
+    last steps + 1 but two."""
     rows = sorted(rows)
     w, k = b["warmup"], b["steps"]
-    if name == "k_integrate_pre":
-        return [v for _, v in rows[-(k - 1):]]
+    if name == "k_frame":
+        return [v for _, v in rows[-(k + 1):-2]]
     return [v for _, v in rows[w:w + k]]
 
 
@@ -78,7 +80,7 @@ def main(out):
                 (int(r["Dispatch_Id"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
         res["timed_window"] = {}
         for name, rows in per.items():
-            if not name.startswith("k_") or len(rows) < b0["steps"] - 1:
+            if not name.startswith("k_") or len(rows) < b0["steps"] - 1 or (name == "k_frame" and len(rows) < b0["steps"] + 1):
                 continue
             win = window(rows, b0, name)
             res["timed_window"][name] = {"launches": len(win), "avg_us": statistics.mean(win) / 1e3,
@@ -99,15 +101,15 @@ def main(out):
             per.setdefault(kname(kn), []).append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
         corr = 2.0 if c == "FETCH_SIZE" else 1.0
         for name, rows in per.items():
-            full = len(rows) >= b["warmup"] + b["steps"] or (name == "k_integrate_pre" and len(rows) >= b["steps"] - 1)
+            full = len(rows) >= b["warmup"] + b["steps"] or (name == "k_frame" and len(rows) >= b["steps"] + 1)
             win = window(rows, b, name) if full else [v for _, v in sorted(rows)]
             res["pmc"].setdefault(name, {})[c] = {
                 "bytes_per_launch": statistics.mean(win) * 1024 * corr, "dispatches": len(win),
                 "timed_window": full}
     if b0:
         res["bench"] = b0
-    # the update launch of the line: k_integrate_pre for pipelined frames, else k_integrate
-    ki = res["pmc"].get("k_integrate_pre") or res["pmc"].get("k_integrate", {})
+    # the frame launch of the line: k_frame for pipelined frames, else k_integrate
+    ki = res["pmc"].get("k_frame") or res["pmc"].get("k_integrate", {})
     if "FETCH_SIZE" in ki and "WRITE_SIZE" in ki:
         bf, bw = pmc_lines["FETCH_SIZE"], pmc_lines["WRITE_SIZE"]
         same = (bf["sum_visible"], bf["sum_updated"]) == (bw["sum_visible"], bw["sum_updated"])

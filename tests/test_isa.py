@@ -86,3 +86,74 @@ def test_publication_is_agent_scope():
     assert any(i.startswith("global_store_dwordx2") and "sc1" in i for i in ing)   # nk_list entries
     assert any(i.startswith("global_load_dwordx2") and "sc1" in i for i in ing)    # resolver prologue
     assert any(i.startswith("global_store_dwordx2") and "sc1" in i for i in integ)  # candidate records
+
+
+def _kframe():
+    funcs = _functions(_disassemble())
+    names = [n for n in funcs if n.startswith("_ZN4tsdf7k_frame")]
+    assert names, sorted(funcs)[:20]
+    return funcs[names[0]]
+
+
+def _addr(ins):
+    m = re.search(r"//\s*([0-9A-F]+):", ins)
+    return int(m.group(1), 16) if m else None
+
+
+def test_k_frame_flags_follow_a_drained_barrier():
+    """k_frame (the pipelined frame, tsdf_fuse.hip): workgroup 0 publishes the carving and then the
+    allocation with one flag per XCD (publish_flags: an agent-scope atomic exchange, the kernel's only
+    global_atomic_swap_x2). Every flag must follow a workgroup barrier with no global store or atomic
+    between them, and a vmcnt(0) wait must come before that barrier (drain_barrier): the table /
+    free-stack / new-key / rtag writes the flags publish are complete when another XCD sees the tag."""
+    body = _kframe()
+    swaps = [i for i, ins in enumerate(body) if ins.startswith("global_atomic_swap_x2")]
+    assert len(swaps) >= 2, "carving and allocation flags"
+    for i in swaps:
+        j = max(k for k in range(i) if body[k].startswith("s_barrier"))
+        between = body[j + 1:i]
+        assert not any(b.startswith(("global_store", "flat_store", "buffer_store", "global_atomic"))
+                       for b in between), between
+        window = body[max(0, j - 40):j]
+        assert any(re.match(r"s_waitcnt\b.*vmcnt\(0\)", w) for w in window), window[-10:]
+
+
+def test_k_frame_hand_offs_are_agent_scope():
+    """The carving / allocation outputs other XCDs read in the same launch are written through (sc1):
+    table entries as three sc1 dwords (store_ent_co), never a plain 16-bit offset store (store_off);
+    new-key-list / fresh-list / candidate records as sc1 dwordx2. Every flag poll (a loop with
+    s_sleep: wait_tag, the fresh workgroups, the deferred blocks) reads with an sc1 load or an atomic,
+    never a plain load (it would be served from this CU's L1 / the XCD's L2 forever)."""
+    body = _kframe()
+    assert not any(ins.startswith("global_store_short") for ins in body), "plain store_off in k_frame"
+    ok = 0
+    for i in range(len(body) - 2):
+        a, b, c = body[i], body[i + 1], body[i + 2]
+        if all(x.startswith("global_store_dword ") and "sc1" in x for x in (a, b, c)) and \
+                "offset:4" in b and "offset:8" in c and "offset" not in a.split("//")[0]:
+            ok += 1
+    assert ok >= 1, "store_ent_co (3 sc1 dwords) not found"
+    assert sum(1 for ins in body if ins.startswith("global_store_dwordx2") and "sc1" in ins) >= 6
+    polls = 0
+    for i, ins in enumerate(body):
+        if not ins.startswith("s_sleep"):
+            continue
+        # the loop around the sleep: the next backward branch
+        here = _addr(ins)
+        for k in range(i + 1, min(len(body), i + 80)):
+            m = re.match(r"s_c?branch\S*\s+(-?\d+)", body[k])
+            if not m:
+                continue
+            off = int(m.group(1))
+            off = off - 65536 if off >= 32768 else off
+            tgt = _addr(body[k]) + 4 + 4 * off
+            if tgt > here:
+                continue
+            loop = [x for x in body if _addr(x) is not None and tgt <= _addr(x) <= _addr(body[k])]
+            loads = [x for x in loop if x.startswith(("global_load", "buffer_load", "flat_load"))]
+            atomics = [x for x in loop if x.startswith("global_atomic")]
+            assert loads or atomics, loop[:12]
+            assert all("sc1" in x for x in loads), [x for x in loads if "sc1" not in x]
+            polls += 1
+            break
+    assert polls >= 3, polls
