@@ -249,8 +249,8 @@ PIX_RECORD_BYTES = 20  # pixA {depth, range, w_new, rgb} + pixB log-odds, writte
 
 
 def pipe_fraction(prof):
-    """Share of the update launches that also prepared the next frame's pixel tiles (pipelined
-    frames: k_integrate_pre)."""
+    """Share of the frames whose update ran in a pipelined frame launch (k_frame: the update beside
+    the previous frame's carving and the next frame's ingest)."""
     return prof.get("pipelined", 0) / max(prof.get("calls", 0), 1)
 
 
@@ -340,11 +340,11 @@ def device_spans(prof, n):
     return {"ingest_dda": us("ms_ingest_device"), "resolve_alloc": us("ms_resolve_alloc_device"),
             "integrate": us("ms_integrate_device"), "resolve_delete": us("ms_resolve_delete_device"),
             "note": "in-kernel 100 MHz clock, mean per timed frame: ingest = k_ingest_dda start -> "
-                    "last workgroup arrival; resolve_* = the resolvers in the last-arriving workgroups "
-                    "of k_ingest_dda / k_integrate; integrate = k_integrate start -> last arrival. "
-                    "Pipelined frames (one k_integrate_pre per frame): integrate = the update's start -> "
-                    "its last arrival, ingest = the carving published -> the next frame's last chained "
-                    "workgroup counted"}
+                    "last workgroup arrival; resolve_* = the resolvers (last-arriving workgroups of "
+                    "k_ingest_dda / k_integrate, or k_frame's workgroup 0); integrate = the update's "
+                    "first workgroup start -> its last workgroup end. Pipelined frames (one k_frame per "
+                    "frame): ingest = the previous frame's allocation published -> the frame's last "
+                    "tile / sweep workgroup end"}
 
 
 def main():
@@ -462,9 +462,9 @@ def main():
         pf = pipe_fraction(prof)
         roof = {
             "kernel": "k_integrate" if pf == 0 else
-                      "k_integrate_pre (the whole pipelined frame in one launch: frame n's update + "
-                      "carving, then frame n+1's pixel records, DDA, key dedupe, visibility sweep, probe, "
-                      "insert and allocation resolver)",
+                      "k_frame (one launch per frame: frame b-1's carving then frame b's allocation in "
+                      "workgroup 0, frame b's update beside them, frame b+1's pixel records, DDA, key "
+                      "dedupe, probe / insert and visibility sweep)",
             "pipelined_fraction": round(pf, 4),
             "bound": "hbm",
             "achieved": round(achieved, 1),

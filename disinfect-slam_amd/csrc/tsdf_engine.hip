@@ -167,12 +167,15 @@ struct tsdf_engine {
   // allocation and update are pending (p_fid's tiles probed and inserted its keys, its sweep listed
   // its blocks). Every other entry point first completes them (flush_pending).
   bool pipeline = true;
-  static constexpr int kPipeNone = 0, kPipeU = 1, kPipeCAU = 2;
+  static constexpr int kPipeNone = 0, kPipeU = 1, kPipeCAU = 2, kPipeAU = 3;  // kPipeAU: p_fid's
+  // allocation and update are pending with no carving (after a graph frame that started a stream)
   int ps = kPipeNone;
   uint32_t fid_next = 1;  // engine-wide frame ids (views, tags; never 0)
   uint32_t p_carve = 0, p_fid = 0;
   FrameParams p_P{};      // frame p_fid's camera / frame / pixel-record buffer
   uint32_t pipe_tag = 0;  // one per k_frame launch: its flags' value
+  int frame_order = 0;    // PipeArgs.order (TSDF_FRAME_ORDER)
+  int ray_segs = 1;       // lanes per ray of k_raycast (TSDF_RAYCAST_SEGS: 1, 2, 4)
   // feed_rgbd_frame staging: raw full-size inputs (host frames) and the half-size outputs
   uint8_t* fe_rgb = nullptr;
   uint16_t* fe_depth = nullptr;
@@ -521,6 +524,11 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.pixA, 2 * e->max_pixels);  // two buffers: a pipelined frame's and the next one's
   ALLOC(D.pixB, 2 * e->max_pixels);
   if (const char* v = std::getenv("TSDF_PIPELINE")) e->pipeline = v[0] != '0';
+  if (const char* v = std::getenv("TSDF_FRAME_ORDER")) e->frame_order = std::min(2, std::max(0, std::atoi(v)));
+  if (const char* v = std::getenv("TSDF_RAYCAST_SEGS")) {
+    const int k = std::atoi(v);
+    e->ray_segs = k == 2 || k == 4 ? k : 1;
+  }
   ALLOC(D.visbits, kOccWords);
   ALLOC(D.wgcnt, kOccWords / 256);
   ALLOC(D.dbg, (size_t)kDiagKernels * kDiagMaxWg * kDiagStamps);
@@ -711,19 +719,25 @@ int frame_update(tsdf_engine* e, const EngineDev& Dv, FrameParams P, std::array<
   return TSDF_OK;
 }
 
+// the launch-wide fields of a k_frame's arguments
+void finish_args(tsdf_engine* e, PipeArgs& A, const FrameParams& Pu) {
+  A.tag = ++e->pipe_tag ? e->pipe_tag : ++e->pipe_tag;  // (0: the flags' initial value)
+  A.nint = e->D.integrate_grid_pre;
+  A.order = e->frame_order;
+  A.range = A.has_alloc ? (uint32_t)((size_t)Pu.W * Pu.H * e->maxs) : 0u;
+  if (!A.has_frame) A.tiles = A.tiles_x = 0;
+}
+
 // One k_frame launch (tsdf_fuse.hip): frame A.fid_carve's carving, frame A.fid_alloc's allocation and
 // update (camera / pixel records Pu), frame A.fid_new's ingest (Pn) -- the parts A enables.
 int launch_frame(tsdf_engine* e, PipeArgs A, const FrameParams& Pu, const FrameParams& Pn,
                  std::array<hipEvent_t, 5>* ev) {
   hipStream_t s = e->stream;
   JOIN_RENDER(e);
-  A.tag = ++e->pipe_tag ? e->pipe_tag : ++e->pipe_tag;  // (0: the flags' initial value)
-  A.nint = e->D.integrate_grid_pre;
-  A.range = A.has_alloc ? (uint32_t)((size_t)Pu.W * Pu.H * e->maxs) : 0u;
-  if (!A.has_frame) A.tiles = A.tiles_x = 0;
+  finish_args(e, A, Pu);
   const int nwg = kPipeHead + (A.has_update ? A.nint : 0) + (A.has_update && !A.fresh_ready ? kPipeFreshWG : 0) +
                   (A.has_frame ? A.tiles + kVisWorkgroups : 0);
-  if (e->profiling) ++e->prof_pipelined;
+  if (e->profiling && A.has_frame) ++e->prof_pipelined;  // (frame launches; not the flush's)
   if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
     hipExtLaunchKernelGGL(k_frame, dim3(nwg), dim3(kIntegrateThreads), 0, s, (*ev)[2], (*ev)[3], 0, e->D, Pu, Pn, A);
   } else {
@@ -742,6 +756,43 @@ int launch_frame(tsdf_engine* e, PipeArgs A, const FrameParams& Pu, const FrameP
 
 bool sharded(const tsdf_engine* e) { return e->cfg.shard_count > 1; }
 
+// The k_frame launch that continues the pending frames, with (has_frame) the ingest of a new frame
+// fid whose parameters are Pn; the state moves to kPipeCAU (or kPipeAU from kPipeNone).
+PipeArgs pipe_step(tsdf_engine* e, bool has_frame, uint32_t fid, const FrameParams& Pn) {
+  PipeArgs A{};
+  const int ps = e->ps;
+  if (ps != tsdf_engine::kPipeNone) {
+    A.has_update = 1;
+    A.fid_alloc = e->p_fid;
+    A.fresh_ready = ps == tsdf_engine::kPipeU;  // p_fid's new blocks were listed by its k_ingest_dda
+    A.has_alloc = ps != tsdf_engine::kPipeU;
+    A.has_carve = ps == tsdf_engine::kPipeCAU;
+    A.fid_carve = e->p_carve;
+  }
+  if (has_frame) {
+    A.has_frame = 1;
+    A.fid_new = fid;
+    A.tiles_x = (Pn.W + 15) / 16;
+    A.tiles = A.tiles_x * ((Pn.H + 15) / 16);
+  }
+  return A;
+}
+void pipe_advance(tsdf_engine* e, uint32_t fid, const FrameParams& Pn) {
+  if (e->ps == tsdf_engine::kPipeNone) {
+    e->ps = tsdf_engine::kPipeAU;
+  } else {
+    e->p_carve = e->p_fid;
+    e->ps = tsdf_engine::kPipeCAU;
+  }
+  e->p_fid = fid;
+  e->p_P = Pn;
+}
+uint32_t next_fid(tsdf_engine* e) {
+  uint32_t fid = e->fid_next++;
+  if (fid == 0u) fid = e->fid_next++;
+  return fid;
+}
+
 // complete the pending frames (pipelined): kPipeU -- the frame's update with its carving in its last
 // workgroup (k_integrate); kPipeCAU -- one k_frame for the pending carving, allocation and update,
 // then one for that frame's own carving
@@ -752,7 +803,7 @@ int flush_pending(tsdf_engine* e) {
   e->ps = tsdf_engine::kPipeNone;
   if (ps == tsdf_engine::kPipeU) return frame_update(e, frame_view(e->D, e->p_fid), e->p_P, nullptr);
   PipeArgs A{};
-  A.has_carve = 1;
+  A.has_carve = ps == tsdf_engine::kPipeCAU;
   A.fid_carve = e->p_carve;
   A.has_alloc = 1;
   A.has_update = 1;
@@ -787,8 +838,7 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
     int rc = flush_pending(e);
     if (rc) return rc;
   }
-  uint32_t fid = e->fid_next++;
-  if (fid == 0u) fid = e->fid_next++;
+  const uint32_t fid = next_fid(e);
   const EngineDev Dv = frame_view(e->D, fid);
   FrameParams P;
   std::array<hipEvent_t, 5>* ev = nullptr;
@@ -800,28 +850,13 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
   if (ingest_alone) {
     if (ev) --e->ev_used;  // (no k_frame / k_integrate launch to time in this call)
     e->ps = tsdf_engine::kPipeU;
-  } else {
-    PipeArgs A{};
-    A.has_update = 1;
-    A.fid_alloc = e->p_fid;
-    A.has_frame = 1;
-    A.fid_new = fid;
-    A.tiles_x = (P.W + 15) / 16;
-    A.tiles = A.tiles_x * ((P.H + 15) / 16);
-    if (e->ps == tsdf_engine::kPipeU) {
-      A.fresh_ready = 1;  // p_fid's new blocks were listed by its k_ingest_dda
-    } else {
-      A.has_carve = 1;
-      A.fid_carve = e->p_carve;
-      A.has_alloc = 1;
-    }
-    rc = launch_frame(e, A, e->p_P, P, ev);
-    if (rc) return rc;
-    e->p_carve = e->p_fid;
-    e->ps = tsdf_engine::kPipeCAU;
+    e->p_fid = fid;
+    e->p_P = P;
+    return TSDF_OK;
   }
-  e->p_fid = fid;
-  e->p_P = P;
+  rc = launch_frame(e, pipe_step(e, true, fid, P), e->p_P, P, ev);
+  if (rc) return rc;
+  pipe_advance(e, fid, P);
   return TSDF_OK;
 }
 
@@ -1019,6 +1054,7 @@ struct tsdf_graph {
   tsdf_engine* e = nullptr;
   int W = 0, H = 0, RW = 0, RH = 0;
   bool shard = false;     // a shard engine's graph (tsdf_graph_create_shard)
+  bool pipe = false;      // pipelined frames: each launch is one k_frame_g (no render camera)
   int slice_index = 0, slice_count = 1;
   int cur = -1;           // a shard's frame in flight: its slot
   hipStream_t cap = nullptr;  // capture stream (the engine stream may be a legacy default stream)
@@ -1069,6 +1105,9 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
   g->H = height;
   g->RW = render_width;
   g->RH = render_height;
+  // frames without a render camera pipeline like tsdf_integrate; a render camera needs each frame
+  // complete before its raycast, so those graphs keep the two-launch frame
+  g->pipe = render_width == 0 && e->pipeline && e->maxs <= 3;
   auto fail = [&](hipError_t err, const char* what) {
     set_error(what, err);
     graph_free(g);
@@ -1093,17 +1132,27 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
     else  // one wave reads the pinned slot over the fabric: a kernel node, no DMA engine in the graph
       hipLaunchKernelGGL(k_copy_words, dim3(1), dim3(64), 0, g->cap, reinterpret_cast<uint32_t*>(g->d_args + k),
                          reinterpret_cast<const uint32_t*>(g->h_args + k), (int)(sizeof(FrameArgs) / 4));
-    if (e->maxs <= 3)
-      hipLaunchKernelGGL(k_ingest_dda_g<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
-    else
-      hipLaunchKernelGGL(k_ingest_dda_g<2048>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
-    hipLaunchKernelGGL((k_integrate_t<true, false>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0, g->cap,
-                       e->D, FrameParams{}, A);
+    if (g->pipe) {  // one k_frame per frame, its grid sized for the largest launch (steady state)
+      const int nwg = kPipeHead + kPipeFreshWG + e->D.integrate_grid_pre + tiles + kVisWorkgroups;
+      hipLaunchKernelGGL(k_frame_g, dim3(nwg), dim3(kIntegrateThreads), 0, g->cap, e->D, A);
+    } else {
+      if (e->maxs <= 3)
+        hipLaunchKernelGGL(k_ingest_dda_g<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
+      else
+        hipLaunchKernelGGL(k_ingest_dda_g<2048>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
+      hipLaunchKernelGGL((k_integrate_t<true, false>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0,
+                         g->cap, e->D, FrameParams{}, A);
+    }
     if (render_width) {
       hipLaunchKernelGGL(k_view_grid_g, dim3(kOccWords / 256), dim3(256), 0, g->cap, e->D, A);
       hipLaunchKernelGGL(k_view_pack_g, dim3(kViewPackGrid), dim3(256), 0, g->cap, A);
-      hipLaunchKernelGGL(k_raycast_g, dim3((render_width + 15) / 16, (render_height + 15) / 16), dim3(256), 0,
-                         g->cap, e->D, A);
+      const dim3 rgrid((render_width + 15) / 16, (render_height + 15) / 16);
+      if (e->ray_segs == 4)
+        hipLaunchKernelGGL(k_raycast_g<4>, rgrid, dim3(1024), 0, g->cap, e->D, A);
+      else if (e->ray_segs == 2)
+        hipLaunchKernelGGL(k_raycast_g<2>, rgrid, dim3(512), 0, g->cap, e->D, A);
+      else
+        hipLaunchKernelGGL(k_raycast_g<1>, rgrid, dim3(256), 0, g->cap, e->D, A);
     }
     if ((err = hipStreamEndCapture(g->cap, &g->graph[k][0])) != hipSuccess) return fail(err, "hipStreamEndCapture");
     if ((err = hipGraphInstantiate(&g->exec[k][0], g->graph[k][0], nullptr, nullptr, 0)) != hipSuccess)
@@ -1287,7 +1336,10 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  ENTER(e);
+  if (g->pipe)
+    JOIN_RENDER(e);  // (the pending frames continue in this launch)
+  else
+    ENTER(e);
   const int k = g->next;
   g->next = (k + 1) % tsdf_graph::kSlots;
   if (g->used[k]) HIP_OK(hipEventSynchronize(g->done[k]));  // slot k's upload has run
@@ -1308,9 +1360,23 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
   a.range = (uint32_t)((size_t)f->width * f->height * e->maxs);
   a.tiles_x = (f->width + 15) / 16;
   a.tiles = a.tiles_x * ((f->height + 15) / 16);
+  uint32_t fid = 0;
+  if (g->pipe) {  // this frame's ingest + the pending frames' carving / allocation / update
+    fid = next_fid(e);
+    a.P.depth = f->depth;
+    a.P.rgb = f->rgb;
+    a.P.ht = f->ht;
+    a.P.lt = f->lt;
+    a.P.pix_off = (fid & 1u) ? (int)e->max_pixels : 0;
+    a.Pu = e->p_P;
+    a.pipe = pipe_step(e, true, fid, a.P);
+    finish_args(e, a.pipe, a.Pu);
+    if (e->profiling && a.pipe.has_update) ++e->prof_pipelined;
+  }
   HIP_OK(hipGraphLaunch(g->exec[k][0], e->stream));
   HIP_OK(hipEventRecord(g->done[k], e->stream));
   g->used[k] = true;
+  if (g->pipe) pipe_advance(e, fid, a.P);
   return TSDF_OK;
 }
 
@@ -1466,8 +1532,13 @@ int raycast_impl(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const t
     HIP_OK(hipEventRecord(e->rs_ready, e->stream));
     HIP_OK(hipStreamWaitEvent(rs, e->rs_ready, 0));
   }
-  hipLaunchKernelGGL(k_raycast, dim3((W + 15) / 16, (nrows + 15) / 16), dim3(256), lds, rs, e->D,
-                     P, step, V, o1, o2);
+  const dim3 rgrid((W + 15) / 16, (nrows + 15) / 16);
+  if (e->ray_segs == 4)
+    hipLaunchKernelGGL(k_raycast<4>, rgrid, dim3(1024), lds, rs, e->D, P, step, V, o1, o2);
+  else if (e->ray_segs == 2)
+    hipLaunchKernelGGL(k_raycast<2>, rgrid, dim3(512), lds, rs, e->D, P, step, V, o1, o2);
+  else
+    hipLaunchKernelGGL(k_raycast<1>, rgrid, dim3(256), lds, rs, e->D, P, step, V, o1, o2);
   LAUNCH_OK("k_raycast");
   if (overlap) {
     HIP_OK(hipEventRecord(e->rs_done, rs));

@@ -571,7 +571,7 @@ __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const Pip
   const uint32_t fb = A.fid_alloc;
   const unsigned long long* carved = Db.pipe + kPipeCarved + (blockIdx.x & 7) * 16;
   if (threadIdx.x == 0) s_ncand = 0;  // (ordered before its first use by the loop's barriers)
-  if (kind == 0 && (int)blockIdx.x == kPipeHead && threadIdx.x == 0)  // the update's device-clock start
+  if (kind == 0 && wi == 0 && threadIdx.x == 0)  // the update's device-clock start
     st_co(Db.pipe + kPipeT0 + 16 * (fb & 1u), (unsigned long long)__builtin_amdgcn_s_memrealtime());
   int bstart[kBands];
   int nvis = 0, nband = 0, p, p_hi, pstep;
@@ -584,8 +584,8 @@ __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const Pip
     nband = nvis;
     if (A.fresh_ready) nvis += Db.ctr->n_fresh;
     // group g = blockIdx % 8 (one XCD) takes the g-th contiguous eighth of the pairs in band order
-    const int g = blockIdx.x & 7, npairs = (nvis + 1) >> 1;
-    p = (int)(((long long)npairs * g) >> 3) + (((int)blockIdx.x - kPipeHead) >> 3);
+    const int g = wi & 7, npairs = (nvis + 1) >> 1;
+    p = (int)(((long long)npairs * g) >> 3) + (wi >> 3);
     p_hi = (int)(((long long)npairs * (g + 1)) >> 3);
     pstep = A.nint >> 3;
   } else {
@@ -718,31 +718,63 @@ __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const Pip
 // grid: kPipeHead head workgroups (0: carving + allocation), A.nint update workgroups (listed blocks),
 // kPipeFreshWG (this launch's new blocks), then frame c's A.tiles pixel tiles and kVisWorkgroups
 // sweep workgroups -- each part only when the launch has it
-__global__ __launch_bounds__(kIntegrateThreads)
-__attribute__((amdgpu_waves_per_eu(TSDF_FRAME_WAVES, TSDF_FRAME_WAVES))) void k_frame(
-    EngineDev D, FrameParams Pu, FrameParams Pn, PipeArgs A) {
-  __shared__ FrameLds U;
+__device__ __forceinline__ void frame_body(const EngineDev& D, const FrameParams& Pu, const FrameParams& Pn,
+                                           const PipeArgs& A, FrameLds& U) {
   int w = (int)blockIdx.x;
   if (w < kPipeHead) {
     if (w == 0) pipe_head(D, Pu, A, U);
     return;
   }
   w -= kPipeHead;
-  const int nold = A.has_update ? A.nint : 0;
   const int nfr = A.has_update && !A.fresh_ready ? kPipeFreshWG : 0;
-  if (w < nold + nfr) {
-    pipe_update(frame_view(D, A.fid_alloc), Pu, A, w < nold ? 0 : 1, w - nold);
+  if (w < nfr) {  // the blocks this launch's allocation creates (they wait for it: dispatched early)
+    pipe_update(frame_view(D, A.fid_alloc), Pu, A, 1, w);
     return;
   }
-  w -= nold + nfr;
+  w -= nfr;
+  // the other parts in the launch's grid order: update (u), tiles (t), sweep (s)
+  const int nold = A.has_update ? A.nint : 0, ns = A.has_frame ? kVisWorkgroups : 0;
+  const int n[3] = {nold, A.tiles, ns};
+  int part = -1, o = w;
+  const int seq[3][3] = {{0, 1, 2}, {1, 2, 0}, {2, 0, 1}};
+  for (int k = 0; k < 3; ++k) {
+    const int q = seq[A.order][k];
+    if (o < n[q]) {
+      part = q;
+      break;
+    }
+    o -= n[q];
+  }
+  if (part < 0) return;  // (a graph's grid is sized for the largest launch)
+  if (part == 0) {
+    // (its XCD split takes o % 8 as the XCD: exact when the parts before it are multiples of 8 long,
+    // as at 640x480; correct either way)
+    pipe_update(frame_view(D, A.fid_alloc), Pu, A, 0, o);
+    return;
+  }
   const unsigned long long* aflag = D.pipe + kPipeAlloc + (blockIdx.x & 7) * 16;
-  if (w < A.tiles)
-    ingest_tile<1024, kTileChained>(D, Pn, Pn.depth, Pn.rgb, Pn.ht, Pn.lt, A.tiles_x, w, U.ing, aflag, A.tag,
+  if (part == 1)
+    ingest_tile<1024, kTileChained>(D, Pn, Pn.depth, Pn.rgb, Pn.ht, Pn.lt, A.tiles_x, o, U.ing, aflag, A.tag,
                                     A.fid_new);
   else
-    vis_sweep_chained<1024>(frame_view(D, A.fid_new), Pn, w - A.tiles, U.ing, aflag, A.tag);
+    vis_sweep_chained<1024>(frame_view(D, A.fid_new), Pn, o, U.ing, aflag, A.tag);
   if (threadIdx.x == 0)  // the ingest's span ends with its last workgroup
     atomicMax(D.pipe + kPipeIngEnd + 16 * (A.fid_new & 1u), (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__global__ __launch_bounds__(kIntegrateThreads)
+__attribute__((amdgpu_waves_per_eu(TSDF_FRAME_WAVES, TSDF_FRAME_WAVES))) void k_frame(
+    EngineDev D, FrameParams Pu, FrameParams Pn, PipeArgs A) {
+  __shared__ FrameLds U;
+  frame_body(D, Pu, Pn, A, U);
+}
+// the graph-captured form: its arguments from the FrameArgs block the graph's first node uploads
+__global__ __launch_bounds__(kIntegrateThreads)
+__attribute__((amdgpu_waves_per_eu(TSDF_FRAME_WAVES, TSDF_FRAME_WAVES))) void k_frame_g(
+    EngineDev D, const FrameArgs* __restrict__ FA) {
+  __shared__ FrameLds U;
+  const PipeArgs A = FA->pipe;
+  const FrameParams Pu = FA->Pu, Pn = FA->P;
+  frame_body(D, Pu, Pn, A, U);
 }
 
 template __global__ void k_integrate_t<false, false>(EngineDev, FrameParams, const FrameArgs*);

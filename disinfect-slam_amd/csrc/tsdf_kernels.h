@@ -34,7 +34,7 @@ struct EngineDev {
   DevCounters* ctr;
   int32_t nblocks;
   int32_t integrate_grid;       // k_integrate workgroups (resident capacity, multiple of 8)
-  int32_t integrate_grid_pre;   // k_integrate_pre's update workgroups (its resident capacity)
+  int32_t integrate_grid_pre;   // k_frame's update workgroups (its resident capacity)
   // per-frame allocation scratch
   unsigned long long* nk_key;   // kNewKeyCap new-key set
   uint32_t* nk_order;           // kNewKeyCap smallest candidate order per key
@@ -95,6 +95,48 @@ __device__ __forceinline__ int view_origin(float wt, float voxel, int half) {
   return (f2i(floorf(wt / voxel)) >> kBlockLenBits) - half;
 }
 
+// ---- pipelined frames (k_frame, tsdf_fuse.hip; DESIGN.md 4 "Pipelined frames") ----
+// A frame f in flight keeps its visible lists at vis + (f & 1) * kBands * nblocks, their counts at
+// band + (f % 3) * kBands * kBandStride (reset by f's carving, two launches after the sweep wrote
+// them), its carve candidates at cand + (f & 1) * cand_cap with the count in pipe[kPipeNCand + 16 (f & 1)].
+// D.pipe layout (u64 words; every hot word on its own 128-B line):
+constexpr int kPipeNCand = 0;                   // + 16 p: carve-candidate count of parity p (int32)
+constexpr int kPipeCarved = 32;                 // + 16 x: the carving-done flag, copy of XCD x (= tag)
+constexpr int kPipeAlloc = kPipeCarved + 128;   // + 16 x: the allocation-done flag (= tag)
+constexpr int kPipeT0 = kPipeAlloc + 128;       // + 16 p: first update workgroup's start (parity p)
+constexpr int kPipeIngEnd = kPipeT0 + 32;       // + 16 p: the latest sweep / tile workgroup end
+constexpr int kPipeAPub = kPipeIngEnd + 32;     // + 16 p: allocation published (the ingest span start)
+constexpr int kPipeStats = 512;                 // + 1024 p + 16 i: payload (blocks << 40 | voxels) and,
+constexpr int kPipeStatLines = 64;              //   at +1, the latest end stamp of update counter i
+constexpr int kPipeWords = kPipeStats + 2 * kPipeStatLines * 16;
+constexpr int kPipeHead = 8;                    // workgroups before the update's (0: carving + allocation)
+constexpr int kPipeFreshWG = 64;                // workgroups that update the blocks allocated in the launch
+constexpr int kPipeDefer = 32;                  // deferred (carve-pending) blocks one update workgroup holds
+// What one k_frame launch does. Frame ids f are engine-wide (1, 2, ...); frame b's update, frame
+// b - 1's carving and frame c = b + 1's ingest share the launch (any part may be absent).
+struct PipeArgs {
+  int has_carve;        // carve frame fid_carve (its candidates, listed by its update last launch)
+  int has_alloc;        // allocate frame fid_alloc (= b: its new keys, inserted by last launch's tiles)
+  int has_update;       // update frame b's blocks (its lists from last launch's sweep)
+  int fresh_ready;      // b's new blocks were listed by an earlier launch (no allocation in this one)
+  int has_frame;        // frame c's ingest: pixel records, DDA, probe / insert, visibility sweep
+  uint32_t fid_carve, fid_alloc, fid_new;
+  uint32_t tag;         // this launch's flag value
+  uint32_t range;       // candidate order space of frame b (W H maxs)
+  int tiles_x, tiles;   // frame c's pixel tiles
+  int nint;             // update workgroups (a multiple of 8)
+  int order;            // grid order of the parts after the head (TSDF_FRAME_ORDER): 0 fresh, update,
+                        //   tiles, sweep; 1 fresh, tiles, sweep, update; 2 fresh, sweep, update, tiles
+};
+// frame f's view of the engine: its visible lists, their counts, its carve candidates and count
+__device__ __host__ __forceinline__ EngineDev frame_view(const EngineDev& D, uint32_t f) {
+  EngineDev V = D;
+  V.vis = D.vis + (size_t)(f & 1u) * kBands * (size_t)D.nblocks;
+  V.band = D.band + (size_t)(f % 3u) * kBands * kBandStride;
+  V.cand = D.cand + (size_t)(f & 1u) * (size_t)D.cand_cap;
+  V.ncand = reinterpret_cast<int32_t*>(D.pipe + kPipeNCand + 16 * (f & 1u));
+  return V;
+}
 // per-frame arguments of the graph-captured frame loop (tsdf_graph_*): the graph's first node
 // copies them from a pinned host slot, every graph kernel reads its camera / frame pointers here
 struct FrameArgs {
@@ -117,6 +159,10 @@ struct FrameArgs {
   ShardRec* cands_out;       // k_integrate_t<true, .>'s tail packs the carve candidates here
   const ShardRec* cands_in;  // k_resolve_delete_g merges the all-gathered candidate slots
   int cand_cap, nshard;
+  // a pipelined graph frame (k_frame_g): P is the new frame's (depth ... lt set in it), Pu the
+  // camera / pixel records of the frame whose allocation and update run, pipe what the launch does
+  FrameParams Pu;
+  PipeArgs pipe;
 };
 
 __global__ void k_init_table(int4* table);
@@ -164,51 +210,13 @@ __global__ void k_resolve_alloc_g(EngineDev D, const FrameArgs* A);
 __global__ void k_resolve_delete_g(EngineDev D, const FrameArgs* A);
 template <bool Graph, bool Raw>
 __global__ void k_integrate_t(EngineDev D, FrameParams P, const FrameArgs* A);
-// ---- pipelined frames (k_frame, tsdf_fuse.hip; DESIGN.md 4 "Pipelined frames") ----
-// A frame f in flight keeps its visible lists at vis + (f & 1) * kBands * nblocks, their counts at
-// band + (f % 3) * kBands * kBandStride (reset by f's carving, two launches after the sweep wrote
-// them), its carve candidates at cand + (f & 1) * cand_cap with the count in pipe[kPipeNCand + 16 (f & 1)].
-// D.pipe layout (u64 words; every hot word on its own 128-B line):
-constexpr int kPipeNCand = 0;                   // + 16 p: carve-candidate count of parity p (int32)
-constexpr int kPipeCarved = 32;                 // + 16 x: the carving-done flag, copy of XCD x (= tag)
-constexpr int kPipeAlloc = kPipeCarved + 128;   // + 16 x: the allocation-done flag (= tag)
-constexpr int kPipeT0 = kPipeAlloc + 128;       // + 16 p: first update workgroup's start (parity p)
-constexpr int kPipeIngEnd = kPipeT0 + 32;       // + 16 p: the latest sweep / tile workgroup end
-constexpr int kPipeAPub = kPipeIngEnd + 32;     // + 16 p: allocation published (the ingest span start)
-constexpr int kPipeStats = 512;                 // + 1024 p + 16 i: payload (blocks << 40 | voxels) and,
-constexpr int kPipeStatLines = 64;              //   at +1, the latest end stamp of update counter i
-constexpr int kPipeWords = kPipeStats + 2 * kPipeStatLines * 16;
-constexpr int kPipeHead = 8;                    // workgroups before the update's (0: carving + allocation)
-constexpr int kPipeFreshWG = 64;                // workgroups that update the blocks allocated in the launch
-constexpr int kPipeDefer = 32;                  // deferred (carve-pending) blocks one update workgroup holds
-// What one k_frame launch does. Frame ids f are engine-wide (1, 2, ...); frame b's update, frame
-// b - 1's carving and frame c = b + 1's ingest share the launch (any part may be absent).
-struct PipeArgs {
-  int has_carve;        // carve frame fid_carve (its candidates, listed by its update last launch)
-  int has_alloc;        // allocate frame fid_alloc (= b: its new keys, inserted by last launch's tiles)
-  int has_update;       // update frame b's blocks (its lists from last launch's sweep)
-  int fresh_ready;      // b's new blocks were listed by an earlier launch (no allocation in this one)
-  int has_frame;        // frame c's ingest: pixel records, DDA, probe / insert, visibility sweep
-  uint32_t fid_carve, fid_alloc, fid_new;
-  uint32_t tag;         // this launch's flag value
-  uint32_t range;       // candidate order space of frame b (W H maxs)
-  int tiles_x, tiles;   // frame c's pixel tiles
-  int nint;             // update workgroups (a multiple of 8)
-};
-// frame f's view of the engine: its visible lists, their counts, its carve candidates and count
-__device__ __host__ __forceinline__ EngineDev frame_view(const EngineDev& D, uint32_t f) {
-  EngineDev V = D;
-  V.vis = D.vis + (size_t)(f & 1u) * kBands * (size_t)D.nblocks;
-  V.band = D.band + (size_t)(f % 3u) * kBands * kBandStride;
-  V.cand = D.cand + (size_t)(f & 1u) * (size_t)D.cand_cap;
-  V.ncand = reinterpret_cast<int32_t*>(D.pipe + kPipeNCand + 16 * (f & 1u));
-  return V;
-}
 __global__ void k_frame(EngineDev D, FrameParams Pu, FrameParams Pn, PipeArgs A);
+__global__ void k_frame_g(EngineDev D, const FrameArgs* FA);
 // the update of one frame b with its carving in the same launch (unpipelined tail form): see k_integrate_t
 // graph-captured forms of the frame kernels: identical bodies, arguments from FrameArgs
 template <int TS>
 __global__ void k_ingest_dda_g(EngineDev D, const FrameArgs* A);
+template <int K>  // K lanes per ray (tsdf_extract.hip), workgroups of 256 K threads
 __global__ void k_raycast_g(EngineDev D, const FrameArgs* A);
 // cands_in: optional inbox of nshard carve-candidate slots (then recs / count are D.cand / n_cand)
 __global__ void k_resolve_delete(EngineDev D, const VisRec* recs, const int32_t* count, int direct,
@@ -233,6 +241,7 @@ template <bool Emit>
 __global__ void k_mesh(EngineDev D, const VisRec* sel, MeshParams M, int32_t* counts,
                        const int32_t* offsets, float* out);
 __global__ void k_scan_counts(const int32_t* counts, int n, int32_t* offsets, int64_t* total);
+template <int K>
 __global__ void k_raycast(EngineDev D, FrameParams P, float step_size, ViewGrid V, uchar4* rgba,
                           uchar4* normal);
 // view grid of a raycast: grid kOccWords / 256 workgroups of 256

@@ -63,3 +63,39 @@ def test_graph_rejects_host_frames_and_wrong_size():
             g.close()
         with pytest.raises(tsdf_amd.TSDFError):
             e.frame_graph(128, 48)
+
+
+def test_pipelined_graph_frames_equal_unpipelined():
+    """Graph frames without a render camera are pipelined like tsdf_integrate (one k_frame_g launch per
+    frame: the pending frames' carving / allocation / update beside this frame's ingest). Mixed with
+    eager frames (every transition of the pending state: a graph frame after a flush, after an eager
+    frame, an eager frame after a graph frame) and reads that flush, the whole state must equal an
+    unpipelined engine's bit for bit."""
+    import os
+
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    from test_gpu_pipeline import _engine, _same
+    W, H, n = 320, 240, 24
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    fr = synth.render_torch(cam, list(range(n)), device="cuda")
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    a = _engine(True, 0.005, 0.03, max_width=W, max_height=H, num_block_bits=16)
+    b = _engine(False, 0.005, 0.03, max_width=W, max_height=H, num_block_bits=16)
+    g = a.frame_graph(W, H)
+    eager = {3, 4, 9, 15, 16, 17}  # frames a integrates eagerly (the others through the graph)
+    try:
+        for i in range(n):
+            pose = tsdf_amd.SE3(fr["q"][i], fr["t"][i])
+            args = (fr["rgb"][i], fr["depth"][i], fr["ht"][i], fr["lt"][i], K, pose, 4.0)
+            (a.integrate if i in eager else g.frame)(*args)
+            b.integrate(*args)
+            if i in (7, 12, n - 1):  # (reads flush the pending frames)
+                torch.cuda.synchronize()
+                _same(a, b, f"frame {i}")
+        assert a.stats()["status"] == 0
+    finally:
+        g.close()
+        a.close(), b.close()
