@@ -81,10 +81,11 @@ def parse():
                    help="sharded modes: carve-candidate records per rank per frame (0 = 16384 / G)")
     p.add_argument("--cpu-frames", type=int, default=-1, help="oracle sample size (-1 = auto)")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--broadcast-frames", action="store_true",
+    p.add_argument("--broadcast-frames", dest="broadcast_frames", action="store_true", default=None,
                    help="sharded modes: rank 0 broadcasts every frame to the other ranks inside the timed "
-                        "loop (one camera feeding the node); otherwise each rank holds the stream and the "
-                        "broadcast is timed beside the line")
+                        "loop (one camera feeding the node) -- the default with the nccl backend")
+    p.add_argument("--no-broadcast-frames", dest="broadcast_frames", action="store_false",
+                   help="sharded modes: every rank holds the stream; the broadcast is timed beside the line")
     p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                    help="process-group backend for N > 1: nccl (RCCL over xGMI, one GPU per rank) or gloo "
                         "(a rehearsal of the multi-rank code path; ranks may share a GPU, exchanges staged "
@@ -168,9 +169,14 @@ class Run:
                 for t in (fr["rgb"][i], fr["depth"][i], ht, lt):
                     if t is not None:
                         self.dist.broadcast(t, src=0)
-            tdist.integrate_sharded(self.eng, self.bufs, fr["rgb"][i], fr["depth"][i], ht, lt, K, pose,
-                                    a.max_depth, split=self.mode == "routed", graph=self.sgraph)
+            if self.mode == "sharded" and self.sgraph is None:  # pipelined: one exchange per frame
+                tdist.integrate_sharded_pipe(self.eng, self.bufs, fr["rgb"][i], fr["depth"][i], ht, lt, K, pose,
+                                             a.max_depth)
+            else:
+                tdist.integrate_sharded(self.eng, self.bufs, fr["rgb"][i], fr["depth"][i], ht, lt, K, pose,
+                                        a.max_depth, split=self.mode == "routed", graph=self.sgraph)
             if c5:
+                self.flush()  # (the render reads the volume as of this frame)
                 tdist.render_sharded(self.eng, self.replica, K, a.width, a.height, pose, a.max_depth,
                                      rgba=self.rgba, normal=self.normal)
         else:
@@ -184,6 +190,15 @@ class Run:
                 n = self.eng.extract_mesh(None, 0.99, 0, out=self.mesh_buf).shape[0]
             self.mesh_tris.append(int(n))
 
+    def flush(self):
+        """Complete the pending frames (pipelined single volume: tsdf_flush; pipelined sharded frames:
+        the exchange protocol's steps)."""
+        from tsdf_amd import dist as tdist
+        if self.sharded and self.mode == "sharded" and self.sgraph is None:
+            tdist.flush_sharded_pipe(self.eng, self.bufs)
+        else:
+            self.eng.flush()
+
     def timed(self):
         """warmup, then exactly `steps` timed frames between barrier + synchronize; returns the
         max-over-ranks elapsed seconds and this rank's profile of the timed window."""
@@ -192,7 +207,7 @@ class Run:
         a = self.a
         for i in range(a.warmup):
             self.step(i)
-        self.eng.flush()
+        self.flush()
         torch.cuda.synchronize()
         if self.dist:
             self.dist.barrier()
@@ -206,8 +221,8 @@ class Run:
         t0 = time.perf_counter()
         for i in range(a.warmup, a.warmup + a.steps):
             self.step(i)
-        # pipelined frames: the last frame's update is enqueued here, inside the timed region
-        self.eng.flush()
+        # pipelined frames: the last frames' updates / carvings are enqueued here, inside the timed region
+        self.flush()
         t_enq = time.perf_counter()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
@@ -378,6 +393,8 @@ def main():
     nframes = a.warmup + a.steps
     if a.shard:
         return rehearsal(a, cam, K, dev)
+    if a.broadcast_frames is None:  # one camera feeds the node: its broadcast is part of the frame
+        a.broadcast_frames = a.backend == "nccl" and world > 1 and a.mode in ("routed", "sharded")
     if a.broadcast_frames and a.backend == "gloo":
         raise SystemExit("--broadcast-frames broadcasts device frames (RCCL); gloo is host-only")
     mode = a.mode if world > 1 else "single"
@@ -579,11 +596,12 @@ def rehearsal(a, cam, K, dev):
     nframes = a.warmup + a.steps
     fr = synth.render_torch(cam, list(range(nframes)), device=dev)
     poses = [tsdf_amd.SE3(fr["q"][i], fr["t"][i]) for i in range(nframes)]
+    pipe = a.mode == "sharded" and not a.graph  # pipelined sharded frames: one exchange per frame
     grp = tsdf_amd.ShardGroup(G, a.voxel, a.trunc, max_width=a.width, max_height=a.height,
                               num_block_bits=a.block_bits, device=torch.cuda.current_device(),
                               key_cap=a.key_cap or max(1024, 32768 // G),
                               cand_cap=a.cand_cap or max(1024, 16384 // G), split=a.mode != "sharded",
-                              graph=(a.width, a.height) if a.graph else None)
+                              graph=(a.width, a.height) if a.graph else None, pipe=pipe)
 
     def step(i):
         ht = None if a.depth_only else fr["ht"][i]
@@ -592,12 +610,14 @@ def rehearsal(a, cam, K, dev):
 
     for i in range(a.warmup):
         step(i)
+    grp.flush()
     torch.cuda.synchronize()
     for e in grp.engines:
         e.profile_begin(integrate_only=True, every=1 << 30)
     t0 = time.perf_counter()
     for i in range(a.warmup, nframes):
         step(i)
+    grp.flush()  # (pipelined: the last frames complete inside the timed region)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     profs = [e.profile_end() for e in grp.engines]
@@ -623,7 +643,7 @@ def rehearsal(a, cam, K, dev):
         "dtype": "f32",
         "data": "synthetic (analytic room scene rendered on GPU, resident in HBM)",
         "config": {"workload": workload_name(a), "width": a.width, "height": a.height,
-                   "parallelism": f"{G} {'routed' if a.mode != 'sharded' else 'sharded'} shards on one GPU"},
+                   "parallelism": f"{G} {'routed' if a.mode != 'sharded' else 'sharded (pipelined, one exchange per frame)'} shards on one GPU"},
         "shards": G,
         "group_ms_per_frame": round(el / n * 1e3, 4),
         "per_shard_device_us": spans,

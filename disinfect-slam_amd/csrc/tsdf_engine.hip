@@ -167,8 +167,9 @@ struct tsdf_engine {
   // allocation and update are pending (p_fid's tiles probed and inserted its keys, its sweep listed
   // its blocks). Every other entry point first completes them (flush_pending).
   bool pipeline = true;
-  static constexpr int kPipeNone = 0, kPipeU = 1, kPipeCAU = 2, kPipeAU = 3;  // kPipeAU: p_fid's
-  // allocation and update are pending with no carving (after a graph frame that started a stream)
+  static constexpr int kPipeNone = 0, kPipeU = 1, kPipeCAU = 2, kPipeAU = 3, kPipeC = 4;  // kPipeAU:
+  // p_fid's allocation and update are pending with no carving (after a graph frame that started a
+  // stream); kPipeC: only p_fid's carving is pending (a shard's pipelined frames, between flush steps)
   int ps = kPipeNone;
   uint32_t fid_next = 1;  // engine-wide frame ids (views, tags; never 0)
   uint32_t p_carve = 0, p_fid = 0;
@@ -407,7 +408,7 @@ bool init_state(tsdf_engine* e, bool with_pool = true) {
   ok &= hipMemsetAsync(D.pipe, 0, sizeof(unsigned long long) * kPipeWords, s) == hipSuccess;
   ok &= hipMemsetAsync(D.ctag, 0, sizeof(uint32_t) * 2 * (size_t)nb, s) == hipSuccess;
   ok &= hipMemsetAsync(D.rtag, 0, sizeof(uint32_t) * (size_t)nb, s) == hipSuccess;
-  ok &= hipMemsetAsync(D.fo, 0xFF, sizeof(unsigned long long) * (size_t)nb, s) == hipSuccess;
+  ok &= hipMemsetAsync(D.fo, 0xFF, sizeof(unsigned long long) * (size_t)kNumEntry, s) == hipSuccess;
   ok &= hipMemsetAsync(D.visbits, 0, sizeof(unsigned long long) * kOccWords, s) == hipSuccess;
   ok &= hipMemsetAsync(D.arrive, 0, sizeof(unsigned long long) * kArriveWords, s) == hipSuccess;
   ok &= hipMemsetAsync(D.swdirty, 0, sizeof(unsigned long long) * (kOccWords / 64), s) == hipSuccess;
@@ -493,7 +494,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.pipe, kPipeWords);
   ALLOC(D.ctag, (size_t)2 * nb);
   ALLOC(D.rtag, nb);
-  ALLOC(D.fo, nb);
+  ALLOC(D.fo, kNumEntry);
   // carve candidates of one frame: a shard's list takes every shard's (their visible blocks and the
   // entries exhausted pools left without voxels), so it is sized like the resolver's D.pairs scratch;
   // more are clamped with TSDF_STATUS_SHARD_OVERFLOW. TSDF_CAND_CAP (tests) sets a smaller list.
@@ -798,6 +799,11 @@ uint32_t next_fid(tsdf_engine* e) {
 // then one for that frame's own carving
 int flush_pending(tsdf_engine* e) {
   if (e->ps == tsdf_engine::kPipeNone) return TSDF_OK;
+  if (sharded(e)) {  // its carvings need every shard's candidates: only the exchange protocol can
+    set_error("a pipelined sharded frame is pending: complete it with tsdf_integrate_shard_pipe(frame = "
+              "NULL) until *pending == 0");
+    return TSDF_ERR_INVALID_ARG;
+  }
   HIP_OK(hipSetDevice(e->device));
   const int ps = e->ps;
   e->ps = tsdf_engine::kPipeNone;
@@ -943,6 +949,89 @@ int tsdf_integrate_shard_end(tsdf_engine* e, const void* cands_in, int32_t cand_
   e->shard_phase = 0;
   std::array<hipEvent_t, 5>* ev = e->shard_ev;
   if (ev && e->prof_mode == TSDF_PROFILE_PHASES) HIP_OK(hipEventRecord((*ev)[4], e->stream));
+  return TSDF_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pipelined sharded frames (one exchange per frame): every shard runs the whole frame's
+// DDA against its copy of the index (no key exchange: --mode sharded), so only the carve candidates
+// cross the shards. Call n launches one k_frame: frame n - 2's carving of every shard's candidates
+// (cands_in: the all-gathered slots of call n - 1), frame n - 1's allocation and update (its
+// candidates into cands_out, for the exchange after this call), frame n's ingest.
+// ---------------------------------------------------------------------------------------------
+int tsdf_integrate_shard_pipe(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
+                              const tsdf_pose* pose, float max_depth, const void* cands_in, void* cands_out,
+                              int32_t cand_cap, int32_t* pending) {
+  TraceRange trace_("tsdf_integrate_shard_pipe");
+  if (!e || !sharded(e) || e->shard_phase != 0 || !cands_in || !cands_out || cand_cap < 1 || !pending ||
+      (f && (!K || !pose)) || e->maxs > 3) {
+    set_error("tsdf_integrate_shard_pipe: invalid argument (a shard engine between frames, both slots, "
+              "<= 3 DDA samples per pixel)");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  JOIN_RENDER(e);
+  *pending = 0;
+  const ShardRec* in = reinterpret_cast<const ShardRec*>(cands_in);
+  ShardRec* out = reinterpret_cast<ShardRec*>(cands_out);
+  auto shard_args = [&](PipeArgs& A) {
+    A.cands_in = A.has_carve ? in : nullptr;
+    A.cands_out = A.has_update ? out : nullptr;
+    A.cand_cap = cand_cap;
+    A.nshard = e->cfg.shard_count;
+  };
+  const FrameParams none{};
+  if (!f) {  // one step of completing the pending frames
+    const int ps = e->ps;
+    if (ps == tsdf_engine::kPipeNone) return TSDF_OK;
+    PipeArgs A{};
+    if (ps == tsdf_engine::kPipeC) {
+      A.has_carve = 1;
+      A.fid_carve = e->p_fid;
+      shard_args(A);
+      int rc = launch_frame(e, A, none, none, nullptr);
+      if (rc) return rc;
+      e->ps = tsdf_engine::kPipeNone;
+      return TSDF_OK;
+    }
+    A = pipe_step(e, false, 0u, none);
+    shard_args(A);
+    int rc = launch_frame(e, A, e->p_P, none, nullptr);
+    if (rc) return rc;
+    e->ps = tsdf_engine::kPipeC;  // (p_fid's carving, after the exchange of its candidates)
+    *pending = 1;
+    return TSDF_OK;
+  }
+  if (e->ps == tsdf_engine::kPipeC) {
+    set_error("tsdf_integrate_shard_pipe: a flush is in progress (call with frame = NULL until *pending == 0)");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  const uint32_t fid = next_fid(e);
+  FrameParams P;
+  std::array<hipEvent_t, 5>* ev = nullptr;
+  int rc = frame_ingest(e, frame_view(e->D, fid), f, K, pose, max_depth, 0, 1, &P, &ev, nullptr, 0, false,
+                        (int)(fid & 1u));
+  if (rc) return rc;
+  P.pack_pixels = 1;  // every shard packs the whole frame's pixel records (its blocks project anywhere)
+  if (e->ps == tsdf_engine::kPipeNone) {  // the first frame: ingest + allocation in one launch
+    const EngineDev Dv = frame_view(e->D, fid);
+    const int tiles = P.tile_hi - P.tile_lo, tiles_x = (P.W + 15) / 16;
+    HIP_OK(hipMemsetAsync(&e->D.ctr->n_pend, 0, sizeof(int32_t), e->stream));  // (its allocation's list)
+    hipLaunchKernelGGL(k_ingest_dda<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, e->stream, Dv, P, P.depth,
+                       P.rgb, P.ht, P.lt, tiles_x, tiles);
+    LAUNCH_OK("k_ingest_dda");
+    HIP_OK(hipMemsetAsync(out, 0, sizeof(ShardRec), e->stream));  // (no candidates from this call)
+    if (ev) --e->ev_used;
+    e->ps = tsdf_engine::kPipeU;
+    e->p_fid = fid;
+    e->p_P = P;
+    return TSDF_OK;
+  }
+  PipeArgs A = pipe_step(e, true, fid, P);
+  shard_args(A);
+  rc = launch_frame(e, A, e->p_P, P, ev);
+  if (rc) return rc;
+  pipe_advance(e, fid, P);
   return TSDF_OK;
 }
 

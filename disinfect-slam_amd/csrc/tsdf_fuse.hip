@@ -47,7 +47,7 @@ __device__ void frame_end(const EngineDev& D) {
 // this launch)
 __device__ void pack_cands_wg(const EngineDev& D, ShardRec* __restrict__ out, int cap) {
   const int nc = ld_co(D.ncand);
-  const int np = min(D.ctr->n_pend, (int)kNewKeyCap);
+  const int np = min(ld_co(&D.ctr->n_pend), (int)kNewKeyCap);
   const int n = nc + np;
   const unsigned long long* rq = reinterpret_cast<const unsigned long long*>(D.cand);
   for (int i = threadIdx.x; i < min(n, cap); i += blockDim.x) {
@@ -57,8 +57,8 @@ __device__ void pack_cands_wg(const EngineDev& D, ShardRec* __restrict__ out, in
       b = ld_co(&rq[2 * i + 1]);
     } else {
       const unsigned long long* pq = reinterpret_cast<const unsigned long long*>(D.pend + (i - nc));
-      a = pq[0];
-      b = pq[1];
+      a = ld_co(&pq[0]);
+      b = ld_co(&pq[1]);
     }
     ShardRec r;
     r.x = (int16_t)(a & 0xFFFF);
@@ -524,17 +524,26 @@ union FrameLds {
   IngestLds<1024> ing;
 };
 
-// workgroup 0: frame fid_carve's carving, then frame fid_alloc's allocation, each published
+__device__ void merge_cands_inbox(const EngineDev& D, const ShardRec* __restrict__ cands_in, int cap, int nshard,
+                                  int* s_base);
+
+// workgroup 0: frame fid_carve's carving, then frame fid_alloc's allocation, each published. A shard's
+// pipelined frame first lists every shard's candidates of fid_carve (the all-gathered inbox).
 __device__ void pipe_head(const EngineDev& D, const FrameParams& Pu, const PipeArgs& A, FrameLds& U) {
+  __shared__ int s_base[kMaxShards + 1];
   const int t = threadIdx.x;
   if (A.has_carve) {
     const EngineDev Dk = frame_view(D, A.fid_carve);
+    if (A.cands_in) merge_cands_inbox(Dk, A.cands_in, A.cand_cap, A.nshard, s_base);
     resolve_delete_wg(Dk, Dk.cand, Dk.ncand, 0, U.del, A.fid_carve, A.has_alloc ? A.fid_alloc : 0u);
     lds_barrier();
     // the carved frame's candidate count and band counts start empty for frame fid_carve + 2 / + 3
     if (t < kBands) st_co(&Dk.band[t * kBandStride], 0);
     if (t == 0) st_co(Dk.ncand, 0);
   }
+  // (a shard: the owned entries this launch's allocation leaves without voxels are listed from here;
+  // without an allocation the list is the last one's, packed by this launch's update)
+  if (t == 0 && A.cands_out && A.has_alloc) st_co(&D.ctr->n_pend, 0);
   drain_barrier();
   publish_flags(D.pipe + kPipeCarved, A.tag);
   if (A.has_alloc) {
@@ -545,8 +554,8 @@ __device__ void pipe_head(const EngineDev& D, const FrameParams& Pu, const PipeA
       *ie = 0ull;
     }
     resolve_alloc_wg(D, Pu, A.range, 1, U.ing.u.res);
-    drain_barrier();
   }
+  drain_barrier();
   const unsigned long long t_pub = __builtin_amdgcn_s_memrealtime();
   publish_flags(D.pipe + kPipeAlloc, A.tag);
   if (t == 0) D.pipe[kPipeAPub + 16 * (A.fid_new & 1u)] = t_pub;
@@ -710,6 +719,15 @@ __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const Pip
     if (vis | upd) atomicAdd(st, (vis << 40) | upd);
     atomicMax(st + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
+  if (A.cands_out) {  // a shard's pipelined frame: the last update workgroup fills the exchange slot
+    __shared__ int s_last;
+    const int nold = A.nint, nfr = A.fresh_ready ? 0 : kPipeFreshWG;
+    const uint32_t idx = (uint32_t)(kind ? nold + wi : wi);  // (this workgroup among the update's)
+    if (arrive_last(Db.arrive + kArrIntegrate, 0ull, &s_last, true, (uint32_t)(nold + nfr), idx)) {
+      if (threadIdx.x == 0) arrive_reset(Db.arrive + kArrIntegrate);
+      pack_cands_wg(Db, A.cands_out, A.cand_cap);
+    }
+  }
 }
 
 #ifndef TSDF_FRAME_WAVES
@@ -788,53 +806,57 @@ template __global__ void k_integrate_t<true, true>(EngineDev, FrameParams, const
 // the candidate set of one volume -- so every shard's index takes the same deletes), and the
 // hash-level test path (direct: the keys in list order, one per round).
 // ---------------------------------------------------------------------------------------------
+// every shard's candidate slot (nshard slots of cap records) listed as D.cand / *D.ncand: the candidate
+// set of one volume, so that every shard's index takes the same deletes
+__device__ void merge_cands_inbox(const EngineDev& D, const ShardRec* __restrict__ cands_in, int cap, int nshard,
+                                  int* s_base) {
+  if (threadIdx.x == 0) {
+    // the union is listed in D.cand (cand_cap records; the resolver's D.pairs scratch holds at
+    // least as many): more candidates than that is a shard overflow, the rest are dropped
+    int run = 0;
+    bool ovf = false;
+    for (int s = 0; s < nshard; ++s) {
+      s_base[s] = run;
+      int n = min((int)cands_in[(size_t)s * (cap + 1)].val, cap);
+      if (n > D.cand_cap - run) {
+        n = D.cand_cap - run;
+        ovf = true;
+      }
+      run += n;
+    }
+    s_base[nshard] = run;
+    st_co(D.ncand, run);
+    if (ovf) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_SHARD_OVERFLOW
+  }
+  __syncthreads();
+  unsigned long long* cq = reinterpret_cast<unsigned long long*>(D.cand);
+  for (int s = 0; s < nshard; ++s) {
+    const ShardRec* slot = cands_in + (size_t)s * (cap + 1) + 1;
+    const int n = s_base[s + 1] - s_base[s];
+    for (int i = threadIdx.x; i < n; i += kRT) {
+      const ShardRec r = slot[i];
+      VisRec c;
+      c.x = r.x;
+      c.y = r.y;
+      c.z = r.z;
+      c.pad = 0;
+      c.idx = -1;
+      c.entry = (int32_t)r.val;
+      const unsigned long long* cv = reinterpret_cast<const unsigned long long*>(&c);
+      st_co(&cq[2 * (s_base[s] + i)], cv[0]);
+      st_co(&cq[2 * (s_base[s] + i) + 1], cv[1]);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+}
 __device__ __forceinline__ void resolve_delete_merged(EngineDev D, const VisRec* __restrict__ recs,
                                                       const int32_t* __restrict__ count, int direct,
                                                       const ShardRec* __restrict__ cands_in, int cap,
                                                       int nshard) {
   __shared__ DeleteLds L;
   __shared__ int s_base[kMaxShards + 1];
-  if (cands_in) {
-    if (threadIdx.x == 0) {
-      // the union is listed in D.cand (cand_cap records; the resolver's D.pairs scratch holds at
-      // least as many): more candidates than that is a shard overflow, the rest are dropped
-      int run = 0;
-      bool ovf = false;
-      for (int s = 0; s < nshard; ++s) {
-        s_base[s] = run;
-        int n = min((int)cands_in[(size_t)s * (cap + 1)].val, cap);
-        if (n > D.cand_cap - run) {
-          n = D.cand_cap - run;
-          ovf = true;
-        }
-        run += n;
-      }
-      s_base[nshard] = run;
-      st_co(D.ncand, run);
-      if (ovf) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_SHARD_OVERFLOW
-    }
-    __syncthreads();
-    unsigned long long* cq = reinterpret_cast<unsigned long long*>(D.cand);
-    for (int s = 0; s < nshard; ++s) {
-      const ShardRec* slot = cands_in + (size_t)s * (cap + 1) + 1;
-      const int n = s_base[s + 1] - s_base[s];
-      for (int i = threadIdx.x; i < n; i += kRT) {
-        const ShardRec r = slot[i];
-        VisRec c;
-        c.x = r.x;
-        c.y = r.y;
-        c.z = r.z;
-        c.pad = 0;
-        c.idx = -1;
-        c.entry = (int32_t)r.val;
-        const unsigned long long* cv = reinterpret_cast<const unsigned long long*>(&c);
-        st_co(&cq[2 * (s_base[s] + i)], cv[0]);
-        st_co(&cq[2 * (s_base[s] + i) + 1], cv[1]);
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-  }
+  if (cands_in) merge_cands_inbox(D, cands_in, cap, nshard, s_base);
   resolve_delete_wg(D, recs, count, direct, L);
   if (!direct) frame_end(D);
 }

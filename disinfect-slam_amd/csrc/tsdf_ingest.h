@@ -432,9 +432,9 @@ __device__ void vis_sweep_chained(const EngineDev& D, const FrameParams& P, int 
 // while frame c - 1's blocks are updated; the probe and insert wait until frame c - 1's allocation has
 // been published (*flag == tag) and read the table coherently (the allocation ran on another XCD). Frame
 // c - 2's carving has not run yet (it runs in the next launch), so a key found now may be missing after
-// it: a found key records its smallest candidate order in D.fo of its pool block, tagged ~fid, and the
-// carving re-inserts the keys of the blocks it releases (tsdf_resolve.h released_block). Missing keys
-// stay missing (a carving only deletes), so they go to the new-key set now.
+// it: a found key records its smallest candidate order in D.fo at its hash entry, tagged ~fid, and the
+// carving re-inserts the keys it deletes (tsdf_resolve.h carved_key). Missing keys stay missing (a
+// carving only deletes), so they go to the new-key set now.
 constexpr int kTileFull = 0, kTileChained = 1;
 #ifdef TSDF_CHAIN_PLAIN
 constexpr bool kChainCoherentLoads = false;
@@ -600,10 +600,9 @@ __device__ __forceinline__ void ingest_tile(const EngineDev& D, const FrameParam
     const unsigned long long key = s_key[slot];
     int16_t kx, ky, kz;
     unpack_key(key, kx, ky, kz);
-    int32_t idx = -1;
-    if (find_entry_t<Mode == kTileChained && kChainCoherentLoads>(D.table, kx, ky, kz, &idx) >= 0) {
-      if (Mode == kTileChained && local_idx(idx))
-        atomicMin(&D.fo[idx], ((unsigned long long)~fid << 32) | s_ord[slot]);
+    const int32_t e = find_entry_t<Mode == kTileChained && kChainCoherentLoads>(D.table, kx, ky, kz);
+    if (e >= 0) {
+      if (Mode == kTileChained) atomicMin(&D.fo[e], ((unsigned long long)~fid << 32) | s_ord[slot]);
       continue;
     }
     nk_insert(D, key, s_ord[slot]);

@@ -60,8 +60,8 @@ struct EngineDev {
   uint32_t* ctag;               // 2 x nblocks: ctag[(f & 1) * nblocks + b] == f: block b was a carve
                                 //   candidate of frame f
   uint32_t* rtag;               // nblocks: rtag[b] == f: frame f's carving released block b
-  unsigned long long* fo;       // nblocks: (~f << 32) | order: frame f's DDA found block b's key in
-                                //   the table, with this smallest candidate order
+  unsigned long long* fo;       // kNumEntry: (~f << 32) | order: frame f's DDA found the key of entry
+                                //   e in the table, with this smallest candidate order
   // query scratch
   unsigned long long* visbits;  // kOccWords
   int32_t* wgcnt;               // kOccWords / 256
@@ -127,6 +127,12 @@ struct PipeArgs {
   int nint;             // update workgroups (a multiple of 8)
   int order;            // grid order of the parts after the head (TSDF_FRAME_ORDER): 0 fresh, update,
                         //   tiles, sweep; 1 fresh, tiles, sweep, update; 2 fresh, sweep, update, tiles
+  // a shard's pipelined frame (tsdf_integrate_shard_pipe): every shard's carve candidates of frame
+  // fid_carve, all-gathered (nshard slots of cand_cap records; merged before the carving), and this
+  // shard's slot that the update's last workgroup fills with frame fid_alloc's candidates
+  const struct ShardRec* cands_in;
+  struct ShardRec* cands_out;
+  int cand_cap, nshard;
 };
 // frame f's view of the engine: its visible lists, their counts, its carve candidates and count
 __device__ __host__ __forceinline__ EngineDev frame_view(const EngineDev& D, uint32_t f) {

@@ -144,14 +144,16 @@ __device__ __forceinline__ void nk_insert(const EngineDev& D, uint64_t key, uint
 constexpr int kArrLine = 16;  // u64 per 128-B line
 // drain: this wave published data (wave-uniform); other waves' outstanding stores stay in flight
 // nwg: the arriving workgroups, blocks [0, nwg) of the launch (0: the whole grid)
+// idx: the arriving workgroup's index among the nwg (default blockIdx.x)
 __device__ __forceinline__ bool arrive_last(unsigned long long* words, unsigned long long payload,
-                                            int* s_flag, bool drain = true, uint32_t nwg = 0u) {
+                                            int* s_flag, bool drain = true, uint32_t nwg = 0u,
+                                            uint32_t idx = 0xFFFFFFFFu) {
   if (drain) __builtin_amdgcn_s_waitcnt(0);
   lds_barrier();
   if (threadIdx.x == 0) {
     constexpr uint32_t NG = (uint32_t)kArrGroups;
     const uint32_t nw = nwg ? nwg : gridDim.x;
-    const uint32_t g = blockIdx.x % NG, ngrp = nw < NG ? nw : NG;
+    const uint32_t g = (idx == 0xFFFFFFFFu ? blockIdx.x : idx) % NG, ngrp = nw < NG ? nw : NG;
     const uint32_t expect = (nw - g + NG - 1u) / NG;
     const unsigned long long old = __hip_atomic_fetch_add(&words[g * kArrLine], (1ull << 40) | payload,
                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -546,7 +548,7 @@ __device__ void resolve_alloc_wave(const EngineDev& D, const FrameParams& P, int
             pr.pad = 0;
             pr.idx = kForeignIdx;
             pr.entry = (int32_t)e;
-            D.pend[pk] = pr;
+            st_rec_co(&D.pend[pk], pr);
           }
         }
         if (local_idx(idx)) {
@@ -948,7 +950,7 @@ __device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint3
                 pr.pad = 0;
                 pr.idx = kForeignIdx;
                 pr.entry = (int32_t)e;
-                D.pend[pk] = pr;
+                st_rec_co(&D.pend[pk], pr);
               }
             }
             L.changed = 1;  // (a benign race: every writer stores 1)
@@ -1034,17 +1036,16 @@ constexpr uint32_t kHintSlot0 = 1u << 9;  // (with kHintValid) slot 0 holds the 
 // nothing another delete writes, so the entry-ordered linearisation commits them all; only
 // ReleaseBlock's pushes are ordered (by hash entry). Any other launch returns false before anything
 // global is written and the ordered rounds below handle it.
-// rel_fid != 0 (pipelined frames): ReleaseBlock also tags the block rtag = rel_fid, and when fo_fid
-// != 0 a released block whose key frame fo_fid's DDA found in the table (D.fo, tsdf_ingest.h) goes back
-// into the new-key set with that frame's smallest candidate order: its key is missing again.
-__device__ __forceinline__ void released_block(const EngineDev& D, int32_t idx, int16_t x, int16_t y, int16_t z,
-                                               uint32_t rel_fid, uint32_t fo_fid) {
-  if (!rel_fid) return;
-  st_co(&D.rtag[idx], rel_fid);
-  if (fo_fid) {
-    const unsigned long long w = D.fo[idx];
-    if ((uint32_t)(w >> 32) == ~fo_fid) nk_insert(D, pack_key(x, y, z), (uint32_t)w);
-  }
+// Pipelined frames. rel_fid != 0: ReleaseBlock also tags the released pool block rtag = rel_fid (the
+// update workgroups that deferred it drop it). fo_fid != 0: a deleted key that frame fo_fid's DDA
+// found in the table -- at entry e, where the key sat when it was deleted (one structural change per
+// bucket per launch: its entry cannot have moved in between) -- goes back into the new-key set with
+// that frame's smallest candidate order (D.fo, tsdf_ingest.h): its key is missing again.
+__device__ __forceinline__ void carved_key(const EngineDev& D, uint32_t e, int16_t x, int16_t y, int16_t z,
+                                           uint32_t fo_fid) {
+  if (!fo_fid) return;
+  const unsigned long long w = D.fo[e];
+  if ((uint32_t)(w >> 32) == ~fo_fid) nk_insert(D, pack_key(x, y, z), (uint32_t)w);
 }
 __device__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32_t epoch, int direct,
                                     const unsigned long long (&a)[2], DeleteLds& L, unsigned long long tick0,
@@ -1100,8 +1101,9 @@ __device__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32
         rank += (v.x < entry[r]) + (v.y < entry[r]) + (v.z < entry[r]) + (v.w < entry[r]);
       }
       D.heap[free0 + rank] = idx[r];
-      released_block(D, idx[r], x[r], y[r], z[r], rel_fid, fo_fid);
+      if (rel_fid) st_co(&D.rtag[idx[r]], rel_fid);
     }
+    carved_key(D, cur, x[r], y[r], z[r], fo_fid);
   }
   if (t == 0) {
     D.ctr->lock_epoch = epoch;
@@ -1315,8 +1317,9 @@ __device__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__
       const int rank = wg_excl_scan(rel ? 1 : 0, L.scan, &nrel);
       if (rel) {
         D.heap[L.sfree + rank] = released;
-        released_block(D, released, x, y, z, rel_fid, fo_fid);
+        if (rel_fid) st_co(&D.rtag[released], rel_fid);
       }
+      if (ok) carved_key(D, kind == 2 ? prev : cur, x, y, z, fo_fid);  // (a list head's key lived at prev)
       if (base + kRT < m || done + m < n) __syncthreads(); else lds_barrier();
       if (t == 0) {
         L.sfree += nrel;

@@ -480,6 +480,34 @@ class Engine:
                    "tsdf_integrate_shard_end")
         self._signal_torch(cands_in)
 
+    def integrate_shard_pipe(self, rgb, depth, ht, lt, K, cam_T_world, max_depth: float, cands_in, cands_out,
+                             cand_cap: int) -> bool:
+        """Pipelined sharded frame, one exchange per frame (tsdf_integrate_shard_pipe): this frame's
+        ingest (the whole frame's DDA on every shard), the previous frame's allocation and update (this
+        shard's carve candidates into cands_out, one slot), the frame before's carving of every shard's
+        candidates (cands_in: the all-gathered slots of the previous call). depth None: one step of
+        completing the pending frames. Returns True while more such steps (each after an exchange)
+        are needed."""
+        self._check_slot(cands_out, cand_cap, 1, "cands_out")
+        self._check_slot(cands_in, cand_cap, self.shard_count, "cands_in")
+        pend = C.c_int32(0)
+        if depth is None:
+            self._wait_torch(cands_in, cands_out)
+            _lib.check(_lib.load().tsdf_integrate_shard_pipe(self._h, None, None, None, max_depth, _ptr(cands_in),
+                                                             _ptr(cands_out), cand_cap, C.byref(pend)),
+                       "tsdf_integrate_shard_pipe")
+            self._signal_torch(cands_in, cands_out)
+            return bool(pend.value)
+        fr, keep = self._frame(rgb, depth, ht, lt)
+        Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        self._wait_torch(depth, cands_in, cands_out)
+        _lib.check(_lib.load().tsdf_integrate_shard_pipe(self._h, C.byref(fr), C.byref(Kc), C.byref(cam_T_world._c()),
+                                                         max_depth, _ptr(cands_in), _ptr(cands_out), cand_cap,
+                                                         C.byref(pend)), "tsdf_integrate_shard_pipe")
+        self._signal_torch(depth, cands_in, cands_out)  # (the frame is read by this call only)
+        del keep
+        return bool(pend.value)
+
     def integrate_shard_abort(self):
         """Abort a pending sharded frame (tsdf_integrate_shard_abort): the engine is between frames
         again; STATUS_SHARD_ABORTED is set because shards may have diverged (restore snapshots)."""
@@ -800,9 +828,14 @@ class ShardGroup:
 
     def __init__(self, shard_count: int, voxel_size=0.005, truncation=0.03, max_width=1920,
                  max_height=1080, num_block_bits=18, device=0, key_cap=16384, cand_cap=16384,
-                 split=True, stream=None, graph=None):
+                 split=True, stream=None, graph=None, pipe=False):
         import torch
         self.G = shard_count
+        # pipe: pipelined sharded frames (tsdf_integrate_shard_pipe, one exchange per frame, every shard
+        # runs the whole DDA); reads of the volume need flush() first
+        self.pipe = pipe
+        if pipe and (split or graph is not None):
+            raise ValueError("pipelined sharded frames run the whole DDA on every shard (split=False, no graph)")
         self.graph_size = graph  # (width, height): frames through each shard's captured graph
         self.split = split
         self.key_cap, self.cand_cap = key_cap, cand_cap
@@ -818,6 +851,11 @@ class ShardGroup:
         self.keys_exchanged = 0   # key records that went through the exchange (all frames)
         self.cands_exchanged = 0  # carve-candidate records likewise
         self.cands_by_shard = [0] * shard_count  # ... by the shard that sent them
+        # pipelined: call n writes its candidates into slot set n % 2 and reads set (n - 1) % 2 (the
+        # "all-gather" of the previous call: every shard's slot)
+        self._pc = torch.zeros((2, shard_count, Engine.shard_slot_bytes(cand_cap)), dtype=torch.uint8,
+                               device=dev) if pipe else None
+        self._ncall = 0
         self.graphs = None
         if graph is not None:
             w, h = graph
@@ -837,8 +875,24 @@ class ShardGroup:
                     pass
             raise
 
+    def _pipe_step(self, rgb, depth, ht, lt, K, cam_T_world, max_depth):
+        out, inb = self._pc[self._ncall & 1], self._pc[(self._ncall + 1) & 1]
+        pend = [e.integrate_shard_pipe(rgb, depth, ht, lt, K, cam_T_world, max_depth, inb, out[i], self.cand_cap)
+                for i, e in enumerate(self.engines)]
+        self._ncall += 1
+        return any(pend)
+
+    def flush(self):
+        """Pipelined: complete the pending frames (steps with their exchanges); a no-op otherwise."""
+        if self.pipe:
+            while self._pipe_step(None, None, None, None, None, None, 4.0):
+                pass
+
     def _integrate(self, rgb, depth, ht, lt, K, cam_T_world, max_depth, count):
         G = self.G
+        if self.pipe:
+            self._pipe_step(rgb, depth, ht, lt, K, cam_T_world, max_depth)
+            return
         if self.graphs is not None:
             for i, g in enumerate(self.graphs):
                 g.begin(rgb, depth, ht, lt, K, cam_T_world, max_depth, self._keys[i], self._keys, self.key_cap,
@@ -875,10 +929,12 @@ class ShardGroup:
             self.cands_exchanged += hdr(self._cands)
 
     def synchronize(self):
+        self.flush()
         for e in self.engines:
             e.synchronize()
 
     def stats(self):
+        self.flush()
         return [e.stats() for e in self.engines]
 
     def close(self):

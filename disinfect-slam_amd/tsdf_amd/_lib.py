@@ -22,6 +22,7 @@ STATUS_RESOLVE_ABORT = 8
 STATUS_SHARD_OVERFLOW = 16
 STATUS_SHARD_ABORTED = 32
 STATUS_PIPELINE_TIMEOUT = 64
+TSDF_ERR_PIPELINE = 6
 SHARD_RECORD_BYTES = 16
 
 
@@ -110,6 +111,7 @@ EXPORTS = [
     "tsdf_render_blocks", "tsdf_import_blocks", "tsdf_reset", "tsdf_pack_blocks",
     "tsdf_raycast_rows", "tsdf_render_bands", "tsdf_pack_halo", "tsdf_extract_mesh_owned",
     "tsdf_graph_create_shard", "tsdf_graph_shard_begin", "tsdf_graph_shard_update", "tsdf_graph_shard_end",
+    "tsdf_integrate_shard_pipe",
 ]
 
 _lib = None
@@ -139,6 +141,8 @@ def load(path: str | None = None):
     L.tsdf_integrate_shard_update.argtypes = [P, P, C.c_int32, P, C.c_int32]
     L.tsdf_integrate_shard_end.argtypes = [P, P, C.c_int32]
     L.tsdf_integrate_shard_abort.argtypes = [P]
+    L.tsdf_integrate_shard_pipe.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f, P, P,
+                                            C.c_int32, C.POINTER(C.c_int32)]
     L.tsdf_stream_wait.argtypes = [P, P]
     L.tsdf_stream_signal.argtypes = [P, P]
     L.tsdf_get_stream.argtypes = [P, C.POINTER(P)]
@@ -204,7 +208,7 @@ def load(path: str | None = None):
                  "tsdf_extract_mesh", "tsdf_raycast_rows", "tsdf_render_bands", "tsdf_pack_halo",
                  "tsdf_extract_mesh_owned", "tsdf_render_blocks", "tsdf_import_blocks", "tsdf_reset",
                  "tsdf_pack_blocks", "tsdf_graph_create_shard", "tsdf_graph_shard_begin",
-                 "tsdf_graph_shard_update", "tsdf_graph_shard_end",
+                 "tsdf_graph_shard_update", "tsdf_graph_shard_end", "tsdf_integrate_shard_pipe",
                  "tsdf_get_stats", "tsdf_synchronize", "tsdf_flush", "tsdf_profile_begin", "tsdf_profile_end",
                  "tsdf_debug_dump", "tsdf_debug_stamps", "tsdf_hash_allocate", "tsdf_hash_delete",
                  "tsdf_hash_retrieve",

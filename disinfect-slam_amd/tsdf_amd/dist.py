@@ -93,6 +93,23 @@ def integrate_sharded(engine, bufs, rgb, depth, ht, lt, K, cam_T_world, max_dept
         raise
 
 
+def integrate_sharded_pipe(engine, bufs, rgb, depth, ht, lt, K, cam_T_world, max_depth):
+    """One pipelined sharded frame on this rank (tsdf_integrate_shard_pipe): ONE
+    all-gather per frame -- this call's carve candidates (bufs.cands_out) into every rank's inbox
+    (bufs.cands_in, read by the next call). depth None: one step of completing the pending frames.
+    Returns True while more steps are needed (flush_sharded_pipe loops)."""
+    pend = engine.integrate_shard_pipe(rgb, depth, ht, lt, K, cam_T_world, max_depth, bufs.cands_in, bufs.cands_out,
+                                       bufs.cand_cap)
+    all_gather_slots(bufs.cands_out, bufs.cands_in)
+    return pend
+
+
+def flush_sharded_pipe(engine, bufs):
+    """Complete this rank's pipelined sharded frames (every rank calls it: each step exchanges)."""
+    while integrate_sharded_pipe(engine, bufs, None, None, None, None, None, None, 4.0):
+        pass
+
+
 def _integrate_sharded(engine, bufs, rgb, depth, ht, lt, K, cam_T_world, max_depth, split, rank, world):
     if split:
         engine.integrate_shard_begin(rgb, depth, ht, lt, K, cam_T_world, max_depth, rank, world,

@@ -172,6 +172,20 @@ int tsdf_flush(tsdf_engine* e);
  * tsdf_integrate / feed / graph frames refuse a shard. More records than a slot holds set
  * TSDF_STATUS_SHARD_OVERFLOW (the shards then diverge: size the caps for the first frame). */
 int64_t tsdf_shard_slot_bytes(int32_t cap);
+/* Pipelined sharded frames: ONE exchange per frame (no reference counterpart; the sharded form of
+ * TSDFGrid::Integrate, voxel_tsdf.cu:347-375, pipelined like tsdf_integrate). Every shard runs the
+ * whole frame's DDA against its copy of the index, so the new keys need no exchange and only the
+ * carve candidates cross the shards. Per frame, on every shard: tsdf_integrate_shard_pipe(frame,
+ * cands_in, cands_out), then the caller all-gathers cands_out (one slot of
+ * tsdf_shard_slot_bytes(cand_cap)) into cands_in (shard_count slots, slot s from shard s) for the next
+ * call. The call carves the frame before the previous one (every shard's candidates, from cands_in),
+ * allocates and updates the previous frame (this shard's candidates into cands_out) and ingests this
+ * one. To complete the frames: call with frame == NULL (and the exchange after each call) until
+ * *pending is 0. Until then every other volume entry point returns TSDF_ERR_INVALID_ARG. The frame's
+ * buffers are read by this call only. */
+int tsdf_integrate_shard_pipe(tsdf_engine* e, const tsdf_frame* frame, const tsdf_intrinsics* K,
+                              const tsdf_pose* cam_T_world, float max_depth, const void* cands_in,
+                              void* cands_out, int32_t cand_cap, int32_t* pending);
 int tsdf_integrate_shard_begin(tsdf_engine* e, const tsdf_frame* frame, const tsdf_intrinsics* K,
                                const tsdf_pose* cam_T_world, float max_depth, int32_t slice_index,
                                int32_t slice_count, void* keys_out, int32_t key_cap);

@@ -422,3 +422,79 @@ def test_halo_sharded_mesh_equals_unsharded(G):
             np.testing.assert_array_equal(_tri_set(np.concatenate(tris)), _tri_set(exp))
     finally:
         _close(full, replica, group)
+
+
+def _halo_mesh(shards, replica):
+    """tsdf_amd.dist.mesh_sharded with the all-to-all done in-process: shard s meshes its own blocks
+    in a replica holding them plus the halo the other shards send it."""
+    import torch
+    G = len(shards)
+    halos = [e.pack_halo(device=True) for e in shards]
+    tris = []
+    for s, e in enumerate(shards):
+        own = e.pack_blocks(None, device=True)
+        halo = torch.cat([r[int(c[:s].sum()):int(c[:s + 1].sum())] for c, r in halos])
+        replica.import_blocks(torch.cat([own, halo]), replace=True)
+        tris.append(replica.extract_mesh(None, owner=(s, G)))
+    return np.concatenate(tris)
+
+
+def test_halo_sharded_mesh_equals_unsharded_eight_shards():
+    """The halo mesh at G = 8: the union of the 8 shards' triangles is the
+    unsharded mesh."""
+    from tsdf_amd import synth
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    full, group, replica = _engines(8)
+    try:
+        _integrate([full, group], cam, 6)
+        exp = full.extract_mesh(None)
+        assert exp.shape[0] > 100
+        np.testing.assert_array_equal(_tri_set(_halo_mesh(group.engines, replica)), _tri_set(exp))
+    finally:
+        _close(full, replica, group)
+
+
+def test_c5_loop_eight_shards_graph_frames():
+    """BASELINE C5 on an 8-way sharded volume as one loop: 640x480 frames of the
+    bench stream through each shard's graph-captured sharded frame (ShardGroup graph=...), the banded
+    render of the sharded volume every 10 frames equal to the unsharded engine's raycast bit for bit,
+    and at frame 30 the halo mesh of the 8 shards equal to the unsharded mesh and to the CPU oracle's."""
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import dist as tdist
+    from tsdf_amd import synth
+    from _oracle import OracleGrid
+    w, h, G, n = 640, 480, 8, 30
+    cam = synth.camera(w, h, synth.TUM_FR1)
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    full = tsdf_amd.Engine(0.005, 0.03, max_width=w, max_height=h, num_block_bits=18)
+    group = tsdf_amd.ShardGroup(G, 0.005, 0.03, max_width=w, max_height=h, num_block_bits=16,
+                                graph=(w, h))
+    replica = tsdf_amd.Engine(0.005, 0.03, max_width=w, max_height=h, num_block_bits=18)
+    ora = OracleGrid(0.005, 0.03, 18)
+    try:
+        rows = tdist.band_rows(h, G)
+        for i in range(n):
+            fr = synth.render(cam, i)
+            dev = {k: torch.from_numpy(fr[k]).to("cuda") for k in ("rgb", "depth", "ht", "lt")}
+            pose = tsdf_amd.SE3(fr["q"], fr["t"])
+            full.integrate(dev["rgb"], dev["depth"], dev["ht"], dev["lt"], K, pose, 4.0)
+            group.integrate(dev["rgb"], dev["depth"], dev["ht"], dev["lt"], K, pose, 4.0)
+            ora.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], 4.0, cam.K, fr["q"], fr["t"])
+            if (i + 1) % 10 == 0:
+                exp = full.raycast(K, w, h, pose, 4.0)
+                got = _banded_render(group.engines, replica, K, w, h, pose, rows)
+                assert (exp[0][..., 3] == 255).mean() > 0.5, i
+                np.testing.assert_array_equal(got[0], exp[0])
+                np.testing.assert_array_equal(got[1], exp[1])
+        for e in group.engines:
+            assert e.stats()["status"] == 0
+        exp = full.extract_mesh(None, 0.99, 0)
+        m_o = ora.extract_mesh(None, 0.99, 0)
+        assert exp.shape[0] > 100000
+        np.testing.assert_array_equal(np.asarray(exp).view(np.uint32), np.asarray(m_o).view(np.uint32))
+        np.testing.assert_array_equal(_tri_set(_halo_mesh(group.engines, replica)), _tri_set(exp))
+    finally:
+        _close(full, replica, group)
+        ora.close()

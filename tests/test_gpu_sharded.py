@@ -22,7 +22,7 @@ MAXD = 4.0
 
 
 def _run(G, W, H, voxel, trunc, frames, nb_bits, shard_bits, split=True, stride=1, intrinsics=None,
-         oracle_shards=True, semantic=True, graph=False):
+         oracle_shards=True, semantic=True, graph=False, pipe=False, checks=None):
     import torch
 
     import tsdf_amd
@@ -30,7 +30,7 @@ def _run(G, W, H, voxel, trunc, frames, nb_bits, shard_bits, split=True, stride=
     from _oracle import OracleGrid, lib
     cam = synth.camera(W, H, intrinsics or synth.TUM_FR1)
     group = tsdf_amd.ShardGroup(G, voxel, trunc, max_width=W, max_height=H, num_block_bits=shard_bits,
-                                split=split, graph=(W, H) if graph else None)
+                                split=split, graph=(W, H) if graph else None, pipe=pipe)
     full = OracleGrid(voxel, trunc, nb_bits)
     oshards = []
     if oracle_shards:
@@ -56,12 +56,15 @@ def _run(G, W, H, voxel, trunc, frames, nb_bits, shard_bits, split=True, stride=
             if oshards:
                 oracle_shard_frame(oshards, fr, cam, MAXD, split=split)
                 cross += oshards[0].stats()["last_cross_losses"]
+            if checks is not None and f not in checks:  # (pipelined: a read completes the frames)
+                continue
             st = group.stats()
             assert all(s["status"] == 0 for s in st), (f, st)
             fs = full.stats()
             assert sum(s["last_num_visible"] for s in st) == fs["last_num_visible"], (f, st, fs)
             assert sum(s["last_num_updated"] for s in st) == fs["last_num_updated"], (f, st, fs)
             assert sum(s["active_blocks"] for s in st) == fs["active_blocks"], (f, st, fs)
+        group.flush()
         dumps = [e.dump() for e in group.engines]
         nblk = assert_union_equals(dumps, full.dump(), tag=f"G={G}")
         for i, o in enumerate(oshards):
@@ -361,5 +364,87 @@ def test_sharded_graph_frames_equal_oracle(split):
     nblk, cross, group = _run(3, 160, 120, 0.005, 0.03, 6, nb_bits=15, shard_bits=14, split=split, graph=True)
     try:
         assert nblk > 500
+    finally:
+        group.close()
+
+
+@pytest.mark.parametrize("G", [2, 8])
+def test_sharded_pipe_c3_union_equals_unsharded(G):
+    """Pipelined sharded frames (tsdf_integrate_shard_pipe: one exchange per frame, every shard runs
+    the whole DDA): C3 640x480, 12 frames back to back with one mid-stream read (which completes the
+    pending frames through the exchange protocol): the union is the unsharded oracle volume, each
+    shard its oracle shard."""
+    nblk, cross, group = _run(G, 640, 480, 0.005, 0.03, 12, nb_bits=16, shard_bits=16 if G == 2 else 14,
+                              split=False, pipe=True, checks={5})
+    try:
+        assert nblk > 5000
+    finally:
+        group.close()
+
+
+def test_sharded_pipe_heavy_carving():
+    """Pipelined sharded frames under heavy carving (2 cm, fast orbit, 8 shards, 20 frames back to
+    back): carvings of every shard's candidates run a frame late beside the next frame's update,
+    deleted keys the next frame's DDA had found are re-inserted; shards stay bit-exact against the
+    oracle's."""
+    nblk, cross, group = _run(8, 160, 120, 0.02, 0.06, 20, nb_bits=14, shard_bits=12, split=False, stride=3,
+                              pipe=True, checks={9})
+    try:
+        assert nblk > 200
+    finally:
+        group.close()
+
+
+def test_sharded_pipe_pool_exhaustion_matches_oracle_shards():
+    """Pipelined sharded frames with shard pools far smaller than the scene: the owned entries an
+    exhausted pool leaves without voxels go out with the candidates and are carved on every shard."""
+    import tsdf_amd
+    from tsdf_amd import synth
+    from _oracle import OracleGrid, lib
+    W, H, G, bits = 160, 120, 3, 8
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    group = tsdf_amd.ShardGroup(G, 0.005, 0.03, max_width=W, max_height=H, num_block_bits=bits, split=False,
+                                pipe=True)
+    oshards = []
+    for i in range(G):
+        o = OracleGrid(0.005, 0.03, bits)
+        lib().ora_set_shard(o.h, i, G)
+        oshards.append(o)
+    try:
+        for f in range(8):
+            fr = synth.render(cam, 2 * f)
+            group.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, tsdf_amd.SE3(fr["q"], fr["t"]), MAXD)
+            oracle_shard_frame(oshards, fr, cam, MAXD, split=False)
+        st = group.stats()
+        assert any(s["status"] & tsdf_amd.STATUS_POOL_EXHAUSTED for s in st)
+        assert all((s["status"] & ~tsdf_amd.STATUS_POOL_EXHAUSTED) == 0 for s in st), [s["status"] for s in st]
+        for i, o in enumerate(oshards):
+            compare(group.engines[i], o, tag=f"shard {i}/{G}")
+        _no_owned_voxelless_entries(group)
+    finally:
+        group.close()
+        for o in oshards:
+            o.close()
+
+
+def test_sharded_pipe_protocol():
+    """Reads are refused while pipelined sharded frames are pending (only the exchange protocol can
+    complete them); flush() completes them, after which reads work and a new stream starts."""
+    import tsdf_amd
+    from tsdf_amd import synth
+    cam = synth.camera(80, 60, synth.TUM_FR1)
+    group = tsdf_amd.ShardGroup(2, 0.01, 0.04, max_width=80, max_height=60, num_block_bits=12, split=False,
+                                pipe=True)
+    try:
+        for f in range(3):
+            fr = synth.render(cam, f)
+            group.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, tsdf_amd.SE3(fr["q"], fr["t"]), MAXD)
+        with pytest.raises(tsdf_amd.TSDFError):
+            group.engines[0].dump()
+        group.flush()
+        assert all(s["status"] == 0 and s["frames"] == 3 for s in group.stats())
+        fr = synth.render(cam, 3)
+        group.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, tsdf_amd.SE3(fr["q"], fr["t"]), MAXD)
+        assert all(s["frames"] == 4 for s in group.stats())
     finally:
         group.close()

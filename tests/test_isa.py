@@ -107,7 +107,9 @@ def test_k_frame_flags_follow_a_drained_barrier():
     between them, and a vmcnt(0) wait must come before that barrier (drain_barrier): the table /
     free-stack / new-key / rtag writes the flags publish are complete when another XCD sees the tag."""
     body = _kframe()
-    swaps = [i for i, ins in enumerate(body) if ins.startswith("global_atomic_swap_x2")]
+    # (non-returning: a returning swap, sc0, is a bucket lock of the hash-level resolver path)
+    swaps = [i for i, ins in enumerate(body) if ins.startswith("global_atomic_swap_x2")
+             and not ins.split("//")[0].rstrip().endswith("sc0")]
     assert len(swaps) >= 2, "carving and allocation flags"
     for i in swaps:
         j = max(k for k in range(i) if body[k].startswith("s_barrier"))
