@@ -257,7 +257,7 @@ __device__ __forceinline__ void batch_sort(ResolveLds& L, int m, bool single) {
             __builtin_amdgcn_s_memrealtime();                                                  \
     }                                                                                          \
   } while (0)
-// explicit slot (k_integrate_pre's chained workgroups and its tail: kernel 5)
+// explicit workgroup slot (kernel 5)
 #define TSDF_STAMP_WG(D, kern, wg, k)                                                                    \
   do {                                                                                                   \
     if (threadIdx.x == 0 && (D).dbg && (unsigned)(wg) < (unsigned)::tsdf::kDiagMaxWg)                    \

@@ -1,8 +1,8 @@
 // tsdf_ingest.h -- the per-pixel-tile part of a frame's ingest: pixel records, the block-allocation
 // DDA (block_allocate_kernel, utils/tsdf/voxel_tsdf.cu:104-147) into a per-tile LDS key set, the
 // all-corners visibility of its keys and their table probe / new-key-set insert. Shared by
-// k_ingest_dda (tsdf_alloc.hip) and the pipelined frame's k_integrate_pre (tsdf_fuse.hip), which
-// prepares the next frame's tiles while the current frame's blocks are updated.
+// k_ingest_dda (tsdf_alloc.hip) and the pipelined frame's k_frame (tsdf_fuse.hip), which runs the next
+// frame's tiles while the current frame's blocks are updated.
 #pragma once
 
 #include "tsdf_block.h"
@@ -148,8 +148,8 @@ __device__ __forceinline__ int32_t find_entry_t(const int4* __restrict__ table, 
 // blocks it creates. Order within a list is irrelevant to the update; the carving resolver
 // restores the reference's entry order for the deletes.
 // ---------------------------------------------------------------------------------------------
-// Co: the sweep of a chained frame (k_integrate_pre, after frame n's carving was published): the
-// occupancy words and entries are read at agent scope
+// Co: the sweep of a pipelined frame after its wait (the chained sweep's fallback): the occupancy
+// words and entries are read at agent scope
 template <int TS, bool Co = false>
 __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, IngestLds<TS>& S) {
   const int lane = lane_id(), wave = threadIdx.x >> 6;
@@ -233,8 +233,9 @@ __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, Inge
   }
 }
 
-// The chained sweep of a pipelined frame (k_integrate_pre, frame n + 1's sweep inside frame n's
-// launch). Frame n's carving only clears entries and moves a list element into its head entry, and it
+// The chained sweep of a pipelined frame (k_frame: frame c's sweep inside the launch that carves
+// frame c - 2 and allocates frame c - 1; "the carving" below is that launch's carving and allocation,
+// both of which mark the words they change). Frame n's carving only clears entries and moves a list element into its head entry, and it
 // marks every occupancy word it changes (D.swdirty, tsdf_resolve.h mark_swept_dirty); nothing else
 // writes the table in the launch. So the listing and the visibility tests run BEFORE the carving is
 // published (possibly while it runs), keeping each wave's visible blocks in LDS (entry | band << 24 in
@@ -247,7 +248,7 @@ __device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, Inge
 // tiles' agent-scope probes after the wait would then read. A wave with more than kPreMax live
 // entries (far above the bench's ~1 % occupancy) makes the workgroup wait and run the agent-scope
 // sweep instead.
-#ifndef TSDF_PRE_MAX  // (a test build lowers it to run the fallback: scripts/gpu_r3_premax.sh)
+#ifndef TSDF_PRE_MAX  // (a test build lowers it to run the fallback)
 #define TSDF_PRE_MAX 256
 #endif
 constexpr int kPreMax = TSDF_PRE_MAX;

@@ -185,23 +185,8 @@ __global__ void k_init_logodds(uint8_t* pool, int nb);
 constexpr int kArrGroups = TSDF_ARRIVE_GROUPS;
 static_assert(kArrGroups % 8 == 0 && kArrGroups <= 128, "arrival counters");
 constexpr int kArrStride = (kArrGroups + 1) * 16;  // u64 words of one kernel's counter lines
-// pipelined frames: kArrCarved + 16 f: copy f of the carving-published flag, polled by the waiting
-// workgroups b with b % kCarvedFlags == f (a line each; 8: one per XCD under round-robin placement); kArrChained + 16 c: the chained workgroups
-// b with b % kChainCounters == c that finished (~1,500 atomics on one word serialise for ~15 us; 8
-// counters, one per XCD, still queue the end burst)
-#ifndef TSDF_CHAIN_COUNTERS  // k_integrate_pre's completion counters (one 128-B line each)
-#define TSDF_CHAIN_COUNTERS 64
-#endif
-constexpr int kChainCounters = TSDF_CHAIN_COUNTERS;
-#ifndef TSDF_CARVED_FLAGS  // copies of k_integrate_pre's carving-published flag (one 128-B line each)
-#define TSDF_CARVED_FLAGS 8  // (64 measured equal: the waiters wake ~0.9 us after the publish either way)
-#endif
-constexpr int kCarvedFlags = TSDF_CARVED_FLAGS;
-static_assert(kCarvedFlags % 8 == 0 && kCarvedFlags <= 256, "the tail stores one per thread");
-static_assert(kChainCounters == 8 || kChainCounters == 64, "a wave polls them");
 constexpr int kArrIngest = 0, kArrIntegrate = kArrStride, kArrStart = 2 * kArrStride,
-              kArrCarved = 2 * kArrStride + 16, kArrChained = kArrCarved + kCarvedFlags * 16,
-              kArriveWords = kArrChained + TSDF_CHAIN_COUNTERS * 16;
+              kArriveWords = 2 * kArrStride + 32;
 // per frame (2 launches; the resolvers run in the last workgroup of each)
 constexpr int kVisWorkgroups = kOccWords / 256;  // visibility-sweep workgroups of k_ingest_dda
 template <int TS>  // LDS key-set slots per tile (tsdf_alloc.hip): 1024 for maxs <= 3, else 2048

@@ -73,7 +73,7 @@ __device__ __forceinline__ R ld_rec_co(const R* src) {
 // Table stores of the carving resolver, written through at agent scope (32-bit sc1 stores; the
 // 16-bit offset by read-modify-write of its dword -- nothing else writes the table meanwhile): a
 // pipelined frame's chained sweep and probes on other XCDs read the carved table right after the
-// carving is published, with no L2 write-back in between (tsdf_fuse.hip k_integrate_pre).
+// carving is published, with no L2 write-back in between (tsdf_fuse.hip k_frame).
 __device__ __forceinline__ void store_ent_co(int4* table, uint32_t e, int16_t x, int16_t y, int16_t z, int16_t off,
                                              int32_t idx) {
   uint32_t* p = reinterpret_cast<uint32_t*>(&table[e]);
@@ -1024,8 +1024,6 @@ struct DeleteLds {
   uint32_t lock[kRLockD];
   int scan[8];
   int sfree, ndel, changed, m;
-  int bcnt[kBands];                // (k_integrate_pre) the frame's band counts, for integrate_stats
-  unsigned long long tend;         // (k_integrate_pre) the update's end, for integrate_stats
 };
 constexpr uint32_t kHintSlot0 = 1u << 9;  // (with kHintValid) slot 0 holds the key
 

@@ -1,6 +1,6 @@
-"""Pipelined frames: tsdf_integrate defers a frame's update / carving into the next
-frame's launch (k_integrate_pre, together with that frame's pixel tiles), and every other entry point
-enqueues a deferred update first. Every observable result must be that of the frames in order: the
+"""Pipelined frames: tsdf_integrate of frame c launches one k_frame that carves frame
+c - 2, allocates and updates frame c - 1 (its listed blocks before that carving) and runs frame c's
+ingest; every other entry point completes the pending frames first. Every observable result must be that of the frames in order: the
 oracle decides at the small sizes, the unpipelined engine (TSDF_PIPELINE=0, the two-launch frame the
 other GPU tests pin to the oracle frame by frame) at full size, with frames integrated back to back
 so that the fused launch and the probe-only ingest actually run (a read between frames would flush)."""
