@@ -12,6 +12,19 @@ __device__ __forceinline__ float wave_min(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
   return v;
 }
+// wave-wide minimum as a wave-uniform value (every lane of the wave active): DPP row reductions --
+// quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror -- then the four rows' minima read as
+// scalars. No permute addresses: __shfl_xor's ds_bpermute lane addresses are loop-invariant VGPRs
+// that the update loops keep live and spill to scratch.
+__device__ __forceinline__ float wave_min_u(float v) {
+  v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));
+  v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));
+  v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false)));
+  v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false)));
+  const int x = __float_as_int(v);
+  return fminf(fminf(__int_as_float(__builtin_amdgcn_readlane(x, 0)), __int_as_float(__builtin_amdgcn_readlane(x, 16))),
+               fminf(__int_as_float(__builtin_amdgcn_readlane(x, 32)), __int_as_float(__builtin_amdgcn_readlane(x, 48))));
+}
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -176,7 +176,6 @@ struct tsdf_engine {
   FrameParams p_P{};      // frame p_fid's camera / frame / pixel-record buffer
   uint32_t pipe_tag = 0;  // one per k_frame launch: its flags' value
   int frame_order = 0;    // PipeArgs.order (TSDF_FRAME_ORDER)
-  int ray_segs = 1;       // lanes per ray of k_raycast (TSDF_RAYCAST_SEGS: 1, 2, 4)
   // feed_rgbd_frame staging: raw full-size inputs (host frames) and the half-size outputs
   uint8_t* fe_rgb = nullptr;
   uint16_t* fe_depth = nullptr;
@@ -526,10 +525,6 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.pixB, 2 * e->max_pixels);
   if (const char* v = std::getenv("TSDF_PIPELINE")) e->pipeline = v[0] != '0';
   if (const char* v = std::getenv("TSDF_FRAME_ORDER")) e->frame_order = std::min(2, std::max(0, std::atoi(v)));
-  if (const char* v = std::getenv("TSDF_RAYCAST_SEGS")) {
-    const int k = std::atoi(v);
-    e->ray_segs = k == 2 || k == 4 ? k : 1;
-  }
   ALLOC(D.visbits, kOccWords);
   ALLOC(D.wgcnt, kOccWords / 256);
   ALLOC(D.dbg, (size_t)kDiagKernels * kDiagMaxWg * kDiagStamps);
@@ -1101,7 +1096,7 @@ int view_grid_for(tsdf_engine* e, const FrameParams& P, float step_size, int lds
   if (!(reach < 1e6) || n > kViewMaxN || nw > lds_words ||
       e->D.nblocks > (1 << kViewIdxBits))
     return TSDF_OK;
-  const int64_t cells = (int64_t)n * n * n;
+  const int64_t cells = (int64_t)nb * nb * nb * 64;  // brick-major (view_cell)
   if (cells > e->vg_cap) {
     if (e->vg_cell) HIP_OK(hipFree(e->vg_cell));
     e->vg_cell = nullptr;
@@ -1236,12 +1231,7 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
       hipLaunchKernelGGL(k_view_grid_g, dim3(kOccWords / 256), dim3(256), 0, g->cap, e->D, A);
       hipLaunchKernelGGL(k_view_pack_g, dim3(kViewPackGrid), dim3(256), 0, g->cap, A);
       const dim3 rgrid((render_width + 15) / 16, (render_height + 15) / 16);
-      if (e->ray_segs == 4)
-        hipLaunchKernelGGL(k_raycast_g<4>, rgrid, dim3(1024), 0, g->cap, e->D, A);
-      else if (e->ray_segs == 2)
-        hipLaunchKernelGGL(k_raycast_g<2>, rgrid, dim3(512), 0, g->cap, e->D, A);
-      else
-        hipLaunchKernelGGL(k_raycast_g<1>, rgrid, dim3(256), 0, g->cap, e->D, A);
+      hipLaunchKernelGGL(k_raycast_g, rgrid, dim3(256), 0, g->cap, e->D, A);
     }
     if ((err = hipStreamEndCapture(g->cap, &g->graph[k][0])) != hipSuccess) return fail(err, "hipStreamEndCapture");
     if ((err = hipGraphInstantiate(&g->exec[k][0], g->graph[k][0], nullptr, nullptr, 0)) != hipSuccess)
@@ -1622,12 +1612,7 @@ int raycast_impl(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const t
     HIP_OK(hipStreamWaitEvent(rs, e->rs_ready, 0));
   }
   const dim3 rgrid((W + 15) / 16, (nrows + 15) / 16);
-  if (e->ray_segs == 4)
-    hipLaunchKernelGGL(k_raycast<4>, rgrid, dim3(1024), lds, rs, e->D, P, step, V, o1, o2);
-  else if (e->ray_segs == 2)
-    hipLaunchKernelGGL(k_raycast<2>, rgrid, dim3(512), lds, rs, e->D, P, step, V, o1, o2);
-  else
-    hipLaunchKernelGGL(k_raycast<1>, rgrid, dim3(256), lds, rs, e->D, P, step, V, o1, o2);
+  hipLaunchKernelGGL(k_raycast, rgrid, dim3(256), lds, rs, e->D, P, step, V, o1, o2);
   LAUNCH_OK("k_raycast");
   if (overlap) {
     HIP_OK(hipEventRecord(e->rs_done, rs));

@@ -129,8 +129,9 @@ __device__ __forceinline__ void view_grid(const EngineDev& D, const FrameParams&
     if ((unsigned)lx >= (unsigned)V.n || (unsigned)ly >= (unsigned)V.n || (unsigned)lz >= (unsigned)V.n ||
         !local_idx(en.idx))
       continue;
-    V.cell[((size_t)lz * V.n + ly) * V.n + lx] = (V.gen << kViewIdxBits) | (uint32_t)en.idx;
-    V.flags[((lz >> 2) * V.nb + (ly >> 2)) * V.nb + (lx >> 2)] = 1;
+    const int k = ((lz >> 2) * V.nb + (ly >> 2)) * V.nb + (lx >> 2);  // brick
+    V.cell[view_cell(k, lx, ly, lz)] = (V.gen << kViewIdxBits) | (uint32_t)en.idx;
+    V.flags[k] = 1;
     V.flags[V.nbw * 32 + ((lz >> 4) * V.ns + (ly >> 4)) * V.ns + (lx >> 4)] = 1;
   }
 }
@@ -192,7 +193,7 @@ __device__ __forceinline__ void ray_block(const EngineDev& D, const RayView& R, 
       c.empty = 2 - (int)((ws >> (q & 31)) & 1u);
       return;
     }
-    const uint32_t v = R.cell[((size_t)lz * n + ly) * n + lx];
+    const uint32_t v = R.cell[view_cell(k, lx, ly, lz)];
     c.idx = (v >> kViewIdxBits) == R.gen ? (int32_t)(v & ((1u << kViewIdxBits) - 1)) : -1;
     return;
   }
@@ -256,39 +257,31 @@ __device__ __forceinline__ void ray_shade(const EngineDev& D, const RayView& R, 
   if (normal) normal[idx] = make_uchar4(f2u8(alpha * 255 + sh), f2u8(sh), f2u8(sh), 255);
 }
 
-// K lanes per ray (K = 1, 2, 4; DESIGN.md 4 "Raycast"): the ray's steps i = 1 .. max_step - 1 are cut
-// into K segments of L steps, lane k of the ray's group marches segment k. The positions are the
-// sequential float sums of the reference (pos_i = pos_{i-1} + step), so lane k first adds k L steps to
-// the origin, reads the value at pos_{i0 - 1} for its first comparison, and then marches exactly the
-// reference's steps of its segment; the ray's hit is the first hit of the first segment that has one
-// (a lane stops once a lower segment of its ray has hit). Every lookup is the reference's lookup of
-// that step, so the result is bit-identical for every K; K > 1 trades the prefix additions and the
-// marching of segments past the hit for K times shorter dependent-lookup chains per lane and K times
-// more waves to hide them. The workgroup is 256 K threads: one 16 x 16 pixel tile.
-template <int K>
+// The march (DESIGN.md 4 "Raycast") is VALU-issue bound: ~4.7 waves per SIMD each step ~135 times,
+// and a step in empty space (most of them) is only the position update and the region test. Along a
+// ray each coordinate of the reference's sequential float sums pos_{i+1} = fl(pos_i + step) is
+// monotone (the step's sign is fixed, rounding is monotone), so after a lookup the positions never
+// cross the region's entry faces again: the test is the three exit faces, s_a * pos_a < e_a per axis
+// (s = the step's sign), as one fma each (s_a * pos_a is exact, the sign of the rounded sum is the
+// sign of the exact one). The step counter is wave-uniform (scalar).
 __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P, float step_size,
                                         const ViewGrid& V, uint32_t* sbits, uchar4* __restrict__ rgba,
                                         uchar4* __restrict__ normal) {
-  static_assert(K == 1 || K == 2 || K == 4, "segments per ray");
-  constexpr int NT = 256 * K;
   // stage the bitmaps (all threads, before any ray returns)
   const int nw = V.n ? V.nw : 0;
-  for (int i = threadIdx.x; i < nw; i += NT) sbits[i] = V.bits[i];
+  for (int i = threadIdx.x; i < nw; i += 256) sbits[i] = V.bits[i];
   __syncthreads();
   // XCD-aware tiles: workgroups wg and wg + 8 share an XCD (and its L2), so XCD g takes the g-th
   // contiguous run of 16x16 tiles in raster order -- neighbouring rays' blocks stay in one L2
   const int gx = gridDim.x, nwg = gx * gridDim.y, wg = blockIdx.y * gx + blockIdx.x;
   const int g = wg & 7, tile = g * (nwg >> 3) + min(g, nwg & 7) + (wg >> 3);
-  // each wave a compact patch of 64 / K rays (K = 1: an 8x8 quadrant of the tile -- a tighter ray
-  // bundle than 16x4 rows, whose lanes leave their regions at closer steps, 101.3 vs 103.8 us at C5;
-  // K = 2: 8x4; K = 4: 4x4), the K lanes of a ray adjacent
-  constexpr int PW = K == 4 ? 4 : 8, PH = 64 / K / PW, WX = 16 / PW;
+  // each wave an 8x8 quadrant of the tile (a tighter ray bundle than 16x4 rows, whose lanes leave
+  // their regions at closer steps, 101.3 vs 103.8 us at C5)
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  const int ray = ln / K, seg = ln % K;
   // rows [P.row0, P.row0 + P.nrows) of the W x H camera (a band of a sharded render, else all);
   // the outputs hold the band's rows only
-  const int x = (tile % gx) * 16 + (wv % WX) * PW + (ray % PW);
-  const int yb = (tile / gx) * 16 + (wv / WX) * PH + (ray / PW);
+  const int x = (tile % gx) * 16 + (wv & 1) * 8 + (ln & 7);
+  const int yb = (tile / gx) * 16 + (wv >> 1) * 8 + (ln >> 3);
   const int y = P.row0 + yb;
   const bool valid = x < P.W && yb < P.nrows && y < P.H;
   const int idx = valid ? yb * P.W + x : 0;
@@ -319,51 +312,35 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
   const f3 dw = qrot(P.wq, dc);
   const f3 sg = {dw.x * step_size / P.voxel, dw.y * step_size / P.voxel, dw.z * step_size / P.voxel};
   const int max_step = f2i(ceilf(P.max_depth / step_size));  // wave-uniform
-  // this lane's steps [i, i_end); the comparison before its first step needs the value at i - 1
-  const int L = K == 1 ? max_step : (max_step - 1 + K - 1) / K;
-  int i = K == 1 ? 1 : min(max_step, 1 + seg * L);
-  const int i_end = K == 1 ? max_step : min(max_step, 1 + (seg + 1) * L);
+  // steps i = 1 .. max_step - 1; the comparison of step 1 needs the value at the origin
   f3 pos = {P.wt.x / P.voxel, P.wt.y / P.voxel, P.wt.z / P.voxel};
-  if (K > 1)
-    for (int j = 1; j < i; ++j) {  // pos_{i - 1}: the reference's sequential sums
-      pos.x += sg.x;
-      pos.y += sg.y;
-      pos.z += sg.z;
-    }
-  bool done = !valid || i >= i_end;
+  bool active = valid && 1 < max_step;
   bool hit = false;
   f3 hit_pos = pos;
   float prev = 1.0f;
-  if (!done) prev = ray_tsdf(D, R, c, round_s16(pos.x), round_s16(pos.y), round_s16(pos.z));
-  pos.x += sg.x;
-  pos.y += sg.y;
-  pos.z += sg.z;
-  // (K > 1) the lanes of this ray's lower segments: once one of them has hit, this lane's steps no
-  // longer matter
-  const unsigned long long lower = K > 1 ? (((1ull << seg) - 1ull) << (ray * K)) : 0ull;
-  // Region of the last lookup, as float bounds x in (lo, hi) per axis of the positions that surely
-  // round into it: the missing block or the empty brick / superbrick around it (reads +1: no lookup,
-  // no hit), or the present block (only the voxel offset and its load). The lanes of a wave step
-  // together (a tight per-lane loop through empty regions measured slower: the lanes' dependent
-  // loads then no longer overlap in time -- the kernel is bound by those load chains).
-  f3 rlo = {1.f, 1.f, 1.f}, rhi = {0.f, 0.f, 0.f};
+  if (active) prev = ray_tsdf(D, R, c, round_s16(pos.x), round_s16(pos.y), round_s16(pos.z));
+  pos = {pos.x + sg.x, pos.y + sg.y, pos.z + sg.z};
+  // Region of the last lookup: the missing block or the empty brick / superbrick around it (reads +1:
+  // no lookup, no hit), or the present block (only the voxel offset and its load), held as its exit
+  // faces: inside while fma(pos_a, s_a, ne_a) < 0 on every axis (ne = -e; +inf before the first lookup).
+  const f3 sgn = {sg.x >= 0.0f ? 1.0f : -1.0f, sg.y >= 0.0f ? 1.0f : -1.0f, sg.z >= 0.0f ? 1.0f : -1.0f};
+  f3 ne = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
   int32_t ridx = -1;  // pool index of the present block of the region, -1 missing
 #ifdef TSDF_DIAG_STAMPS
-  // diagnostic step statistics (per lane and per wave), summed per workgroup into D.dbg kernel 5
-  int d_it = 0, d_blk = 0, d_ld = 0, dw_blk = 0, dw_ld = 0;
+  // diagnostic step statistics (per lane), summed per workgroup into D.dbg kernel 5; the wave's
+  // start / end clock into kernel 6 (wave w of the workgroup at 2 w / 2 w + 1)
+  int d_it = 0, d_blk = 0, d_ld = 0;
+  const unsigned long long d_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  while (i < i_end && !done) {
-    // the six strict bounds as one maximum: for finite floats fl(a - b) < 0 iff a < b (a flushed
-    // denormal difference only reads as "outside", which costs a lookup, never a result); VALU
-    // max3 instead of six compares chained through scalar masks: 101.3 -> 92.8 us at C5
-    const bool inside = fmaxf(fmaxf(fmaxf(rlo.x - pos.x, pos.x - rhi.x), fmaxf(rlo.y - pos.y, pos.y - rhi.y)),
-                              fmaxf(rlo.z - pos.z, pos.z - rhi.z)) < 0.0f;
+  // The lanes of a wave step together (a tight per-lane loop through empty regions measured slower:
+  // the lanes' dependent loads then no longer overlap in time).
+  int i = 1;
+  while (active) {
+    const bool inside = fmaxf(fmaxf(fmaf(pos.x, sgn.x, ne.x), fmaf(pos.y, sgn.y, ne.y)), fmaf(pos.z, sgn.z, ne.z)) < 0.0f;
 #ifdef TSDF_DIAG_STAMPS
     d_it += 1;
     d_blk += !inside;
     d_ld += ridx >= 0;
-    dw_blk += __ballot(!inside) != 0ull;
-    dw_ld += __ballot(ridx >= 0) != 0ull;
 #endif
     // a lane inside an empty region reads +1 and needs nothing else this step (no rounding either:
     // when every lane of the wave is there, the wave skips the block below)
@@ -380,90 +357,71 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
         const int ry = (R.oy + (((c.by - R.oy) >> sh) << sh)) * kBlockLen;
         const int rz = (R.oz + (((c.bz - R.oz) >> sh) << sh)) * kBlockLen;
         const float len = (float)(kBlockLen << sh);
-        rlo = {(float)rx - 0.5f, (float)ry - 0.5f, (float)rz - 0.5f};
-        rhi = {rlo.x + len, rlo.y + len, rlo.z + len};
+        // faces at r - 0.5 and r + len - 0.5: the exit face of the step's direction, negated
+        // (s = +1: pos < hi; s = -1: -pos < -lo)
+        const float lx = (float)rx - 0.5f, ly = (float)ry - 0.5f, lz = (float)rz - 0.5f;
+        ne = {sgn.x > 0.0f ? -(lx + len) : lx, sgn.y > 0.0f ? -(ly + len) : ly, sgn.z > 0.0f ? -(lz + len) : lz};
       }
       if (ridx >= 0) {
         cur = reinterpret_cast<const float*>(D.pool + (size_t)ridx * kBlockBytes)[voxel_off(px, py, pz)];
         if (prev > 0 && cur <= 0 && (double)(prev - cur) <= 1.5) {
           hit_pos = pos;  // shaded after the march (below)
           hit = true;
-          done = true;
         }
       }
     }
     prev = cur;
-    pos.x += sg.x;
-    pos.y += sg.y;
-    pos.z += sg.z;
+    pos = {pos.x + sg.x, pos.y + sg.y, pos.z + sg.z};
     ++i;
-    if (K > 1 && (__ballot(hit) & lower)) done = true;
-  }
-  // the ray's hit: the first segment that has one (its lane shades; K == 1: every lane is its ray)
-  bool shade = hit, miss = !hit && valid;
-  if (K > 1) {
-    const unsigned long long hb = (__ballot(hit) >> (ray * K)) & ((1ull << K) - 1ull);
-    shade = hit && !(hb & ((1ull << seg) - 1ull));
-    miss = valid && hb == 0ull && seg == 0;
+    active = !hit && i < max_step;
   }
   // The hits are shaded together after the march: inside it, the lanes of a wave hit at different
   // steps, and each step with a hit ran the whole shading (binary search + 7 lookups) for a few lanes.
   // The shading reads only the static volume (the block cache is a memo), so where it runs changes
   // nothing.
-  if (shade) {
+  if (hit) {
 #if defined(TSDF_EXP) && (TSDF_EXP & 8)  // experiment build: no shading (timing of the march alone)
     if (rgba) rgba[idx] = make_uchar4(255, 255, 255, 255);
 #else
     ray_shade(D, R, c, hit_pos, sg, dw, rgba, normal, idx);
 #endif
-  } else if (miss) {
+  } else if (valid) {
     if (rgba) rgba[idx] = make_uchar4(0, 0, 0, 0);
     if (normal) normal[idx] = make_uchar4(0, 0, 0, 0);
   }
 #ifdef TSDF_DIAG_STAMPS
   if (D.dbg) {
-    int mx_it = d_it, mx_blk = dw_blk, mx_ld = dw_ld;
-    for (int o = 32; o > 0; o >>= 1) {
-      mx_it = max(mx_it, __shfl_xor(mx_it, o, 64));
-      mx_blk = max(mx_blk, __shfl_xor(mx_blk, o, 64));
-      mx_ld = max(mx_ld, __shfl_xor(mx_ld, o, 64));
-    }
+    int mx_it = d_it;
+    for (int o = 32; o > 0; o >>= 1) mx_it = max(mx_it, __shfl_xor(mx_it, o, 64));
     const unsigned wg = blockIdx.y * gridDim.x + blockIdx.x;
     if (wg < (unsigned)kDiagMaxWg) {
       unsigned long long* q = D.dbg + ((size_t)5 * kDiagMaxWg + wg) * kDiagStamps;
       atomicAdd(&q[0], (unsigned long long)d_it);
       atomicAdd(&q[1], (unsigned long long)d_blk);
       atomicAdd(&q[2], (unsigned long long)d_ld);
-      atomicAdd(&q[6], (unsigned long long)(valid && done));
+      atomicAdd(&q[6], (unsigned long long)hit);
       if (lane_id() == 0) {
         atomicAdd(&q[3], (unsigned long long)mx_it);
-        atomicAdd(&q[4], (unsigned long long)mx_blk);
-        atomicAdd(&q[5], (unsigned long long)mx_ld);
         atomicAdd(&q[7], 1ull);
+        unsigned long long* q6 = D.dbg + ((size_t)6 * kDiagMaxWg + wg) * kDiagStamps;
+        q6[2 * (threadIdx.x >> 6)] = d_t0;
+        q6[2 * (threadIdx.x >> 6) + 1] = __builtin_amdgcn_s_memrealtime();
       }
     }
   }
 #endif
 }
-template <int K>
-__global__ __launch_bounds__(256 * K) void k_raycast(EngineDev D, FrameParams P, float step_size, ViewGrid V,
-                                                     uchar4* __restrict__ rgba, uchar4* __restrict__ normal) {
+__global__ __launch_bounds__(256) void k_raycast(EngineDev D, FrameParams P, float step_size, ViewGrid V,
+                                                 uchar4* __restrict__ rgba, uchar4* __restrict__ normal) {
   extern __shared__ uint32_t sbits[];
-  raycast<K>(D, P, step_size, V, sbits, rgba, normal);
+  raycast(D, P, step_size, V, sbits, rgba, normal);
 }
-template <int K>
-__global__ __launch_bounds__(256 * K) void k_raycast_g(EngineDev D, const FrameArgs* __restrict__ A) {
+__global__ __launch_bounds__(256) void k_raycast_g(EngineDev D, const FrameArgs* __restrict__ A) {
   __shared__ uint32_t sbits[kViewGraphBitmapWords];
   const FrameParams R = A->R;
   const ViewGrid V = A->V;
-  raycast<K>(D, R, A->step_size, V, sbits, A->rgba, A->normal);
+  raycast(D, R, A->step_size, V, sbits, A->rgba, A->normal);
 }
-template __global__ void k_raycast<1>(EngineDev, FrameParams, float, ViewGrid, uchar4*, uchar4*);
-template __global__ void k_raycast<2>(EngineDev, FrameParams, float, ViewGrid, uchar4*, uchar4*);
-template __global__ void k_raycast<4>(EngineDev, FrameParams, float, ViewGrid, uchar4*, uchar4*);
-template __global__ void k_raycast_g<1>(EngineDev, const FrameArgs*);
-template __global__ void k_raycast_g<2>(EngineDev, const FrameArgs*);
-template __global__ void k_raycast_g<4>(EngineDev, const FrameArgs*);
 
 // download_tsdf_kernel (voxel_tsdf.cu:34-46): one workgroup of 512 threads per selected block
 __global__ __launch_bounds__(512) void k_query_download(EngineDev D, const VisRec* __restrict__ sel,

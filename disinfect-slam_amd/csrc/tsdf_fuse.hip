@@ -309,6 +309,29 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
   my_upd += __popc(upd_mask);
 }
 
+// The concatenated band lists: band i holds visible-block indices [start_i, start_i + count_i).
+// Lane i < kBands keeps start_i (one VGPR; an indexed array of 16 starts is spilled to scratch in
+// the big kernels), and the wave-uniform search for index b is a ballot: the starts are
+// non-decreasing, so the lanes with start <= b are a prefix and the band is its last lane.
+__device__ __forceinline__ int band_starts(const EngineDev& D, int lane, int* total) {
+  const int c = lane < kBands ? D.band[lane * kBandStride] : 0;
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < kBands; o <<= 1) {
+    const int n = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += n;
+  }
+  *total = __builtin_amdgcn_readlane(incl, kBands - 1);
+  return incl - c;
+}
+// (b wave-uniform, 0 <= b < total) -> the band's list record index: band * nblocks + offset
+__device__ __forceinline__ size_t band_find(const EngineDev& D, int bst, int lane, int b) {
+  const unsigned long long m = __ballot(lane < kBands && b >= bst);
+  const int bd = __popcll(m) - 1;
+  const int ofs = b - __builtin_amdgcn_readlane(bst, bd);
+  return (size_t)bd * D.nblocks + (size_t)__builtin_amdgcn_readfirstlane(ofs);
+}
+
 // 64 VGPRs: 8 waves per SIMD (65 without the bound: 7). Graph: the graph-captured form reads its
 // camera from the FrameArgs block the graph's first node uploads.
 // The visible blocks are the sweep's band lists (blocks that existed before the frame) followed by
@@ -342,14 +365,8 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
   // SALU / scalar loads instead of per-lane selects
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pair = wave >> 1, hf = wave & 1;
-  // concatenated band lists: band i holds visible-block indices [bstart_i, bstart_i + count_i)
-  int bstart[kBands];
   int nvis = 0;
-#pragma unroll
-  for (int i = 0; i < kBands; ++i) {
-    bstart[i] = nvis;
-    nvis += D.band[i * kBandStride];
-  }
+  const int bst = band_starts(D, lane, &nvis);
   const int nband = nvis;
   nvis += D.ctr->n_fresh;
   const int g = blockIdx.x & 7, ngrp = nint >> 3;
@@ -375,18 +392,11 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
       if (b >= nband) {
         r = D.fresh_vis[b - nband];
       } else {
-        int bd = 0, ofs = b;
-#pragma unroll
-        for (int i = 1; i < kBands; ++i)
-          if (b >= bstart[i]) {
-            bd = i;
-            ofs = b - bstart[i];
-          }
-        r = D.vis[(size_t)bd * D.nblocks + __builtin_amdgcn_readfirstlane(ofs)];
+        r = D.vis[band_find(D, bst, lane, b)];
       }
       update_block<Raw>(D, P, r, lane, hf, mn, my_upd);
     }
-    mn = wave_min(mn);
+    mn = wave_min_u(mn);
     if (lane == 0) s_min[wave] = mn;
     lds_barrier();  // (LDS only: this pair's pool stores stay in flight)
     if (hf == 0 && lane == 0 && b < nvis) {
@@ -546,6 +556,7 @@ __device__ void pipe_head(const EngineDev& D, const FrameParams& Pu, const PipeA
   if (t == 0 && A.cands_out && A.has_alloc) st_co(&D.ctr->n_pend, 0);
   drain_barrier();
   publish_flags(D.pipe + kPipeCarved, A.tag);
+  TSDF_STAMP_WG(D, 8, 0, 3);
   if (A.has_alloc) {
     if (t == 0) {  // frame fid_alloc's ingest span (last launch): allocation flag -> last tile / sweep end
       unsigned long long* ie = D.pipe + kPipeIngEnd + 16 * (A.fid_alloc & 1u);
@@ -558,6 +569,7 @@ __device__ void pipe_head(const EngineDev& D, const FrameParams& Pu, const PipeA
   drain_barrier();
   const unsigned long long t_pub = __builtin_amdgcn_s_memrealtime();
   publish_flags(D.pipe + kPipeAlloc, A.tag);
+  TSDF_STAMP_WG(D, 8, 0, 4);
   if (t == 0) D.pipe[kPipeAPub + 16 * (A.fid_new & 1u)] = t_pub;
   if (A.has_carve) pipe_frame_stats(D, A.fid_carve);  // off the chain
 }
@@ -568,12 +580,17 @@ __device__ void pipe_head(const EngineDev& D, const FrameParams& Pu, const PipeA
 // after its flag. Frame b - 1's carve candidates among the listed blocks (ctag) are deferred to the
 // end of the workgroup's work, after the carving flag, and updated unless the carving released them
 // (rtag); more than kPipeDefer of them: the workgroup waits for the carving at once.
+// The work alternates between collecting up to kPipeList records into LDS (the list walk, the tag
+// tests, the waits) and updating them in a loop that does nothing else: the walk's scalar state then
+// stays out of the update loop, whose scalar registers are the camera and the pool's (in one loop the
+// two spilled ~230 SGPRs to VGPR lanes, read back in every block's update).
 __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const PipeArgs& A, int kind, int wi) {
   __shared__ float s_min[4];
   __shared__ int s_upd[4], s_vis[4];
   __shared__ int s_ncand;
   __shared__ VisRec s_cand[kIntegrateCandBuf];  // this workgroup's carve candidates
   __shared__ VisRec s_def[kPipeDefer];          // deferred (candidate of frame b - 1) blocks
+  __shared__ VisRec s_list[kPipeList];          // the records of one collection
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pair = wave >> 1, hf = wave & 1;
@@ -582,14 +599,10 @@ __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const Pip
   if (threadIdx.x == 0) s_ncand = 0;  // (ordered before its first use by the loop's barriers)
   if (kind == 0 && wi == 0 && threadIdx.x == 0)  // the update's device-clock start
     st_co(Db.pipe + kPipeT0 + 16 * (fb & 1u), (unsigned long long)__builtin_amdgcn_s_memrealtime());
-  int bstart[kBands];
+  int bst = 0;
   int nvis = 0, nband = 0, p, p_hi, pstep;
   if (kind == 0) {
-#pragma unroll
-    for (int i = 0; i < kBands; ++i) {
-      bstart[i] = nvis;
-      nvis += Db.band[i * kBandStride];
-    }
+    bst = band_starts(Db, lane, &nvis);
     nband = nvis;
     if (A.fresh_ready) nvis += Db.ctr->n_fresh;
     // group g = blockIdx % 8 (one XCD) takes the g-th contiguous eighth of the pairs in band order
@@ -598,8 +611,6 @@ __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const Pip
     p_hi = (int)(((long long)npairs * (g + 1)) >> 3);
     pstep = A.nint >> 3;
   } else {
-#pragma unroll
-    for (int i = 0; i < kBands; ++i) bstart[i] = 0;
     wait_tag(Db.pipe + kPipeAlloc + (blockIdx.x & 7) * 16, A.tag, &Db.ctr->status);
     nvis = ld_co(&Db.ctr->n_fresh);
     p = wi;
@@ -610,14 +621,7 @@ __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const Pip
   const uint32_t* ct = Db.ctag + (size_t)(A.fid_carve & 1u) * Db.nblocks;
   auto fetch = [&](int b) -> VisRec {
     if (b >= nband) return kind ? ld_rec_co(&Db.fresh_vis[b - nband]) : Db.fresh_vis[b - nband];
-    int bd = 0, ofs = b;
-#pragma unroll
-    for (int i = 1; i < kBands; ++i)
-      if (b >= bstart[i]) {
-        bd = i;
-        ofs = b - bstart[i];
-      }
-    return Db.vis[(size_t)bd * Db.nblocks + __builtin_amdgcn_readfirstlane(ofs)];
+    return Db.vis[band_find(Db, bst, lane, b)];
   };
   // a candidate of frame b - 1 the carving has run for: kept unless released (one lane's atomic read:
   // rtag was written through by workgroup 0 on another XCD)
@@ -627,75 +631,81 @@ __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const Pip
       v = __hip_atomic_fetch_or(&Db.rtag[r.idx], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return (uint32_t)__builtin_amdgcn_readfirstlane(v) != A.fid_carve;
   };
-  int my_upd = 0, my_vis = 0, ndef = 0, dpos = 0;
-  bool phase1 = false, carved_known = false;
-  for (;;) {  // (all control flow below is workgroup-uniform)
-    VisRec r{};
-    bool have = false;
-    if (!phase1) {
-      if (p >= p_hi) {
-        if (ndef == 0) break;
-        if (!carved_known) wait_tag(carved, A.tag, &Db.ctr->status);  // (its barrier publishes s_def)
-        else lds_barrier();
-        carved_known = true;
-        phase1 = true;
-        continue;
-      }
-      const int b0 = 2 * p;
-      const VisRec r0 = b0 < nvis ? fetch(b0) : VisRec{}, r1 = b0 + 1 < nvis ? fetch(b0 + 1) : VisRec{};
-      const bool t0 = chk && b0 < nvis && r0.pad == 0 && ct[r0.idx] == A.fid_carve;
-      const bool t1 = chk && b0 + 1 < nvis && r1.pad == 0 && ct[r1.idx] == A.fid_carve;
-      r = pair ? r1 : r0;
-      const bool mine_t = pair ? t1 : t0;
-      have = b0 + pair < nvis;
-      if (t0 || t1) {
-        const int nt = (int)t0 + (int)t1;
-        if (!carved_known && ndef + nt <= kPipeDefer) {  // deferred to the end
-          if (threadIdx.x == 0) {
-            if (t0) s_def[ndef] = r0;
-            if (t1) s_def[ndef + (int)t0] = r1;
+  int my_upd = 0, my_vis = 0, ndef = 0;
+  bool carved_known = false, def_done = false;
+  for (;;) {  // (all control flow below is workgroup-uniform; thread 0 writes the LDS lists)
+    // ---- collect: the next records of the list walk, or (at its end) the deferred ones
+    int n = 0;
+    auto add = [&](const VisRec& r) {
+      if (threadIdx.x == 0) s_list[n] = r;
+      ++n;
+    };
+    if (p < p_hi) {
+      while (p < p_hi && n + 2 <= kPipeList) {
+        const int b0 = 2 * p;  // (< nvis)
+        const bool two = b0 + 1 < nvis;
+        const VisRec r0 = fetch(b0), r1 = two ? fetch(b0 + 1) : VisRec{};
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          if (e == 1 && !two) break;
+          const VisRec& r = e ? r1 : r0;
+          if (chk && r.pad == 0 && ct[r.idx] == A.fid_carve) {
+            if (!carved_known && ndef < kPipeDefer) {  // deferred to the end
+              if (threadIdx.x == 0) s_def[ndef] = r;
+              ++ndef;
+              continue;
+            }
+            if (!carved_known) wait_tag(carved, A.tag, &Db.ctr->status);
+            carved_known = true;
+            if (!kept(r)) continue;
           }
-          ndef += nt;
-          have = have && !mine_t;
-        } else {
-          if (!carved_known) wait_tag(carved, A.tag, &Db.ctr->status);
-          carved_known = true;
-          if (have && mine_t) have = kept(r);
+          add(r);
         }
+        p += pstep;
       }
-      p += pstep;
+    } else if (ndef > 0 && !def_done) {
+      if (!carved_known) wait_tag(carved, A.tag, &Db.ctr->status);  // (its barrier publishes s_def)
+      else lds_barrier();
+      carved_known = true;
+      for (int d = 0; d < ndef; ++d) {
+        const VisRec r = s_def[d];
+        if (kept(r)) add(r);
+      }
+      def_done = true;
     } else {
-      if (dpos >= ndef) break;
-      const int d = dpos + pair;
-      dpos += 2;
-      if (d < ndef) {
-        r = s_def[d];
-        have = kept(r);
+      break;
+    }
+    lds_barrier();  // (publishes s_list)
+    // ---- update: the two pairs of waves take records 2 j + pair
+    for (int j = 0; 2 * j < n; ++j) {
+      const int k = 2 * j + pair;
+      const bool have = k < n;
+      VisRec r{};
+      float mn = __builtin_inff();
+      if (have) {
+        r = s_list[k];
+        update_block<false>(Db, P, r, lane, hf, mn, my_upd);
+        my_vis += hf == 0 ? 1 : 0;
       }
-    }
-    float mn = __builtin_inff();
-    if (have) {
-      update_block<false>(Db, P, r, lane, hf, mn, my_upd);
-      my_vis += hf == 0 ? 1 : 0;
-    }
-    mn = wave_min(mn);
-    if (lane == 0) s_min[wave] = mn;
-    lds_barrier();  // (LDS only: this pair's pool stores stay in flight)
-    if (hf == 0 && lane == 0 && have) {
-      const float m2 = fminf(s_min[wave], s_min[wave + 1]);
-      if (m2 >= 0.9f) {  // space_carving_kernel threshold (voxel_tsdf.cu:227, :485)
-        Db.ctag[(size_t)(fb & 1u) * Db.nblocks + r.idx] = fb;  // (read by the next launch's update)
-        const int k = atomicAdd(&s_ncand, 1);
-        if (k < kIntegrateCandBuf) {
-          s_cand[k] = r;
-        } else {  // buffer full (heavy carving): this one now
-          const int kg = atomicAdd(Db.ncand, 1);
-          if (kg < Db.cand_cap) st_rec_co(&Db.cand[kg], r);
-          else atomicOr(&Db.ctr->status, 16u);  // (a list longer than the pool: internal error)
+      mn = wave_min_u(mn);
+      if (lane == 0) s_min[wave] = mn;
+      lds_barrier();  // (LDS only: this pair's pool stores stay in flight)
+      if (hf == 0 && lane == 0 && have) {
+        const float m2 = fminf(s_min[wave], s_min[wave + 1]);
+        if (m2 >= 0.9f) {  // space_carving_kernel threshold (voxel_tsdf.cu:227, :485)
+          Db.ctag[(size_t)(fb & 1u) * Db.nblocks + r.idx] = fb;  // (read by the next launch's update)
+          const int kc = atomicAdd(&s_ncand, 1);
+          if (kc < kIntegrateCandBuf) {
+            s_cand[kc] = r;
+          } else {  // buffer full (heavy carving): this one now
+            const int kg = atomicAdd(Db.ncand, 1);
+            if (kg < Db.cand_cap) st_rec_co(&Db.cand[kg], r);
+            else atomicOr(&Db.ctr->status, 16u);  // (a list longer than the pool: internal error)
+          }
         }
       }
+      lds_barrier();
     }
-    lds_barrier();
   }
   // the workgroup's carve candidates (read by the next launch's carving) and statistics
   const int tot = wave_sum(my_upd);
@@ -736,34 +746,42 @@ __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const Pip
 // grid: kPipeHead head workgroups (0: carving + allocation), A.nint update workgroups (listed blocks),
 // kPipeFreshWG (this launch's new blocks), then frame c's A.tiles pixel tiles and kVisWorkgroups
 // sweep workgroups -- each part only when the launch has it
-__device__ __forceinline__ void frame_body(const EngineDev& D, const FrameParams& Pu, const FrameParams& Pn,
-                                           const PipeArgs& A, FrameLds& U) {
+// (diagnostic build: each workgroup's part code, start and end into D.dbg kernel 8 -- 1 head, 2 fresh
+// update, 3 listed update, 4 tile, 5 sweep; the head's carving / allocation ends at 3 / 4)
+__device__ __forceinline__ void frame_part(const EngineDev& D, const FrameParams& Pu, const FrameParams& Pn,
+                                           const PipeArgs& A, FrameLds& U, int& code) {
   int w = (int)blockIdx.x;
   if (w < kPipeHead) {
-    if (w == 0) pipe_head(D, Pu, A, U);
+    if (w == 0) {
+      code = 1;
+      pipe_head(D, Pu, A, U);
+    }
     return;
   }
   w -= kPipeHead;
   const int nfr = A.has_update && !A.fresh_ready ? kPipeFreshWG : 0;
   if (w < nfr) {  // the blocks this launch's allocation creates (they wait for it: dispatched early)
+    code = 2;
     pipe_update(frame_view(D, A.fid_alloc), Pu, A, 1, w);
     return;
   }
   w -= nfr;
   // the other parts in the launch's grid order: update (u), tiles (t), sweep (s)
   const int nold = A.has_update ? A.nint : 0, ns = A.has_frame ? kVisWorkgroups : 0;
-  const int n[3] = {nold, A.tiles, ns};
+  // (order r runs the parts r, r + 1, r + 2 mod 3; scalar selects, no indexed arrays: those live in
+  // scratch)
   int part = -1, o = w;
-  const int seq[3][3] = {{0, 1, 2}, {1, 2, 0}, {2, 0, 1}};
   for (int k = 0; k < 3; ++k) {
-    const int q = seq[A.order][k];
-    if (o < n[q]) {
+    const int q = (A.order + k) % 3;
+    const int nq = q == 0 ? nold : (q == 1 ? A.tiles : ns);
+    if (o < nq) {
       part = q;
       break;
     }
-    o -= n[q];
+    o -= nq;
   }
   if (part < 0) return;  // (a graph's grid is sized for the largest launch)
+  code = 3 + part;
   if (part == 0) {
     // (its XCD split takes o % 8 as the XCD: exact when the parts before it are multiples of 8 long,
     // as at 640x480; correct either way)
@@ -778,6 +796,24 @@ __device__ __forceinline__ void frame_body(const EngineDev& D, const FrameParams
     vis_sweep_chained<1024>(frame_view(D, A.fid_new), Pn, o, U.ing, aflag, A.tag);
   if (threadIdx.x == 0)  // the ingest's span ends with its last workgroup
     atomicMax(D.pipe + kPipeIngEnd + 16 * (A.fid_new & 1u), (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void frame_body(const EngineDev& D, const FrameParams& Pu, const FrameParams& Pn,
+                                           const PipeArgs& A, FrameLds& U) {
+#ifdef TSDF_DIAG_STAMPS
+  const unsigned long long d_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  int code = 0;
+  frame_part(D, Pu, Pn, A, U, code);
+#ifdef TSDF_DIAG_STAMPS
+  if (threadIdx.x == 0 && D.dbg && blockIdx.x < (unsigned)kDiagMaxWg) {
+    unsigned long long* q = D.dbg + ((size_t)8 * kDiagMaxWg + blockIdx.x) * kDiagStamps;
+    q[0] = (unsigned long long)code;
+    q[1] = d_t0;
+    q[2] = __builtin_amdgcn_s_memrealtime();
+  }
+#else
+  (void)code;
+#endif
 }
 __global__ __launch_bounds__(kIntegrateThreads)
 __attribute__((amdgpu_waves_per_eu(TSDF_FRAME_WAVES, TSDF_FRAME_WAVES))) void k_frame(

@@ -6,7 +6,7 @@
 namespace tsdf {
 
 // diagnostic stamp buffer geometry (tsdf_debug_stamps, TSDF_STAMP in tsdf_block.h)
-constexpr int kDiagKernels = 8, kDiagMaxWg = 4096, kDiagStamps = 8;
+constexpr int kDiagKernels = 9, kDiagMaxWg = 4096, kDiagStamps = 8;
 
 // visible-block lists: one per horizontal image band of the block centre's projection, so the
 // integrate kernel can hand each XCD a contiguous, spatially compact slice (its pixel gathers stay
@@ -82,7 +82,7 @@ constexpr int kViewBitmapWords = (kViewMaxN / 4) * (kViewMaxN / 4) * (kViewMaxN 
                                  (kViewMaxN / 16) * (kViewMaxN / 16) * (kViewMaxN / 16) / 32;
 constexpr int kViewGraphBitmapWords = 4608;       // LDS bitmap words of the graph's raycast node
 struct ViewGrid {
-  uint32_t* cell;          // n^3: gen << kViewIdxBits | pool index
+  uint32_t* cell;          // nb^3 bricks x 64 cells, brick-major: gen << kViewIdxBits | pool index
   uint8_t* flags;          // kViewBitmapWords * 32 bytes: brick / superbrick occupied (1), word w's bits
                            // at bytes [32 w, 32 w + 32); zero between calls (k_view_pack clears them)
   uint32_t* bits;          // the packed bitmaps: nb^3 brick bits, then ns^3 superbrick bits
@@ -90,6 +90,11 @@ struct ViewGrid {
   int nbw, nw;             // brick words, all bitmap words
   uint32_t gen;
 };
+// cell of block (lx, ly, lz) of the grid in brick k: the 4x4x4 cells of a brick are one 256-B run, so
+// the blocks a ray bundle meets in one brick share cache lines
+__device__ __forceinline__ size_t view_cell(int k, int lx, int ly, int lz) {
+  return ((size_t)k << 6) | (uint32_t)(((lz & 3) << 4) | ((ly & 3) << 2) | (lx & 3));
+}
 // origin (block coordinates) of the view grid of camera centre wt: both kernels compute it alike
 __device__ __forceinline__ int view_origin(float wt, float voxel, int half) {
   return (f2i(floorf(wt / voxel)) >> kBlockLenBits) - half;
@@ -112,6 +117,7 @@ constexpr int kPipeWords = kPipeStats + 2 * kPipeStatLines * 16;
 constexpr int kPipeHead = 8;                    // workgroups before the update's (0: carving + allocation)
 constexpr int kPipeFreshWG = 64;                // workgroups that update the blocks allocated in the launch
 constexpr int kPipeDefer = 32;                  // deferred (carve-pending) blocks one update workgroup holds
+constexpr int kPipeList = 64;                   // records one update workgroup collects before updating them
 // What one k_frame launch does. Frame ids f are engine-wide (1, 2, ...); frame b's update, frame
 // b - 1's carving and frame c = b + 1's ingest share the launch (any part may be absent).
 struct PipeArgs {
@@ -207,7 +213,6 @@ __global__ void k_frame_g(EngineDev D, const FrameArgs* FA);
 // graph-captured forms of the frame kernels: identical bodies, arguments from FrameArgs
 template <int TS>
 __global__ void k_ingest_dda_g(EngineDev D, const FrameArgs* A);
-template <int K>  // K lanes per ray (tsdf_extract.hip), workgroups of 256 K threads
 __global__ void k_raycast_g(EngineDev D, const FrameArgs* A);
 // cands_in: optional inbox of nshard carve-candidate slots (then recs / count are D.cand / n_cand)
 __global__ void k_resolve_delete(EngineDev D, const VisRec* recs, const int32_t* count, int direct,
@@ -232,7 +237,6 @@ template <bool Emit>
 __global__ void k_mesh(EngineDev D, const VisRec* sel, MeshParams M, int32_t* counts,
                        const int32_t* offsets, float* out);
 __global__ void k_scan_counts(const int32_t* counts, int n, int32_t* offsets, int64_t* total);
-template <int K>
 __global__ void k_raycast(EngineDev D, FrameParams P, float step_size, ViewGrid V, uchar4* rgba,
                           uchar4* normal);
 // view grid of a raycast: grid kOccWords / 256 workgroups of 256

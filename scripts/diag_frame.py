@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Per-part timeline of the pipelined frame kernel k_frame from the DIAG=1 library (diagnostic only).
+
+Usage (GPU box): TSDF_AMD_LIB=disinfect-slam_amd/libdisinfect_tsdf_diag.so python scripts/diag_frame.py
+The driver's workload (bench.py C3: 640x480, frames 0-24, the first five warm-up): after each
+tsdf_integrate (one k_frame) the stamps of every workgroup -- part, start, end (D.dbg kernel 8) --
+relative to the launch's first workgroup start, in microseconds, as medians over the launches.
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "disinfect-slam_amd"))
+NK, NWG, NS = 9, 4096, 8
+PARTS = {1: "head", 2: "fresh update", 3: "listed update", 4: "tiles", 5: "sweep"}
+
+
+def main():
+    import ctypes as C
+    import torch
+    import tsdf_amd
+    from tsdf_amd import _lib, synth
+
+    L = _lib.load()
+    dev = torch.device("cuda", 0)
+    cam = synth.camera(640, 480, synth.TUM_FR1)
+    nfr = 25
+    fr = synth.render_torch(cam, list(range(nfr)), device=dev)
+    torch.cuda.synchronize()
+    eng = tsdf_amd.Engine(0.005, 0.03, max_width=640, max_height=480, num_block_bits=18,
+                          device=0, stream=torch.cuda.current_stream().cuda_stream)
+    en = C.c_int(0)
+    L.tsdf_debug_stamps(eng._h, None, 0, C.byref(en))
+    if not en.value:
+        raise SystemExit("library built without TSDF_DIAG_STAMPS")
+    buf = np.zeros(NK * NWG * NS, np.uint64)
+    rows = {k: [] for k in PARTS}
+    head = []
+    for i in range(nfr):
+        torch.cuda.synchronize()
+        L.tsdf_debug_stamps(eng._h, buf.ctypes.data, buf.size, None)  # (clears)
+        eng.integrate(fr["rgb"][i], fr["depth"][i], fr["ht"][i], fr["lt"][i], cam.K,
+                      tsdf_amd.SE3(fr["q"][i], fr["t"][i]), 4.0)
+        torch.cuda.synchronize()
+        L.tsdf_debug_stamps(eng._h, buf.ctypes.data, buf.size, None)
+        if i < 6:
+            continue
+        S = buf.reshape(NK, NWG, NS)[8].astype(np.int64)
+        ok = S[:, 0] > 0
+        if not ok.any():
+            continue
+        t0 = S[ok, 1].min()
+        for k in PARTS:
+            m = S[:, 0] == k
+            if m.any():
+                st, en_ = (S[m, 1] - t0) * 1e-2, (S[m, 2] - t0) * 1e-2
+                rows[k].append((m.sum(), np.median(st), st.max(), np.median(en_), np.percentile(en_, 90),
+                                en_.max(), np.median(en_ - st)))
+        h = S[0]
+        if h[0] == 1:
+            head.append(((h[3] - t0) * 1e-2 if h[3] else np.nan, (h[4] - t0) * 1e-2 if h[4] else np.nan,
+                         (h[2] - t0) * 1e-2))
+    print("k_frame part timeline, us from the launch's first workgroup start (medians over launches)")
+    print(f"{'part':>14} {'WGs':>5} {'start p50':>9} {'start max':>9} {'end p50':>8} {'end p90':>8} "
+          f"{'end max':>8} {'dur p50':>8}")
+    for k, name in PARTS.items():
+        if rows[k]:
+            a = np.median(np.array(rows[k], dtype=float), axis=0)
+            print(f"{name:>14} {a[0]:5.0f} {a[1]:9.1f} {a[2]:9.1f} {a[3]:8.1f} {a[4]:8.1f} {a[5]:8.1f} {a[6]:8.1f}")
+    if head:
+        a = np.nanmedian(np.array(head), axis=0)
+        print(f"head: carving published {a[0]:.1f}, allocation published {a[1]:.1f}, head end {a[2]:.1f}")
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

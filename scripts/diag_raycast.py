@@ -12,7 +12,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "disinfect-slam_amd"))
-NK, NWG, NS = 8, 4096, 8
+NK, NWG, NS = 9, 4096, 8
 
 
 def main():
@@ -50,7 +50,7 @@ def main():
         rays, waves = 640 * 480, int(q[7])
         print(f"frame {i}: waves {waves} hits {q[6]} / {rays}")
         print(f"  per ray : iterations {q[0] / rays:7.1f}  block lookups {q[1] / rays:6.1f}  voxel reads {q[2] / rays:6.1f}")
-        print(f"  per wave: iterations {q[3] / waves:7.1f}  with a lookup {q[4] / waves:6.1f}  with a read {q[5] / waves:6.1f}")
+        print(f"  per wave: iterations {q[3] / waves:7.1f}")
         # per-wave lifetimes (kernel 6 stamps: wave w of workgroup wg at 2w / 2w + 1)
         S6 = buf.reshape(NK, NWG, NS)[6].astype(np.int64)
         nwg = 40 * 30

@@ -20,7 +20,7 @@ KERNELS = {0: ("ingest", ["lds_init", "pix_write", "dda", "barrier", "sweep"]),
            4: ("resolve_delete", ["sum+prepare", "rounds"]),
            6: ("ingest_tail", ["resolve", "ticks"]),
            7: ("integrate_tail", ["carve", "stats"])}
-NK, NWG, NS = 8, 4096, 8
+NK, NWG, NS = 9, 4096, 8
 ORDER = [2, 0, 1, 6, 3, 4, 7]  # dispatch / execution order of the stamped phases
 
 

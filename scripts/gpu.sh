@@ -10,9 +10,11 @@
 #                     (scripts/profile_integrate.sh; summary + pmc_entry.json under <tag>/prof_driver)
 #   default           bench.py (300 timed frames, CPU baseline)
 #   c5 | c5graph | c4 | c2 | graph   bench.py --loop c5 [--graph] / 1280x720 / --depth-only / --graph
+#   c5tests           the raycast / render / C5 GPU tests
 #   shard8            bench.py --width 1280 --height 720 --shard 8 (single-GPU 8-shard rehearsal)
 #   sq:<kernel>       SQ counter passes of one kernel on the default command (profile_kernel_sq.sh)
-#   stamps            per-workgroup chain stamps (diagnostic library, scripts/diag_chain.py)
+#   raydiag           raycast step statistics and wave lifetimes (diagnostic library, scripts/diag_raycast.py)
+#   framediag         k_frame per-part timeline (diagnostic library, scripts/diag_frame.py)
 #   ab:<lib1>,<lib2>  interleaved A/B of engine builds on the driver command (scripts/ab.sh)
 set -uo pipefail
 TAG=${1:?tag}; shift
@@ -54,12 +56,16 @@ for st in "$@"; do
            line $OUT/bench_c4.json ;;
     c2) timeout -k 10 300 python3 bench.py --no-cpu --depth-only > $OUT/bench_c2.json 2> $OUT/bench_c2.err || fail $st $OUT/bench_c2.err
            line $OUT/bench_c2.json ;;
+    c5tests) timeout -k 10 600 $PYT tests/test_gpu_c5.py tests/test_gpu_render.py tests/test_gpu_parity.py tests/test_gpu_golden.py tests/test_gpu_graph.py -m gpu > $OUT/pytest_c5.log 2>&1 || fail $st $OUT/pytest_c5.log
+           tail -1 $OUT/pytest_c5.log ;;
     shard8) timeout -k 10 300 python3 bench.py --no-cpu --steps 100 --width 1280 --height 720 --shard 8 > $OUT/shard8_c4.json 2> $OUT/shard8_c4.err || fail $st $OUT/shard8_c4.err
            line $OUT/shard8_c4.json ;;
     sq:*) k=${st#sq:}; bash scripts/profile_kernel_sq.sh $OUT/sq_$k $k > $OUT/sq_$k.txt 2>&1 || fail $st $OUT/sq_$k.txt
            tail -8 $OUT/sq_$k.txt ;;
-    stamps) TSDF_AMD_LIB=disinfect-slam_amd/libdisinfect_tsdf_diag.so timeout -k 10 120 python3 scripts/diag_chain.py > $OUT/chain_stamps.txt 2>&1 || fail $st $OUT/chain_stamps.txt
-           tail -20 $OUT/chain_stamps.txt ;;
+    raydiag) TSDF_AMD_LIB=disinfect-slam_amd/libdisinfect_tsdf_diag.so timeout -k 10 180 python3 scripts/diag_raycast.py > $OUT/raycast_diag.txt 2>&1 || fail $st $OUT/raycast_diag.txt
+           tail -12 $OUT/raycast_diag.txt ;;
+    framediag*) e=${st#framediag}; e=${e#:}; env ${e:+$e} TSDF_AMD_LIB=disinfect-slam_amd/libdisinfect_tsdf_diag.so timeout -k 10 120 python3 scripts/diag_frame.py > $OUT/frame_diag${e:+_$e}.txt 2>&1 || fail $st $OUT/frame_diag${e:+_$e}.txt
+           tail -9 $OUT/frame_diag${e:+_$e}.txt ;;
     ab:*) IFS=, read -ra LIBS <<< "${st#ab:}"; bash scripts/ab.sh 20 "${LIBS[@]}" || exit 1 ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
