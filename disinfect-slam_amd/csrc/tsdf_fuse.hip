@@ -45,11 +45,13 @@ __device__ void frame_end(const EngineDev& D) {
 // a shard's frame: its carve candidates into the exchange slot, then the owned entries its
 // exhausted pool left without voxels this frame (D.pend, written by the allocation resolver before
 // this launch)
-__device__ void pack_cands_wg(const EngineDev& D, ShardRec* __restrict__ out, int cap) {
-  const int nc = ld_co(D.ncand);
+// (cand / ncand: the frame's candidate list, D.cand / D.ncand of its view)
+__device__ void pack_cands_wg(const EngineDev& D, const VisRec* cand, const int32_t* ncand, ShardRec* __restrict__ out,
+                              int cap) {
+  const int nc = ld_co(ncand);
   const int np = min(ld_co(&D.ctr->n_pend), (int)kNewKeyCap);
   const int n = nc + np;
-  const unsigned long long* rq = reinterpret_cast<const unsigned long long*>(D.cand);
+  const unsigned long long* rq = reinterpret_cast<const unsigned long long*>(cand);
   for (int i = threadIdx.x; i < min(n, cap); i += blockDim.x) {
     unsigned long long a, b;
     if (i < nc) {
@@ -111,7 +113,7 @@ __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FramePa
   const unsigned long long tend = __builtin_amdgcn_s_memrealtime();  // the update's span ends here
   TSDF_STAMP(D, 7, 0);
   if (P.tail == kTailPack)
-    pack_cands_wg(D, P.slot, P.slot_cap);
+    pack_cands_wg(D, D.cand, D.ncand, P.slot, P.slot_cap);
   else
     resolve_delete_wg(D, D.cand, D.ncand, 0, L);
   TSDF_STAMP(D, 7, 1);
@@ -313,8 +315,8 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
 // Lane i < kBands keeps start_i (one VGPR; an indexed array of 16 starts is spilled to scratch in
 // the big kernels), and the wave-uniform search for index b is a ballot: the starts are
 // non-decreasing, so the lanes with start <= b are a prefix and the band is its last lane.
-__device__ __forceinline__ int band_starts(const EngineDev& D, int lane, int* total) {
-  const int c = lane < kBands ? D.band[lane * kBandStride] : 0;
+__device__ __forceinline__ int band_starts_p(const int32_t* band, int lane, int* total) {
+  const int c = lane < kBands ? band[lane * kBandStride] : 0;
   int incl = c;
 #pragma unroll
   for (int o = 1; o < kBands; o <<= 1) {
@@ -324,12 +326,18 @@ __device__ __forceinline__ int band_starts(const EngineDev& D, int lane, int* to
   *total = __builtin_amdgcn_readlane(incl, kBands - 1);
   return incl - c;
 }
+__device__ __forceinline__ int band_starts(const EngineDev& D, int lane, int* total) {
+  return band_starts_p(D.band, lane, total);
+}
 // (b wave-uniform, 0 <= b < total) -> the band's list record index: band * nblocks + offset
-__device__ __forceinline__ size_t band_find(const EngineDev& D, int bst, int lane, int b) {
+__device__ __forceinline__ size_t band_find_n(int nblocks, int bst, int lane, int b) {
   const unsigned long long m = __ballot(lane < kBands && b >= bst);
   const int bd = __popcll(m) - 1;
   const int ofs = b - __builtin_amdgcn_readlane(bst, bd);
-  return (size_t)bd * D.nblocks + (size_t)__builtin_amdgcn_readfirstlane(ofs);
+  return (size_t)bd * nblocks + (size_t)__builtin_amdgcn_readfirstlane(ofs);
+}
+__device__ __forceinline__ size_t band_find(const EngineDev& D, int bst, int lane, int b) {
+  return band_find_n(D.nblocks, bst, lane, b);
 }
 
 // 64 VGPRs: 8 waves per SIMD (65 without the bound: 7). Graph: the graph-captured form reads its
@@ -534,22 +542,24 @@ union FrameLds {
   IngestLds<1024> ing;
 };
 
-__device__ void merge_cands_inbox(const EngineDev& D, const ShardRec* __restrict__ cands_in, int cap, int nshard,
-                                  int* s_base);
+__device__ void merge_cands_inbox(const EngineDev& D, VisRec* cand, int32_t* ncand, const ShardRec* __restrict__ cands_in,
+                                  int cap, int nshard, int* s_base);
 
 // workgroup 0: frame fid_carve's carving, then frame fid_alloc's allocation, each published. A shard's
 // pipelined frame first lists every shard's candidates of fid_carve (the all-gathered inbox).
 __device__ void pipe_head(const EngineDev& D, const FrameParams& Pu, const PipeArgs& A, FrameLds& U) {
   __shared__ int s_base[kMaxShards + 1];
   const int t = threadIdx.x;
-  if (A.has_carve) {
-    const EngineDev Dk = frame_view(D, A.fid_carve);
-    if (A.cands_in) merge_cands_inbox(Dk, A.cands_in, A.cand_cap, A.nshard, s_base);
-    resolve_delete_wg(Dk, Dk.cand, Dk.ncand, 0, U.del, A.fid_carve, A.has_alloc ? A.fid_alloc : 0u);
+  if (A.has_carve) {  // (the view's pointers as scalars: a copied EngineDev view can land in scratch)
+    const uint32_t f = A.fid_carve;
+    VisRec* cand = D.cand + (size_t)(f & 1u) * (size_t)D.cand_cap;
+    int32_t* ncand = reinterpret_cast<int32_t*>(D.pipe + kPipeNCand + 16 * (f & 1u));
+    if (A.cands_in) merge_cands_inbox(D, cand, ncand, A.cands_in, A.cand_cap, A.nshard, s_base);
+    resolve_delete_wg(D, cand, ncand, 0, U.del, f, A.has_alloc ? A.fid_alloc : 0u);
     lds_barrier();
     // the carved frame's candidate count and band counts start empty for frame fid_carve + 2 / + 3
-    if (t < kBands) st_co(&Dk.band[t * kBandStride], 0);
-    if (t == 0) st_co(Dk.ncand, 0);
+    if (t < kBands) st_co(&D.band[(size_t)(f % 3u) * kBands * kBandStride + t * kBandStride], 0);
+    if (t == 0) st_co(ncand, 0);
   }
   // (a shard: the owned entries this launch's allocation leaves without voxels are listed from here;
   // without an allocation the list is the last one's, packed by this launch's update)
@@ -584,7 +594,16 @@ __device__ void pipe_head(const EngineDev& D, const FrameParams& Pu, const PipeA
 // tests, the waits) and updating them in a loop that does nothing else: the walk's scalar state then
 // stays out of the update loop, whose scalar registers are the camera and the pool's (in one loop the
 // two spilled ~230 SGPRs to VGPR lanes, read back in every block's update).
-__device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const PipeArgs& A, int kind, int wi) {
+// a candidate of frame fc the carving has run for: kept unless released (one lane's atomic read: rtag
+// was written through by workgroup 0 on another XCD)
+__device__ __forceinline__ bool pipe_kept(uint32_t* rtag, int32_t idx, uint32_t fc, int lane) {
+  uint32_t v = 0u;
+  if (lane == 0) v = __hip_atomic_fetch_or(&rtag[idx], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (uint32_t)__builtin_amdgcn_readfirstlane(v) != fc;
+}
+// (D: the base view; frame b's lists are addressed through scalar pointers here -- an EngineDev view
+// copied by value, or captured by reference in a lambda, can be materialised in scratch)
+__device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParams& P, const PipeArgs& A, int kind, int wi) {
   __shared__ float s_min[4];
   __shared__ int s_upd[4], s_vis[4];
   __shared__ int s_ncand;
@@ -594,82 +613,82 @@ __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const Pip
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pair = wave >> 1, hf = wave & 1;
-  const uint32_t fb = A.fid_alloc;
-  const unsigned long long* carved = Db.pipe + kPipeCarved + (blockIdx.x & 7) * 16;
-  if (threadIdx.x == 0) s_ncand = 0;  // (ordered before its first use by the loop's barriers)
-  if (kind == 0 && wi == 0 && threadIdx.x == 0)  // the update's device-clock start
-    st_co(Db.pipe + kPipeT0 + 16 * (fb & 1u), (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  const bool t0 = threadIdx.x == 0;
+  const uint32_t fb = A.fid_alloc, fc = A.fid_carve;
+  // frame b's view (frame_view)
+  const VisRec* vis = D.vis + (size_t)(fb & 1u) * kBands * (size_t)D.nblocks;
+  VisRec* cand = D.cand + (size_t)(fb & 1u) * (size_t)D.cand_cap;
+  int32_t* ncand = reinterpret_cast<int32_t*>(D.pipe + kPipeNCand + 16 * (fb & 1u));
+  const unsigned long long* carved = D.pipe + kPipeCarved + (blockIdx.x & 7) * 16;
+  if (t0) s_ncand = 0;  // (ordered before its first use by the loop's barriers)
+  if (kind == 0 && wi == 0 && t0)  // the update's device-clock start
+    st_co(D.pipe + kPipeT0 + 16 * (fb & 1u), (unsigned long long)__builtin_amdgcn_s_memrealtime());
   int bst = 0;
-  int nvis = 0, nband = 0, p, p_hi, pstep;
+  int nvis = 0, nband = 0, p = 0, p_hi = 0, pstep = 1;
   if (kind == 0) {
-    bst = band_starts(Db, lane, &nvis);
+    bst = band_starts_p(D.band + (size_t)(fb % 3u) * kBands * kBandStride, lane, &nvis);
     nband = nvis;
-    if (A.fresh_ready) nvis += Db.ctr->n_fresh;
+    if (A.fresh_ready) nvis += D.ctr->n_fresh;
     // group g = blockIdx % 8 (one XCD) takes the g-th contiguous eighth of the pairs in band order
+    // (a compact image region: its pixel records stay in that XCD's L2). (Measured and not kept:
+    // pairs taken from 8 per-XCD queues by atomics, two at a time -- the update span grew 28 -> 38 us.)
     const int g = wi & 7, npairs = (nvis + 1) >> 1;
     p = (int)(((long long)npairs * g) >> 3) + (wi >> 3);
     p_hi = (int)(((long long)npairs * (g + 1)) >> 3);
     pstep = A.nint >> 3;
   } else {
-    wait_tag(Db.pipe + kPipeAlloc + (blockIdx.x & 7) * 16, A.tag, &Db.ctr->status);
-    nvis = ld_co(&Db.ctr->n_fresh);
+    wait_tag(D.pipe + kPipeAlloc + (blockIdx.x & 7) * 16, A.tag, &D.ctr->status);
+    nvis = ld_co(&D.ctr->n_fresh);
     p = wi;
     p_hi = (nvis + 1) >> 1;
     pstep = kPipeFreshWG;
   }
   const bool chk = A.has_carve && kind == 0;
-  const uint32_t* ct = Db.ctag + (size_t)(A.fid_carve & 1u) * Db.nblocks;
-  auto fetch = [&](int b) -> VisRec {
-    if (b >= nband) return kind ? ld_rec_co(&Db.fresh_vis[b - nband]) : Db.fresh_vis[b - nband];
-    return Db.vis[band_find(Db, bst, lane, b)];
-  };
-  // a candidate of frame b - 1 the carving has run for: kept unless released (one lane's atomic read:
-  // rtag was written through by workgroup 0 on another XCD)
-  auto kept = [&](const VisRec& r) -> bool {
-    uint32_t v = 0u;
-    if (lane == 0)
-      v = __hip_atomic_fetch_or(&Db.rtag[r.idx], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return (uint32_t)__builtin_amdgcn_readfirstlane(v) != A.fid_carve;
-  };
+  const uint32_t* ct = D.ctag + (size_t)(fc & 1u) * D.nblocks;
   int my_upd = 0, my_vis = 0, ndef = 0;
   bool carved_known = false, def_done = false;
   for (;;) {  // (all control flow below is workgroup-uniform; thread 0 writes the LDS lists)
     // ---- collect: the next records of the list walk, or (at its end) the deferred ones
     int n = 0;
-    auto add = [&](const VisRec& r) {
-      if (threadIdx.x == 0) s_list[n] = r;
-      ++n;
-    };
     if (p < p_hi) {
       while (p < p_hi && n + 2 <= kPipeList) {
-        const int b0 = 2 * p;  // (< nvis)
-        const bool two = b0 + 1 < nvis;
-        const VisRec r0 = fetch(b0), r1 = two ? fetch(b0 + 1) : VisRec{};
-#pragma unroll
         for (int e = 0; e < 2; ++e) {
-          if (e == 1 && !two) break;
-          const VisRec& r = e ? r1 : r0;
-          if (chk && r.pad == 0 && ct[r.idx] == A.fid_carve) {
-            if (!carved_known && ndef < kPipeDefer) {  // deferred to the end
-              if (threadIdx.x == 0) s_def[ndef] = r;
+          const int b = 2 * p + e;
+          if (b >= nvis) break;
+          VisRec r;
+          if (b >= nband)
+            r = kind ? ld_rec_co(&D.fresh_vis[b - nband]) : D.fresh_vis[b - nband];
+          else
+            r = vis[band_find_n(D.nblocks, bst, lane, b)];
+          bool take = true;
+          if (chk && r.pad == 0 && ct[r.idx] == fc) {  // a candidate of frame b - 1
+            if (!carved_known && ndef < kPipeDefer) {   // deferred to the end
+              if (t0) s_def[ndef] = r;
               ++ndef;
-              continue;
+              take = false;
+            } else {
+              if (!carved_known) wait_tag(carved, A.tag, &D.ctr->status);
+              carved_known = true;
+              take = pipe_kept(D.rtag, r.idx, fc, lane);
             }
-            if (!carved_known) wait_tag(carved, A.tag, &Db.ctr->status);
-            carved_known = true;
-            if (!kept(r)) continue;
           }
-          add(r);
+          if (take) {
+            if (t0) s_list[n] = r;
+            ++n;
+          }
         }
         p += pstep;
       }
     } else if (ndef > 0 && !def_done) {
-      if (!carved_known) wait_tag(carved, A.tag, &Db.ctr->status);  // (its barrier publishes s_def)
+      if (!carved_known) wait_tag(carved, A.tag, &D.ctr->status);  // (its barrier publishes s_def)
       else lds_barrier();
       carved_known = true;
       for (int d = 0; d < ndef; ++d) {
         const VisRec r = s_def[d];
-        if (kept(r)) add(r);
+        if (pipe_kept(D.rtag, r.idx, fc, lane)) {
+          if (t0) s_list[n] = r;
+          ++n;
+        }
       }
       def_done = true;
     } else {
@@ -684,7 +703,7 @@ __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const Pip
       float mn = __builtin_inff();
       if (have) {
         r = s_list[k];
-        update_block<false>(Db, P, r, lane, hf, mn, my_upd);
+        update_block<false>(D, P, r, lane, hf, mn, my_upd);
         my_vis += hf == 0 ? 1 : 0;
       }
       mn = wave_min_u(mn);
@@ -693,14 +712,14 @@ __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const Pip
       if (hf == 0 && lane == 0 && have) {
         const float m2 = fminf(s_min[wave], s_min[wave + 1]);
         if (m2 >= 0.9f) {  // space_carving_kernel threshold (voxel_tsdf.cu:227, :485)
-          Db.ctag[(size_t)(fb & 1u) * Db.nblocks + r.idx] = fb;  // (read by the next launch's update)
+          D.ctag[(size_t)(fb & 1u) * D.nblocks + r.idx] = fb;  // (read by the next launch's update)
           const int kc = atomicAdd(&s_ncand, 1);
           if (kc < kIntegrateCandBuf) {
             s_cand[kc] = r;
           } else {  // buffer full (heavy carving): this one now
-            const int kg = atomicAdd(Db.ncand, 1);
-            if (kg < Db.cand_cap) st_rec_co(&Db.cand[kg], r);
-            else atomicOr(&Db.ctr->status, 16u);  // (a list longer than the pool: internal error)
+            const int kg = atomicAdd(ncand, 1);
+            if (kg < D.cand_cap) st_rec_co(&cand[kg], r);
+            else atomicOr(&D.ctr->status, 16u);  // (a list longer than the pool: internal error)
           }
         }
       }
@@ -717,25 +736,25 @@ __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const Pip
   const int nc = min(s_ncand, kIntegrateCandBuf);
   if (wave == 0 && nc > 0) {
     int k0 = 0;
-    if (lane == 0) k0 = atomicAdd(Db.ncand, nc);
+    if (lane == 0) k0 = atomicAdd(ncand, nc);
     k0 = __shfl(k0, 0, 64);
-    if (lane < nc && k0 + lane < Db.cand_cap) st_rec_co(&Db.cand[k0 + lane], s_cand[lane]);
+    if (lane < nc && k0 + lane < D.cand_cap) st_rec_co(&cand[k0 + lane], s_cand[lane]);
   }
-  if (threadIdx.x == 0) {
+  if (t0) {
     const unsigned long long upd = (unsigned long long)(s_upd[0] + s_upd[1] + s_upd[2] + s_upd[3]);
-    const unsigned long long vis = (unsigned long long)(s_vis[0] + s_vis[1] + s_vis[2] + s_vis[3]);
-    unsigned long long* st = Db.pipe + kPipeStats + (size_t)(fb & 1u) * (kPipeStatLines * 16) +
+    const unsigned long long nv = (unsigned long long)(s_vis[0] + s_vis[1] + s_vis[2] + s_vis[3]);
+    unsigned long long* st = D.pipe + kPipeStats + (size_t)(fb & 1u) * (kPipeStatLines * 16) +
                              (blockIdx.x % kPipeStatLines) * 16;
-    if (vis | upd) atomicAdd(st, (vis << 40) | upd);
+    if (nv | upd) atomicAdd(st, (nv << 40) | upd);
     atomicMax(st + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
   if (A.cands_out) {  // a shard's pipelined frame: the last update workgroup fills the exchange slot
     __shared__ int s_last;
     const int nold = A.nint, nfr = A.fresh_ready ? 0 : kPipeFreshWG;
     const uint32_t idx = (uint32_t)(kind ? nold + wi : wi);  // (this workgroup among the update's)
-    if (arrive_last(Db.arrive + kArrIntegrate, 0ull, &s_last, true, (uint32_t)(nold + nfr), idx)) {
-      if (threadIdx.x == 0) arrive_reset(Db.arrive + kArrIntegrate);
-      pack_cands_wg(Db, A.cands_out, A.cand_cap);
+    if (arrive_last(D.arrive + kArrIntegrate, 0ull, &s_last, true, (uint32_t)(nold + nfr), idx)) {
+      if (t0) arrive_reset(D.arrive + kArrIntegrate);
+      pack_cands_wg(D, cand, ncand, A.cands_out, A.cand_cap);
     }
   }
 }
@@ -748,22 +767,19 @@ __device__ void pipe_update(const EngineDev& Db, const FrameParams& P, const Pip
 // sweep workgroups -- each part only when the launch has it
 // (diagnostic build: each workgroup's part code, start and end into D.dbg kernel 8 -- 1 head, 2 fresh
 // update, 3 listed update, 4 tile, 5 sweep; the head's carving / allocation ends at 3 / 4)
-__device__ __forceinline__ void frame_part(const EngineDev& D, const FrameParams& Pu, const FrameParams& Pn,
-                                           const PipeArgs& A, FrameLds& U, int& code) {
+__device__ __forceinline__ int frame_part(const EngineDev& D, const FrameParams& Pu, const FrameParams& Pn,
+                                          const PipeArgs& A, FrameLds& U) {
   int w = (int)blockIdx.x;
   if (w < kPipeHead) {
-    if (w == 0) {
-      code = 1;
-      pipe_head(D, Pu, A, U);
-    }
-    return;
+    if (w != 0) return 0;
+    pipe_head(D, Pu, A, U);
+    return 1;
   }
   w -= kPipeHead;
   const int nfr = A.has_update && !A.fresh_ready ? kPipeFreshWG : 0;
   if (w < nfr) {  // the blocks this launch's allocation creates (they wait for it: dispatched early)
-    code = 2;
-    pipe_update(frame_view(D, A.fid_alloc), Pu, A, 1, w);
-    return;
+    pipe_update(D, Pu, A, 1, w);
+    return 2;
   }
   w -= nfr;
   // the other parts in the launch's grid order: update (u), tiles (t), sweep (s)
@@ -780,13 +796,12 @@ __device__ __forceinline__ void frame_part(const EngineDev& D, const FrameParams
     }
     o -= nq;
   }
-  if (part < 0) return;  // (a graph's grid is sized for the largest launch)
-  code = 3 + part;
+  if (part < 0) return 0;  // (a graph's grid is sized for the largest launch)
   if (part == 0) {
     // (its XCD split takes o % 8 as the XCD: exact when the parts before it are multiples of 8 long,
     // as at 640x480; correct either way)
-    pipe_update(frame_view(D, A.fid_alloc), Pu, A, 0, o);
-    return;
+    pipe_update(D, Pu, A, 0, o);
+    return 3;
   }
   const unsigned long long* aflag = D.pipe + kPipeAlloc + (blockIdx.x & 7) * 16;
   if (part == 1)
@@ -796,14 +811,14 @@ __device__ __forceinline__ void frame_part(const EngineDev& D, const FrameParams
     vis_sweep_chained<1024>(frame_view(D, A.fid_new), Pn, o, U.ing, aflag, A.tag);
   if (threadIdx.x == 0)  // the ingest's span ends with its last workgroup
     atomicMax(D.pipe + kPipeIngEnd + 16 * (A.fid_new & 1u), (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  return 3 + part;
 }
 __device__ __forceinline__ void frame_body(const EngineDev& D, const FrameParams& Pu, const FrameParams& Pn,
                                            const PipeArgs& A, FrameLds& U) {
 #ifdef TSDF_DIAG_STAMPS
   const unsigned long long d_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  int code = 0;
-  frame_part(D, Pu, Pn, A, U, code);
+  const int code = frame_part(D, Pu, Pn, A, U);
 #ifdef TSDF_DIAG_STAMPS
   if (threadIdx.x == 0 && D.dbg && blockIdx.x < (unsigned)kDiagMaxWg) {
     unsigned long long* q = D.dbg + ((size_t)8 * kDiagMaxWg + blockIdx.x) * kDiagStamps;
@@ -844,10 +859,10 @@ template __global__ void k_integrate_t<true, true>(EngineDev, FrameParams, const
 // ---------------------------------------------------------------------------------------------
 // every shard's candidate slot (nshard slots of cap records) listed as D.cand / *D.ncand: the candidate
 // set of one volume, so that every shard's index takes the same deletes
-__device__ void merge_cands_inbox(const EngineDev& D, const ShardRec* __restrict__ cands_in, int cap, int nshard,
-                                  int* s_base) {
+__device__ void merge_cands_inbox(const EngineDev& D, VisRec* cand, int32_t* ncand, const ShardRec* __restrict__ cands_in,
+                                  int cap, int nshard, int* s_base) {
   if (threadIdx.x == 0) {
-    // the union is listed in D.cand (cand_cap records; the resolver's D.pairs scratch holds at
+    // the union is listed in cand (D.cand_cap records; the resolver's D.pairs scratch holds at
     // least as many): more candidates than that is a shard overflow, the rest are dropped
     int run = 0;
     bool ovf = false;
@@ -861,11 +876,11 @@ __device__ void merge_cands_inbox(const EngineDev& D, const ShardRec* __restrict
       run += n;
     }
     s_base[nshard] = run;
-    st_co(D.ncand, run);
+    st_co(ncand, run);
     if (ovf) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_SHARD_OVERFLOW
   }
   __syncthreads();
-  unsigned long long* cq = reinterpret_cast<unsigned long long*>(D.cand);
+  unsigned long long* cq = reinterpret_cast<unsigned long long*>(cand);
   for (int s = 0; s < nshard; ++s) {
     const ShardRec* slot = cands_in + (size_t)s * (cap + 1) + 1;
     const int n = s_base[s + 1] - s_base[s];
@@ -892,7 +907,7 @@ __device__ __forceinline__ void resolve_delete_merged(EngineDev D, const VisRec*
                                                       int nshard) {
   __shared__ DeleteLds L;
   __shared__ int s_base[kMaxShards + 1];
-  if (cands_in) merge_cands_inbox(D, cands_in, cap, nshard, s_base);
+  if (cands_in) merge_cands_inbox(D, D.cand, D.ncand, cands_in, cap, nshard, s_base);
   resolve_delete_wg(D, recs, count, direct, L);
   if (!direct) frame_end(D);
 }

@@ -14,7 +14,7 @@
 #   shard8            bench.py --width 1280 --height 720 --shard 8 (single-GPU 8-shard rehearsal)
 #   sq:<kernel>       SQ counter passes of one kernel on the default command (profile_kernel_sq.sh)
 #   raydiag           raycast step statistics and wave lifetimes (diagnostic library, scripts/diag_raycast.py)
-#   framediag         k_frame per-part timeline (diagnostic library, scripts/diag_frame.py)
+#   framediag[:A=1,B=2]  k_frame per-part timeline (diagnostic library, scripts/diag_frame.py), optional env
 #   ab:<lib1>,<lib2>  interleaved A/B of engine builds on the driver command (scripts/ab.sh)
 set -uo pipefail
 TAG=${1:?tag}; shift
@@ -64,8 +64,8 @@ for st in "$@"; do
            tail -8 $OUT/sq_$k.txt ;;
     raydiag) TSDF_AMD_LIB=disinfect-slam_amd/libdisinfect_tsdf_diag.so timeout -k 10 180 python3 scripts/diag_raycast.py > $OUT/raycast_diag.txt 2>&1 || fail $st $OUT/raycast_diag.txt
            tail -12 $OUT/raycast_diag.txt ;;
-    framediag*) e=${st#framediag}; e=${e#:}; env ${e:+$e} TSDF_AMD_LIB=disinfect-slam_amd/libdisinfect_tsdf_diag.so timeout -k 10 120 python3 scripts/diag_frame.py > $OUT/frame_diag${e:+_$e}.txt 2>&1 || fail $st $OUT/frame_diag${e:+_$e}.txt
-           tail -9 $OUT/frame_diag${e:+_$e}.txt ;;
+    framediag*) e=${st#framediag}; e=${e#:}; f=$OUT/frame_diag${e:+_$e}.txt; env ${e//,/ } TSDF_AMD_LIB=disinfect-slam_amd/libdisinfect_tsdf_diag.so timeout -k 10 120 python3 scripts/diag_frame.py > $f 2>&1 || fail $st $f
+           tail -9 $f ;;
     ab:*) IFS=, read -ra LIBS <<< "${st#ab:}"; bash scripts/ab.sh 20 "${LIBS[@]}" || exit 1 ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac

@@ -159,3 +159,53 @@ def test_k_frame_hand_offs_are_agent_scope():
             polls += 1
             break
     assert polls >= 3, polls
+
+
+def _loops(body):
+    """(first, last) instruction indices of every backward branch's loop body."""
+    addrs = []
+    for x in body:
+        m = re.search(r"// ([0-9A-F]+):", x)
+        addrs.append(int(m.group(1), 16) if m else None)
+    base = addrs[0]
+    idx = {a: i for i, a in enumerate(addrs) if a is not None}
+    for i, x in enumerate(body):
+        if re.match(r"s_cbranch_\w+|s_branch", x):
+            t = re.search(r"<\S+\+0x([0-9a-f]+)>", x)
+            j = idx.get(base + int(t.group(1), 16)) if t and base is not None else None
+            if j is not None and j < i:
+                yield j, i
+
+
+def test_update_loops_keep_their_state_in_registers():
+    """The voxel-update loops of k_integrate_t and k_frame (three 16-B pool loads, the reciprocal
+    estimates) touch no scratch: a spilled value there is re-read for every block (round 4: the
+    __shfl_xor lane addresses of the carve minimum and an indexed band-start array were spilled and
+    made the update ~30 % slower). k_raycast uses no scratch at all."""
+    funcs = _functions(_disassemble())
+    seen = set()
+    for name, body in funcs.items():
+        kern = next((k for k in ("_ZN4tsdf7k_frame", "_ZN4tsdf9k_frame_g", "_ZN4tsdf13k_integrate_t")
+                     if name.startswith(k)), None)
+        if kern:
+            for j, i in _loops(body):
+                ops = [x.split()[0] for x in body[j:i + 1]]
+                if i - j < 1600 and ops.count("global_load_dwordx4") >= 3 and "v_rcp_f32_e32" in ops:
+                    seen.add(kern)
+                    assert not any(o.startswith("scratch_") for o in ops), (name, j, i)
+        if name.startswith("_ZN4tsdf9k_raycast"):
+            assert not any(x.startswith("scratch_") for x in body), name
+    assert seen == {"_ZN4tsdf7k_frame", "_ZN4tsdf9k_frame_g", "_ZN4tsdf13k_integrate_t"}, seen
+
+
+def test_frame_kernels_make_no_calls():
+    """Every device function of the frame kernels is inlined: a real call (s_swappc) passes the
+    kernel's EngineDev by reference, so the kernel first copies it (240 B per lane) to scratch and
+    the callee reads every field from there (round 4: pipe_update grew past the inliner's threshold
+    and the k_frame update ran from scratch)."""
+    funcs = _functions(_disassemble())
+    kernels = [n for n in funcs if n.startswith(("_ZN4tsdf7k_frame", "_ZN4tsdf9k_frame_g", "_ZN4tsdf13k_integrate_t",
+                                                 "_ZN4tsdf12k_ingest_dda", "_ZN4tsdf9k_raycast"))]
+    assert kernels
+    for name in kernels:
+        assert not any(x.startswith("s_swappc") for x in funcs[name]), name
