@@ -528,7 +528,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.pixA, 2 * e->max_pixels);  // two buffers: a pipelined frame's and the next one's
   ALLOC(D.pixB, 2 * e->max_pixels);
   if (const char* v = std::getenv("TSDF_PIPELINE")) e->pipeline = v[0] != '0';
-  if (const char* v = std::getenv("TSDF_FRAME_ORDER")) e->frame_order = std::min(2, std::max(0, std::atoi(v)));
+  if (const char* v = std::getenv("TSDF_FRAME_ORDER")) e->frame_order = std::min(3, std::max(0, std::atoi(v)));
   ALLOC(D.visbits, kOccWords);
   ALLOC(D.wgcnt, kOccWords / 256);
   ALLOC(D.dbg, (size_t)kDiagKernels * kDiagMaxWg * kDiagStamps);
@@ -735,7 +735,7 @@ int launch_frame(tsdf_engine* e, PipeArgs A, const FrameParams& Pu, const FrameP
   hipStream_t s = e->stream;
   JOIN_RENDER(e);
   finish_args(e, A, Pu);
-  const int nwg = kPipeHead + (A.has_update ? A.nint : 0) + (A.has_update && !A.fresh_ready ? kPipeFreshWG : 0) +
+  const int nwg = kPipeHead + (A.has_update ? A.nint : 0) + pipe_fresh_wgs(A) +
                   (A.has_frame ? A.tiles + kVisWorkgroups : 0);
   if (e->profiling && A.has_frame) ++e->prof_pipelined;  // (frame launches; not the flush's)
   if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {

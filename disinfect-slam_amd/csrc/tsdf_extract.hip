@@ -200,6 +200,31 @@ __device__ __forceinline__ void ray_block(const EngineDev& D, const RayView& R, 
   const int32_t e = find_local(D.table, (int16_t)bx, (int16_t)by, (int16_t)bz);  // outside the grid / none
   c.idx = e < 0 ? -1 : D.table[e].z;
 }
+// The march's lookup of block (bx, by, bz) after its region was left: ray_block without the block
+// cache (a step that leaves the region reads another block, except on an entry face, where the
+// lookup repeats and returns the same) and with 32-bit index arithmetic (the cell offset from a
+// scalar base). *empty as RayCache.empty.
+__device__ __forceinline__ int32_t march_lookup(const EngineDev& D, const RayView& R, int bx, int by, int bz,
+                                                int& empty) {
+  empty = 0;
+  const int lx = bx - R.ox, ly = by - R.oy, lz = bz - R.oz;
+  const unsigned n = (unsigned)R.n;
+  if ((unsigned)lx < n && (unsigned)ly < n && (unsigned)lz < n) {
+    const uint32_t nb = (uint32_t)R.nb, ns = (uint32_t)R.ns;
+    const uint32_t k = __umul24(__umul24((uint32_t)lz >> 2, nb) + ((uint32_t)ly >> 2), nb) + ((uint32_t)lx >> 2);
+    const uint32_t q = __umul24(__umul24((uint32_t)lz >> 4, ns) + ((uint32_t)ly >> 4), ns) + ((uint32_t)lx >> 4);
+    const uint32_t wb = R.bits[k >> 5], ws = R.bits[R.nbw + (q >> 5)];
+    if (!((wb >> (k & 31)) & 1u)) {
+      empty = 2 - (int)((ws >> (q & 31)) & 1u);
+      return -1;
+    }
+    const uint32_t off = ((k << 6) | (((uint32_t)lz & 3) << 4) | (((uint32_t)ly & 3) << 2) | ((uint32_t)lx & 3)) * 4u;
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(R.cell) + off);
+    return (v >> kViewIdxBits) == R.gen ? (int32_t)(v & ((1u << kViewIdxBits) - 1)) : -1;
+  }
+  const int32_t e = find_local(D.table, (int16_t)bx, (int16_t)by, (int16_t)bz);  // outside the grid / none
+  return e < 0 ? -1 : D.table[e].z;
+}
 __device__ __forceinline__ int voxel_off(int16_t px, int16_t py, int16_t pz) {
   return (px & 7) + (py & 7) * kBlockLen + (pz & 7) * kBlockLen * kBlockLen;
 }
@@ -348,14 +373,15 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
     if (!inside || ridx >= 0) {
       const int16_t px = round_s16(pos.x), py = round_s16(pos.y), pz = round_s16(pos.z);
       if (!inside) {
-        ray_block(D, R, c, px >> kBlockLenBits, py >> kBlockLenBits, pz >> kBlockLenBits);
-        ridx = c.idx;
+        const int bx = px >> kBlockLenBits, by = py >> kBlockLenBits, bz = pz >> kBlockLenBits;
+        int empty;
+        ridx = march_lookup(D, R, bx, by, bz, empty);
         // 2^sh blocks per axis: 0 for a block (present, or missing in an occupied brick), 2 for an
-        // empty brick, 4 for an empty superbrick (c.empty 0 / 1 / 2); selects, not branches
-        const int sh = 2 * c.empty;
-        const int rx = (R.ox + (((c.bx - R.ox) >> sh) << sh)) * kBlockLen;
-        const int ry = (R.oy + (((c.by - R.oy) >> sh) << sh)) * kBlockLen;
-        const int rz = (R.oz + (((c.bz - R.oz) >> sh) << sh)) * kBlockLen;
+        // empty brick, 4 for an empty superbrick (empty 0 / 1 / 2); selects, not branches
+        const int sh = 2 * empty;
+        const int rx = (R.ox + (((bx - R.ox) >> sh) << sh)) * kBlockLen;
+        const int ry = (R.oy + (((by - R.oy) >> sh) << sh)) * kBlockLen;
+        const int rz = (R.oz + (((bz - R.oz) >> sh) << sh)) * kBlockLen;
         const float len = (float)(kBlockLen << sh);
         // faces at r - 0.5 and r + len - 0.5: the exit face of the step's direction, negated
         // (s = +1: pos < hi; s = -1: -pos < -lo)

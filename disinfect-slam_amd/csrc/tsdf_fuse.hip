@@ -625,10 +625,20 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
     st_co(D.pipe + kPipeT0 + 16 * (fb & 1u), (unsigned long long)__builtin_amdgcn_s_memrealtime());
   int bst = 0;
   int nvis = 0, nband = 0, p = 0, p_hi = 0, pstep = 1;
+  bool carved_known = false;
+  // order 3: the whole update after the allocation flag -- no update traffic beside the head's
+  // carving and allocation (their chains of dependent round trips stretch ~4x under it), the new
+  // blocks listed after the band lists, and no deferral (the head publishes the carving first)
+  const bool after_alloc = kind == 0 && A.order == 3;
   if (kind == 0) {
+    if (after_alloc) {
+      wait_tag(D.pipe + kPipeAlloc + (blockIdx.x & 7) * 16, A.tag, &D.ctr->status);
+      carved_known = true;
+    }
     bst = band_starts_p(D.band + (size_t)(fb % 3u) * kBands * kBandStride, lane, &nvis);
     nband = nvis;
     if (A.fresh_ready) nvis += D.ctr->n_fresh;
+    else if (after_alloc) nvis += ld_co(&D.ctr->n_fresh);
     // group g = blockIdx % 8 (one XCD) takes the g-th contiguous eighth of the pairs in band order
     // (a compact image region: its pixel records stay in that XCD's L2). (Measured and not kept:
     // pairs taken from 8 per-XCD queues by atomics, two at a time -- the update span grew 28 -> 38 us.)
@@ -646,7 +656,8 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
   const bool chk = A.has_carve && kind == 0;
   const uint32_t* ct = D.ctag + (size_t)(fc & 1u) * D.nblocks;
   int my_upd = 0, my_vis = 0, ndef = 0;
-  bool carved_known = false, def_done = false;
+  bool def_done = false;
+  const bool fresh_co = kind != 0 || (after_alloc && !A.fresh_ready);  // (written in this launch)
   for (;;) {  // (all control flow below is workgroup-uniform; thread 0 writes the LDS lists)
     // ---- collect: the next records of the list walk, or (at its end) the deferred ones
     int n = 0;
@@ -657,7 +668,7 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
           if (b >= nvis) break;
           VisRec r;
           if (b >= nband)
-            r = kind ? ld_rec_co(&D.fresh_vis[b - nband]) : D.fresh_vis[b - nband];
+            r = fresh_co ? ld_rec_co(&D.fresh_vis[b - nband]) : D.fresh_vis[b - nband];
           else
             r = vis[band_find_n(D.nblocks, bst, lane, b)];
           bool take = true;
@@ -750,7 +761,7 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
   }
   if (A.cands_out) {  // a shard's pipelined frame: the last update workgroup fills the exchange slot
     __shared__ int s_last;
-    const int nold = A.nint, nfr = A.fresh_ready ? 0 : kPipeFreshWG;
+    const int nold = A.nint, nfr = pipe_fresh_wgs(A);
     const uint32_t idx = (uint32_t)(kind ? nold + wi : wi);  // (this workgroup among the update's)
     if (arrive_last(D.arrive + kArrIntegrate, 0ull, &s_last, true, (uint32_t)(nold + nfr), idx)) {
       if (t0) arrive_reset(D.arrive + kArrIntegrate);
@@ -776,7 +787,7 @@ __device__ __forceinline__ int frame_part(const EngineDev& D, const FrameParams&
     return 1;
   }
   w -= kPipeHead;
-  const int nfr = A.has_update && !A.fresh_ready ? kPipeFreshWG : 0;
+  const int nfr = pipe_fresh_wgs(A);
   if (w < nfr) {  // the blocks this launch's allocation creates (they wait for it: dispatched early)
     pipe_update(D, Pu, A, 1, w);
     return 2;
@@ -787,8 +798,9 @@ __device__ __forceinline__ int frame_part(const EngineDev& D, const FrameParams&
   // (order r runs the parts r, r + 1, r + 2 mod 3; scalar selects, no indexed arrays: those live in
   // scratch)
   int part = -1, o = w;
+  const int ord = A.order == 3 ? 1 : A.order;
   for (int k = 0; k < 3; ++k) {
-    const int q = (A.order + k) % 3;
+    const int q = (ord + k) % 3;
     const int nq = q == 0 ? nold : (q == 1 ? A.tiles : ns);
     if (o < nq) {
       part = q;

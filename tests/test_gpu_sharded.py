@@ -448,3 +448,52 @@ def test_sharded_pipe_protocol():
         assert all(s["frames"] == 4 for s in group.stats())
     finally:
         group.close()
+
+
+def test_shard_frame_buffers_may_be_dropped_after_begin():
+    """a shard's update reads the raw device frame it was given at _begin. The
+    Python wrapper keeps that frame referenced until _update, so a caller may pass temporaries and
+    drop them at once; here every frame tensor is a temporary, torch's cache is emptied and refilled
+    with garbage of the same size between _begin and _update, and the volume still equals a
+    ShardGroup's (which holds its frames)."""
+    import gc
+
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H, G = 160, 120, 2
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    ref = tsdf_amd.ShardGroup(G, 0.02, 0.08, max_width=W, max_height=H, num_block_bits=12, split=False)
+    eng = [tsdf_amd.Engine(0.02, 0.08, W, H, 12, 0, shard_index=i, shard_count=G,
+                           stream=torch.cuda.current_stream(0)) for i in range(G)]
+    cap = 4096
+    cands = torch.zeros((G, tsdf_amd.Engine.shard_slot_bytes(cap)), dtype=torch.uint8, device="cuda")
+    try:
+        for f in range(6):
+            fr = synth.render(cam, 3 * f)
+            pose = tsdf_amd.SE3(fr["q"], fr["t"])
+            ref.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, pose, MAXD)
+            dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+            for e in eng:
+                e.integrate_shard_begin(dev(fr["rgb"]), dev(fr["depth"]), dev(fr["ht"]), dev(fr["lt"]), cam.K,
+                                        pose, MAXD)
+            gc.collect()
+            torch.cuda.empty_cache()
+            junk = [torch.full((H, W), -7.0, device="cuda") for _ in range(16)]
+            junk += [torch.full((H, W, 3), 255, dtype=torch.uint8, device="cuda") for _ in range(8)]
+            for i, e in enumerate(eng):
+                e.integrate_shard_update(None, 0, cands[i], cap)
+            for e in eng:
+                e.integrate_shard_end(cands, cap)
+            del junk
+        ref.flush()
+        for a, b in zip(ref.engines, eng):
+            da, db = a.dump(), b.dump()
+            assert set(da) == set(db)
+            for k in da:
+                np.testing.assert_array_equal(np.asarray(da[k]), np.asarray(db[k]), err_msg=k)
+    finally:
+        ref.close()
+        for e in eng:
+            e.close()
