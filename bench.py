@@ -47,7 +47,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 BLOCK_READ_BYTES = 512 * 12 + 12  # voxel state + metadata of one visible block
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_integrate_r4.json")
 # SQ counters of k_raycast (rocprofv3 --pmc passes of `bench.py --loop c5`, scripts/profile_kernel_sq.sh)
-RAYCAST_SQ_FILE = os.path.join(ROOT, "profiles", "r3_raycast_sq.json")
+RAYCAST_SQ_FILE = os.path.join(ROOT, "profiles", "r4_raycast_sq.json")
 VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each
 
 
@@ -307,8 +307,8 @@ def raycast_roofline(a, us_call):
     VALU fraction shows how much issue bandwidth that chain leaves idle). The rate is taken over the
     whole call (view grid + bitmaps + k_raycast), so it is a lower bound for the kernel's own."""
     rays = a.width * a.height
-    out = {"kernel": "k_raycast", "bound": "latency (each wave's chain of dependent view-grid lookups and "
-                                           "voxel reads; VALU second)",
+    out = {"kernel": "k_raycast", "bound": "VALU issue (~4.7 waves per SIMD stepping their rays; the lookups' "
+                                           "dependent loads second, DESIGN.md 4 Raycast)",
            "us_per_call": round(us_call, 3), "rays_per_s": round(rays / (us_call * 1e-6), 1),
            "timing": "events around 50 back-to-back tsdf_raycast calls of the last timed camera, after the loop"}
     try:

@@ -14,7 +14,7 @@ namespace tsdf {
 
 // a shard's split frame: the new-key set (this slice's keys) into the exchange slot, drained for
 // the merge of every shard's slots (k_resolve_alloc after the all-gather)
-__device__ void pack_keys_wg(const EngineDev& D, ShardRec* __restrict__ out, int cap) {
+__device__ __forceinline__ void pack_keys_wg(const EngineDev& D, ShardRec* __restrict__ out, int cap) {
   const int n = ld_co(&D.ctr->nk_count);
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const int h = (int)ld_co(&D.nk_list[i].slot);

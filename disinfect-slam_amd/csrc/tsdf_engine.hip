@@ -528,7 +528,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.pixA, 2 * e->max_pixels);  // two buffers: a pipelined frame's and the next one's
   ALLOC(D.pixB, 2 * e->max_pixels);
   if (const char* v = std::getenv("TSDF_PIPELINE")) e->pipeline = v[0] != '0';
-  if (const char* v = std::getenv("TSDF_FRAME_ORDER")) e->frame_order = std::min(3, std::max(0, std::atoi(v)));
+  if (const char* v = std::getenv("TSDF_FRAME_ORDER")) e->frame_order = std::min(4, std::max(0, std::atoi(v)));
   ALLOC(D.visbits, kOccWords);
   ALLOC(D.wgcnt, kOccWords / 256);
   ALLOC(D.dbg, (size_t)kDiagKernels * kDiagMaxWg * kDiagStamps);

@@ -336,7 +336,7 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
   }
   const f3 dw = qrot(P.wq, dc);
   const f3 sg = {dw.x * step_size / P.voxel, dw.y * step_size / P.voxel, dw.z * step_size / P.voxel};
-  const int max_step = f2i(ceilf(P.max_depth / step_size));  // wave-uniform
+  const int max_step = __builtin_amdgcn_readfirstlane(f2i(ceilf(P.max_depth / step_size)));  // (uniform)
   // steps i = 1 .. max_step - 1; the comparison of step 1 needs the value at the origin
   f3 pos = {P.wt.x / P.voxel, P.wt.y / P.voxel, P.wt.z / P.voxel};
   bool active = valid && 1 < max_step;
@@ -360,8 +360,26 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
   // The lanes of a wave step together (a tight per-lane loop through empty regions measured slower:
   // the lanes' dependent loads then no longer overlap in time).
   int i = 1;
+  auto in_region = [&](const f3& q) -> bool {
+    return fmaxf(fmaxf(fmaf(q.x, sgn.x, ne.x), fmaf(q.y, sgn.y, ne.y)), fmaf(q.z, sgn.z, ne.z)) < 0.0f;
+  };
   while (active) {
-    const bool inside = fmaxf(fmaxf(fmaf(pos.x, sgn.x, ne.x), fmaf(pos.y, sgn.y, ne.y)), fmaf(pos.z, sgn.z, ne.z)) < 0.0f;
+    bool inside = in_region(pos);
+    // every active lane of the wave inside an empty region (most steps): a tight wave-uniform loop of
+    // steps that read +1 -- the additions and the exit-face test -- until some lane leaves its region
+    // (that step runs below) or the steps run out
+    if (__ballot(!inside || ridx >= 0) == 0ull) {
+      int iu = __builtin_amdgcn_readfirstlane(i);  // (the active lanes' step count is one value)
+      do {
+        pos = {pos.x + sg.x, pos.y + sg.y, pos.z + sg.z};
+        ++iu;
+        inside = in_region(pos);
+      } while (iu < max_step && __ballot(!inside) == 0ull);
+      i = iu;
+      prev = 1.0f;
+      active = iu < max_step;
+      continue;
+    }
 #ifdef TSDF_DIAG_STAMPS
     d_it += 1;
     d_blk += !inside;

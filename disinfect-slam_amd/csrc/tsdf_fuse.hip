@@ -30,7 +30,7 @@ __device__ __forceinline__ void setu(uint4& v, int j, uint32_t f) {
 }
 
 // end of a frame's bookkeeping (after its carving): running totals, empty candidate / band lists
-__device__ void frame_end(const EngineDev& D) {
+__device__ __forceinline__ void frame_end(const EngineDev& D) {
   lds_barrier();
   if (threadIdx.x == 0) {
     D.ctr->total_visible += (unsigned long long)D.ctr->n_vis;
@@ -46,7 +46,7 @@ __device__ void frame_end(const EngineDev& D) {
 // exhausted pool left without voxels this frame (D.pend, written by the allocation resolver before
 // this launch)
 // (cand / ncand: the frame's candidate list, D.cand / D.ncand of its view)
-__device__ void pack_cands_wg(const EngineDev& D, const VisRec* cand, const int32_t* ncand, ShardRec* __restrict__ out,
+__device__ __forceinline__ void pack_cands_wg(const EngineDev& D, const VisRec* cand, const int32_t* ncand, ShardRec* __restrict__ out,
                               int cap) {
   const int nc = ld_co(ncand);
   const int np = min(ld_co(&D.ctr->n_pend), (int)kNewKeyCap);
@@ -497,7 +497,7 @@ __attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES)))
 
 // frame f's statistics from its update workgroups' counters (the update ran in an earlier launch),
 // zeroed for frame f + 2. Wave 0.
-__device__ void pipe_frame_stats(const EngineDev& D, uint32_t f) {
+__device__ __forceinline__ void pipe_frame_stats(const EngineDev& D, uint32_t f) {
   const int t = threadIdx.x;
   if (t >= 64) return;
   unsigned long long* base = D.pipe + kPipeStats + (size_t)(f & 1u) * (kPipeStatLines * 16);
@@ -542,12 +542,12 @@ union FrameLds {
   IngestLds<1024> ing;
 };
 
-__device__ void merge_cands_inbox(const EngineDev& D, VisRec* cand, int32_t* ncand, const ShardRec* __restrict__ cands_in,
+__device__ __forceinline__ void merge_cands_inbox(const EngineDev& D, VisRec* cand, int32_t* ncand, const ShardRec* __restrict__ cands_in,
                                   int cap, int nshard, int* s_base);
 
 // workgroup 0: frame fid_carve's carving, then frame fid_alloc's allocation, each published. A shard's
 // pipelined frame first lists every shard's candidates of fid_carve (the all-gathered inbox).
-__device__ void pipe_head(const EngineDev& D, const FrameParams& Pu, const PipeArgs& A, FrameLds& U) {
+__device__ __forceinline__ void pipe_head(const EngineDev& D, const FrameParams& Pu, const PipeArgs& A, FrameLds& U) {
   __shared__ int s_base[kMaxShards + 1];
   const int t = threadIdx.x;
   if (A.has_carve) {  // (the view's pointers as scalars: a copied EngineDev view can land in scratch)
@@ -629,7 +629,7 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
   // order 3: the whole update after the allocation flag -- no update traffic beside the head's
   // carving and allocation (their chains of dependent round trips stretch ~4x under it), the new
   // blocks listed after the band lists, and no deferral (the head publishes the carving first)
-  const bool after_alloc = kind == 0 && A.order == 3;
+  const bool after_alloc = kind == 0 && A.order >= 3;
   if (kind == 0) {
     if (after_alloc) {
       wait_tag(D.pipe + kPipeAlloc + (blockIdx.x & 7) * 16, A.tag, &D.ctr->status);
@@ -787,6 +787,8 @@ __device__ __forceinline__ int frame_part(const EngineDev& D, const FrameParams&
     return 1;
   }
   w -= kPipeHead;
+  if (A.order == 4)  // every part after the head's carving and allocation
+    wait_tag(D.pipe + kPipeAlloc + (blockIdx.x & 7) * 16, A.tag, &D.ctr->status);
   const int nfr = pipe_fresh_wgs(A);
   if (w < nfr) {  // the blocks this launch's allocation creates (they wait for it: dispatched early)
     pipe_update(D, Pu, A, 1, w);
@@ -798,7 +800,7 @@ __device__ __forceinline__ int frame_part(const EngineDev& D, const FrameParams&
   // (order r runs the parts r, r + 1, r + 2 mod 3; scalar selects, no indexed arrays: those live in
   // scratch)
   int part = -1, o = w;
-  const int ord = A.order == 3 ? 1 : A.order;
+  const int ord = A.order == 3 ? 1 : (A.order == 4 ? 0 : A.order);
   for (int k = 0; k < 3; ++k) {
     const int q = (ord + k) % 3;
     const int nq = q == 0 ? nold : (q == 1 ? A.tiles : ns);
@@ -871,7 +873,7 @@ template __global__ void k_integrate_t<true, true>(EngineDev, FrameParams, const
 // ---------------------------------------------------------------------------------------------
 // every shard's candidate slot (nshard slots of cap records) listed as D.cand / *D.ncand: the candidate
 // set of one volume, so that every shard's index takes the same deletes
-__device__ void merge_cands_inbox(const EngineDev& D, VisRec* cand, int32_t* ncand, const ShardRec* __restrict__ cands_in,
+__device__ __forceinline__ void merge_cands_inbox(const EngineDev& D, VisRec* cand, int32_t* ncand, const ShardRec* __restrict__ cands_in,
                                   int cap, int nshard, int* s_base) {
   if (threadIdx.x == 0) {
     // the union is listed in cand (D.cand_cap records; the resolver's D.pairs scratch holds at

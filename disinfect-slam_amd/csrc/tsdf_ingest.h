@@ -151,7 +151,7 @@ __device__ __forceinline__ int32_t find_entry_t(const int4* __restrict__ table, 
 // Co: the sweep of a pipelined frame after its wait (the chained sweep's fallback): the occupancy
 // words and entries are read at agent scope
 template <int TS, bool Co = false>
-__device__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, IngestLds<TS>& S) {
+__device__ __forceinline__ void vis_sweep(const EngineDev& D, const FrameParams& P, int wg, IngestLds<TS>& S) {
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   uint32_t* L = S.u.sweep.list[wave];
   int* s_cnt = S.u.sweep.cnt;
@@ -265,7 +265,7 @@ __device__ __forceinline__ Ent load_ent_rmw(int4* table, uint32_t e) {
   return r;
 }
 template <int TS>
-__device__ void vis_sweep_chained(const EngineDev& D, const FrameParams& P, int wg, IngestLds<TS>& S,
+__device__ __forceinline__ void vis_sweep_chained(const EngineDev& D, const FrameParams& P, int wg, IngestLds<TS>& S,
                                   const unsigned long long* flag, uint32_t tag) {
   static_assert(kVisChunk >= 4 * kPreMax && kPreMax <= 256, "list + records of kPreMax blocks per wave");
   const int lane = lane_id(), wave = threadIdx.x >> 6;

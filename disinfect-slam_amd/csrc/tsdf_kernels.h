@@ -135,7 +135,8 @@ struct PipeArgs {
   int order;            // grid order of the parts after the head (TSDF_FRAME_ORDER): 0 fresh, update,
                         //   tiles, sweep; 1 fresh, tiles, sweep, update; 2 fresh, sweep, update, tiles;
                         //   3 tiles, sweep, update, the update after the allocation flag (no fresh
-                        //   workgroups: the update takes the new blocks too)
+                        //   workgroups: the update takes the new blocks too); 4 update, tiles, sweep,
+                        //   every part after the allocation flag (the head's resolvers alone)
   // a shard's pipelined frame (tsdf_integrate_shard_pipe): every shard's carve candidates of frame
   // fid_carve, all-gathered (nshard slots of cand_cap records; merged before the carving), and this
   // shard's slot that the update's last workgroup fills with frame fid_alloc's candidates
@@ -154,7 +155,7 @@ __device__ __host__ __forceinline__ EngineDev frame_view(const EngineDev& D, uin
 }
 // the workgroups that update the blocks a launch's allocation creates (orders 0-2)
 __device__ __host__ __forceinline__ int pipe_fresh_wgs(const PipeArgs& A) {
-  return A.has_update && !A.fresh_ready && A.order != 3 ? kPipeFreshWG : 0;
+  return A.has_update && !A.fresh_ready && A.order < 3 ? kPipeFreshWG : 0;
 }
 // per-frame arguments of the graph-captured frame loop (tsdf_graph_*): the graph's first node
 // copies them from a pinned host slot, every graph kernel reads its camera / frame pointers here

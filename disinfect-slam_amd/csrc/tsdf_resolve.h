@@ -296,7 +296,7 @@ __device__ __forceinline__ void rank_sort(unsigned long long* a, unsigned long l
 // Threshold search for multi-batch launches: keys[i] >> 32 (unique in [lo, range)) for i < n in
 // global scratch; returns thr > lo with count(lo <= key < thr) in [1, RB] (some key remains).
 template <int RB = kRB>
-__device__ uint32_t batch_threshold(const unsigned long long* __restrict__ keys, int n, uint32_t lo,
+__device__ __forceinline__ uint32_t batch_threshold(const unsigned long long* __restrict__ keys, int n, uint32_t lo,
                                     uint32_t range, uint32_t* hist, int* scratch) {
   uint32_t hi = range;
   for (;;) {
@@ -406,7 +406,7 @@ __device__ __forceinline__ uint32_t push_to(uint32_t v, int rank) {
   return (uint32_t)__builtin_amdgcn_ds_permute(rank << 2, (int)v);
 }
 
-__device__ void resolve_alloc_wave(const EngineDev& D, const FrameParams& P, int frame_mode, int n, int free0,
+__device__ __forceinline__ void resolve_alloc_wave(const EngineDev& D, const FrameParams& P, int frame_mode, int n, int free0,
                                    unsigned long long key_in, int32_t slot_in, uint32_t* lockset,
                                    unsigned long long tick0) {
   const int l = lane_id();
@@ -709,7 +709,7 @@ __device__ FAST_INLINE bool resolve_alloc_fast(const EngineDev& D, const FramePa
 // frame_mode 1: new blocks this engine holds are listed in D.fresh_vis (flagged fresh, visible this
 // frame); 0 (hash-level test path): their pool indices in D.fresh for k_fresh_init.
 template <int RB>
-__device__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint32_t range, int frame_mode,
+__device__ __forceinline__ void resolve_alloc_wg(const EngineDev& D, const FrameParams& P, uint32_t range, int frame_mode,
                                  AllocLdsT<RB>& L) {
   constexpr int NR = RB / kRT;  // keys per thread and round
   constexpr int NC = AllocLdsT<RB>::kClaim, NL = AllocLdsT<RB>::kLock;
@@ -1045,7 +1045,7 @@ __device__ __forceinline__ void carved_key(const EngineDev& D, uint32_t e, int16
   const unsigned long long w = D.fo[e];
   if ((uint32_t)(w >> 32) == ~fo_fid) nk_insert(D, pack_key(x, y, z), (uint32_t)w);
 }
-__device__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32_t epoch, int direct,
+__device__ __forceinline__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32_t epoch, int direct,
                                     const unsigned long long (&a)[2], DeleteLds& L, unsigned long long tick0,
                                     uint32_t rel_fid, uint32_t fo_fid) {
   const int t = threadIdx.x, wave = t >> 6;
@@ -1121,7 +1121,7 @@ __device__ bool resolve_delete_fast(const EngineDev& D, int n, int free0, uint32
 // rel_fid / fo_fid: pipelined frames (released_block above). The deletes are ordered by the entry each
 // candidate holds in the table NOW (its record's entry may predate an earlier carving that moved a list
 // element into its bucket's head).
-__device__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__ recs,
+__device__ __forceinline__ void resolve_delete_wg(const EngineDev& D, const VisRec* __restrict__ recs,
                                   const int32_t* __restrict__ count, int direct, DeleteLds& L,
                                   uint32_t rel_fid = 0u, uint32_t fo_fid = 0u) {
   const int t = threadIdx.x;

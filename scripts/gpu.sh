@@ -13,6 +13,7 @@
 #   c5tests           the raycast / render / C5 GPU tests
 #   shard8            bench.py --width 1280 --height 720 --shard 8 (single-GPU 8-shard rehearsal)
 #   sq:<kernel>       SQ counter passes of one kernel on the default command (profile_kernel_sq.sh)
+#   raysq             SQ / FETCH / WRITE passes of k_raycast on the C5 loop -> <tag>/r4_raycast_sq.json
 #   raydiag           raycast step statistics and wave lifetimes (diagnostic library, scripts/diag_raycast.py)
 #   framediag[:A=1,B=2]  k_frame per-part timeline (diagnostic library, scripts/diag_frame.py), optional env
 #   ab:<lib1>,<lib2>  interleaved A/B of engine builds on the driver command (scripts/ab.sh)
@@ -60,6 +61,9 @@ for st in "$@"; do
            tail -1 $OUT/pytest_c5.log ;;
     shard8) timeout -k 10 300 python3 bench.py --no-cpu --steps 100 --width 1280 --height 720 --shard 8 > $OUT/shard8_c4.json 2> $OUT/shard8_c4.err || fail $st $OUT/shard8_c4.err
            line $OUT/shard8_c4.json ;;
+    raysq) bash scripts/profile_kernel_sq.sh $OUT/sq_ray k_raycast --loop c5 --steps 30 > $OUT/sq_ray.txt 2>&1 || fail $st $OUT/sq_ray.txt
+           python3 scripts/sq_json.py $OUT/sq_ray k_raycast "python3 bench.py --no-cpu --loop c5 --steps 30" 640 480 > $OUT/r4_raycast_sq.json
+           grep -E "VALU_per_wave|SALU_per_wave" $OUT/r4_raycast_sq.json ;;
     sq:*) k=${st#sq:}; bash scripts/profile_kernel_sq.sh $OUT/sq_$k $k > $OUT/sq_$k.txt 2>&1 || fail $st $OUT/sq_$k.txt
            tail -8 $OUT/sq_$k.txt ;;
     raydiag) TSDF_AMD_LIB=disinfect-slam_amd/libdisinfect_tsdf_diag.so timeout -k 10 180 python3 scripts/diag_raycast.py > $OUT/raycast_diag.txt 2>&1 || fail $st $OUT/raycast_diag.txt
