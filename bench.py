@@ -307,8 +307,8 @@ def raycast_roofline(a, us_call):
     VALU fraction shows how much issue bandwidth that chain leaves idle). The rate is taken over the
     whole call (view grid + bitmaps + k_raycast), so it is a lower bound for the kernel's own."""
     rays = a.width * a.height
-    out = {"kernel": "k_raycast", "bound": "VALU issue (~4.7 waves per SIMD stepping their rays; the lookups' "
-                                           "dependent loads second, DESIGN.md 4 Raycast)",
+    out = {"kernel": "k_raycast", "bound": "latency (each wave's ~31 lookup trips: a view-grid cell load, then "
+                                           "the voxel read, with ~4.7 waves per SIMD to hide them; DESIGN.md 4)",
            "us_per_call": round(us_call, 3), "rays_per_s": round(rays / (us_call * 1e-6), 1),
            "timing": "events around 50 back-to-back tsdf_raycast calls of the last timed camera, after the loop"}
     try:

@@ -364,22 +364,7 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
     return fmaxf(fmaxf(fmaf(q.x, sgn.x, ne.x), fmaf(q.y, sgn.y, ne.y)), fmaf(q.z, sgn.z, ne.z)) < 0.0f;
   };
   while (active) {
-    bool inside = in_region(pos);
-    // every active lane of the wave inside an empty region (most steps): a tight wave-uniform loop of
-    // steps that read +1 -- the additions and the exit-face test -- until some lane leaves its region
-    // (that step runs below) or the steps run out
-    if (__ballot(!inside || ridx >= 0) == 0ull) {
-      int iu = __builtin_amdgcn_readfirstlane(i);  // (the active lanes' step count is one value)
-      do {
-        pos = {pos.x + sg.x, pos.y + sg.y, pos.z + sg.z};
-        ++iu;
-        inside = in_region(pos);
-      } while (iu < max_step && __ballot(!inside) == 0ull);
-      i = iu;
-      prev = 1.0f;
-      active = iu < max_step;
-      continue;
-    }
+    const bool inside = in_region(pos);
 #ifdef TSDF_DIAG_STAMPS
     d_it += 1;
     d_blk += !inside;
