@@ -757,6 +757,12 @@ int launch_frame(tsdf_engine* e, PipeArgs A, const FrameParams& Pu, const FrameP
 }
 
 bool sharded(const tsdf_engine* e) { return e->cfg.shard_count > 1; }
+// Frames up to kPipeMaxPixels are pipelined (k_frame). Larger frames take the two launches: their
+// ingest (3,600 tiles at 1280x720) no longer fits beside the update in one launch's resident
+// workgroups, and the serialised launch is slower (C4, driver-size runs: 13.0-13.3k frames/s
+// pipelined against 14.6-14.8k in two launches; at 640x480 21.4k against 19.1k).
+constexpr int64_t kPipeMaxPixels = 1 << 19;
+bool pipe_frame_size(int w, int h) { return (int64_t)w * h <= kPipeMaxPixels; }
 
 // The k_frame launch that continues the pending frames, with (has_frame) the ingest of a new frame
 // fid whose parameters are Pn; the state moves to kPipeCAU (or kPipeAU from kPipeNone).
@@ -845,7 +851,7 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
     return TSDF_ERR_INVALID_ARG;
   }
   if (!e) return TSDF_ERR_INVALID_ARG;
-  const bool pipe = e->pipeline && e->maxs <= 3;
+  const bool pipe = e->pipeline && e->maxs <= 3 && pipe_frame_size(f->width, f->height);
   if (!pipe) {
     int rc = flush_pending(e);
     if (rc) return rc;
@@ -1202,7 +1208,7 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
   g->RH = render_height;
   // frames without a render camera pipeline like tsdf_integrate; a render camera needs each frame
   // complete before its raycast, so those graphs keep the two-launch frame
-  g->pipe = render_width == 0 && e->pipeline && e->maxs <= 3;
+  g->pipe = render_width == 0 && e->pipeline && e->maxs <= 3 && pipe_frame_size(width, height);
   auto fail = [&](hipError_t err, const char* what) {
     set_error(what, err);
     graph_free(g);
