@@ -518,8 +518,9 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_pre, reinterpret_cast<const void*>(k_frame),
                                                      kIntegrateThreads, 0) != hipSuccess)
       return fail(TSDF_ERR_HIP);
-    // 5 update workgroups per CU by default (of 7 that fit): the other slots take the sweep's and the
-    // tiles' workgroups from the start (measured: 21.2k frames/s against 18.7k at 7, driver command)
+    // 3 update workgroups per CU by default (of 7 that fit): the other slots take the sweep's and the
+    // tiles' workgroups from the start (driver command, same box: 22.3-22.5k frames/s at 3, 22.0-22.1k
+    // at 4, 21.0-21.3k at 5, 18.5-18.7k at 7, 17.9-18.1k at 2; 300 frames: 24.0k at 3 and at 5)
     int want = kFrameWgPerCu;
     if (const char* v = std::getenv("TSDF_FRAME_WG_PER_CU")) want = std::max(1, std::atoi(v));
     per_cu_pre = std::min(per_cu_pre, want);
