@@ -117,8 +117,9 @@ typedef struct tsdf_profile { /* device time of the integrate phases between beg
   double ms_ingest_device;          /* k_ingest_dda start -> its last workgroup's arrival */
   double ms_resolve_alloc_device;   /* ordered allocation resolve (VoxelHashTable::Allocate) */
   double ms_resolve_delete_device;  /* ordered carving resolve (VoxelHashTable::Delete) */
-  int64_t pipelined;   /* update launches that also prepared the next frame's pixel tiles
-                          (k_integrate_pre; their events / device clock include that work) */
+  int64_t pipelined;   /* pipelined frame launches (k_frame: the previous frame's carving, this
+                          frame's allocation and update, the next frame's ingest; their events /
+                          device clock include that work) */
 } tsdf_profile;
 
 /* ---- engine lifetime: TSDFGrid::TSDFGrid / ~TSDFGrid (voxel_tsdf.cu:309-345) ---- */
