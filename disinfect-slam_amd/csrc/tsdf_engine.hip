@@ -133,6 +133,7 @@ struct tsdf_engine {
   int32_t* m_counts = nullptr;
   int32_t* m_offsets = nullptr;
   int64_t* m_total = nullptr;
+  int mesh_grid = 0;            // k_mesh workgroups: min(kMeshGrid, pool blocks)
   float* m_out = nullptr;
   int64_t m_out_cap = 0;  // triangles
   int16_t* t_keys = nullptr;
@@ -550,6 +551,8 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(e->m_counts, nb);
   ALLOC(e->m_offsets, nb);
   ALLOC(e->m_total, 1);
+  e->mesh_grid = std::min(kMeshGrid, nb);
+  if (const char* v = std::getenv("TSDF_MESH_GRID")) e->mesh_grid = std::max(1, std::min(e->mesh_grid, std::atoi(v)));  // tests
   ALLOC(e->t_count, 1);
 #undef ALLOC
   D = frame_view(D, 0u);  // the base view (sharded / graph / hash-level paths): frame parity 0
@@ -2050,43 +2053,43 @@ int extract_mesh_impl(tsdf_engine* e, const float* bounds, float missing_tsdf, i
   hipLaunchKernelGGL(k_vis_emit, dim3(kOccWords / 256), dim3(256), 0, s, e->D, e->q_sel,
                      e->q_count);
   LAUNCH_OK("mesh select");
-  int32_t nsel = 0;
-  HIP_OK(hipMemcpyAsync(&nsel, e->q_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  HIP_OK(hipStreamSynchronize(s));
-  *num_triangles = 0;
-  if (nsel == 0) return TSDF_OK;
+  // selection, count, scan and (device output) emission enqueued back to back: the kernels read
+  // the selected-block count and the triangle total from device memory, and the host reads the
+  // total once at the end (a host output needs it first, to size the staging buffer)
   const MeshParams M{e->cfg.voxel_size, missing_tsdf, min_weight, own_index, own_count};
-  hipLaunchKernelGGL(k_mesh<false>, dim3(nsel), dim3(256), 0, s, e->D, e->q_sel, M, e->m_counts,
-                     (const int32_t*)nullptr, (float*)nullptr);
-  hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, e->m_counts, nsel, e->m_offsets,
+  hipLaunchKernelGGL(k_mesh<false>, dim3(e->mesh_grid), dim3(256), 0, s, e->D, e->q_sel, e->q_count, M,
+                     e->m_counts, (const int32_t*)nullptr, (const int64_t*)nullptr, (int64_t)0, (float*)nullptr);
+  hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, e->m_counts, e->q_count, e->m_offsets,
                      e->m_total);
   LAUNCH_OK("mesh count");
+  const bool dev_out = triangles && mem_kind == TSDF_MEM_DEVICE;
+  if (dev_out) {
+    hipLaunchKernelGGL(k_mesh<true>, dim3(e->mesh_grid), dim3(256), 0, s, e->D, e->q_sel, e->q_count, M,
+                       (int32_t*)nullptr, (const int32_t*)e->m_offsets, (const int64_t*)e->m_total, capacity,
+                       reinterpret_cast<float*>(triangles));
+    LAUNCH_OK("mesh emit");
+  }
   int64_t ntri = 0;
   HIP_OK(hipMemcpyAsync(&ntri, e->m_total, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
   *num_triangles = ntri;
   if (!triangles || ntri == 0) return TSDF_OK;
-  if (capacity < ntri) {
+  if (capacity < ntri) {  // (device output: the emit pass wrote nothing)
     set_error("tsdf_extract_mesh: capacity too small");
     return TSDF_ERR_CAPACITY;
   }
-  float* dst = reinterpret_cast<float*>(triangles);
-  if (mem_kind == TSDF_MEM_HOST) {
-    if (e->m_out_cap < ntri) {
-      if (e->m_out) (void)hipFree(e->m_out);
-      e->m_out = nullptr;
-      e->m_out_cap = 0;
-      HIP_OK(dmalloc(&e->m_out, (size_t)ntri * 9));
-      e->m_out_cap = ntri;
-    }
-    dst = e->m_out;
+  if (dev_out) return TSDF_OK;
+  if (e->m_out_cap < ntri) {
+    if (e->m_out) (void)hipFree(e->m_out);
+    e->m_out = nullptr;
+    e->m_out_cap = 0;
+    HIP_OK(dmalloc(&e->m_out, (size_t)ntri * 9));
+    e->m_out_cap = ntri;
   }
-  hipLaunchKernelGGL(k_mesh<true>, dim3(nsel), dim3(256), 0, s, e->D, e->q_sel, M,
-                     (int32_t*)nullptr, (const int32_t*)e->m_offsets, dst);
+  hipLaunchKernelGGL(k_mesh<true>, dim3(e->mesh_grid), dim3(256), 0, s, e->D, e->q_sel, e->q_count, M,
+                     (int32_t*)nullptr, (const int32_t*)e->m_offsets, (const int64_t*)e->m_total, ntri, e->m_out);
   LAUNCH_OK("mesh emit");
-  if (mem_kind == TSDF_MEM_HOST)
-    HIP_OK(hipMemcpyAsync(triangles, e->m_out, (size_t)ntri * 9 * sizeof(float),
-                          hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(triangles, e->m_out, (size_t)ntri * 9 * sizeof(float), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
   return TSDF_OK;
 }

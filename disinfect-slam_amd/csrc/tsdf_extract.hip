@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void k_vis_emit(EngineDev D, VisRec* __restric
   const int w = blockIdx.x * 256 + threadIdx.x;
   unsigned long long v = D.visbits[w];
   int blk_total;
-  int pos = base + block_excl_scan(__popcll(v), scan_scratch, &blk_total);
+  int pos = base + block_excl_scan<4>(__popcll(v), scan_scratch, &blk_total);
   while (v) {
     const int b = __ffsll((long long)v) - 1;
     v &= v - 1;

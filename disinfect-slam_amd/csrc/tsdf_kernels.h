@@ -241,10 +241,15 @@ struct MeshParams {
   int own_index, own_count;  // own_count > 1: only blocks whose brick owner is own_index emit (a
                              // shard's part of a sharded mesh; the other selected blocks are its halo)
 };
+// k_mesh / k_scan_counts read the selected-block count from device memory (*nsel, written by
+// k_vis_emit), so a whole extraction is enqueued without a host round trip: k_mesh runs
+// min(kMeshGrid, pool blocks) workgroups, one selected block each (the rest exit) and grid-stride
+// past kMeshGrid; the emit pass writes nothing when the total exceeds `capacity` triangles.
+constexpr int kMeshGrid = 8192;
 template <bool Emit>
-__global__ void k_mesh(EngineDev D, const VisRec* sel, MeshParams M, int32_t* counts,
-                       const int32_t* offsets, float* out);
-__global__ void k_scan_counts(const int32_t* counts, int n, int32_t* offsets, int64_t* total);
+__global__ void k_mesh(EngineDev D, const VisRec* sel, const int32_t* nsel, MeshParams M, int32_t* counts,
+                       const int32_t* offsets, const int64_t* total, int64_t capacity, float* out);
+__global__ void k_scan_counts(const int32_t* counts, const int32_t* nsel, int32_t* offsets, int64_t* total);
 __global__ void k_raycast(EngineDev D, FrameParams P, float step_size, ViewGrid V, uchar4* rgba,
                           uchar4* normal);
 // view grid of a raycast: grid kOccWords / 256 workgroups of 256

@@ -694,12 +694,14 @@ class Engine:
         fn = lambda ptr, cap, n, kind: L.tsdf_extract_mesh_owned(self._h, _ptr(b), missing_tsdf, min_weight,
                                                                  oi, oc, ptr, cap, C.byref(n), kind)
         n = C.c_int64()
-        _lib.check(fn(None, 0, n, TSDF_MEM_HOST), "tsdf_extract_mesh")
-        if out is not None:
+        if out is not None:  # one call: count, scan and emission enqueued together, one host read
+            if not (_is_torch_cuda(out) and out.is_contiguous() and str(out.dtype) == "torch.float32"):
+                raise ValueError("out must be a contiguous float32 device tensor")
             self._wait_torch(out)
             _lib.check(fn(_ptr(out), out.numel() // 9, n, TSDF_MEM_DEVICE), "tsdf_extract_mesh")
             self._signal_torch(out)
             return out[:9 * n.value].view(-1, 3, 3)
+        _lib.check(fn(None, 0, n, TSDF_MEM_HOST), "tsdf_extract_mesh")
         tris = np.zeros((n.value, 3, 3), np.float32)
         if n.value:
             _lib.check(fn(_ptr(tris), n.value, n, TSDF_MEM_HOST), "tsdf_extract_mesh")

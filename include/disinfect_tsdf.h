@@ -329,7 +329,9 @@ int tsdf_extract_mesh_owned(tsdf_engine* e, const float* bounds, float missing_t
  * missing_tsdf (KrisLibrary defaultValue = truncation distance; 0.99 ~ the reference's auto
  * value). Output: triangles[9 * i .. 9 * i + 8] = three xyz vertices, normals (right-hand
  * rule) toward increasing tsdf; deterministic order (blocks in hash-entry order). Two-call:
- * triangles == NULL returns the count only. mem_kind: where `triangles` lives. */
+ * triangles == NULL returns the count only. mem_kind: where `triangles` lives. A device
+ * `triangles` buffer may be passed in ONE call: *num_triangles is always set, and when it
+ * exceeds capacity nothing is written and TSDF_ERR_CAPACITY is returned. */
 int tsdf_extract_mesh(tsdf_engine* e, const float* bounds, float missing_tsdf, int min_weight,
                       float* triangles, int64_t capacity, int64_t* num_triangles, int mem_kind);
 

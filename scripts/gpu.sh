@@ -13,6 +13,7 @@
 #   c5tests           the raycast / render / C5 GPU tests
 #   shard8            bench.py --width 1280 --height 720 --shard 8 (single-GPU 8-shard rehearsal)
 #   sq:<kernel>       SQ counter passes of one kernel on the default command (profile_kernel_sq.sh)
+#   c5trace|c5gtrace  kernel trace (eager / graph) of the C5 loop -> per-frame kernel chain and gaps (scripts/chain_timeline.py)
 #   raysq             SQ / FETCH / WRITE passes of k_raycast on the C5 loop -> <tag>/r4_raycast_sq.json
 #   raydiag           raycast step statistics and wave lifetimes (diagnostic library, scripts/diag_raycast.py)
 #   framediag[:A=1,B=2]  k_frame per-part timeline (diagnostic library, scripts/diag_frame.py), optional env
@@ -62,6 +63,9 @@ for st in "$@"; do
            tail -1 $OUT/pytest_c5.log ;;
     shard8) timeout -k 10 300 python3 bench.py --no-cpu --steps 100 --width 1280 --height 720 --shard 8 > $OUT/shard8_c4.json 2> $OUT/shard8_c4.err || fail $st $OUT/shard8_c4.err
            line $OUT/shard8_c4.json ;;
+    c5trace|c5gtrace) g=; [ $st = c5gtrace ] && g=--graph
+           timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$st -o run -- python3 bench.py --no-cpu --loop c5 --steps 120 $g > $OUT/$st.log 2>&1 || fail $st $OUT/$st.log
+           python3 scripts/chain_timeline.py $OUT/$st "k_ingest_dda|k_frame|k_copy_words" > $OUT/${st}_chain.txt && tail -30 $OUT/${st}_chain.txt ;;
     raysq) bash scripts/profile_kernel_sq.sh $OUT/sq_ray k_raycast --loop c5 --steps 30 > $OUT/sq_ray.txt 2>&1 || fail $st $OUT/sq_ray.txt
            python3 scripts/sq_json.py $OUT/sq_ray k_raycast "python3 bench.py --no-cpu --loop c5 --steps 30" 640 480 > $OUT/r4_raycast_sq.json
            grep -E "VALU_per_wave|SALU_per_wave" $OUT/r4_raycast_sq.json ;;

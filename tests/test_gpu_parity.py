@@ -171,11 +171,14 @@ def test_pool_exhaustion_is_reported():
         eng.close(), ora.close()
 
 
-@pytest.mark.parametrize("min_weight,bounded", [(0, False), (1, False), (1, True)])
-def test_marching_cubes_matches_oracle(min_weight, bounded):
+@pytest.mark.parametrize("min_weight,bounded,grid", [(0, False, 0), (1, False, 0), (1, True, 0), (0, False, 7)])
+def test_marching_cubes_matches_oracle(min_weight, bounded, grid, monkeypatch):
     """GPU marching cubes (tsdf_extract_mesh) == the oracle's restatement, bit for bit and in
-    the same order (KrisLibrary itself is absent: parity unpinned)."""
+    the same order (KrisLibrary itself is absent: parity unpinned). grid: k_mesh
+    workgroups (TSDF_MESH_GRID; 7 walks the selection grid-stride, as selections past kMeshGrid do)."""
     import tsdf_amd
+    if grid:
+        monkeypatch.setenv("TSDF_MESH_GRID", str(grid))
     eng, ora, cam = run_sequence(96, 72, 0.01, 0.04, 4, nb_bits=13, check_every=4)
     try:
         bounds = None
@@ -189,5 +192,17 @@ def test_marching_cubes_matches_oracle(min_weight, bounded):
         assert exp.shape[0] > (20 if bounded else 100)
         assert got.shape == exp.shape
         np.testing.assert_array_equal(got.view(np.uint32), exp.view(np.uint32))
+        # the one-call device form (count, scan and emission enqueued together) gives the same
+        # triangles; too small a buffer raises and is left untouched
+        import torch
+        n = exp.shape[0]
+        out = torch.full((9 * n + 90,), -7.0, dtype=torch.float32, device="cuda")
+        dev = eng.extract_mesh(bounds, 0.99, min_weight, out=out)
+        np.testing.assert_array_equal(dev.cpu().numpy().view(np.uint32), exp.view(np.uint32))
+        assert bool((out[9 * n:] == -7.0).all())
+        small = torch.full((9 * (n - 1),), -7.0, dtype=torch.float32, device="cuda")
+        with pytest.raises(tsdf_amd._lib.TSDFError):
+            eng.extract_mesh(bounds, 0.99, min_weight, out=small)
+        assert bool((small == -7.0).all())
     finally:
         eng.close(), ora.close()
