@@ -133,6 +133,7 @@ struct tsdf_engine {
   int32_t* m_counts = nullptr;
   int32_t* m_offsets = nullptr;
   int64_t* m_total = nullptr;
+  int32_t* m_nbr = nullptr;     // k_mesh: 27 neighbour pool indices per selected block
   int mesh_grid = 0;            // k_mesh workgroups: min(kMeshGrid, pool blocks)
   float* m_out = nullptr;
   int64_t m_out_cap = 0;  // triangles
@@ -198,7 +199,7 @@ void free_all(tsdf_engine* e) {
                   D.vis,     D.band,    D.cand,     D.arrive, D.swdirty, D.fresh_vis, D.pend, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
                   e->vg_cell, e->vg_flags, e->vg_bits, e->g_visbits, e->g_wgcnt, e->g_sel, e->g_count,
-                  e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
+                  e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_nbr, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
                   e->t_i32,  e->t_u32,   e->t_f0,    e->t_f1,   e->t_s4};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -551,6 +552,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(e->m_counts, nb);
   ALLOC(e->m_offsets, nb);
   ALLOC(e->m_total, 1);
+  ALLOC(e->m_nbr, (size_t)27 * nb);
   e->mesh_grid = std::min(kMeshGrid, nb);
   if (const char* v = std::getenv("TSDF_MESH_GRID")) e->mesh_grid = std::max(1, std::min(e->mesh_grid, std::atoi(v)));  // tests
   ALLOC(e->t_count, 1);
@@ -2058,14 +2060,14 @@ int extract_mesh_impl(tsdf_engine* e, const float* bounds, float missing_tsdf, i
   // total once at the end (a host output needs it first, to size the staging buffer)
   const MeshParams M{e->cfg.voxel_size, missing_tsdf, min_weight, own_index, own_count};
   hipLaunchKernelGGL(k_mesh<false>, dim3(e->mesh_grid), dim3(256), 0, s, e->D, e->q_sel, e->q_count, M,
-                     e->m_counts, (const int32_t*)nullptr, (const int64_t*)nullptr, (int64_t)0, (float*)nullptr);
+                     e->m_counts, (const int32_t*)nullptr, (const int64_t*)nullptr, (int64_t)0, e->m_nbr, (float*)nullptr);
   hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, e->m_counts, e->q_count, e->m_offsets,
                      e->m_total);
   LAUNCH_OK("mesh count");
   const bool dev_out = triangles && mem_kind == TSDF_MEM_DEVICE;
   if (dev_out) {
     hipLaunchKernelGGL(k_mesh<true>, dim3(e->mesh_grid), dim3(256), 0, s, e->D, e->q_sel, e->q_count, M,
-                       (int32_t*)nullptr, (const int32_t*)e->m_offsets, (const int64_t*)e->m_total, capacity,
+                       e->m_counts, (const int32_t*)e->m_offsets, (const int64_t*)e->m_total, capacity, e->m_nbr,
                        reinterpret_cast<float*>(triangles));
     LAUNCH_OK("mesh emit");
   }
@@ -2087,7 +2089,7 @@ int extract_mesh_impl(tsdf_engine* e, const float* bounds, float missing_tsdf, i
     e->m_out_cap = ntri;
   }
   hipLaunchKernelGGL(k_mesh<true>, dim3(e->mesh_grid), dim3(256), 0, s, e->D, e->q_sel, e->q_count, M,
-                     (int32_t*)nullptr, (const int32_t*)e->m_offsets, (const int64_t*)e->m_total, ntri, e->m_out);
+                     e->m_counts, (const int32_t*)e->m_offsets, (const int64_t*)e->m_total, ntri, e->m_nbr, e->m_out);
   LAUNCH_OK("mesh emit");
   HIP_OK(hipMemcpyAsync(triangles, e->m_out, (size_t)ntri * 9 * sizeof(float), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));

@@ -244,11 +244,13 @@ struct MeshParams {
 // k_mesh / k_scan_counts read the selected-block count from device memory (*nsel, written by
 // k_vis_emit), so a whole extraction is enqueued without a host round trip: k_mesh runs
 // min(kMeshGrid, pool blocks) workgroups, one selected block each (the rest exit) and grid-stride
-// past kMeshGrid; the emit pass writes nothing when the total exceeds `capacity` triangles.
+// past kMeshGrid; the emit pass writes nothing when the total exceeds `capacity` triangles. The count
+// pass keeps each block's 27 neighbour pool indices in nbr (27 per selected block) and its triangle
+// count in counts; the emit pass reads both (no hash probes, blocks without triangles skipped).
 constexpr int kMeshGrid = 8192;
 template <bool Emit>
 __global__ void k_mesh(EngineDev D, const VisRec* sel, const int32_t* nsel, MeshParams M, int32_t* counts,
-                       const int32_t* offsets, const int64_t* total, int64_t capacity, float* out);
+                       const int32_t* offsets, const int64_t* total, int64_t capacity, int32_t* nbr, float* out);
 __global__ void k_scan_counts(const int32_t* counts, const int32_t* nsel, int32_t* offsets, int64_t* total);
 __global__ void k_raycast(EngineDev D, FrameParams P, float step_size, ViewGrid V, uchar4* rgba,
                           uchar4* normal);

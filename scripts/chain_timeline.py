@@ -1,46 +1,48 @@
 #!/usr/bin/env python3
-"""Per-frame kernel chain of a rocprofv3 kernel trace (diagnostic): for every kernel name its mean
-duration and the mean idle gap before it (the previous dispatch's end -> its start), over the last
-half of the trace (the timed frames), plus the total busy / idle time per frame.
-Usage: chain_timeline.py <rocprofv3 output dir> [frame-kernel regex]"""
+"""Per-frame kernel chain of a rocprofv3 kernel trace of a frame loop (diagnostic).
+
+A frame starts at each dispatch of its first kernel (regex, default k_ingest_dda / k_frame /
+k_copy_words); frames holding only engine kernels (k_* and the runtime's copies) are kept. Prints
+the frame period (median over the plain frames, and each marching-cubes frame's period with its
+kernels) and, per kernel, the median duration in the plain frames.
+Usage: chain_timeline.py <rocprofv3 output dir> [first-kernel regex]"""
 import csv
 import glob
 import re
+import statistics as st
 import sys
 from collections import defaultdict
 
 
+def short(n):
+    return re.sub(r"\(.*", "", n).replace("tsdf::", "").replace("void ", "")
+
+
 def main():
     d = sys.argv[1]
-    first = re.compile(sys.argv[2] if len(sys.argv) > 2 else r"k_ingest_dda|k_frame")
+    first = re.compile(sys.argv[2] if len(sys.argv) > 2 else r"k_ingest_dda|k_frame|k_copy_words")
     f = sorted(glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True))[0]
-    rows = []
-    with open(f) as fh:
-        for r in csv.DictReader(fh):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
-    rows.sort()
-    rows = rows[len(rows) // 2:]
-    short = lambda n: re.sub(r"\(.*", "", n).replace("tsdf::", "").replace("void ", "")
-    dur, gap, cnt = defaultdict(float), defaultdict(float), defaultdict(int)
-    nfr = sum(1 for r in rows if first.search(r[2]))
-    prev = None
-    busy = idle = 0
-    for s, e, n in rows:
-        k = short(n)
-        dur[k] += (e - s) / 1e3
-        cnt[k] += 1
-        if prev is not None:
-            g = max(0, s - prev) / 1e3
-            gap[k] += g
-            idle += g
-        busy += (e - s) / 1e3 if prev is None or s >= prev else max(0, e - prev) / 1e3
-        prev = max(prev or 0, e)
-    print(f"{f}\n{len(rows)} dispatches, {nfr} frames (first kernel /{first.pattern}/)")
-    print(f"{'kernel':>40} {'per frame':>9} {'mean us':>8} {'gap us':>7} {'us/frame':>9}")
-    for k in sorted(dur, key=lambda k: -dur[k]):
-        print(f"{k[:40]:>40} {cnt[k] / max(nfr, 1):9.2f} {dur[k] / cnt[k]:8.2f} {gap[k] / cnt[k]:7.2f} "
-              f"{dur[k] / max(nfr, 1):9.2f}")
-    print(f"per frame: busy {busy / max(nfr, 1):.1f} us, idle {idle / max(nfr, 1):.1f} us")
+    rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]))
+                  for r in csv.DictReader(open(f)))
+    idx = [i for i, r in enumerate(rows) if first.match(r[2])]
+    engine = lambda n: n.startswith("k_") or n.startswith("__amd_rocclr_copy")
+    segs = [rows[a:b] for a, b in zip(idx, idx[1:]) if all(engine(r[2]) for r in rows[a:b])]
+    plain_len = st.mode(len(s) for s in segs)
+    plain = [s for s in segs if len(s) == plain_len]
+    print(f"{f}: {len(idx)} frames, {len(plain)} plain frames of {plain_len} dispatches")
+    per = [(s[-1][1] - s[0][0]) / 1e3 for s in plain]
+    print(f"plain frame, first start -> last end: median {st.median(per):.1f} us")
+    dur = defaultdict(list)
+    for s in plain:
+        for a, b, n in s:
+            dur[n].append((b - a) / 1e3)
+    for n, v in dur.items():
+        print(f"  {n[:40]:>40}  {st.median(v):7.1f} us")
+    for a, b in zip(idx, idx[1:]):
+        s = rows[a:b]
+        if len(s) > plain_len and all(engine(r[2]) for r in s):
+            extra = "  ".join(f"{n[:14]}={(e - t) / 1e3:.1f}" for t, e, n in s[plain_len:])
+            print(f"mesh frame: period {(rows[b][0] - rows[a][0]) / 1e3:.0f} us; {extra}")
 
 
 if __name__ == "__main__":

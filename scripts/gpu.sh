@@ -65,7 +65,7 @@ for st in "$@"; do
            line $OUT/shard8_c4.json ;;
     c5trace|c5gtrace) g=; [ $st = c5gtrace ] && g=--graph
            timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$st -o run -- python3 bench.py --no-cpu --loop c5 --steps 120 $g > $OUT/$st.log 2>&1 || fail $st $OUT/$st.log
-           python3 scripts/chain_timeline.py $OUT/$st "k_ingest_dda|k_frame|k_copy_words" > $OUT/${st}_chain.txt && tail -30 $OUT/${st}_chain.txt ;;
+           python3 scripts/chain_timeline.py $OUT/$st > $OUT/${st}_chain.txt && tail -30 $OUT/${st}_chain.txt ;;
     raysq) bash scripts/profile_kernel_sq.sh $OUT/sq_ray k_raycast --loop c5 --steps 30 > $OUT/sq_ray.txt 2>&1 || fail $st $OUT/sq_ray.txt
            python3 scripts/sq_json.py $OUT/sq_ray k_raycast "python3 bench.py --no-cpu --loop c5 --steps 30" 640 480 > $OUT/r4_raycast_sq.json
            grep -E "VALU_per_wave|SALU_per_wave" $OUT/r4_raycast_sq.json ;;
