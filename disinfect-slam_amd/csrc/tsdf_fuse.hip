@@ -778,11 +778,27 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
 // sweep workgroups -- each part only when the launch has it
 // (diagnostic build: each workgroup's part code, start and end into D.dbg kernel 8 -- 1 head, 2 fresh
 // update, 3 listed update, 4 tile, 5 sweep; the head's carving / allocation ends at 3 / 4)
+// Wave priorities of the parts (s_setprio: the SIMD's issue arbitration among its waves): the head
+// (carving and allocation, which the fresh updates and the tiles' probes wait for) highest, the
+// update (the launch's critical path) next, the tiles and the sweep lowest. Driver command, same
+// box, interleaved (scripts/ab.sh lib, 4 runs each): 22.63k frames/s against 22.36k without
+// priorities; head 3 / update 3 and head 3 / update 1 alike within noise; tiles above the update
+// 19.6-19.9k. Experiment builds override them (-DTSDF_PRIO_HEAD=0 ...; 0 = no s_setprio).
+#ifndef TSDF_PRIO_HEAD
+#define TSDF_PRIO_HEAD 3
+#endif
+#ifndef TSDF_PRIO_UPD
+#define TSDF_PRIO_UPD 2
+#endif
+#ifndef TSDF_PRIO_TILE
+#define TSDF_PRIO_TILE 0
+#endif
 __device__ __forceinline__ int frame_part(const EngineDev& D, const FrameParams& Pu, const FrameParams& Pn,
                                           const PipeArgs& A, FrameLds& U) {
   int w = (int)blockIdx.x;
   if (w < kPipeHead) {
     if (w != 0) return 0;
+    if (TSDF_PRIO_HEAD) __builtin_amdgcn_s_setprio(TSDF_PRIO_HEAD);
     pipe_head(D, Pu, A, U);
     return 1;
   }
@@ -791,6 +807,7 @@ __device__ __forceinline__ int frame_part(const EngineDev& D, const FrameParams&
     wait_tag(D.pipe + kPipeAlloc + (blockIdx.x & 7) * 16, A.tag, &D.ctr->status);
   const int nfr = pipe_fresh_wgs(A);
   if (w < nfr) {  // the blocks this launch's allocation creates (they wait for it: dispatched early)
+    if (TSDF_PRIO_UPD) __builtin_amdgcn_s_setprio(TSDF_PRIO_UPD);
     pipe_update(D, Pu, A, 1, w);
     return 2;
   }
@@ -814,9 +831,11 @@ __device__ __forceinline__ int frame_part(const EngineDev& D, const FrameParams&
   if (part == 0) {
     // (its XCD split takes o % 8 as the XCD: exact when the parts before it are multiples of 8 long,
     // as at 640x480; correct either way)
+    if (TSDF_PRIO_UPD) __builtin_amdgcn_s_setprio(TSDF_PRIO_UPD);
     pipe_update(D, Pu, A, 0, o);
     return 3;
   }
+  if (TSDF_PRIO_TILE) __builtin_amdgcn_s_setprio(TSDF_PRIO_TILE);
   const unsigned long long* aflag = D.pipe + kPipeAlloc + (blockIdx.x & 7) * 16;
   if (part == 1)
     ingest_tile<1024, kTileChained>(D, Pn, Pn.depth, Pn.rgb, Pn.ht, Pn.lt, A.tiles_x, o, U.ing, aflag, A.tag,
