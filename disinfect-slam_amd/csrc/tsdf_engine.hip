@@ -169,6 +169,7 @@ struct tsdf_engine {
   // allocation and update are pending (p_fid's tiles probed and inserted its keys, its sweep listed
   // its blocks). Every other entry point first completes them (flush_pending).
   bool pipeline = true;
+  int64_t pipe_max_pixels = (int64_t)1 << 19;  // larger frames take two launches (pipe_frame_size)
   static constexpr int kPipeNone = 0, kPipeU = 1, kPipeCAU = 2, kPipeAU = 3, kPipeC = 4;  // kPipeAU:
   // p_fid's allocation and update are pending with no carving (after a graph frame that started a
   // stream); kPipeC: only p_fid's carving is pending (a shard's pipelined frames, between flush steps)
@@ -531,6 +532,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.pixA, 2 * e->max_pixels);  // two buffers: a pipelined frame's and the next one's
   ALLOC(D.pixB, 2 * e->max_pixels);
   if (const char* v = std::getenv("TSDF_PIPELINE")) e->pipeline = v[0] != '0';
+  if (const char* v = std::getenv("TSDF_PIPE_MAX_PIXELS")) e->pipe_max_pixels = std::atoll(v);  // tuning
   if (const char* v = std::getenv("TSDF_FRAME_ORDER")) e->frame_order = std::min(4, std::max(0, std::atoi(v)));
   ALLOC(D.visbits, kOccWords);
   ALLOC(D.wgcnt, kOccWords / 256);
@@ -763,12 +765,11 @@ int launch_frame(tsdf_engine* e, PipeArgs A, const FrameParams& Pu, const FrameP
 }
 
 bool sharded(const tsdf_engine* e) { return e->cfg.shard_count > 1; }
-// Frames up to kPipeMaxPixels are pipelined (k_frame). Larger frames take the two launches: their
+// Frames up to pipe_max_pixels (2^19; TSDF_PIPE_MAX_PIXELS) are pipelined (k_frame). Larger frames take the two launches: their
 // ingest (3,600 tiles at 1280x720) no longer fits beside the update in one launch's resident
 // workgroups, and the serialised launch is slower (C4, driver-size runs: 13.0-13.3k frames/s
 // pipelined against 14.6-14.8k in two launches; at 640x480 21.4k against 19.1k).
-constexpr int64_t kPipeMaxPixels = 1 << 19;
-bool pipe_frame_size(int w, int h) { return (int64_t)w * h <= kPipeMaxPixels; }
+bool pipe_frame_size(const tsdf_engine* e, int w, int h) { return (int64_t)w * h <= e->pipe_max_pixels; }
 
 // The k_frame launch that continues the pending frames, with (has_frame) the ingest of a new frame
 // fid whose parameters are Pn; the state moves to kPipeCAU (or kPipeAU from kPipeNone).
@@ -857,7 +858,7 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
     return TSDF_ERR_INVALID_ARG;
   }
   if (!e) return TSDF_ERR_INVALID_ARG;
-  const bool pipe = e->pipeline && e->maxs <= 3 && pipe_frame_size(f->width, f->height);
+  const bool pipe = e->pipeline && e->maxs <= 3 && pipe_frame_size(e, f->width, f->height);
   if (!pipe) {
     int rc = flush_pending(e);
     if (rc) return rc;
@@ -1214,7 +1215,7 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
   g->RH = render_height;
   // frames without a render camera pipeline like tsdf_integrate; a render camera needs each frame
   // complete before its raycast, so those graphs keep the two-launch frame
-  g->pipe = render_width == 0 && e->pipeline && e->maxs <= 3 && pipe_frame_size(width, height);
+  g->pipe = render_width == 0 && e->pipeline && e->maxs <= 3 && pipe_frame_size(e, width, height);
   auto fail = [&](hipError_t err, const char* what) {
     set_error(what, err);
     graph_free(g);
