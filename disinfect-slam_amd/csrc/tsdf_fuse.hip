@@ -143,6 +143,7 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
   const int32_t pidx = r.idx;
   uint8_t* blk = D.pool + (size_t)pidx * kBlockBytes;
 #if defined(TSDF_EXP) && (TSDF_EXP & 2)  // experiment build: no pool state loads
+  bool fresh;
   float4 ts = make_float4(0.5f, 0.5f, 0.5f, 0.5f), pr = ts;
   uint4 cw = make_uint4(0x05808080u, 0x05808080u, 0x05808080u, 0x05808080u);
 #else
@@ -601,6 +602,24 @@ __device__ __forceinline__ bool pipe_kept(uint32_t* rtag, int32_t idx, uint32_t 
   if (lane == 0) v = __hip_atomic_fetch_or(&rtag[idx], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return (uint32_t)__builtin_amdgcn_readfirstlane(v) != fc;
 }
+// wave_wait_tag: wait_tag for one wave (lane 0 polls; no workgroup barrier)
+__device__ __forceinline__ void wave_wait_tag(const unsigned long long* flag, uint32_t tag, uint32_t* status) {
+  if (lane_id() == 0) {
+    uint32_t n = 0;
+    while ((uint32_t)__hip_atomic_fetch_or(const_cast<unsigned long long*>(flag), 0ull, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT) != tag) {
+      __builtin_amdgcn_s_sleep(TSDF_PIPE_SLEEP);
+      if (++n > (1u << 22)) {
+        atomicOr(status, 64u);  // TSDF_STATUS_PIPELINE_TIMEOUT
+        break;
+      }
+    }
+  }
+}
+// pipe_kept for one record per lane (each lane's own atomic read of its block's release tag)
+__device__ __forceinline__ bool lane_kept(uint32_t* rtag, int32_t idx, uint32_t fc) {
+  return __hip_atomic_fetch_or(&rtag[idx], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != fc;
+}
 // (D: the base view; frame b's lists are addressed through scalar pointers here -- an EngineDev view
 // copied by value, or captured by reference in a lambda, can be materialised in scratch)
 __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParams& P, const PipeArgs& A, int kind, int wi) {
@@ -658,9 +677,84 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
   int my_upd = 0, my_vis = 0, ndef = 0;
   bool def_done = false;
   const bool fresh_co = kind != 0 || (after_alloc && !A.fresh_ready);  // (written in this launch)
+#ifndef TSDF_SERIAL_COLLECT
+  // the collection is wave 0's: one record per lane (its list record and candidate tag gathered
+  // together, two dependent round trips per collection instead of two per record), compacted into
+  // s_list by ballot; the deferred candidates' release tags likewise one per lane
+  __shared__ int s_n, s_ndef;
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  if (t0) s_ndef = 0;  // (ordered before its first read by the loop's barrier)
+#endif
   for (;;) {  // (all control flow below is workgroup-uniform; thread 0 writes the LDS lists)
     // ---- collect: the next records of the list walk, or (at its end) the deferred ones
     int n = 0;
+#ifndef TSDF_SERIAL_COLLECT
+    lds_barrier();  // (every wave has read the previous collection's s_n / s_ndef)
+    if (p < p_hi) {
+      const int npr = min((p_hi - p + pstep - 1) / pstep, kPipeList / 2);  // pairs in this collection
+      if (wave == 0) {
+        const int b = 2 * (p + (lane >> 1) * pstep) + (lane & 1);
+        const bool valid = lane < 2 * npr && b < nvis;
+        // the band of list index b: the last band whose start is <= b (starts non-decreasing)
+        int bd = 0, bs = 0;
+#pragma unroll
+        for (int k = 1; k < kBands; ++k) {
+          const int sk = __builtin_amdgcn_readlane(bst, k);
+          if (b >= sk) {
+            bd = k;
+            bs = sk;
+          }
+        }
+        VisRec r{};
+        if (valid) {
+          if (b >= nband)
+            r = fresh_co ? ld_rec_co(&D.fresh_vis[b - nband]) : D.fresh_vis[b - nband];
+          else
+            r = vis[(size_t)bd * D.nblocks + (size_t)(b - bs)];
+        }
+        const bool cand = valid && chk && r.pad == 0 && ct[r.idx] == fc;  // a candidate of frame b - 1
+        bool take = valid && !cand;
+        const unsigned long long cm = __ballot(cand);
+        if (cm) {
+          const int nc = __popcll(cm);
+          if (!carved_known && ndef + nc <= kPipeDefer) {  // deferred to the end
+            if (cand) s_def[ndef + __popcll(cm & lt_mask)] = r;
+            ndef += nc;
+          } else {
+            if (!carved_known) wave_wait_tag(carved, A.tag, &D.ctr->status);
+            carved_known = true;
+            if (cand) take = lane_kept(D.rtag, r.idx, fc);
+          }
+        }
+        const unsigned long long tm = __ballot(take);
+        if (take) s_list[__popcll(tm & lt_mask)] = r;
+        if (lane == 0) {
+          s_n = __popcll(tm);
+          s_ndef = ndef;
+        }
+      }
+      p += npr * pstep;
+    } else if (!def_done && s_ndef > 0) {  // (s_ndef: read before the next collection's barrier)
+      if (wave == 0) {
+        if (!carved_known) wave_wait_tag(carved, A.tag, &D.ctr->status);
+        carved_known = true;
+        bool take = false;
+        VisRec r{};
+        if (lane < ndef) {
+          r = s_def[lane];
+          take = lane_kept(D.rtag, r.idx, fc);
+        }
+        const unsigned long long tm = __ballot(take);
+        if (take) s_list[__popcll(tm & lt_mask)] = r;
+        if (lane == 0) s_n = __popcll(tm);
+      }
+      def_done = true;
+    } else {
+      break;
+    }
+    lds_barrier();  // (publishes s_list, s_n, s_ndef)
+    n = s_n;
+#else
     if (p < p_hi) {
       while (p < p_hi && n + 2 <= kPipeList) {
         for (int e = 0; e < 2; ++e) {
@@ -706,6 +800,16 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
       break;
     }
     lds_barrier();  // (publishes s_list)
+#endif
+#ifdef TSDF_DIAG_STAMPS
+    if (t0 && D.dbg && blockIdx.x < (unsigned)kDiagMaxWg) {  // collect ends: first (3), last (4); records (5)
+      unsigned long long* q = D.dbg + ((size_t)8 * kDiagMaxWg + blockIdx.x) * kDiagStamps;
+      const unsigned long long tnow = __builtin_amdgcn_s_memrealtime();
+      if (q[5] == 0ull) q[3] = tnow;
+      q[4] = tnow;
+      q[5] += (unsigned long long)n + 1ull;
+    }
+#endif
     // ---- update: the two pairs of waves take records 2 j + pair
     for (int j = 0; 2 * j < n; ++j) {
       const int k = 2 * j + pair;

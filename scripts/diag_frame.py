@@ -38,6 +38,7 @@ def main():
     buf = np.zeros(NK * NWG * NS, np.uint64)
     rows = {k: [] for k in PARTS}
     head = []
+    coll = []
     for i in range(nfr):
         torch.cuda.synchronize()
         L.tsdf_debug_stamps(eng._h, buf.ctypes.data, buf.size, None)  # (clears)
@@ -58,6 +59,11 @@ def main():
                 st, en_ = (S[m, 1] - t0) * 1e-2, (S[m, 2] - t0) * 1e-2
                 rows[k].append((m.sum(), np.median(st), st.max(), np.median(en_), np.percentile(en_, 90),
                                 en_.max(), np.median(en_ - st)))
+        m = S[:, 0] == 3
+        if m.any() and (S[m, 5] > 0).any():  # listed update: collect phases (first / last end), records
+            st = S[m, 1]
+            coll.append((np.median((S[m, 3] - st) * 1e-2), np.percentile((S[m, 3] - st) * 1e-2, 90),
+                         np.median((S[m, 4] - st) * 1e-2), np.median(S[m, 5] & 0xFFFF)))
         h = S[0]
         if h[0] == 1:
             head.append(((h[3] - t0) * 1e-2 if h[3] else np.nan, (h[4] - t0) * 1e-2 if h[4] else np.nan,
@@ -69,6 +75,10 @@ def main():
         if rows[k]:
             a = np.median(np.array(rows[k], dtype=float), axis=0)
             print(f"{name:>14} {a[0]:5.0f} {a[1]:9.1f} {a[2]:9.1f} {a[3]:8.1f} {a[4]:8.1f} {a[5]:8.1f} {a[6]:8.1f}")
+    if coll:
+        a = np.median(np.array(coll), axis=0)
+        print(f"listed update: first collect done {a[0]:.1f} (p90 {a[1]:.1f}), last collect done {a[2]:.1f} us "
+              f"after the workgroup start; records + collections {a[3]:.0f}")
     if head:
         a = np.nanmedian(np.array(head), axis=0)
         print(f"head: carving published {a[0]:.1f}, allocation published {a[1]:.1f}, head end {a[2]:.1f}")
