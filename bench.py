@@ -45,7 +45,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BLOCK_READ_BYTES = 512 * 12 + 12  # voxel state + metadata of one visible block
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_integrate_r4.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_integrate_r5.json")
 # SQ counters of k_raycast (rocprofv3 --pmc passes of `bench.py --loop c5`, scripts/profile_kernel_sq.sh)
 RAYCAST_SQ_FILE = os.path.join(ROOT, "profiles", "r4_raycast_sq.json")
 VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each
@@ -269,24 +269,30 @@ def pipe_fraction(prof):
     return prof.get("pipelined", 0) / max(prof.get("calls", 0), 1)
 
 
-def kernel_roofline(a, prof, n_frames):
-    """The frame launch: SURVEY.md 8(d) algorithmic bytes of ONE frame (every launch of the timed
-    window processes one frame's update, carving, allocation and ingest) / its average launch
-    duration (this rank):  N_vis * 6156 + N_upd * 12 + 15 W H  (12 W H depth-only). What the launch
-    moves beyond that -- the pixel records written by the ingest and gathered by the update, the next
-    frame's image, table probes, the occupancy bitmap -- is implementation traffic: it shows up in
-    roofline.traffic (rocprofv3 PMC), not here."""
+def kernel_roofline(a, prof, n_frames, pmc):
+    """The frame kernel: SURVEY.md 8(d) algorithmic bytes of ONE frame / its average launch duration
+    (this rank). Pipelined frames (k_frame: every launch of the timed window runs one frame's update,
+    carving and allocation and the next frame's ingest): N_vis * 6156 + N_upd * 12 + 15 W H (12 W H
+    depth-only). Unpipelined frames (k_integrate, e.g. the C5 loop, whose raycast reads every frame's
+    finished volume): N_vis * 6156 + N_upd * 12 -- the frame image is read by k_ingest_dda, not by this
+    kernel. What the launch moves beyond that (the pixel records, table probes, the occupancy bitmap)
+    is implementation traffic: roofline.traffic (rocprofv3 PMC). The duration is the mean over the
+    HIP start/stop events bound to the kernel's own dispatches; where none exist (graph-launched
+    frames) it is the timed-window kernel-trace mean of this same command committed under profiles/
+    (scripts/profile_integrate.sh), else unknown. Returns (read, write bytes, seconds, kind)."""
     W, H = a.width, a.height
-    img_bytes = (12 if a.depth_only else 15) * W * H
-    alg = (prof["sum_visible"] * BLOCK_READ_BYTES + prof["sum_updated"] * 12) / n_frames + img_bytes
-    if a.graph or a.no_events or prof["frames"] == 0:  # no dispatch event: the device clock
-        t = prof["ms_integrate_device"] / n_frames / 1e3
-        kind = "in-kernel device clock (first-workgroup start -> last arrival)"
-    else:
+    img_bytes = ((12 if a.depth_only else 15) * W * H) if pipe_fraction(prof) > 0 else 0
+    alg_read = prof["sum_visible"] * BLOCK_READ_BYTES / n_frames + img_bytes
+    alg_write = prof["sum_updated"] * 12 / n_frames
+    t, kind = None, "no kernel duration (no dispatch events and no committed trace of this command)"
+    if prof["frames"] > 0 and not a.no_events:
         t = prof["ms_integrate"] / prof["frames"] / 1e3
         kind = "HIP events bound to the frame kernel's dispatch (hipExtLaunchKernel), engine stream"
-    achieved = alg / t / 1e9 if t > 0 else 0.0
-    return alg, t, achieved, kind
+    elif pmc is not None and pmc.get("trace_kernel_avg_us"):
+        t = pmc["trace_kernel_avg_us"] * 1e-6
+        kind = ("rocprofv3 kernel trace of this command, timed-window mean of " + pmc.get("trace_kernel", "?") +
+                " (" + os.path.relpath(PMC_FILE, ROOT) + ")")
+    return alg_read, alg_write, t, kind
 
 
 def implementation_bytes(a, prof):
@@ -416,9 +422,12 @@ def main():
     W, H = a.width, a.height
     img_bytes = (12 if a.depth_only else 15) * W * H
 
-    # ---- kernel-level roofline (this rank's k_integrate) ----
-    alg, t_int, achieved, ev_kind = kernel_roofline(a, prof, a.steps)
+    # ---- kernel-level roofline (this rank's frame kernel) ----
     pmc, pmc_src = pmc_traffic(a, mode, world, prof)
+    alg_r, alg_w, t_int, ev_kind = kernel_roofline(a, prof, a.steps, pmc)
+    alg = alg_r + alg_w
+    achieved = alg / t_int / 1e9 if t_int else None
+    achieved_r = alg_r / t_int / 1e9 if t_int else None
     # ---- frame-level roofline, SURVEY.md 8d (whole job) ----
     # bytes per frame of the job: sharded -- the ranks' visible blocks sum to the frame's, and every
     # rank reads its frame; streams / single -- every rank its own frame
@@ -484,20 +493,26 @@ def main():
                       "dedupe, probe / insert and visibility sweep)",
             "pipelined_fraction": round(pf, 4),
             "bound": "hbm",
-            "achieved": round(achieved, 1),
+            "achieved": None if achieved is None else round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            # frac: the launch's algorithmic read + write bytes (reads and writes share the HBM);
+            # frac_read: SURVEY 8(d)'s read bytes alone, over the same duration
+            "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
+            "frac_read_write": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
+            "frac_read": None if achieved_r is None else round(achieved_r / HBM_PEAK_GBS, 4),
             "traffic": None if pmc is None else int(pmc["hbm_bytes_per_launch"]),
             "traffic_read": None if pmc is None else int(pmc["fetch_bytes_per_launch"]),
             "traffic_write": None if pmc is None else int(pmc["write_bytes_per_launch"]),
             "traffic_source": pmc_src,
             "alg_bytes_per_launch": int(alg),
-            "alg_read_bytes_per_launch": int(prof["sum_visible"] * BLOCK_READ_BYTES / a.steps + img_bytes),
-            "alg_def": "SURVEY 8(d) per frame launch: N_vis * 6156 + N_upd * 12 + 15 W H (N_vis, N_upd counted on "
-                       "device over the timed frames)",
+            "alg_read_bytes_per_launch": int(alg_r),
+            "alg_def": ("SURVEY 8(d) per frame launch: N_vis * 6156 + N_upd * 12 + 15 W H (N_vis, N_upd counted on "
+                        "device over the timed frames)") if pf > 0 else
+                       ("SURVEY 8(d) per k_integrate launch: N_vis * 6156 + N_upd * 12 (the frame image is read "
+                        "by k_ingest_dda)"),
             "implementation_bytes_per_launch": implementation_bytes(a, prof),
-            "us_per_launch": round(t_int * 1e6, 3),
+            "us_per_launch": None if t_int is None else round(t_int * 1e6, 3),
             "event_timed_launches": prof["frames"],
             "event_kind": ev_kind,
             "us_per_launch_device_clock": round(prof["ms_integrate_device"] / a.steps * 1e3, 3),
@@ -693,7 +708,8 @@ def cpu_baseline(a, cam, fr):
         "kind": "port",
         "sample": f"frames 0..{done - 1} of this bench's own {cam.width}x{cam.height} stream (GPU-rendered "
                   f"frames copied to the host) from an empty map, single thread, oracle/tsdf_oracle.c -O2 "
-                  f"(host: {model}, nproc={os.cpu_count()})",
+                  f"(host: {model}, nproc={os.cpu_count()}); the GPU line times frames {a.warmup}.."
+                  f"{a.warmup + a.steps - 1} of the same stream after {a.warmup} warm-up frames",
     }
 
 

@@ -85,6 +85,48 @@ hipError_t dmalloc(T** p, size_t count) {
 
 }  // namespace
 
+// ---------------------------------------------------------------------------------------------
+// Environment knobs: A/B experiments and tests only (the defaults are the measured best; nothing a
+// drop-in caller needs to set). Read once by tsdf_create (read_env_knobs); every other file reads
+// none. TSDF_ROCTX (roctx ranges) is read on first use by the tracing wrapper.
+//   TSDF_PIPELINE=0               unpipelined frames: two launches per frame (k_ingest_dda, k_integrate)
+//   TSDF_PIPE_MAX_PIXELS=n        largest frame (pixels) that is pipelined (default 2^19; C4 above it)
+//   TSDF_FRAME_ORDER=0..4         k_frame grid order of its parts (PipeArgs.order; default 2)
+//   TSDF_FRAME_WG_PER_CU=n        k_frame update workgroups per CU (default kFrameWgPerCu = 3)
+//   TSDF_INTEGRATE_WG_PER_CU=n    cap on k_integrate's resident workgroups per CU
+//   TSDF_CAND_CAP=n               (tests) smaller carve-candidate list, to exercise its overflow
+//   TSDF_MESH_GRID=n              (tests) fewer k_mesh workgroups, to exercise its grid stride
+//   TSDF_RENDER_OVERLAP=1         raycast on a second stream overlapping the next frame
+//   TSDF_GRAPH_MEMCPY_NODE=1      (A/B) graph frames upload their arguments with a memcpy node
+// ---------------------------------------------------------------------------------------------
+struct EnvKnobs {
+  bool pipeline = true;
+  int64_t pipe_max_pixels = -1;
+  int frame_order = -1, frame_wg_per_cu = 0, integrate_wg_per_cu = 0, cand_cap = 0, mesh_grid = 0;
+  bool render_overlap = false, graph_memcpy_node = false;
+};
+static EnvKnobs read_env_knobs() {
+  EnvKnobs k;
+  auto num = [](const char* n, long long dflt) {
+    const char* v = std::getenv(n);
+    return v ? std::atoll(v) : dflt;
+  };
+  auto flag = [](const char* n, bool dflt) {
+    const char* v = std::getenv(n);
+    return v ? v[0] == '1' : dflt;
+  };
+  if (const char* v = std::getenv("TSDF_PIPELINE")) k.pipeline = v[0] != '0';
+  k.pipe_max_pixels = num("TSDF_PIPE_MAX_PIXELS", -1);
+  k.frame_order = (int)std::max(-1ll, num("TSDF_FRAME_ORDER", -1));
+  k.frame_wg_per_cu = (int)num("TSDF_FRAME_WG_PER_CU", 0);
+  k.integrate_wg_per_cu = (int)num("TSDF_INTEGRATE_WG_PER_CU", 0);
+  k.cand_cap = (int)num("TSDF_CAND_CAP", 0);
+  k.mesh_grid = (int)num("TSDF_MESH_GRID", 0);
+  k.render_overlap = flag("TSDF_RENDER_OVERLAP", false);
+  k.graph_memcpy_node = flag("TSDF_GRAPH_MEMCPY_NODE", false);
+  return k;
+}
+
 struct tsdf_engine {
   tsdf_config cfg{};
   int device = 0;
@@ -177,8 +219,11 @@ struct tsdf_engine {
   uint32_t fid_next = 1;  // engine-wide frame ids (views, tags; never 0)
   uint32_t p_carve = 0, p_fid = 0;
   FrameParams p_P{};      // frame p_fid's camera / frame / pixel-record buffer
+  bool p_sampled = false;  // kPipeU: the frame was sampled for profiling (its update, when flushed
+                           //   as k_integrate, takes an event pair then)
   uint32_t pipe_tag = 0;  // one per k_frame launch: its flags' value
   int frame_order = 2;    // PipeArgs.order (TSDF_FRAME_ORDER): sweep, update, tiles (measured best)
+  EnvKnobs env;           // the environment's A/B and test knobs, read once at tsdf_create
   // feed_rgbd_frame staging: raw full-size inputs (host frames) and the half-size outputs
   uint8_t* fe_rgb = nullptr;
   uint16_t* fe_depth = nullptr;
@@ -452,6 +497,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   HIP_OK(hipSetDevice(device));
   tsdf_engine* e = new tsdf_engine();
   e->cfg = cfg;
+  e->env = read_env_knobs();
   e->device = device;
   // DDA samples per pixel: step_grid = ceil(max|2 trunc dir / voxel| / 8) + 1 (voxel_tsdf.cu:136)
   e->maxs = (int)std::ceil(2.0 * cfg.truncation / cfg.voxel_size * 1.0001 / kBlockLen) + 1;
@@ -501,7 +547,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   // entries exhausted pools left without voxels), so it is sized like the resolver's D.pairs scratch;
   // more are clamped with TSDF_STATUS_SHARD_OVERFLOW. TSDF_CAND_CAP (tests) sets a smaller list.
   D.cand_cap = (int32_t)std::max<size_t>(kNewKeyCap, (size_t)nb);
-  if (const char* v = std::getenv("TSDF_CAND_CAP")) D.cand_cap = std::min(D.cand_cap, std::max(1024, std::atoi(v)));
+  if (e->env.cand_cap > 0) D.cand_cap = std::min(D.cand_cap, std::max(1024, e->env.cand_cap));
   ALLOC(D.cand, (size_t)2 * D.cand_cap);  // two frames' lists (frame_view)
   ALLOC(D.arrive, kArriveWords);
   ALLOC(D.swdirty, kOccWords / 64);
@@ -515,7 +561,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kIntegrateThreads, 0) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
       return fail(TSDF_ERR_HIP);
-    if (const char* v = std::getenv("TSDF_INTEGRATE_WG_PER_CU")) per_cu = std::min(per_cu, std::atoi(v));  // tuning
+    if (e->env.integrate_wg_per_cu > 0) per_cu = std::min(per_cu, e->env.integrate_wg_per_cu);
     D.integrate_grid = std::max(8, std::min(kIntegrateGrid, (per_cu * ncu) & ~7));
     int per_cu_pre = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_pre, reinterpret_cast<const void*>(k_frame),
@@ -525,15 +571,15 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
     // tiles' workgroups from the start (driver command, same box: 22.3-22.5k frames/s at 3, 22.0-22.1k
     // at 4, 21.0-21.3k at 5, 18.5-18.7k at 7, 17.9-18.1k at 2; 300 frames: 24.0k at 3 and at 5)
     int want = kFrameWgPerCu;
-    if (const char* v = std::getenv("TSDF_FRAME_WG_PER_CU")) want = std::max(1, std::atoi(v));
+    if (e->env.frame_wg_per_cu > 0) want = e->env.frame_wg_per_cu;
     per_cu_pre = std::min(per_cu_pre, want);
     D.integrate_grid_pre = std::max(8, std::min(kIntegrateGrid, (per_cu_pre * ncu) & ~7));
   }
   ALLOC(D.pixA, 2 * e->max_pixels);  // two buffers: a pipelined frame's and the next one's
   ALLOC(D.pixB, 2 * e->max_pixels);
-  if (const char* v = std::getenv("TSDF_PIPELINE")) e->pipeline = v[0] != '0';
-  if (const char* v = std::getenv("TSDF_PIPE_MAX_PIXELS")) e->pipe_max_pixels = std::atoll(v);  // tuning
-  if (const char* v = std::getenv("TSDF_FRAME_ORDER")) e->frame_order = std::min(4, std::max(0, std::atoi(v)));
+  e->pipeline = e->env.pipeline;
+  if (e->env.pipe_max_pixels >= 0) e->pipe_max_pixels = e->env.pipe_max_pixels;
+  if (e->env.frame_order >= 0) e->frame_order = std::min(4, e->env.frame_order);
   ALLOC(D.visbits, kOccWords);
   ALLOC(D.wgcnt, kOccWords / 256);
   ALLOC(D.dbg, (size_t)kDiagKernels * kDiagMaxWg * kDiagStamps);
@@ -556,7 +602,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(e->m_total, 1);
   ALLOC(e->m_nbr, (size_t)27 * nb);
   e->mesh_grid = std::min(kMeshGrid, nb);
-  if (const char* v = std::getenv("TSDF_MESH_GRID")) e->mesh_grid = std::max(1, std::min(e->mesh_grid, std::atoi(v)));  // tests
+  if (e->env.mesh_grid > 0) e->mesh_grid = std::min(e->mesh_grid, e->env.mesh_grid);
   ALLOC(e->t_count, 1);
 #undef ALLOC
   D = frame_view(D, 0u);  // the base view (sharded / graph / hash-level paths): frame parity 0
@@ -573,7 +619,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
       hipEventCreateWithFlags(&e->rs_ready, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->rs_done, hipEventDisableTiming) != hipSuccess)
     return fail(TSDF_ERR_HIP);
-  if (const char* v = std::getenv("TSDF_RENDER_OVERLAP")) e->render_overlap = v[0] == '1';
+  e->render_overlap = e->env.render_overlap;
   if (!init_state(e)) {
     set_error("tsdf_create: initialisation failed");
     return fail(TSDF_ERR_HIP);
@@ -596,12 +642,17 @@ int tsdf_synchronize(tsdf_engine* e) {
   if (!e) return TSDF_ERR_INVALID_ARG;
   HIP_OK(hipSetDevice(e->device));
   ENTER(e);
-  HIP_OK(hipStreamSynchronize(e->stream));
   // a pipelined frame whose in-kernel wait timed out has wrong results: an error here, not only a
-  // status bit; the flags are per-launch tags, so later launches are not affected
-  uint32_t st = 0;
-  HIP_OK(hipMemcpy(&st, &e->D.ctr->status, sizeof(st), hipMemcpyDeviceToHost));
-  if (st & TSDF_STATUS_PIPELINE_TIMEOUT) {
+  // status bit. The status word is read on the engine stream into the pinned counter
+  // mirror (no device-wide sync); the timeout bit is reported once and then cleared, so the next
+  // synchronize reports only a new timeout (the flags are per-launch tags: later launches are not
+  // affected). TSDF_STATUS_PIPELINE_TIMEOUT stays visible in tsdf_get_stats until then.
+  HIP_OK(hipMemcpyAsync(&e->h_ctr->status, &e->D.ctr->status, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  if (e->h_ctr->status & TSDF_STATUS_PIPELINE_TIMEOUT) {
+    const uint32_t st = e->h_ctr->status & ~(uint32_t)TSDF_STATUS_PIPELINE_TIMEOUT;
+    HIP_OK(hipMemcpyAsync(&e->D.ctr->status, &st, sizeof(st), hipMemcpyHostToDevice, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
     set_error("tsdf_synchronize: a pipelined frame's in-kernel wait timed out (TSDF_STATUS_PIPELINE_TIMEOUT)");
     return TSDF_ERR_PIPELINE;
   }
@@ -609,6 +660,19 @@ int tsdf_synchronize(tsdf_engine* e) {
 }
 
 namespace {
+
+// the next profiling event set (a std::deque: push_back never moves the sets earlier frames hold)
+int take_events(tsdf_engine* e, std::array<hipEvent_t, 5>** out) {
+  if (e->ev_used == e->events.size()) {
+    std::array<hipEvent_t, 5> a{};
+    // (no system-scope fence when an event completes: with it, the dispatch an event pair is bound to
+    // ran ~6 us longer than the others -- 50.1 vs 44.3 us in the driver command's kernel trace)
+    for (auto& x : a) HIP_OK(hipEventCreateWithFlags(&x, hipEventDisableSystemFence));
+    e->events.push_back(a);
+  }
+  *out = &e->events[e->ev_used++];
+  return TSDF_OK;
+}
 
 // Phase 1 of a frame: stage host inputs, then (launch) k_ingest_dda on view Dv (the frame's lists,
 // counts and candidates: frame_view): pixel records for the whole frame, the DDA over tiles of slice
@@ -672,14 +736,8 @@ int frame_ingest(tsdf_engine* e, const EngineDev& Dv, const tsdf_frame* f, const
   }
   std::array<hipEvent_t, 5>* ev = nullptr;
   if (e->profiling && (e->prof_calls++ % e->prof_every) == 0) {
-    if (e->ev_used == e->events.size()) {
-      std::array<hipEvent_t, 5> a{};
-      // (no system-scope fence when an event completes: with it, the dispatch an event pair is bound to
-      // ran ~6 us longer than the others -- 50.1 vs 44.3 us in the driver command's kernel trace)
-      for (auto& x : a) HIP_OK(hipEventCreateWithFlags(&x, hipEventDisableSystemFence));
-      e->events.push_back(a);
-    }
-    ev = &e->events[e->ev_used++];
+    int rc = take_events(e, &ev);
+    if (rc) return rc;
   }
   *ev_out = ev;
   if (!launch) return TSDF_OK;
@@ -826,7 +884,18 @@ int flush_pending(tsdf_engine* e) {
   HIP_OK(hipSetDevice(e->device));
   const int ps = e->ps;
   e->ps = tsdf_engine::kPipeNone;
-  if (ps == tsdf_engine::kPipeU) return frame_update(e, frame_view(e->D, e->p_fid), e->p_P, nullptr);
+  if (ps == tsdf_engine::kPipeU) {
+    // a sampled frame's update is timed here (the C5 loop: a raycast after every frame flushes it);
+    // (PHASES mode: its allocation ran in the ingest launch before, so event 0 opens at the update)
+    std::array<hipEvent_t, 5>* ev = nullptr;
+    if (e->p_sampled && e->profiling) {
+      int rc = take_events(e, &ev);
+      if (rc) return rc;
+      if (e->prof_mode == TSDF_PROFILE_PHASES) HIP_OK(hipEventRecord((*ev)[0], e->stream));
+    }
+    e->p_sampled = false;
+    return frame_update(e, frame_view(e->D, e->p_fid), e->p_P, ev);
+  }
   PipeArgs A{};
   A.has_carve = ps == tsdf_engine::kPipeCAU;
   A.fid_carve = e->p_carve;
@@ -857,7 +926,10 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
     set_error("tsdf_integrate: a shard of a sharded volume integrates through tsdf_integrate_shard_*");
     return TSDF_ERR_INVALID_ARG;
   }
-  if (!e) return TSDF_ERR_INVALID_ARG;
+  if (!e || !f || !K || !pose) {  // (before anything reads the frame: pipe_frame_size below does)
+    set_error("tsdf_integrate: invalid argument");
+    return TSDF_ERR_INVALID_ARG;
+  }
   const bool pipe = e->pipeline && e->maxs <= 3 && pipe_frame_size(e, f->width, f->height);
   if (!pipe) {
     int rc = flush_pending(e);
@@ -873,7 +945,10 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
   if (rc) return rc;
   if (!pipe) return frame_update(e, Dv, P, ev);
   if (ingest_alone) {
-    if (ev) --e->ev_used;  // (no k_frame / k_integrate launch to time in this call)
+    // (no k_frame / k_integrate launch to time in this call: the slot is released, and the update,
+    // if a flush launches it as k_integrate, takes one then)
+    if (ev) --e->ev_used;
+    e->p_sampled = ev != nullptr;
     e->ps = tsdf_engine::kPipeU;
     e->p_fid = fid;
     e->p_P = P;
@@ -1060,11 +1135,14 @@ int tsdf_integrate_shard_abort(tsdf_engine* e) {
     set_error("tsdf_integrate_shard_abort: not a shard engine");
     return TSDF_ERR_INVALID_ARG;
   }
-  if (e->shard_phase == 0) return TSDF_OK;  // nothing pending
+  if (e->shard_phase == 0 && e->ps == tsdf_engine::kPipeNone) return TSDF_OK;  // nothing pending
   HIP_OK(hipSetDevice(e->device));
-  ENTER(e);
+  // (not ENTER: a pending pipelined sharded frame cannot be flushed without the exchange protocol --
+  // it is dropped here with the rest of the frame's state)
+  JOIN_RENDER(e);
   e->shard_phase = 0;
   e->shard_ev = nullptr;
+  e->ps = tsdf_engine::kPipeNone;
   hipLaunchKernelGGL(k_shard_abort, dim3(1), dim3(256), 0, e->stream, e->D);
   LAUNCH_OK("k_shard_abort");
   return TSDF_OK;
@@ -1235,7 +1313,7 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
     if ((err = hipEventCreateWithFlags(&g->done[k], hipEventDisableTiming)) != hipSuccess) return fail(err, "graph event");
     if ((err = hipStreamBeginCapture(g->cap, hipStreamCaptureModeThreadLocal)) != hipSuccess)
       return fail(err, "hipStreamBeginCapture");
-    if (std::getenv("TSDF_GRAPH_MEMCPY_NODE"))  // A/B: a memcpy node instead of the copy kernel
+    if (e->env.graph_memcpy_node)  // A/B: a memcpy node instead of the copy kernel
       (void)hipMemcpyAsync(g->d_args + k, g->h_args + k, sizeof(FrameArgs), hipMemcpyHostToDevice, g->cap);
     else  // one wave reads the pinned slot over the fabric: a kernel node, no DMA engine in the graph
       hipLaunchKernelGGL(k_copy_words, dim3(1), dim3(64), 0, g->cap, reinterpret_cast<uint32_t*>(g->d_args + k),
@@ -1742,6 +1820,9 @@ int tsdf_reset(tsdf_engine* e) {
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
+  // a shard's pending pipelined frames need the exchange protocol to complete: reset drops them
+  // (init_state below re-initialises every per-frame buffer); one volume's are flushed first
+  if (sharded(e)) e->ps = tsdf_engine::kPipeNone;
   ENTER(e);
   if (!init_state(e)) {
     set_error("tsdf_reset: initialisation failed");

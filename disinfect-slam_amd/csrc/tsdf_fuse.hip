@@ -91,7 +91,11 @@ __global__ __launch_bounds__(256) void k_shard_abort(EngineDev D) {
     D.nk_key[h] = 0ull;
     D.nk_order[h] = 0xFFFFFFFFu;
   }
-  if (threadIdx.x < kBands) D.band[threadIdx.x * kBandStride] = 0;
+  // every frame view's band counts and candidate count, and the pipelined frames' statistics (a
+  // shard's pending pipelined frames are dropped as well; D is the base view)
+  for (int i = threadIdx.x; i < 3 * kBands; i += blockDim.x) D.band[i * kBandStride] = 0;
+  if (threadIdx.x < 2) D.pipe[kPipeNCand + 16 * threadIdx.x] = 0ull;
+  for (int i = kPipeStats + threadIdx.x; i < kPipeWords; i += blockDim.x) D.pipe[i] = 0ull;
   for (int i = threadIdx.x; i < kArriveWords; i += blockDim.x) D.arrive[i] = 0ull;
   __syncthreads();
   if (threadIdx.x == 0) {

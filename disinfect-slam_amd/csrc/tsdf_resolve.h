@@ -650,11 +650,13 @@ __device__ FAST_INLINE bool resolve_alloc_fast(const EngineDev& D, const FramePa
   ordv[t] = owned ? ord : 0xFFFFFFFFu;  // (threads >= n pad the scan with "never smaller")
   L.heap_top[t] = htop;
   const unsigned long long bo = __ballot(owned), bb = __ballot(bad);
+  TSDF_STAMP(D, 1, 3);  // (diag) the keys' orders, buckets and heap top loaded
   if (lane_id() == 0) {
     L.scan[wave] = __popcll(bo);
     L.scan[4 + wave] = __popcll(bb);
   }
   lds_barrier();
+  TSDF_STAMP(D, 1, 4);
   const int nowned = L.scan[0] + L.scan[1] + L.scan[2] + L.scan[3];
   if (L.scan[4] + L.scan[5] + L.scan[6] + L.scan[7] != 0 || nowned > free0) return false;
   if (have) {
@@ -691,6 +693,7 @@ __device__ FAST_INLINE bool resolve_alloc_fast(const EngineDev& D, const FramePa
     st_co(&D.nk_key[slot], 0ull);
     st_co(&D.nk_order[slot], 0xFFFFFFFFu);
   }
+  TSDF_STAMP(D, 1, 5);  // (diag) the commits issued
   if (t == 0) {
     D.ctr->lock_epoch = epoch;
     D.ctr->resolve_alloc_ticks += __builtin_amdgcn_s_memrealtime() - tick0;
@@ -724,6 +727,7 @@ __device__ __forceinline__ void resolve_alloc_wg(const EngineDev& D, const Frame
   int32_t h0 = (int32_t)ld_co(&D.nk_list[t].slot), h1 = NR > 1 ? (int32_t)ld_co(&D.nk_list[t + kRT].slot) : 0;
   const bool single = n <= RB;
   const bool lds_locks = n <= AllocLdsT<RB>::kLockKeys;
+  TSDF_STAMP(D, 1, 7);  // (diag) counters and key list loaded
   const uint32_t epoch = epoch0 + 1u;
   if (n <= kRT && !resolve_fast_off()) {
     if (resolve_alloc_fast<RB>(D, P, frame_mode, n, free0, epoch, k0, h0, L, tick0)) return;
@@ -1079,6 +1083,7 @@ __device__ __forceinline__ bool resolve_delete_fast(const EngineDev& D, int n, i
     L.scan[wave] = __popcll(bb);
     L.scan[4 + wave] = __popcll(br) + __popcll(br1);
   }
+  TSDF_STAMP(D, 4, 3);  // (diag) the candidates' buckets loaded
   lds_barrier();
   if (L.scan[0] + L.scan[1] + L.scan[2] + L.scan[3] != 0) return false;
   const int nrel = L.scan[4] + L.scan[5] + L.scan[6] + L.scan[7];
@@ -1103,6 +1108,7 @@ __device__ __forceinline__ bool resolve_delete_fast(const EngineDev& D, int n, i
     }
     carved_key(D, cur, x[r], y[r], z[r], fo_fid);
   }
+  TSDF_STAMP(D, 4, 4);  // (diag) the deletes issued
   if (t == 0) {
     D.ctr->lock_epoch = epoch;
     D.ctr->free_count = free0 + nrel;

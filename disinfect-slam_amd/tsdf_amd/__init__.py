@@ -868,32 +868,43 @@ class ShardGroup:
         try:
             self._integrate(rgb, depth, ht, lt, K, cam_T_world, max_depth, count)
         except Exception:
-            # no shard stays stuck mid-frame; every shard is aborted even if one abort fails, and the
-            # caller sees the original error
-            for e in self.engines:
-                try:
-                    e.integrate_shard_abort()
-                except Exception:
-                    pass
+            self._abort_all()
             raise
+
+    def _abort_all(self):
+        # no shard stays stuck mid-frame (three-call frames and pipelined ones alike); every shard is
+        # aborted even if one abort fails, and the caller sees the original error
+        for e in self.engines:
+            try:
+                e.integrate_shard_abort()
+            except Exception:
+                pass
 
     def _pipe_step(self, rgb, depth, ht, lt, K, cam_T_world, max_depth):
         out, inb = self._pc[self._ncall & 1], self._pc[(self._ncall + 1) & 1]
+        # (the call counter moves even when a shard fails part-way: the aborted shards restart from
+        # "no pending frame", whose first call reads no inbox)
+        self._ncall += 1
         pend = [e.integrate_shard_pipe(rgb, depth, ht, lt, K, cam_T_world, max_depth, inb, out[i], self.cand_cap)
                 for i, e in enumerate(self.engines)]
-        self._ncall += 1
         return any(pend)
 
     def flush(self):
         """Pipelined: complete the pending frames (steps with their exchanges); a no-op otherwise."""
         if self.pipe:
-            while self._pipe_step(None, None, None, None, None, None, 4.0):
-                pass
+            try:
+                while self._pipe_step(None, None, None, None, None, None, 4.0):
+                    pass
+            except Exception:
+                self._abort_all()
+                raise
 
     def _integrate(self, rgb, depth, ht, lt, K, cam_T_world, max_depth, count):
         G = self.G
         if self.pipe:
             self._pipe_step(rgb, depth, ht, lt, K, cam_T_world, max_depth)
+            # this call's slots hold the candidates of the frame it updated
+            self._count(count, cands=self._pc[(self._ncall - 1) & 1])
             return
         if self.graphs is not None:
             for i, g in enumerate(self.graphs):
@@ -918,17 +929,17 @@ class ShardGroup:
             e.integrate_shard_end(self._cands, self.cand_cap)
         self._count(count)
 
-    def _count(self, count):
-        if count:  # per-shard candidate counts (slot headers), a host sync
-            import torch
-            per = self._cands[:, 8:12].contiguous().view(torch.int32).view(-1).tolist()
-            self.cands_by_shard = [a + b for a, b in zip(self.cands_by_shard, per)]
-        if count:  # slot headers (record 0's count word), a host sync
-            import torch
-            hdr = lambda t: int(t[:, 8:12].contiguous().view(torch.int32).sum())
-            if self.split:
-                self.keys_exchanged += hdr(self._keys)
-            self.cands_exchanged += hdr(self._cands)
+    def _count(self, count, cands=None):
+        if not count:
+            return
+        import torch
+        cands = self._cands if cands is None else cands
+        # per-shard candidate counts (slot headers: record 0's count word), a host sync
+        per = cands[:, 8:12].contiguous().view(torch.int32).view(-1).tolist()
+        self.cands_by_shard = [a + b for a, b in zip(self.cands_by_shard, per)]
+        if self.split:
+            self.keys_exchanged += int(self._keys[:, 8:12].contiguous().view(torch.int32).sum())
+        self.cands_exchanged += sum(per)
 
     def synchronize(self):
         self.flush()

@@ -98,9 +98,18 @@ def integrate_sharded_pipe(engine, bufs, rgb, depth, ht, lt, K, cam_T_world, max
     all-gather per frame -- this call's carve candidates (bufs.cands_out) into every rank's inbox
     (bufs.cands_in, read by the next call). depth None: one step of completing the pending frames.
     Returns True while more steps are needed (flush_sharded_pipe loops)."""
-    pend = engine.integrate_shard_pipe(rgb, depth, ht, lt, K, cam_T_world, max_depth, bufs.cands_in, bufs.cands_out,
-                                       bufs.cand_cap)
-    all_gather_slots(bufs.cands_out, bufs.cands_in)
+    try:
+        pend = engine.integrate_shard_pipe(rgb, depth, ht, lt, K, cam_T_world, max_depth, bufs.cands_in,
+                                           bufs.cands_out, bufs.cand_cap)
+        all_gather_slots(bufs.cands_out, bufs.cands_in)
+    except Exception:
+        # as integrate_sharded: the pending pipelined frames are dropped (STATUS_SHARD_ABORTED), the
+        # caller sees the original error
+        try:
+            engine.integrate_shard_abort()
+        except Exception:
+            pass
+        raise
     return pend
 
 

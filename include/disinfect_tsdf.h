@@ -27,7 +27,8 @@ extern "C" {
 #define TSDF_ERR_HIP 3
 #define TSDF_ERR_CAPACITY 4 /* caller buffer too small (two-call pattern) */
 #define TSDF_ERR_NO_DEVICE 5
-#define TSDF_ERR_PIPELINE 6 /* tsdf_synchronize: TSDF_STATUS_PIPELINE_TIMEOUT is set (results wrong) */
+#define TSDF_ERR_PIPELINE 6 /* tsdf_synchronize: a pipelined frame's wait timed out since the last report
+                               (results wrong); the status bit is cleared once reported */
 
 #define TSDF_MEM_HOST 0   /* pointer is host memory: engine copies it (pageable is fine) */
 #define TSDF_MEM_DEVICE 1 /* pointer is device memory on the engine's GPU */
@@ -193,10 +194,11 @@ int tsdf_integrate_shard_begin(tsdf_engine* e, const tsdf_frame* frame, const ts
 int tsdf_integrate_shard_update(tsdf_engine* e, const void* keys_in, int32_t key_cap, void* cands_out,
                                 int32_t cand_cap);
 int tsdf_integrate_shard_end(tsdf_engine* e, const void* cands_in, int32_t cand_cap);
-/* Abort a pending sharded frame (e.g. a failed exchange between the phases): the engine returns to
- * "between frames" so later calls (a new frame, reset, snapshot_load, ...) work again. Structural
- * changes a phase already made stay, so the shards may no longer agree: TSDF_STATUS_SHARD_ABORTED is
- * set, and the caller should restore every shard from a snapshot (or reset). No pending frame: OK. */
+/* Abort a pending sharded frame (e.g. a failed exchange between the phases) or the pending frames of
+ * tsdf_integrate_shard_pipe: the engine returns to "between frames" so later calls (a new frame,
+ * reset, snapshot_load, ...) work again. Structural changes a phase already made stay, so the shards
+ * may no longer agree: TSDF_STATUS_SHARD_ABORTED is set, and the caller should restore every shard
+ * from a snapshot (or reset, which also drops pending pipelined shard frames). No pending frame: OK. */
 int tsdf_integrate_shard_abort(tsdf_engine* e);
 
 /* Stream ordering with a caller's HIP stream (e.g. torch's current stream) for device buffers

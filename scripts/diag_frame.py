@@ -39,6 +39,7 @@ def main():
     rows = {k: [] for k in PARTS}
     head = []
     coll = []
+    phases = []
     for i in range(nfr):
         torch.cuda.synchronize()
         L.tsdf_debug_stamps(eng._h, buf.ctypes.data, buf.size, None)  # (clears)
@@ -64,6 +65,11 @@ def main():
             st = S[m, 1]
             coll.append((np.median((S[m, 3] - st) * 1e-2), np.percentile((S[m, 3] - st) * 1e-2, 90),
                          np.median((S[m, 4] - st) * 1e-2), np.median(S[m, 5] & 0xFFFF)))
+        A1 = buf.reshape(NK, NWG, NS)[1, 0].astype(np.int64)  # head: allocation resolver stamps
+        D4 = buf.reshape(NK, NWG, NS)[4, 0].astype(np.int64)  # head: carving resolver stamps
+        rel = lambda v: (v - t0) * 1e-2 if v else np.nan
+        phases.append((rel(D4[0]), rel(D4[3]), rel(D4[4]), rel(S[0, 3]), rel(A1[0]), rel(A1[7]), rel(A1[3]),
+                       rel(A1[4]), rel(A1[5]), rel(S[0, 4])))
         h = S[0]
         if h[0] == 1:
             head.append(((h[3] - t0) * 1e-2 if h[3] else np.nan, (h[4] - t0) * 1e-2 if h[4] else np.nan,
@@ -79,6 +85,11 @@ def main():
         a = np.median(np.array(coll), axis=0)
         print(f"listed update: first collect done {a[0]:.1f} (p90 {a[1]:.1f}), last collect done {a[2]:.1f} us "
               f"after the workgroup start; records + collections {a[3]:.0f}")
+    if phases:
+        a = np.nanmedian(np.array(phases), axis=0)
+        print("head phases (us from the launch start): carving start %.1f, buckets loaded %.1f, deletes issued "
+              "%.1f, published %.1f | allocation start %.1f, counters+keys %.1f, orders+buckets+heap %.1f, "
+              "barrier %.1f, commits issued %.1f, published %.1f" % tuple(a))
     if head:
         a = np.nanmedian(np.array(head), axis=0)
         print(f"head: carving published {a[0]:.1f}, allocation published {a[1]:.1f}, head end {a[2]:.1f}")

@@ -8,6 +8,7 @@
 #   driver            the driver's bench command: bench.py --gpus 1 --steps 20 --warmup 5
 #   profile-driver    kernel trace + FETCH_SIZE / WRITE_SIZE PMC passes of the driver command
 #                     (scripts/profile_integrate.sh; summary + pmc_entry.json under <tag>/prof_driver)
+#   profile-c4|c5|c5graph|c2  the same for those bench lines (default steps) -> <tag>/prof_<name>
 #   default           bench.py (300 timed frames, CPU baseline)
 #   c5 | c5graph | c4 | c2 | graph   bench.py --loop c5 [--graph] / 1280x720 / --depth-only / --graph
 #   c5tests           the raycast / render / C5 GPU tests
@@ -47,6 +48,11 @@ for st in "$@"; do
            line $OUT/bench_driver.json ;;
     profile-driver) bash scripts/profile_integrate.sh $OUT/prof_driver $DRIVER || fail $st $OUT/prof_driver/trace_bench.log
            tail -14 $OUT/prof_driver/summary.txt ;;
+    profile-c4|profile-c5|profile-c5graph|profile-c2)
+           case $st in profile-c4) A="--width 1280 --height 720";; profile-c5) A="--loop c5";;
+                       profile-c5graph) A="--loop c5 --graph";; profile-c2) A="--depth-only";; esac
+           bash scripts/profile_integrate.sh $OUT/prof_${st#profile-} $A || fail $st $OUT/prof_${st#profile-}/trace_bench.log
+           tail -14 $OUT/prof_${st#profile-}/summary.txt ;;
     default) timeout -k 10 300 python3 bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || fail $st $OUT/bench_default.err
            line $OUT/bench_default.json ;;
     c5) timeout -k 10 300 python3 bench.py --no-cpu --loop c5 > $OUT/bench_c5.json 2> $OUT/bench_c5.err || fail $st $OUT/bench_c5.err

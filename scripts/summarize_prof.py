@@ -52,7 +52,7 @@ def window(rows, b, name=""):
     last steps + 1 but two."""
     rows = sorted(rows)
     w, k = b["warmup"], b["steps"]
-    if name == "k_frame":
+    if name in ("k_frame", "k_frame_g"):
         return [v for _, v in rows[-(k + 1):-2]]
     return [v for _, v in rows[w:w + k]]
 
@@ -80,7 +80,7 @@ def main(out):
                 (int(r["Dispatch_Id"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
         res["timed_window"] = {}
         for name, rows in per.items():
-            if not name.startswith("k_") or len(rows) < b0["steps"] - 1 or (name == "k_frame" and len(rows) < b0["steps"] + 1):
+            if not name.startswith("k_") or len(rows) < b0["steps"] - 1 or (name in ("k_frame", "k_frame_g") and len(rows) < b0["steps"] + 1):
                 continue
             win = window(rows, b0, name)
             res["timed_window"][name] = {"launches": len(win), "avg_us": statistics.mean(win) / 1e3,
@@ -101,7 +101,7 @@ def main(out):
             per.setdefault(kname(kn), []).append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
         corr = 2.0 if c == "FETCH_SIZE" else 1.0
         for name, rows in per.items():
-            full = len(rows) >= b["warmup"] + b["steps"] or (name == "k_frame" and len(rows) >= b["steps"] + 1)
+            full = len(rows) >= b["warmup"] + b["steps"] or (name in ("k_frame", "k_frame_g") and len(rows) >= b["steps"] + 1)
             win = window(rows, b, name) if full else [v for _, v in sorted(rows)]
             res["pmc"].setdefault(name, {})[c] = {
                 "bytes_per_launch": statistics.mean(win) * 1024 * corr, "dispatches": len(win),
@@ -109,7 +109,8 @@ def main(out):
     if b0:
         res["bench"] = b0
     # the frame launch of the line: k_frame for pipelined frames, else k_integrate
-    ki = res["pmc"].get("k_frame") or res["pmc"].get("k_integrate", {})
+    kn = next((k for k in ("k_frame", "k_frame_g", "k_integrate", "k_integrate_graph") if k in res["pmc"]), None)
+    ki = res["pmc"].get(kn, {}) if kn else {}
     if "FETCH_SIZE" in ki and "WRITE_SIZE" in ki:
         bf, bw = pmc_lines["FETCH_SIZE"], pmc_lines["WRITE_SIZE"]
         same = (bf["sum_visible"], bf["sum_updated"]) == (bw["sum_visible"], bw["sum_updated"])
@@ -122,13 +123,17 @@ def main(out):
                  "alg_bytes_per_launch": bf["roofline"]["alg_bytes_per_launch"],
                  "alg_read_bytes_per_launch": bf["roofline"]["alg_read_bytes_per_launch"],
                  "launches": ki["FETCH_SIZE"]["dispatches"], "passes_saw_same_frames": same,
+                 # the frame kernel's timed-window mean from the kernel trace of the same command: bench.py
+                 # takes it as the launch duration where no dispatch events exist (graph frames)
+                 "trace_kernel": kn,
+                 "trace_kernel_avg_us": res.get("timed_window", {}).get(kn, {}).get("avg_us"),
                  "note": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and --pmc WRITE_SIZE, separate passes of "
                          "the bench command; mean over the timed-window k_integrate dispatches"}
         res["integrate_pmc_entry"] = entry
         json.dump(entry, open(os.path.join(out, "pmc_entry.json"), "w"), indent=1)
         if not same:
             print("WARNING: the passes integrated different frames (N_vis/N_upd sums differ)")
-        print(f"k_integrate PMC (timed window, {entry['launches']} launches): fetch {fetch / 1e6:.3f} MB, "
+        print(f"{kn} PMC (timed window, {entry['launches']} launches): fetch {fetch / 1e6:.3f} MB, "
               f"write {write / 1e6:.3f} MB, total {(fetch + write) / 1e6:.3f} MB vs algorithmic "
               f"{entry['alg_bytes_per_launch'] / 1e6:.3f} MB (read {entry['alg_read_bytes_per_launch'] / 1e6:.3f})")
     json.dump(res, open(os.path.join(out, "summary.json"), "w"), indent=1)
@@ -140,7 +145,7 @@ def main(out):
         print(f"{name} timed window: {t['launches']} launches avg {t['avg_us']:.2f}us "
               f"(min {t['min_us']:.2f}, max {t['max_us']:.2f})")
     if "bench_event_us_per_launch" in res:
-        print(f"bench HIP events (k_integrate): {res['bench_event_us_per_launch']:.2f}us")
+        print(f"bench HIP events (frame kernel): {res['bench_event_us_per_launch']}us")
     for k, v in sorted(res["kernels"].items(), key=lambda kv: -kv[1]["total_ms"]):
         p = res["pmc"].get(k, {})
         fb = p.get("FETCH_SIZE", {}).get("bytes_per_launch")

@@ -127,3 +127,28 @@ def test_device_frames_match_host_frames():
             assert np.array_equal(da[k].view(np.uint32), db[k].view(np.uint32)), k
     finally:
         a.close(), b.close()
+
+
+def test_null_arguments_return_invalid_arg():
+    """tsdf_integrate with a NULL frame, camera or pose returns TSDF_ERR_INVALID_ARG
+    (checked before the pipelining test reads the frame size) and leaves the engine usable."""
+    import ctypes as C
+
+    import tsdf_amd
+    from tsdf_amd import _lib, synth
+    L = _lib.load()
+    cam = synth.camera(64, 48, synth.TUM_FR1)
+    eng = tsdf_amd.Engine(0.01, 0.04, max_width=64, max_height=48, num_block_bits=10)
+    try:
+        K = _lib.Intrinsics(*[float(v) for v in cam.K])
+        pose = _lib.Pose(0, 0, 0, 1, 0, 0, 0)
+        fr = _lib.Frame(64, 48, None, None, None, None, 0)
+        assert L.tsdf_integrate(eng._h, None, C.byref(K), C.byref(pose), 4.0) == 1
+        assert L.tsdf_integrate(eng._h, C.byref(fr), None, C.byref(pose), 4.0) == 1
+        assert L.tsdf_integrate(eng._h, C.byref(fr), C.byref(K), None, 4.0) == 1
+        assert L.tsdf_integrate(None, C.byref(fr), C.byref(K), C.byref(pose), 4.0) == 1
+        f = synth.render(cam, 0)
+        eng.integrate(f["rgb"], f["depth"], f["ht"], f["lt"], cam.K, tsdf_amd.SE3(f["q"], f["t"]), 4.0)
+        assert eng.stats()["status"] == 0 and eng.stats()["active_blocks"] > 0
+    finally:
+        eng.close()

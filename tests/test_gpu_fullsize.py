@@ -151,3 +151,55 @@ def test_bench_stream_oracle_parity_40_frames():
     finally:
         eng.close()
         ora.close()
+
+
+def test_bench_stream_oracle_parity_120_frames_pipelined():
+    """The bench's own stream over 120 frames, integrated back to back as the bench
+    does -- pipelined k_frame launches, nothing read between frames -- against the CPU oracle: the
+    running totals of visible / updated / deleted blocks and voxels, the hash table, free stack and
+    every voxel at frames 40, 80 and 120 (each compare completes the pending frames). By frame 120
+    much of the surface sits at the weight cap (40), so the log-odds state's probability bound (1e-4,
+    DESIGN.md 2) is checked at capped weight over a long orbit."""
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    from _oracle import OracleGrid
+    from test_gpu_parity import PROB_TOL
+
+    def host(x):
+        return x.cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
+
+    W, H, n = 640, 480, 120
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    fr = synth.render_torch(cam, list(range(n)), device="cuda")
+    eng = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=18)
+    ora = OracleGrid(0.005, 0.03, 18)
+    tot = dict(vis=0, upd=0, dele=0)
+    try:
+        for i in range(n):
+            q, t = fr["q"][i], fr["t"][i]
+            eng.integrate(fr["rgb"][i], fr["depth"][i], fr["ht"][i], fr["lt"][i], K, tsdf_amd.SE3(q, t), 4.0)
+            ora.integrate(host(fr["rgb"][i]), host(fr["depth"][i]), host(fr["ht"][i]), host(fr["lt"][i]), 4.0,
+                          cam.K, host(q), host(t))
+            so = ora.stats()
+            tot["vis"] += so["last_num_visible"]
+            tot["upd"] += so["last_num_updated"]
+            tot["dele"] += so["last_num_deleted"]
+            if (i + 1) % 40 == 0:
+                s = eng.stats()
+                assert s["status"] == 0, s
+                assert (s["total_visible"], s["total_updated"], s["total_deleted"]) == \
+                    (tot["vis"], tot["upd"], tot["dele"]), (i, s, tot)
+                assert s["active_blocks"] == so["active_blocks"]
+                compare(eng, ora, tag=f"bench stream frame {i} (pipelined)")
+        d = eng.dump()
+        live = d["entry_idx"][d["entry_idx"] >= 0]
+        w = d["rgbw"].reshape(-1, 512, 4)[live, :, 3]
+        assert (w == 40).sum() > 100000, "the long orbit should drive many voxels to the weight cap"
+        assert PROB_TOL <= 1e-4
+        assert eng.stats()["active_blocks"] > 8000
+    finally:
+        eng.close()
+        ora.close()

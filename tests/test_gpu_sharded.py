@@ -356,6 +356,54 @@ def test_shard_abort_returns_engine_between_frames():
         e.close()
 
 
+def test_shard_pipe_abort_mid_step_and_recover():
+    """a failure part-way through a pipelined sharded step (one shard has launched its
+    k_frame, the next raises) aborts every shard -- the pending pipelined frames are dropped with
+    STATUS_SHARD_ABORTED, nothing stays stuck (stats / snapshot / reset work) -- and after a reset the
+    group integrates a stream exactly like a fresh group (every shard's table and voxels). count=True
+    counts the pipelined slots' candidates."""
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H, G = 160, 120, 2
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    frames = [synth.render(cam, 3 * f) for f in range(6)]
+    mk = lambda: tsdf_amd.ShardGroup(G, 0.01, 0.04, max_width=W, max_height=H, num_block_bits=13, split=False,
+                                     pipe=True, cand_cap=4096)
+    step = lambda g, fr, **kw: g.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K,
+                                           tsdf_amd.SE3(fr["q"], fr["t"]), MAXD, **kw)
+    group, fresh = mk(), mk()
+    try:
+        for fr in frames[:3]:
+            step(group, fr, count=True)
+        assert group.cands_exchanged >= 0 and len(group.cands_by_shard) == G
+        real = group.engines[1].integrate_shard_pipe
+
+        def boom(*a, **k):
+            raise RuntimeError("injected exchange failure")
+        group.engines[1].integrate_shard_pipe = boom
+        with pytest.raises(RuntimeError, match="injected"):
+            step(group, frames[3])
+        group.engines[1].integrate_shard_pipe = real
+        for e in group.engines:  # both shards dropped their pending frames
+            assert e.stats(clear_status=True)["status"] & tsdf_amd.STATUS_SHARD_ABORTED
+            e.snapshot()  # (between frames again: no pending frame to flush)
+            e.reset()
+        for fr in frames:
+            step(group, fr)
+            step(fresh, fr)
+        group.flush()
+        fresh.flush()
+        for a, b in zip(group.engines, fresh.engines):
+            assert a.stats()["status"] == 0 and b.stats()["status"] == 0
+            da, db = a.dump(), b.dump()
+            for k in ("entry_pos", "entry_idx", "heap", "tsdf", "rgbw"):
+                assert np.array_equal(da[k], db[k]), k
+            assert a.stats()["active_blocks"] > 0
+    finally:
+        group.close()
+        fresh.close()
+
+
 @pytest.mark.parametrize("split", [True, False])
 def test_sharded_graph_frames_equal_oracle(split):
     """C5 on a sharded volume: every shard's frame as its three captured graph segments
