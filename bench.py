@@ -90,6 +90,10 @@ def parse():
                    help="process-group backend for N > 1: nccl (RCCL over xGMI, one GPU per rank) or gloo "
                         "(a rehearsal of the multi-rank code path; ranks may share a GPU, exchanges staged "
                         "through the host -- not a performance number)")
+    p.add_argument("--host-frames", choices=("pageable", "pinned"), default=None,
+                   help="single GPU: frames in host memory (the reference API's cv::Mat inputs), passed as "
+                        "TSDF_MEM_HOST -- the engine uploads each frame (voxel_tsdf.cu:358-365) on its upload "
+                        "stream beside the previous frames' kernels; the line reports the upload alone too")
     p.add_argument("--block-bits", type=int, default=18)
     p.add_argument("--event-every", type=int, default=0,
                    help="HIP-event-time the frame kernel on every n-th timed frame (a dispatch with bound "
@@ -109,6 +113,8 @@ def workload_name(a):
         w = f"{W}x{H} depth{'' if a.depth_only else ' + ht/lt semantic'}"
     if a.loop == "c5":
         w = "C5: " + w + ", raycast every frame, marching cubes every 30 frames"
+    if a.host_frames:
+        w += f", {a.host_frames} host frames (TSDF_MEM_HOST: uploaded by the engine every frame)"
     return (w + f", {a.voxel * 1000:g} mm voxel, {a.trunc * 100:g} cm truncation, {a.max_depth:g} m "
             f"max depth, {'TUM fr1' if W <= 640 else 'L515 full-res'} intrinsics, orbit 1 cm + 0.5 deg/frame")
 
@@ -412,6 +418,11 @@ def main():
 
     frames, poses = stream_frames(mode)
     torch.cuda.synchronize()
+    upload = None
+    if a.host_frames:
+        if world > 1:
+            raise SystemExit("--host-frames is a single-GPU line")
+        frames, upload = host_frames(a, frames)
     run = Run(a, mode, rank, world, dev, cam, frames, K, poses, dist)
     elapsed, prof = run.timed()
     st = run.eng.stats()
@@ -559,6 +570,8 @@ def main():
         }
         if ray is not None:
             out["raycast"] = ray
+        if upload is not None:
+            out["host_frames"] = upload
         if world > 1:
             out["frames_per_s_per_stream"] = round(fps_stream, 2)
         if bcast is not None:
@@ -570,6 +583,41 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def host_frames(a, fr, reps=20):
+    """--host-frames: the stream's frames copied to host memory (pageable numpy arrays, or pinned torch
+    tensors), and the upload alone timed: `reps` uploads of one frame's four arrays (rgb u8, depth /
+    ht / lt f32) into device buffers on a side stream, between events -- the PCIe share of a frame."""
+    import numpy as np
+    import torch
+    keys = ("rgb", "depth") + (() if a.depth_only else ("ht", "lt"))
+    out = dict(fr)
+    for k in keys:
+        t = fr[k].cpu()
+        out[k] = [t[i].pin_memory() for i in range(t.shape[0])] if a.host_frames == "pinned" else \
+                 [np.ascontiguousarray(t[i].numpy()) for i in range(t.shape[0])]
+    dst = {k: torch.empty_like(fr[k][0]) for k in keys}
+    src = {k: (out[k][0] if a.host_frames == "pinned" else torch.from_numpy(out[k][0])) for k in keys}
+    st = torch.cuda.Stream()
+    nbytes = sum(v.numel() * v.element_size() for v in dst.values())
+    with torch.cuda.stream(st):
+        for k in keys:
+            dst[k].copy_(src[k], non_blocking=True)
+        st.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            for k in keys:
+                dst[k].copy_(src[k], non_blocking=True)
+        e1.record(st)
+        st.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    return out, {"kind": a.host_frames, "bytes_per_frame": int(nbytes), "h2d_us_per_frame": round(us, 2),
+                 "h2d_gbs": round(nbytes / (us * 1e-6) / 1e9, 2),
+                 "note": "upload alone: 4 host-to-device copies of one frame on a side stream, events, "
+                         f"{reps} reps; the line's value includes the engine's own uploads (its upload stream, "
+                         "overlapped with the previous frames' kernels)"}
 
 
 def frame_broadcast_ms(a, dist, _unused, dev, reps=20):

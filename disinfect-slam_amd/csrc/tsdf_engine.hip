@@ -146,10 +146,18 @@ struct tsdf_engine {
   int64_t order_range = 0;  // candidate order space: max_pixels * maxs
   int64_t max_pixels = 0;
   // host-frame staging
+  // host frames (TSDF_MEM_HOST, voxel_tsdf.cu:358-365): two staging slots filled on the upload stream
+  // (a copy engine) while the engine stream runs the previous frames; slot k at offset k * max_pixels
   uint8_t* s_rgb = nullptr;
   float* s_depth = nullptr;
   float* s_ht = nullptr;
   float* s_lt = nullptr;
+  hipStream_t ustream = nullptr;          // upload stream
+  hipEvent_t up_done[2] = {nullptr, nullptr};  // slot k's upload complete (the engine stream waits)
+  hipEvent_t up_free[2] = {nullptr, nullptr};  // slot k's last reader launched before this (the upload waits)
+  bool up_used[2] = {false, false};       // up_free[k] has been recorded
+  int up_next = 0;                        // the slot of the next host frame
+  int up_pending = -1;                    // the slot of a frame whose reading launch is not enqueued yet
   // raycast / query / test scratch
   uchar4* rc_rgba = nullptr;
   uchar4* rc_norm = nullptr;
@@ -254,6 +262,11 @@ void free_all(tsdf_engine* e) {
     for (hipEvent_t x : ev) (void)hipEventDestroy(x);
   if (e->order_ev) (void)hipEventDestroy(e->order_ev);
   if (e->rstream) (void)hipStreamDestroy(e->rstream);
+  if (e->ustream) (void)hipStreamDestroy(e->ustream);
+  for (int k = 0; k < 2; ++k) {
+    if (e->up_done[k]) (void)hipEventDestroy(e->up_done[k]);
+    if (e->up_free[k]) (void)hipEventDestroy(e->up_free[k]);
+  }
   if (e->rs_ready) (void)hipEventDestroy(e->rs_ready);
   if (e->rs_done) (void)hipEventDestroy(e->rs_done);
   if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
@@ -585,10 +598,10 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
   ALLOC(D.dbg, (size_t)kDiagKernels * kDiagMaxWg * kDiagStamps);
   if (hipMemset(D.dbg, 0, (size_t)kDiagKernels * kDiagMaxWg * kDiagStamps * 8) != hipSuccess)
     return fail(TSDF_ERR_HIP);
-  ALLOC(e->s_rgb, e->max_pixels * 3);
-  ALLOC(e->s_depth, e->max_pixels);
-  ALLOC(e->s_ht, e->max_pixels);
-  ALLOC(e->s_lt, e->max_pixels);
+  ALLOC(e->s_rgb, 2 * e->max_pixels * 3);  // two upload slots (host frames)
+  ALLOC(e->s_depth, 2 * e->max_pixels);
+  ALLOC(e->s_ht, 2 * e->max_pixels);
+  ALLOC(e->s_lt, 2 * e->max_pixels);
   ALLOC(e->rc_rgba, e->max_pixels);
   ALLOC(e->rc_norm, e->max_pixels);
   ALLOC(e->vg_flags, (size_t)kViewBitmapWords * 32);
@@ -615,6 +628,12 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
       return fail(TSDF_ERR_HIP);
     e->own_stream = true;
   }
+  if (hipStreamCreateWithFlags(&e->ustream, hipStreamNonBlocking) != hipSuccess)
+    return fail(TSDF_ERR_HIP);
+  for (int k = 0; k < 2; ++k)
+    if (hipEventCreateWithFlags(&e->up_done[k], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->up_free[k], hipEventDisableTiming) != hipSuccess)
+      return fail(TSDF_ERR_HIP);
   if (hipStreamCreateWithFlags(&e->rstream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&e->rs_ready, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->rs_done, hipEventDisableTiming) != hipSuccess)
@@ -661,6 +680,17 @@ int tsdf_synchronize(tsdf_engine* e) {
 
 namespace {
 
+// the launch that reads the pending uploaded frame has been enqueued on the engine stream: its slot is
+// free for an upload once the engine stream gets here
+int upload_release(tsdf_engine* e) {
+  if (e->up_pending < 0) return TSDF_OK;
+  const int k = e->up_pending;
+  e->up_pending = -1;
+  HIP_OK(hipEventRecord(e->up_free[k], e->stream));
+  e->up_used[k] = true;
+  return TSDF_OK;
+}
+
 // the next profiling event set (a std::deque: push_back never moves the sets earlier frames hold)
 int take_events(tsdf_engine* e, std::array<hipEvent_t, 5>** out) {
   if (e->ev_used == e->events.size()) {
@@ -697,17 +727,35 @@ int frame_ingest(tsdf_engine* e, const EngineDev& Dv, const tsdf_frame* f, const
   const uint8_t* rgb = f->rgb;
   const float* ht = f->ht;
   const float* lt = f->lt;
-  if (f->mem_kind == TSDF_MEM_HOST) {  // voxel_tsdf.cu:358-365 (pageable H2D)
-    HIP_OK(hipMemcpyAsync(e->s_rgb, rgb, np * 3, hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(e->s_depth, depth, np * 4, hipMemcpyHostToDevice, s));
-    rgb = e->s_rgb;
-    depth = e->s_depth;
+  if (f->mem_kind == TSDF_MEM_HOST) {  // voxel_tsdf.cu:358-365 (H2D; pageable or pinned host memory)
+    // The upload runs on the upload stream into the next of two staging slots, beside the frames the
+    // engine stream is still running; the engine stream waits for it (up_done) and the slot's next
+    // upload waits until the launch reading this frame is enqueued and done (up_free, recorded by
+    // upload_release). The call returns once the copies are complete, so the caller may reuse its
+    // buffers (the reference's synchronous cudaMemcpy contract).
+    upload_release(e);
+    const int k = e->up_next;
+    e->up_next ^= 1;
+    hipStream_t u = e->ustream;
+    if (e->up_used[k]) HIP_OK(hipStreamWaitEvent(u, e->up_free[k], 0));
+    uint8_t* d_rgb = e->s_rgb + (size_t)k * e->max_pixels * 3;
+    float* d_depth = e->s_depth + (size_t)k * e->max_pixels;
+    HIP_OK(hipMemcpyAsync(d_rgb, rgb, np * 3, hipMemcpyHostToDevice, u));
+    HIP_OK(hipMemcpyAsync(d_depth, depth, np * 4, hipMemcpyHostToDevice, u));
+    rgb = d_rgb;
+    depth = d_depth;
     if (ht) {
-      HIP_OK(hipMemcpyAsync(e->s_ht, ht, np * 4, hipMemcpyHostToDevice, s));
-      HIP_OK(hipMemcpyAsync(e->s_lt, lt, np * 4, hipMemcpyHostToDevice, s));
-      ht = e->s_ht;
-      lt = e->s_lt;
+      float* d_ht = e->s_ht + (size_t)k * e->max_pixels;
+      float* d_lt = e->s_lt + (size_t)k * e->max_pixels;
+      HIP_OK(hipMemcpyAsync(d_ht, ht, np * 4, hipMemcpyHostToDevice, u));
+      HIP_OK(hipMemcpyAsync(d_lt, lt, np * 4, hipMemcpyHostToDevice, u));
+      ht = d_ht;
+      lt = d_lt;
     }
+    HIP_OK(hipEventRecord(e->up_done[k], u));
+    HIP_OK(hipStreamWaitEvent(s, e->up_done[k], 0));
+    HIP_OK(hipEventSynchronize(e->up_done[k]));  // (the host buffers are free again)
+    e->up_pending = k;
   } else if (f->mem_kind != TSDF_MEM_DEVICE) {
     set_error("tsdf_integrate: bad mem_kind");
     return TSDF_ERR_INVALID_ARG;
@@ -943,7 +991,10 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
   const bool ingest_alone = !pipe || e->ps == tsdf_engine::kPipeNone;
   int rc = frame_ingest(e, Dv, f, K, pose, max_depth, 0, 1, &P, &ev, nullptr, 0, ingest_alone, (int)(fid & 1u));
   if (rc) return rc;
-  if (!pipe) return frame_update(e, Dv, P, ev);
+  if (!pipe) {
+    rc = frame_update(e, Dv, P, ev);
+    return rc ? rc : upload_release(e);
+  }
   if (ingest_alone) {
     // (no k_frame / k_integrate launch to time in this call: the slot is released, and the update,
     // if a flush launches it as k_integrate, takes one then)
@@ -952,12 +1003,12 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
     e->ps = tsdf_engine::kPipeU;
     e->p_fid = fid;
     e->p_P = P;
-    return TSDF_OK;
+    return upload_release(e);  // (k_ingest_dda read the frame)
   }
   rc = launch_frame(e, pipe_step(e, true, fid, P), e->p_P, P, ev);
   if (rc) return rc;
   pipe_advance(e, fid, P);
-  return TSDF_OK;
+  return upload_release(e);  // (the launch's tiles read the frame)
 }
 
 int tsdf_flush(tsdf_engine* e) {
@@ -1024,7 +1075,7 @@ int tsdf_integrate_shard_update(tsdf_engine* e, const void* keys_in, int32_t key
   int rc = frame_update(e, e->D, e->shard_P, e->shard_ev, cands_out, cand_cap);
   if (rc) return rc;
   e->shard_phase = 2;
-  return TSDF_OK;
+  return upload_release(e);  // (a shard's k_integrate reads the raw frame)
 }
 
 int tsdf_integrate_shard_end(tsdf_engine* e, const void* cands_in, int32_t cand_cap) {
@@ -1119,14 +1170,14 @@ int tsdf_integrate_shard_pipe(tsdf_engine* e, const tsdf_frame* f, const tsdf_in
     e->ps = tsdf_engine::kPipeU;
     e->p_fid = fid;
     e->p_P = P;
-    return TSDF_OK;
+    return upload_release(e);
   }
   PipeArgs A = pipe_step(e, true, fid, P);
   shard_args(A);
   rc = launch_frame(e, A, e->p_P, P, ev);
   if (rc) return rc;
   pipe_advance(e, fid, P);
-  return TSDF_OK;
+  return upload_release(e);
 }
 
 int tsdf_integrate_shard_abort(tsdf_engine* e) {
@@ -1145,6 +1196,7 @@ int tsdf_integrate_shard_abort(tsdf_engine* e) {
   e->ps = tsdf_engine::kPipeNone;
   hipLaunchKernelGGL(k_shard_abort, dim3(1), dim3(256), 0, e->stream, e->D);
   LAUNCH_OK("k_shard_abort");
+  if (int rc = upload_release(e)) return rc;
   return TSDF_OK;
 }
 

@@ -368,7 +368,9 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
   } else if (Graph) {
     P.tail = kTailResolve;
   }
+#ifdef TSDF_LOCKSTEP_UPDATE
   __shared__ float s_min[4];
+#endif
   __shared__ int s_upd[4];
   __shared__ int s_last;
   __shared__ int s_ncand, s_ovf;
@@ -397,6 +399,66 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
   // records stay resident in that XCD's L2.
   const int npairs = (nvis + 1) >> 1;
   const int p_lo = (int)(((long long)npairs * g) >> 3), p_hi = (int)(((long long)npairs * (g + 1)) >> 3);
+#ifndef TSDF_LOCKSTEP_UPDATE
+  // Chunks of kPipeList records: wave 0 gathers one record per lane (no serial list walk), then the
+  // two pairs of waves update records pair, pair + 2, ... without a workgroup barrier, the two halves
+  // of a record combining their carve minima through LDS (as pipe_update)
+  __shared__ VisRec s_list[kPipeList];
+  __shared__ float s_pmin[2 * kPipeList];
+  __shared__ int s_pdone[kPipeList];
+  __shared__ int s_n;
+  for (int pp0 = p_lo + (blockIdx.x >> 3); pp0 < p_hi; pp0 += ngrp * (kPipeList / 2)) {
+    lds_barrier();  // (the previous chunk's records are done)
+    if (wave == 0) {
+      const int pp = pp0 + (lane >> 1) * ngrp, b = 2 * pp + (lane & 1);
+      const bool valid = pp < p_hi && b < nvis;
+      int bd = 0, bs = 0;
+#pragma unroll
+      for (int k = 1; k < kBands; ++k) {
+        const int sk = __builtin_amdgcn_readlane(bst, k);
+        if (b >= sk) {
+          bd = k;
+          bs = sk;
+        }
+      }
+      VisRec r{};
+      if (valid) r = b >= nband ? D.fresh_vis[b - nband] : D.vis[(size_t)bd * D.nblocks + (size_t)(b - bs)];
+      const unsigned long long vm = __ballot(valid);
+      if (valid) s_list[__popcll(vm & ((1ull << lane) - 1ull))] = r;
+      s_pdone[lane] = 0;
+      if (lane == 0) s_n = __popcll(vm);
+    }
+    lds_barrier();
+    const int n = s_n;
+    for (int k = pair; k < n; k += 2) {
+      const VisRec r = s_list[k];
+      float mn = __builtin_inff();
+      update_block<Raw>(D, P, r, lane, hf, mn, my_upd);
+      mn = wave_min_u(mn);
+      if (lane == 0) {
+        s_pmin[2 * k + hf] = mn;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // (LDS only: pool stores stay in flight)
+        if (atomicAdd(&s_pdone[k], 1) == 1) {  // the record's other half is done too
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+          const float m2 = fminf(mn, s_pmin[2 * k + (hf ^ 1)]);
+          if (m2 >= 0.9f) {  // space_carving_kernel threshold (voxel_tsdf.cu:227, :485)
+            const int kc = atomicAdd(&s_ncand, 1);
+            if (kc < kIntegrateCandBuf) {
+              s_cand[kc] = r;
+            } else {  // buffer full (heavy carving): publish this one now
+              const int kg = atomicAdd(D.ncand, 1);
+              const unsigned long long* rv = reinterpret_cast<const unsigned long long*>(&r);
+              unsigned long long* dst = reinterpret_cast<unsigned long long*>(&D.cand[kg]);
+              st_co(&dst[0], rv[0]);
+              st_co(&dst[1], rv[1]);
+              s_ovf = 1;
+            }
+          }
+        }
+      }
+    }
+  }
+#else
   for (int pp = p_lo + (blockIdx.x >> 3); pp < p_hi; pp += ngrp) {
     const int b = 2 * pp + pair;
     float mn = __builtin_inff();
@@ -430,6 +492,7 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
     }
     lds_barrier();
   }
+#endif
   // updated-voxel count: the workgroup's total rides on its arrival (summed by the last arriver)
   const int tot = wave_sum(my_upd);
   if (lane == 0) s_upd[wave] = tot;
@@ -463,7 +526,11 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
 #endif
   // waves that published drain their stores before the workgroup arrives (wave 0: the buffer;
   // the even waves' lane 0: overflow records)
+#ifndef TSDF_LOCKSTEP_UPDATE
+  const bool drain = (wave == 0 && nc > 0) || s_ovf;  // (overflow records: published by either half's wave)
+#else
   const bool drain = (wave == 0 && nc > 0) || (s_ovf && (wave & 1) == 0);
+#endif
   if (!arrive_last(D.arrive + kArrIntegrate, wg_upd, &s_last, drain, (uint32_t)nint)) return false;
   integrate_tail(D, P, L);
   return true;
@@ -542,9 +609,225 @@ __device__ __forceinline__ void publish_flags(unsigned long long* flags, uint32_
                                 __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---------------------------------------------------------------------------------------------
+// The head's fast path (k_frame workgroup 0): frame b - 1's carving and frame b's allocation as the
+// commit-all fast paths resolve_delete_fast + resolve_alloc_fast would run them one after the other,
+// but with the allocation's inputs -- its new keys, their candidate orders, their buckets, the free
+// stack's top -- loaded in the same two round trips as the carving's, before the carving commits.
+// The carving changes what the allocation reads in three known ways, applied from LDS instead of
+// re-reading: the entries it clears (a key's bucket then has that slot empty), the blocks it pushes on
+// the free stack (popped first, in reverse push order) and the keys carved_key would re-insert into
+// the new-key set (then this path is not taken). Anything outside both fast paths' conditions returns
+// false before a global write, and the sequential resolvers run. Results are identical either way
+// (tests/test_gpu_pipeline.py, test_gpu_fullsize.py: the oracle decides).
+// ---------------------------------------------------------------------------------------------
+#ifdef TSDF_NO_HEAD_FAST
+__device__ constexpr bool head_fast_off() { return true; }
+#else
+__device__ constexpr bool head_fast_off() { return false; }
+#endif
+constexpr int kHeadCleared = 1024;  // set of the entries the carving clears (<= 2 kRT), open addressing
+struct HeadLds {
+  uint32_t ev[2 * kRT];         // entries of the released candidates (push rank = number smaller)
+  int32_t pushed[2 * kRT];      // pool index pushed at rank r
+  uint32_t cleared[kHeadCleared];
+  uint32_t lock[kFastLockSlots];  // the allocation's bucket locks
+  uint32_t ordv[kRT];           // candidate orders of the owned keys (pop ranks)
+  int32_t htop[kRT];            // the free stack's top before the carving: heap[free0 - 1 - i]
+  int scan[24];
+};
+__device__ __forceinline__ void cleared_insert(uint32_t* S, uint32_t e) {
+  uint32_t h = mix32(e) & (kHeadCleared - 1);
+  for (int p = 0; p < kHeadCleared; ++p) {
+    const uint32_t prev = atomicCAS(&S[h], 0u, e + 1u);
+    if (prev == 0u || prev == e + 1u) return;
+    h = (h + 1) & (kHeadCleared - 1);
+  }
+}
+__device__ __forceinline__ bool cleared_has(const uint32_t* S, uint32_t e) {
+  uint32_t h = mix32(e) & (kHeadCleared - 1);
+  for (int p = 0; p < kHeadCleared; ++p) {
+    const uint32_t v = S[h];
+    if (v == e + 1u) return true;
+    if (v == 0u) return false;
+    h = (h + 1) & (kHeadCleared - 1);
+  }
+  return false;
+}
+// Both round trips, the decision, and (when taken) every commit of the carving and the allocation,
+// issued together: the two write no common word (an entry the carving clears and a key then takes is
+// written by the allocation alone -- the key's full entry supersedes the cleared one, and its occupancy
+// bit stays set), so one drain before the two flags orders them (the sequential resolvers drain twice).
+// No load follows a store (each counter update is computed from round trip 1's values; a load behind
+// the stores would wait for all of them -- gfx950 counts stores in vmcnt). Returns false, with nothing
+// written, when the launch is outside the fast paths.
+__device__ __forceinline__ bool head_fast(const EngineDev& D, const PipeArgs& A, HeadLds& L) {
+  const int t = threadIdx.x, wave = t >> 6;
+  TSDF_STAMP(D, 4, 0);
+  const unsigned long long tick0 = __builtin_amdgcn_s_memrealtime();
+  const uint32_t fcv = A.fid_carve, fo_fid = A.fid_alloc;
+  const VisRec* cand = D.cand + (size_t)(fcv & 1u) * (size_t)D.cand_cap;
+  const int32_t* ncand = reinterpret_cast<const int32_t*>(D.pipe + kPipeNCand + 16 * (fcv & 1u));
+  // ---- round trip 1: both counts, the counters, the candidate records and the new-key list
+  const int nc = ld_co(ncand);
+  const int na = ld_co(&D.ctr->nk_count);
+  const int free0 = D.ctr->free_count;
+  const uint32_t epoch0 = D.ctr->lock_epoch;
+  const unsigned long long tot_del = D.ctr->total_deleted, tot_alloc = D.ctr->total_alloc;
+  const unsigned long long ticks_del = D.ctr->resolve_delete_ticks, ticks_alloc = D.ctr->resolve_alloc_ticks;
+  const unsigned long long* rq = reinterpret_cast<const unsigned long long*>(cand);
+  const unsigned long long a[2] = {ld_co(&rq[2 * t]), ld_co(&rq[2 * (t + kRT)])};
+  const unsigned long long key = ld_co(&D.nk_list[t].key);
+  const int32_t slot = (int32_t)ld_co(&D.nk_list[t].slot);
+  if (nc > 2 * kRT || na > kRT || free0 < 0) return false;  // (uniform)
+  // ---- round trip 2: the candidates' buckets and D.fo words, the keys' orders and buckets, heap top
+  int16_t x[2] = {0, 0}, z[2] = {0, 0};
+  uint32_t cur[2] = {0u, 0u}, rel_e[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+  int32_t idx[2] = {-1, -1};
+  bool bad = false, rel[2] = {false, false};
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (t + r * kRT >= nc) continue;
+    x[r] = (int16_t)(a[r] & 0xFFFF);
+    const int16_t y = (int16_t)((a[r] >> 16) & 0xFFFF);
+    z[r] = (int16_t)((a[r] >> 32) & 0xFFFF);
+    const uint32_t Ab = hash_block(x[r], y, z[r]);
+    const Ent s0 = load_ent(D.table, 2 * Ab), s1 = load_ent(D.table, 2 * Ab + 1);
+    const unsigned long long fo0 = D.fo[2 * Ab], fo1 = D.fo[2 * Ab + 1];
+    const bool in0 = s0.x == x[r] && s0.y == y && s0.z == z[r] && s0.idx >= 0;
+    const bool head = !in0 && s1.x == x[r] && s1.y == y && s1.z == z[r] && s1.idx >= 0 && s1.off == 0;
+    bad |= !(in0 || head);
+    cur[r] = 2 * Ab + (head ? 1u : 0u);
+    idx[r] = in0 ? s0.idx : s1.idx;
+    rel[r] = (in0 || head) && local_idx(idx[r]);
+    if (rel[r]) rel_e[r] = cur[r];
+    // carved_key would put the deleted key back into frame b's new-key set: not this path
+    bad |= (uint32_t)((head ? fo1 : fo0) >> 32) == ~fo_fid;
+  }
+  const bool have = t < na;
+  uint32_t B = 0u, ord = 0xFFFFFFFFu;
+  int16_t kx = 0, ky = 0, kz = 0;
+  Ent sa0{}, sa1{};
+  if (have) {
+    unpack_key(key, kx, ky, kz);
+    B = hash_block(kx, ky, kz);
+    ord = ld_co(&D.nk_order[slot]);
+    sa0 = load_ent(D.table, 2 * B);
+    sa1 = load_ent(D.table, 2 * B + 1);
+  }
+  const int32_t htop = t < min(na, free0) ? D.heap[free0 - 1 - t] : 0;
+  for (int i = t; i < kHeadCleared; i += kRT) L.cleared[i] = 0u;
+  for (int i = t; i < kFastLockSlots; i += kRT) L.lock[i] = 0u;
+  L.ev[t] = rel_e[0];
+  L.ev[t + kRT] = rel_e[1];
+  L.htop[t] = htop;
+  const unsigned long long bb = __ballot(bad), br0 = __ballot(rel[0]), br1 = __ballot(rel[1]);
+  if (lane_id() == 0) {
+    L.scan[wave] = __popcll(bb);
+    L.scan[4 + wave] = __popcll(br0) + __popcll(br1);
+  }
+  lds_barrier();  // (sets zero, ev / htop / scan written)
+  TSDF_STAMP(D, 4, 3);
+  if (L.scan[0] + L.scan[1] + L.scan[2] + L.scan[3] != 0) return false;
+  const int nrel = L.scan[4] + L.scan[5] + L.scan[6] + L.scan[7];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+    if (t + r * kRT < nc) cleared_insert(L.cleared, cur[r]);
+  lds_barrier();  // (the cleared set is complete)
+  // ---- the allocation against the carved table (resolve_alloc_fast's conditions)
+  const bool c0 = have && cleared_has(L.cleared, 2 * B), c1 = have && cleared_has(L.cleared, 2 * B + 1);
+  const bool e0 = sa0.idx < 0 || c0, e1 = sa1.idx < 0 || c1;
+  const bool abad = have && (!(e0 || e1) || !lock_take2<kFastLockSlots>(L.lock, B));
+  const uint32_t e = 2 * B + (e0 ? 0u : 1u);  // the key's entry
+  L.ordv[t] = have ? ord : 0xFFFFFFFFu;  // (one volume: every key is owned)
+  const unsigned long long ab = __ballot(abad);
+  if (lane_id() == 0) L.scan[8 + wave] = __popcll(ab);
+  // an entry the carving clears and a key takes: written by the allocation only (L.lock reused after
+  // the barrier below as the set of refilled entries -- the allocation's locks are no longer needed)
+  lds_barrier();
+  if (L.scan[8] + L.scan[9] + L.scan[10] + L.scan[11] != 0 || na > free0 + nrel) return false;
+  for (int i = t; i < kHeadCleared; i += kRT) L.cleared[i] = 0u;
+  lds_barrier();
+  if (have && ((e0 && c0) || (!e0 && c1))) cleared_insert(L.cleared, e);
+  lds_barrier();  // (L.cleared: the refilled entries)
+  // ---- taken: the carving's commits (resolve_delete_fast) ...
+  const int nq = (min(nc, 2 * kRT) + 3) >> 2;
+  const uint4* v4 = reinterpret_cast<const uint4*>(L.ev);
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (t + r * kRT >= nc) continue;
+    const uint32_t c = cur[r];
+    if (!cleared_has(L.cleared, c)) {
+      // offset 0 and idx -1 (store_off_idx_co without its read: z and the offset share the dword)
+      uint32_t* q = reinterpret_cast<uint32_t*>(&D.table[c]);
+      st_co(&q[1], (uint32_t)(uint16_t)z[r]);
+      st_co(&q[2], 0xFFFFFFFFu);
+      atomicAnd(&D.occ[c >> 6], ~(1ull << (c & 63)));
+    }
+    mark_swept_dirty(D, c);
+    if (rel[r]) {  // ReleaseBlock in entry order among the released blocks (entries are unique)
+      int rank = 0;
+#pragma unroll 2
+      for (int j = 0; j < nq; ++j) {
+        const uint4 v = v4[j];
+        rank += (v.x < c) + (v.y < c) + (v.z < c) + (v.w < c);
+      }
+      D.heap[free0 + rank] = idx[r];
+      L.pushed[rank] = idx[r];
+      st_co(&D.rtag[idx[r]], fcv);
+    }
+  }
+  lds_barrier();  // (L.pushed)
+  TSDF_STAMP(D, 4, 4);
+  const unsigned long long tick1 = __builtin_amdgcn_s_memrealtime();
+  // ---- ... and the allocation's (resolve_alloc_fast): pops from the carving's pushes first, then the
+  // prefetched top of the stack
+  if (have) {
+    int prank = 0;  // keys earlier in candidate order (orders are unique per key)
+    const uint4* o4 = reinterpret_cast<const uint4*>(L.ordv);
+    const int nq2 = (na + 3) >> 2;
+#pragma unroll 2
+    for (int j = 0; j < nq2; ++j) {
+      const uint4 v = o4[j];
+      prank += (v.x < ord) + (v.y < ord) + (v.z < ord) + (v.w < ord);
+    }
+    const int32_t bi = prank < nrel ? L.pushed[nrel - 1 - prank] : L.htop[prank - nrel];
+    store_ent_co(D.table, e, kx, ky, kz, 0, bi);
+    mark_swept_dirty(D, e);
+    atomicOr(&D.occ[e >> 6], 1ull << (e & 63));
+    VisRec vr;
+    vr.x = kx;
+    vr.y = ky;
+    vr.z = kz;
+    vr.pad = 1;
+    vr.idx = bi;
+    vr.entry = (int32_t)e;
+    st_rec_co(&D.fresh_vis[prank], vr);
+    st_co(&D.nk_key[slot], 0ull);
+    st_co(&D.nk_order[slot], 0xFFFFFFFFu);
+  }
+  if (t == 0) {
+    const unsigned long long tick2 = __builtin_amdgcn_s_memrealtime();
+    D.ctr->lock_epoch = epoch0 + 2u;  // (the carving's launch, then the allocation's)
+    D.ctr->free_count = free0 + nrel - na;
+    D.ctr->last_deleted = nrel;
+    D.ctr->total_deleted = tot_del + (unsigned long long)nrel;
+    D.ctr->resolve_delete_ticks = ticks_del + (tick1 - tick0);
+    D.ctr->resolve_alloc_ticks = ticks_alloc + (tick2 - tick1);
+    st_co(&D.ctr->n_fresh, na);
+    st_co(&D.ctr->nk_count, 0);
+    D.ctr->last_alloc = na;
+    D.ctr->last_new_keys = na;
+    D.ctr->total_alloc = tot_alloc + (unsigned long long)na;
+  }
+  TSDF_STAMP(D, 1, 5);
+  return true;
+}
+
 union FrameLds {
   DeleteLds del;
   IngestLds<1024> ing;
+  HeadLds head;
 };
 
 __device__ __forceinline__ void merge_cands_inbox(const EngineDev& D, VisRec* cand, int32_t* ncand, const ShardRec* __restrict__ cands_in,
@@ -555,12 +838,21 @@ __device__ __forceinline__ void merge_cands_inbox(const EngineDev& D, VisRec* ca
 __device__ __forceinline__ void pipe_head(const EngineDev& D, const FrameParams& Pu, const PipeArgs& A, FrameLds& U) {
   __shared__ int s_base[kMaxShards + 1];
   const int t = threadIdx.x;
+  // one volume's carving + allocation: the combined fast path (head_fast) when the launch is within it:
+  // both commit before one drain, then both flags
+  bool fast = false;
+  if (A.has_carve && A.has_alloc && !A.cands_in && !A.cands_out && !resolve_fast_off() && !head_fast_off()) {
+    fast = head_fast(D, A, U.head);
+    if (!fast) lds_barrier();  // (the sequential resolvers below reuse the LDS)
+  }
   if (A.has_carve) {  // (the view's pointers as scalars: a copied EngineDev view can land in scratch)
     const uint32_t f = A.fid_carve;
     VisRec* cand = D.cand + (size_t)(f & 1u) * (size_t)D.cand_cap;
     int32_t* ncand = reinterpret_cast<int32_t*>(D.pipe + kPipeNCand + 16 * (f & 1u));
-    if (A.cands_in) merge_cands_inbox(D, cand, ncand, A.cands_in, A.cand_cap, A.nshard, s_base);
-    resolve_delete_wg(D, cand, ncand, 0, U.del, f, A.has_alloc ? A.fid_alloc : 0u);
+    if (!fast) {
+      if (A.cands_in) merge_cands_inbox(D, cand, ncand, A.cands_in, A.cand_cap, A.nshard, s_base);
+      resolve_delete_wg(D, cand, ncand, 0, U.del, f, A.has_alloc ? A.fid_alloc : 0u);
+    }
     lds_barrier();
     // the carved frame's candidate count and band counts start empty for frame fid_carve + 2 / + 3
     if (t < kBands) st_co(&D.band[(size_t)(f % 3u) * kBands * kBandStride + t * kBandStride], 0);
@@ -569,23 +861,29 @@ __device__ __forceinline__ void pipe_head(const EngineDev& D, const FrameParams&
   // (a shard: the owned entries this launch's allocation leaves without voxels are listed from here;
   // without an allocation the list is the last one's, packed by this launch's update)
   if (t == 0 && A.cands_out && A.has_alloc) st_co(&D.ctr->n_pend, 0);
+  if (!fast) {
+    drain_barrier();
+    publish_flags(D.pipe + kPipeCarved, A.tag);
+    TSDF_STAMP_WG(D, 8, 0, 3);
+    if (A.has_alloc) resolve_alloc_wg(D, Pu, A.range, 1, U.ing.u.res);
+  }
   drain_barrier();
-  publish_flags(D.pipe + kPipeCarved, A.tag);
-  TSDF_STAMP_WG(D, 8, 0, 3);
-  if (A.has_alloc) {
-    if (t == 0) {  // frame fid_alloc's ingest span (last launch): allocation flag -> last tile / sweep end
+  const unsigned long long t_pub = __builtin_amdgcn_s_memrealtime();
+  if (fast) {
+    publish_flags(D.pipe + kPipeCarved, A.tag);
+    TSDF_STAMP_WG(D, 8, 0, 3);
+  }
+  publish_flags(D.pipe + kPipeAlloc, A.tag);
+  TSDF_STAMP_WG(D, 8, 0, 4);
+  if (t == 0) {
+    D.pipe[kPipeAPub + 16 * (A.fid_new & 1u)] = t_pub;
+    if (A.has_alloc) {  // frame fid_alloc's ingest span (last launch): allocation flag -> last tile / sweep end
       unsigned long long* ie = D.pipe + kPipeIngEnd + 16 * (A.fid_alloc & 1u);
       const unsigned long long a0 = D.pipe[kPipeAPub + 16 * (A.fid_alloc & 1u)], a1 = *ie;
       if (a1 > a0) D.ctr->ingest_ticks += a1 - a0;
       *ie = 0ull;
     }
-    resolve_alloc_wg(D, Pu, A.range, 1, U.ing.u.res);
   }
-  drain_barrier();
-  const unsigned long long t_pub = __builtin_amdgcn_s_memrealtime();
-  publish_flags(D.pipe + kPipeAlloc, A.tag);
-  TSDF_STAMP_WG(D, 8, 0, 4);
-  if (t == 0) D.pipe[kPipeAPub + 16 * (A.fid_new & 1u)] = t_pub;
   if (A.has_carve) pipe_frame_stats(D, A.fid_carve);  // off the chain
 }
 
@@ -606,6 +904,9 @@ __device__ __forceinline__ bool pipe_kept(uint32_t* rtag, int32_t idx, uint32_t 
   if (lane == 0) v = __hip_atomic_fetch_or(&rtag[idx], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return (uint32_t)__builtin_amdgcn_readfirstlane(v) != fc;
 }
+#if defined(TSDF_SERIAL_COLLECT) && !defined(TSDF_LOCKSTEP_UPDATE)
+#define TSDF_LOCKSTEP_UPDATE  // (the barrier-free update needs the parallel collection's LDS state)
+#endif
 // wave_wait_tag: wait_tag for one wave (lane 0 polls; no workgroup barrier)
 __device__ __forceinline__ void wave_wait_tag(const unsigned long long* flag, uint32_t tag, uint32_t* status) {
   if (lane_id() == 0) {
@@ -627,7 +928,9 @@ __device__ __forceinline__ bool lane_kept(uint32_t* rtag, int32_t idx, uint32_t 
 // (D: the base view; frame b's lists are addressed through scalar pointers here -- an EngineDev view
 // copied by value, or captured by reference in a lambda, can be materialised in scratch)
 __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParams& P, const PipeArgs& A, int kind, int wi) {
+#ifdef TSDF_LOCKSTEP_UPDATE
   __shared__ float s_min[4];
+#endif
   __shared__ int s_upd[4], s_vis[4];
   __shared__ int s_ncand;
   __shared__ VisRec s_cand[kIntegrateCandBuf];  // this workgroup's carve candidates
@@ -686,6 +989,11 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
   // together, two dependent round trips per collection instead of two per record), compacted into
   // s_list by ballot; the deferred candidates' release tags likewise one per lane
   __shared__ int s_n, s_ndef;
+  __shared__ float s_pmin[2 * kPipeList];  // the two halves' carve minima of each collected record
+  __shared__ int s_pdone[kPipeList];       // halves of the record done
+  __shared__ uint32_t s_fb;                // fb for the candidate path (read from LDS: in a register the
+                                           // frame id was spilled to scratch, reloaded behind a vmcnt(0))
+  if (t0) s_fb = fb;
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
   if (t0) s_ndef = 0;  // (ordered before its first read by the loop's barrier)
 #endif
@@ -732,6 +1040,7 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
         }
         const unsigned long long tm = __ballot(take);
         if (take) s_list[__popcll(tm & lt_mask)] = r;
+        s_pdone[lane] = 0;
         if (lane == 0) {
           s_n = __popcll(tm);
           s_ndef = ndef;
@@ -750,6 +1059,7 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
         }
         const unsigned long long tm = __ballot(take);
         if (take) s_list[__popcll(tm & lt_mask)] = r;
+        s_pdone[lane] = 0;
         if (lane == 0) s_n = __popcll(tm);
       }
       def_done = true;
@@ -814,6 +1124,39 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
       q[5] += (unsigned long long)n + 1ull;
     }
 #endif
+#ifndef TSDF_LOCKSTEP_UPDATE
+    // ---- update: the two pairs of waves take records pair, pair + 2, ...; no workgroup barrier: the
+    // two waves of a record combine their carve minima through LDS (the second to finish decides), so
+    // every wave runs its records at its own pace and one wave's memory waits overlap the others' work
+    for (int k = pair; k < n; k += 2) {
+      const VisRec r = s_list[k];
+      float mn = __builtin_inff();
+      update_block<false>(D, P, r, lane, hf, mn, my_upd);
+      my_vis += hf == 0 ? 1 : 0;
+      mn = wave_min_u(mn);
+      if (lane == 0) {
+        s_pmin[2 * k + hf] = mn;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // (LDS only: pool stores stay in flight)
+        if (atomicAdd(&s_pdone[k], 1) == 1) {  // the record's other half is done too
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+          const float m2 = fminf(mn, s_pmin[2 * k + (hf ^ 1)]);
+          if (m2 >= 0.9f) {  // space_carving_kernel threshold (voxel_tsdf.cu:227, :485)
+            const uint32_t f = s_fb;
+            D.ctag[(size_t)(f & 1u) * D.nblocks + r.idx] = f;  // (read by the next launch's update)
+            const int kc = atomicAdd(&s_ncand, 1);
+            if (kc < kIntegrateCandBuf) {
+              s_cand[kc] = r;
+            } else {  // buffer full (heavy carving): this one now
+              const int kg = atomicAdd(ncand, 1);
+              if (kg < D.cand_cap) st_rec_co(&cand[kg], r);
+              else atomicOr(&D.ctr->status, 16u);  // (a list longer than the pool: internal error)
+            }
+          }
+        }
+      }
+    }
+  }
+#else
     // ---- update: the two pairs of waves take records 2 j + pair
     for (int j = 0; 2 * j < n; ++j) {
       const int k = 2 * j + pair;
@@ -845,6 +1188,7 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
       lds_barrier();
     }
   }
+#endif
   // the workgroup's carve candidates (read by the next launch's carving) and statistics
   const int tot = wave_sum(my_upd);
   if (lane == 0) {

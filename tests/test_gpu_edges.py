@@ -104,6 +104,9 @@ def test_max_image_1920x1080_and_oversized_frames():
 
 
 def test_device_frames_match_host_frames():
+    """Host frames (pageable numpy, then pinned torch, alternating: the engine's two upload slots are
+    each reused several times while the pipelined frames before them run) equal device frames; the
+    host buffers are overwritten right after each call (the upload is complete on return)."""
     import torch
 
     import tsdf_amd
@@ -113,10 +116,16 @@ def test_device_frames_match_host_frames():
     a = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=14)
     b = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=14)
     try:
-        for f in range(4):
+        for f in range(10):
             fr = synth.render(cam, 2 * f)
             pose = tsdf_amd.SE3(fr["q"], fr["t"])
-            a.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, pose, 4.0)
+            if f % 2:
+                hf = {k: torch.from_numpy(np.ascontiguousarray(fr[k])).pin_memory() for k in ("rgb", "depth", "ht", "lt")}
+            else:
+                hf = {k: np.array(fr[k], copy=True) for k in ("rgb", "depth", "ht", "lt")}
+            a.integrate(hf["rgb"], hf["depth"], hf["ht"], hf["lt"], cam.K, pose, 4.0)
+            for k in hf:  # (the caller may reuse its buffers at once)
+                hf[k][...] = 0
             dv = {k: torch.from_numpy(np.ascontiguousarray(fr[k])).cuda() for k in ("rgb", "depth", "ht", "lt")}
             b.integrate(dv["rgb"], dv["depth"], dv["ht"], dv["lt"], cam.K, pose, 4.0)
         b.synchronize()
@@ -138,7 +147,7 @@ def test_null_arguments_return_invalid_arg():
     from tsdf_amd import _lib, synth
     L = _lib.load()
     cam = synth.camera(64, 48, synth.TUM_FR1)
-    eng = tsdf_amd.Engine(0.01, 0.04, max_width=64, max_height=48, num_block_bits=10)
+    eng = tsdf_amd.Engine(0.01, 0.04, max_width=64, max_height=48, num_block_bits=14)
     try:
         K = _lib.Intrinsics(*[float(v) for v in cam.K])
         pose = _lib.Pose(0, 0, 0, 1, 0, 0, 0)
