@@ -682,12 +682,15 @@ namespace {
 
 // the launch that reads the pending uploaded frame has been enqueued on the engine stream: its slot is
 // free for an upload once the engine stream gets here
+// and the call returns only once the upload is complete: the caller may reuse its host buffers (the
+// reference's synchronous cudaMemcpy contract)
 int upload_release(tsdf_engine* e) {
   if (e->up_pending < 0) return TSDF_OK;
   const int k = e->up_pending;
   e->up_pending = -1;
   HIP_OK(hipEventRecord(e->up_free[k], e->stream));
   e->up_used[k] = true;
+  HIP_OK(hipEventSynchronize(e->up_done[k]));
   return TSDF_OK;
 }
 
@@ -733,7 +736,7 @@ int frame_ingest(tsdf_engine* e, const EngineDev& Dv, const tsdf_frame* f, const
     // upload waits until the launch reading this frame is enqueued and done (up_free, recorded by
     // upload_release). The call returns once the copies are complete, so the caller may reuse its
     // buffers (the reference's synchronous cudaMemcpy contract).
-    upload_release(e);
+    if (int rc = upload_release(e)) return rc;
     const int k = e->up_next;
     e->up_next ^= 1;
     hipStream_t u = e->ustream;
@@ -754,7 +757,8 @@ int frame_ingest(tsdf_engine* e, const EngineDev& Dv, const tsdf_frame* f, const
     }
     HIP_OK(hipEventRecord(e->up_done[k], u));
     HIP_OK(hipStreamWaitEvent(s, e->up_done[k], 0));
-    HIP_OK(hipEventSynchronize(e->up_done[k]));  // (the host buffers are free again)
+    // (the host waits for the copies in upload_release, after the launch that reads them is enqueued:
+    // the enqueue overlaps the transfer)
     e->up_pending = k;
   } else if (f->mem_kind != TSDF_MEM_DEVICE) {
     set_error("tsdf_integrate: bad mem_kind");
@@ -990,10 +994,14 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
   // the first frame after a flush runs k_ingest_dda (its ingest and allocation in one launch)
   const bool ingest_alone = !pipe || e->ps == tsdf_engine::kPipeNone;
   int rc = frame_ingest(e, Dv, f, K, pose, max_depth, 0, 1, &P, &ev, nullptr, 0, ingest_alone, (int)(fid & 1u));
-  if (rc) return rc;
+  if (rc) {
+    (void)upload_release(e);  // (a failed launch after the upload: the host buffers are still read)
+    return rc;
+  }
   if (!pipe) {
     rc = frame_update(e, Dv, P, ev);
-    return rc ? rc : upload_release(e);
+    const int ru = upload_release(e);
+    return rc ? rc : ru;
   }
   if (ingest_alone) {
     // (no k_frame / k_integrate launch to time in this call: the slot is released, and the update,
@@ -1006,7 +1014,10 @@ int tsdf_integrate(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K
     return upload_release(e);  // (k_ingest_dda read the frame)
   }
   rc = launch_frame(e, pipe_step(e, true, fid, P), e->p_P, P, ev);
-  if (rc) return rc;
+  if (rc) {
+    (void)upload_release(e);
+    return rc;
+  }
   pipe_advance(e, fid, P);
   return upload_release(e);  // (the launch's tiles read the frame)
 }
@@ -1043,6 +1054,8 @@ int tsdf_integrate_shard_begin(tsdf_engine* e, const tsdf_frame* f, const tsdf_i
   // split DDA: the last workgroup packs this slice's keys into keys_out; whole-frame DDA (no key
   // exchange): it resolves the allocation right away, like one volume
   int rc = frame_ingest(e, e->D, f, K, pose, max_depth, slice_index, slice_count, &P, &ev, keys_out, key_cap);
+  // (a host frame: its upload is complete on return -- the slot itself is released after _update)
+  if (e->up_pending >= 0) HIP_OK(hipEventSynchronize(e->up_done[e->up_pending]));
   if (rc) return rc;
   P.tail = kTailResolve;
   P.slot = nullptr;

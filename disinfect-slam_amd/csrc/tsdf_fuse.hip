@@ -368,9 +368,7 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
   } else if (Graph) {
     P.tail = kTailResolve;
   }
-#ifdef TSDF_LOCKSTEP_UPDATE
   __shared__ float s_min[4];
-#endif
   __shared__ int s_upd[4];
   __shared__ int s_last;
   __shared__ int s_ncand, s_ovf;
@@ -399,66 +397,9 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
   // records stay resident in that XCD's L2.
   const int npairs = (nvis + 1) >> 1;
   const int p_lo = (int)(((long long)npairs * g) >> 3), p_hi = (int)(((long long)npairs * (g + 1)) >> 3);
-#ifndef TSDF_LOCKSTEP_UPDATE
-  // Chunks of kPipeList records: wave 0 gathers one record per lane (no serial list walk), then the
-  // two pairs of waves update records pair, pair + 2, ... without a workgroup barrier, the two halves
-  // of a record combining their carve minima through LDS (as pipe_update)
-  __shared__ VisRec s_list[kPipeList];
-  __shared__ float s_pmin[2 * kPipeList];
-  __shared__ int s_pdone[kPipeList];
-  __shared__ int s_n;
-  for (int pp0 = p_lo + (blockIdx.x >> 3); pp0 < p_hi; pp0 += ngrp * (kPipeList / 2)) {
-    lds_barrier();  // (the previous chunk's records are done)
-    if (wave == 0) {
-      const int pp = pp0 + (lane >> 1) * ngrp, b = 2 * pp + (lane & 1);
-      const bool valid = pp < p_hi && b < nvis;
-      int bd = 0, bs = 0;
-#pragma unroll
-      for (int k = 1; k < kBands; ++k) {
-        const int sk = __builtin_amdgcn_readlane(bst, k);
-        if (b >= sk) {
-          bd = k;
-          bs = sk;
-        }
-      }
-      VisRec r{};
-      if (valid) r = b >= nband ? D.fresh_vis[b - nband] : D.vis[(size_t)bd * D.nblocks + (size_t)(b - bs)];
-      const unsigned long long vm = __ballot(valid);
-      if (valid) s_list[__popcll(vm & ((1ull << lane) - 1ull))] = r;
-      s_pdone[lane] = 0;
-      if (lane == 0) s_n = __popcll(vm);
-    }
-    lds_barrier();
-    const int n = s_n;
-    for (int k = pair; k < n; k += 2) {
-      const VisRec r = s_list[k];
-      float mn = __builtin_inff();
-      update_block<Raw>(D, P, r, lane, hf, mn, my_upd);
-      mn = wave_min_u(mn);
-      if (lane == 0) {
-        s_pmin[2 * k + hf] = mn;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // (LDS only: pool stores stay in flight)
-        if (atomicAdd(&s_pdone[k], 1) == 1) {  // the record's other half is done too
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-          const float m2 = fminf(mn, s_pmin[2 * k + (hf ^ 1)]);
-          if (m2 >= 0.9f) {  // space_carving_kernel threshold (voxel_tsdf.cu:227, :485)
-            const int kc = atomicAdd(&s_ncand, 1);
-            if (kc < kIntegrateCandBuf) {
-              s_cand[kc] = r;
-            } else {  // buffer full (heavy carving): publish this one now
-              const int kg = atomicAdd(D.ncand, 1);
-              const unsigned long long* rv = reinterpret_cast<const unsigned long long*>(&r);
-              unsigned long long* dst = reinterpret_cast<unsigned long long*>(&D.cand[kg]);
-              st_co(&dst[0], rv[0]);
-              st_co(&dst[1], rv[1]);
-              s_ovf = 1;
-            }
-          }
-        }
-      }
-    }
-  }
-#else
+  // (The chunked, barrier-free form of pipe_update measured slower here, 14.07-14.27k vs 14.8k frames/s
+  // at C4 on one box: a k_integrate workgroup updates one or two pairs, so the collection's extra round
+  // trip is not amortised.)
   for (int pp = p_lo + (blockIdx.x >> 3); pp < p_hi; pp += ngrp) {
     const int b = 2 * pp + pair;
     float mn = __builtin_inff();
@@ -492,7 +433,6 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
     }
     lds_barrier();
   }
-#endif
   // updated-voxel count: the workgroup's total rides on its arrival (summed by the last arriver)
   const int tot = wave_sum(my_upd);
   if (lane == 0) s_upd[wave] = tot;
@@ -526,11 +466,7 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
 #endif
   // waves that published drain their stores before the workgroup arrives (wave 0: the buffer;
   // the even waves' lane 0: overflow records)
-#ifndef TSDF_LOCKSTEP_UPDATE
-  const bool drain = (wave == 0 && nc > 0) || s_ovf;  // (overflow records: published by either half's wave)
-#else
   const bool drain = (wave == 0 && nc > 0) || (s_ovf && (wave & 1) == 0);
-#endif
   if (!arrive_last(D.arrive + kArrIntegrate, wg_upd, &s_last, drain, (uint32_t)nint)) return false;
   integrate_tail(D, P, L);
   return true;
@@ -904,9 +840,6 @@ __device__ __forceinline__ bool pipe_kept(uint32_t* rtag, int32_t idx, uint32_t 
   if (lane == 0) v = __hip_atomic_fetch_or(&rtag[idx], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return (uint32_t)__builtin_amdgcn_readfirstlane(v) != fc;
 }
-#if defined(TSDF_SERIAL_COLLECT) && !defined(TSDF_LOCKSTEP_UPDATE)
-#define TSDF_LOCKSTEP_UPDATE  // (the barrier-free update needs the parallel collection's LDS state)
-#endif
 // wave_wait_tag: wait_tag for one wave (lane 0 polls; no workgroup barrier)
 __device__ __forceinline__ void wave_wait_tag(const unsigned long long* flag, uint32_t tag, uint32_t* status) {
   if (lane_id() == 0) {
@@ -928,9 +861,6 @@ __device__ __forceinline__ bool lane_kept(uint32_t* rtag, int32_t idx, uint32_t 
 // (D: the base view; frame b's lists are addressed through scalar pointers here -- an EngineDev view
 // copied by value, or captured by reference in a lambda, can be materialised in scratch)
 __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParams& P, const PipeArgs& A, int kind, int wi) {
-#ifdef TSDF_LOCKSTEP_UPDATE
-  __shared__ float s_min[4];
-#endif
   __shared__ int s_upd[4], s_vis[4];
   __shared__ int s_ncand;
   __shared__ VisRec s_cand[kIntegrateCandBuf];  // this workgroup's carve candidates
@@ -984,7 +914,6 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
   int my_upd = 0, my_vis = 0, ndef = 0;
   bool def_done = false;
   const bool fresh_co = kind != 0 || (after_alloc && !A.fresh_ready);  // (written in this launch)
-#ifndef TSDF_SERIAL_COLLECT
   // the collection is wave 0's: one record per lane (its list record and candidate tag gathered
   // together, two dependent round trips per collection instead of two per record), compacted into
   // s_list by ballot; the deferred candidates' release tags likewise one per lane
@@ -996,11 +925,9 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
   if (t0) s_fb = fb;
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
   if (t0) s_ndef = 0;  // (ordered before its first read by the loop's barrier)
-#endif
   for (;;) {  // (all control flow below is workgroup-uniform; thread 0 writes the LDS lists)
     // ---- collect: the next records of the list walk, or (at its end) the deferred ones
     int n = 0;
-#ifndef TSDF_SERIAL_COLLECT
     lds_barrier();  // (every wave has read the previous collection's s_n / s_ndef)
     if (p < p_hi) {
       const int npr = min((p_hi - p + pstep - 1) / pstep, kPipeList / 2);  // pairs in this collection
@@ -1068,53 +995,6 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
     }
     lds_barrier();  // (publishes s_list, s_n, s_ndef)
     n = s_n;
-#else
-    if (p < p_hi) {
-      while (p < p_hi && n + 2 <= kPipeList) {
-        for (int e = 0; e < 2; ++e) {
-          const int b = 2 * p + e;
-          if (b >= nvis) break;
-          VisRec r;
-          if (b >= nband)
-            r = fresh_co ? ld_rec_co(&D.fresh_vis[b - nband]) : D.fresh_vis[b - nband];
-          else
-            r = vis[band_find_n(D.nblocks, bst, lane, b)];
-          bool take = true;
-          if (chk && r.pad == 0 && ct[r.idx] == fc) {  // a candidate of frame b - 1
-            if (!carved_known && ndef < kPipeDefer) {   // deferred to the end
-              if (t0) s_def[ndef] = r;
-              ++ndef;
-              take = false;
-            } else {
-              if (!carved_known) wait_tag(carved, A.tag, &D.ctr->status);
-              carved_known = true;
-              take = pipe_kept(D.rtag, r.idx, fc, lane);
-            }
-          }
-          if (take) {
-            if (t0) s_list[n] = r;
-            ++n;
-          }
-        }
-        p += pstep;
-      }
-    } else if (ndef > 0 && !def_done) {
-      if (!carved_known) wait_tag(carved, A.tag, &D.ctr->status);  // (its barrier publishes s_def)
-      else lds_barrier();
-      carved_known = true;
-      for (int d = 0; d < ndef; ++d) {
-        const VisRec r = s_def[d];
-        if (pipe_kept(D.rtag, r.idx, fc, lane)) {
-          if (t0) s_list[n] = r;
-          ++n;
-        }
-      }
-      def_done = true;
-    } else {
-      break;
-    }
-    lds_barrier();  // (publishes s_list)
-#endif
 #ifdef TSDF_DIAG_STAMPS
     if (t0 && D.dbg && blockIdx.x < (unsigned)kDiagMaxWg) {  // collect ends: first (3), last (4); records (5)
       unsigned long long* q = D.dbg + ((size_t)8 * kDiagMaxWg + blockIdx.x) * kDiagStamps;
@@ -1124,7 +1004,6 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
       q[5] += (unsigned long long)n + 1ull;
     }
 #endif
-#ifndef TSDF_LOCKSTEP_UPDATE
     // ---- update: the two pairs of waves take records pair, pair + 2, ...; no workgroup barrier: the
     // two waves of a record combine their carve minima through LDS (the second to finish decides), so
     // every wave runs its records at its own pace and one wave's memory waits overlap the others' work
@@ -1156,39 +1035,6 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
       }
     }
   }
-#else
-    // ---- update: the two pairs of waves take records 2 j + pair
-    for (int j = 0; 2 * j < n; ++j) {
-      const int k = 2 * j + pair;
-      const bool have = k < n;
-      VisRec r{};
-      float mn = __builtin_inff();
-      if (have) {
-        r = s_list[k];
-        update_block<false>(D, P, r, lane, hf, mn, my_upd);
-        my_vis += hf == 0 ? 1 : 0;
-      }
-      mn = wave_min_u(mn);
-      if (lane == 0) s_min[wave] = mn;
-      lds_barrier();  // (LDS only: this pair's pool stores stay in flight)
-      if (hf == 0 && lane == 0 && have) {
-        const float m2 = fminf(s_min[wave], s_min[wave + 1]);
-        if (m2 >= 0.9f) {  // space_carving_kernel threshold (voxel_tsdf.cu:227, :485)
-          D.ctag[(size_t)(fb & 1u) * D.nblocks + r.idx] = fb;  // (read by the next launch's update)
-          const int kc = atomicAdd(&s_ncand, 1);
-          if (kc < kIntegrateCandBuf) {
-            s_cand[kc] = r;
-          } else {  // buffer full (heavy carving): this one now
-            const int kg = atomicAdd(ncand, 1);
-            if (kg < D.cand_cap) st_rec_co(&cand[kg], r);
-            else atomicOr(&D.ctr->status, 16u);  // (a list longer than the pool: internal error)
-          }
-        }
-      }
-      lds_barrier();
-    }
-  }
-#endif
   // the workgroup's carve candidates (read by the next launch's carving) and statistics
   const int tot = wave_sum(my_upd);
   if (lane == 0) {

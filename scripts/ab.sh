@@ -23,7 +23,7 @@ r = d.get('roofline', {})
 print(f"{sys.argv[2]:>40} fps={d['value']:9.1f} ms/step={d['ms_per_step']:.4f} launch={r.get('us_per_launch')}us dev={dv}")
 PY
 }
-for rep in 1 2; do
+for rep in $(seq 1 ${AB_REPS:-2}); do
   i=0
   for spec in "$@"; do
     i=$((i+1))

@@ -12,6 +12,7 @@
 #   default           bench.py (300 timed frames, CPU baseline)
 #   c5 | c5graph | c4 | c2 | graph   bench.py --loop c5 [--graph] / 1280x720 / --depth-only / --graph
 #   c5tests           the raycast / render / C5 GPU tests
+#   host-pinned|host-pageable  bench.py --host-frames (C3 frames from host memory through TSDF_MEM_HOST)
 #   shard8            bench.py --width 1280 --height 720 --shard 8 (single-GPU 8-shard rehearsal)
 #   sq:<kernel>       SQ counter passes of one kernel on the default command (profile_kernel_sq.sh)
 #   c5trace|c5gtrace  kernel trace (eager / graph) of the C5 loop -> per-frame kernel chain and gaps (scripts/chain_timeline.py)
@@ -65,6 +66,9 @@ for st in "$@"; do
            line $OUT/bench_c4.json ;;
     c2) timeout -k 10 300 python3 bench.py --no-cpu --depth-only > $OUT/bench_c2.json 2> $OUT/bench_c2.err || fail $st $OUT/bench_c2.err
            line $OUT/bench_c2.json ;;
+    host-pinned|host-pageable) k=${st#host-}
+           timeout -k 10 300 python3 bench.py --no-cpu --host-frames $k > $OUT/bench_host_$k.json 2> $OUT/bench_host_$k.err || fail $st $OUT/bench_host_$k.err
+           line $OUT/bench_host_$k.json; grep -o '"host_frames": {[^}]*}' $OUT/bench_host_$k.json ;;
     c5tests) timeout -k 10 600 $PYT tests/test_gpu_c5.py tests/test_gpu_render.py tests/test_gpu_parity.py tests/test_gpu_golden.py tests/test_gpu_graph.py -m gpu > $OUT/pytest_c5.log 2>&1 || fail $st $OUT/pytest_c5.log
            tail -1 $OUT/pytest_c5.log ;;
     shard8) timeout -k 10 300 python3 bench.py --no-cpu --steps 100 --width 1280 --height 720 --shard 8 > $OUT/shard8_c4.json 2> $OUT/shard8_c4.err || fail $st $OUT/shard8_c4.err
