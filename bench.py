@@ -266,7 +266,7 @@ class Run:
         self.eng.close()
 
 
-PIX_RECORD_BYTES = 20  # pixA {depth, range, w_new, rgb} + pixB log-odds, written once per pixel
+PIX_RECORD_BYTES = 16  # pixA {depth, range, log-odds, rgb}, written once per pixel
 
 
 def pipe_fraction(prof):
@@ -303,7 +303,7 @@ def kernel_roofline(a, prof, n_frames, pmc):
 
 def implementation_bytes(a, prof):
     """Bytes per frame launch that SURVEY 8(d) does not count (a lower bound, by construction): the
-    20 B pixel records the ingest writes and the update gathers back (each once), and -- pipelined --
+    16 B pixel records the ingest writes and the update gathers back (each once), and -- pipelined --
     nothing else by design (the launch reads the next frame's image instead of this frame's; counted
     once in the algorithmic bytes)."""
     W, H = a.width, a.height

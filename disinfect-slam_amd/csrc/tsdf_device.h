@@ -82,7 +82,7 @@ struct FrameParams {
   const float* ht;           // NULL: ones (tsdf_module.cc:29-33)
   const float* lt;
   int row0, nrows;           // raycast: the rows [row0, row0 + nrows) of the W x H camera it renders
-  int pix_off;               // this frame's pixel records: D.pixA / pixB + pix_off (one of the two
+  int pix_off;               // this frame's pixel records: D.pixA + pix_off (one of the two
                              //   buffers: a pipelined frame's are written while the previous frame reads its own)
 };
 // the last-arriving workgroup of k_ingest_dda / k_integrate: resolve (allocation / carving) or, in a

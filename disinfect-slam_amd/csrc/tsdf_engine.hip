@@ -250,7 +250,7 @@ void free_all(tsdf_engine* e) {
                   D.table,   D.lock_tag, D.heap,     D.pool,    D.occ,
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs, D.fresh,
                   e->fe_rgb, e->fe_depth, e->fe_mask, e->fe_out_rgb, e->fe_out_depth,
-                  D.vis,     D.band,    D.cand,     D.arrive, D.swdirty, D.fresh_vis, D.pend, D.pixA,     D.pixB,    D.visbits,    D.wgcnt, D.dbg,
+                  D.vis,     D.band,    D.cand,     D.arrive, D.swdirty, D.fresh_vis, D.pend, D.pixA,     D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
                   e->vg_cell, e->vg_flags, e->vg_bits, e->g_visbits, e->g_wgcnt, e->g_sel, e->g_count,
                   e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_nbr, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
@@ -589,7 +589,6 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
     D.integrate_grid_pre = std::max(8, std::min(kIntegrateGrid, (per_cu_pre * ncu) & ~7));
   }
   ALLOC(D.pixA, 2 * e->max_pixels);  // two buffers: a pipelined frame's and the next one's
-  ALLOC(D.pixB, 2 * e->max_pixels);
   e->pipeline = e->env.pipeline;
   if (e->env.pipe_max_pixels >= 0) e->pipe_max_pixels = e->env.pipe_max_pixels;
   if (e->env.frame_order >= 0) e->frame_order = std::min(4, e->env.frame_order);

@@ -224,9 +224,8 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
                            ((uint32_t)P.rgb[3 * img + 2] << 16);
         px[j] = make_float4(P.depth[img], __int_as_float(uu[e]), __int_as_float(vv[e]), __uint_as_float(c));
         lg[j] = P.ht ? pixel_logodds(P.ht[img], P.lt[img]) : 0.0f;
-      } else {
+      } else {  // x: depth, y: range, z: log-odds, w: rgb (w_new computed in pass 2)
         px[j] = D.pixA[P.pix_off + img];
-        lg[j] = D.pixB[P.pix_off + img];
       }
 #endif
     }
@@ -238,7 +237,7 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
   for (int k = 0; k < 2; ++k) {
     const int j0 = 2 * k, j1 = 2 * k + 1;
     const v2f d = v2(px[j0].x, px[j1].x);
-    v2f rng, w_new;
+    v2f rng, w_new = v2(0.f, 0.f);
     if (Raw) {  // the ingest's per-pixel terms (identical operations)
       const f3 r0 = pixel_ray(P, __float_as_int(px[j0].y), __float_as_int(px[j0].z));
       const f3 r1 = pixel_ray(P, __float_as_int(px[j1].y), __float_as_int(px[j1].z));
@@ -246,13 +245,17 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
       w_new = v2(pixel_w_new(P, d.x), pixel_w_new(P, d.y));
     } else {
       rng = v2(px[j0].y, px[j1].y);
-      w_new = v2(px[j0].z, px[j1].z);
+      lg[j0] = px[j0].z;
+      lg[j1] = px[j1].z;
     }
     const uint32_t n0 = __float_as_uint(px[j0].w), n1 = __float_as_uint(px[j1].w);
     const v2f sdf = rng * (d - hzs[k]);
     const bool a0 = inb[j0] && !(d.x == 0 || d.x > P.max_depth) && sdf.x > neg_trunc;
     const bool a1 = inb[j1] && !(d.y == 0 || d.y > P.max_depth) && sdf.y > neg_trunc;
     if (a0 || a1) {
+      // w_new = (1 - d / max_depth) * 4 (pixel_w_new's operations, on the pair; the 16-B pixel record
+      // has no room for it: one gather per voxel instead of two)
+      if (!Raw) w_new = (v2(1.0f, 1.0f) - quot_const2(d, P.max_depth, P.inv_max_depth, a0, a1)) * v2(4.0f, 4.0f);
       v2f tn = quot_const2(sdf, P.trunc, P.inv_trunc, a0, a1);
       tn = v2(fminf(1.0f, tn.x), fminf(1.0f, tn.y));
       const uint32_t o0 = compu(cw, j0), o1 = compu(cw, j1);
@@ -277,7 +280,7 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
       // semantic fusion (voxel_tsdf.cu:196-202): p' = P / (P + N) with
       //   P = exp((w_old ln p + w_new ln ht) / wc), N = exp((w_old ln(1 - p) + w_new ln lt) / wc)
       // is exactly the logistic of  L' = (w_old L + w_new log2(ht / lt)) / wc  in the base-2
-      // log-odds L = log2(p / (1 - p)) the pool stores (pixB holds log2 ht - log2 lt), so the
+      // log-odds L = log2(p / (1 - p)) the pool stores (the pixel record holds log2 ht - log2 lt), so the
       // update is two products and a sum; readers convert with prob_of_logodds (within 1e-4
       // of the reference's float chain, and L stays exactly 0 -- p 0.5 -- when ht == lt)
       const v2f pn = (w_old * v2(comp(pr, j0), comp(pr, j1)) + w_new * v2(lg[j0], lg[j1])) * iwc;

@@ -13,10 +13,10 @@ namespace tsdf {
 
 // ---------------------------------------------------------------------------------------------
 // k_ingest_dda: 16x16 pixel tile per workgroup.
-//  1. pack the frame into per-pixel records the integrate kernel gathers:
-//       pixA = {depth, range = |K^-1 [x y 1]|, w_new = (1 - d / max_depth) * 4, rgb}
-//       pixB = log2 ht - log2 lt
-//     (exactly the values tsdf_integrate_kernel recomputes per voxel, voxel_tsdf.cu:174-201)
+//  1. pack the frame into per-pixel records the integrate kernel gathers (one 16-B gather per voxel):
+//       pixA = {depth, range = |K^-1 [x y 1]|, log2 ht - log2 lt, rgb}
+//     (exactly the values tsdf_integrate_kernel recomputes per voxel, voxel_tsdf.cu:174-201; the
+//     update computes w_new = (1 - d / max_depth) * 4 from the depth with the same operations)
 //  2. DDA of [p - trunc dir, p + trunc dir] (voxel_tsdf.cu:116-146); block keys deduplicated in
 //     an LDS hash set with their smallest candidate order (y*W + x)*maxs + i
 //  3. each unique key once: all-8-corners visibility (is_block_visible<true>), table probe;
@@ -477,8 +477,7 @@ __device__ __forceinline__ void ingest_tile(const EngineDev& D, const FrameParam
                          ((uint32_t)rgb[3 * i + 2] << 16);
       const float h = ht ? ht[i] : 1.0f;
       const float l = lt ? lt[i] : 1.0f;
-      D.pixA[P.pix_off + i] = make_float4(d, range, pixel_w_new(P, d), __uint_as_float(c));
-      D.pixB[P.pix_off + i] = pixel_logodds(h, l);
+      D.pixA[P.pix_off + i] = make_float4(d, range, pixel_logodds(h, l), __uint_as_float(c));
     }
     TSDF_STAMP(D, 0, 2);
     if (!(d == 0 || d > P.max_depth)) {

@@ -52,9 +52,8 @@ struct EngineDev {
   VisRec* fresh_vis;            // kNewKeyCap blocks created this frame (k_resolve_alloc frame mode)
   VisRec* pend;                 // kNewKeyCap: a shard's owned entries its exhausted pool left without
                                 // voxels this frame (ctr->n_pend); carved in the same frame
-  // packed frame: two buffers of max_pixels records each (FrameParams.pixA / pixB select one)
-  float4* pixA;                 // {depth, range, w_new, rgb}
-  float* pixB;                  // log2 ht - log2 lt (base-2 log-odds of the pixel)
+  // packed frame: two buffers of max_pixels records each (FrameParams.pix_off selects one)
+  float4* pixA;                 // {depth, range, log2 ht - log2 lt (the pixel's base-2 log-odds), rgb}
   // pipelined frames (k_frame): flags, per-frame statistics and the per-pool-block tags
   unsigned long long* pipe;     // kPipeWords (layout below)
   uint32_t* ctag;               // 2 x nblocks: ctag[(f & 1) * nblocks + b] == f: block b was a carve
