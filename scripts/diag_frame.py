@@ -39,6 +39,7 @@ def main():
     rows = {k: [] for k in PARTS}
     head = []
     coll = []
+    tiles = []
     phases = []
     for i in range(nfr):
         torch.cuda.synchronize()
@@ -60,6 +61,12 @@ def main():
                 st, en_ = (S[m, 1] - t0) * 1e-2, (S[m, 2] - t0) * 1e-2
                 rows[k].append((m.sum(), np.median(st), st.max(), np.median(en_), np.percentile(en_, 90),
                                 en_.max(), np.median(en_ - st)))
+        T = buf.reshape(NK, NWG, NS)[0].astype(np.int64)  # tile stamps (tsdf_ingest.h ingest_tile)
+        mt = (S[:, 0] == 4) & (T[:, 0] > 0) & (T[:, 5] > 0)
+        if mt.any():
+            st = T[mt, 0]
+            tiles.append([np.median((T[mt, k] - st) * 1e-2) for k in (1, 2, 3, 6, 7, 5)] +
+                         [np.median((T[mt, 7] - T[mt, 6]) * 1e-2)])
         m = S[:, 0] == 3
         if m.any() and (S[m, 5] > 0).any():  # listed update: collect phases (first / last end), records
             st = S[m, 1]
@@ -81,6 +88,10 @@ def main():
         if rows[k]:
             a = np.median(np.array(rows[k], dtype=float), axis=0)
             print(f"{name:>14} {a[0]:5.0f} {a[1]:9.1f} {a[2]:9.1f} {a[3]:8.1f} {a[4]:8.1f} {a[5]:8.1f} {a[6]:8.1f}")
+    if tiles:
+        a = np.median(np.array(tiles), axis=0)
+        print("tile phases (us from the tile's start, medians): LDS init %.1f, pixel records %.1f, DDA %.1f, "
+              "corner tests %.1f, allocation flag seen %.1f, probes + inserts done %.1f; waiting %.1f" % tuple(a))
     if coll:
         a = np.median(np.array(coll), axis=0)
         print(f"listed update: first collect done {a[0]:.1f} (p90 {a[1]:.1f}), last collect done {a[2]:.1f} us "
