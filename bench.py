@@ -102,6 +102,9 @@ def parse():
     p.add_argument("--no-events", action="store_true",
                    help="diagnostic: no HIP events in the timed loop (kernel roofline then from the "
                         "device clock)")
+    p.add_argument("--no-defer", action="store_true",
+                   help="C5 eager loop: immediate tsdf_raycast instead of tsdf_raycast_deferred (the "
+                        "raycast then runs in its own launch instead of beside the next frame's ingest)")
     return p.parse_args()
 
 
@@ -187,8 +190,9 @@ class Run:
                                      rgba=self.rgba, normal=self.normal)
         else:
             self.eng.integrate(fr["rgb"][i], fr["depth"][i], ht, lt, K, pose, a.max_depth)
-            if c5:
-                self.eng.raycast(K, a.width, a.height, pose, a.max_depth, rgba=self.rgba, normal=self.normal)
+            if c5:  # deferred: launched with the next frame's ingest (k_render_ingest), or by the flush
+                self.eng.raycast(K, a.width, a.height, pose, a.max_depth, rgba=self.rgba, normal=self.normal,
+                                 deferred=not a.no_defer)
         if c5 and (i + 1) % 30 == 0:  # marching cubes of the whole volume, on device
             if self.replica is not None:
                 n = tdist.mesh_sharded(self.eng, self.replica, None, 0.99, 0, out=self.mesh_buf).shape[0]
@@ -371,7 +375,8 @@ def device_spans(prof, n):
                     "k_ingest_dda / k_integrate, or k_frame's workgroup 0); integrate = the update's "
                     "first workgroup start -> its last workgroup end. Pipelined frames (one k_frame per "
                     "frame): ingest = the previous frame's allocation published -> the frame's last "
-                    "tile / sweep workgroup end"}
+                    "tile / sweep workgroup end. C5 eager loop with deferred raycasts: ingest = "
+                    "k_render_ingest, the previous frame's raycast beside this frame's ingest"}
 
 
 def main():

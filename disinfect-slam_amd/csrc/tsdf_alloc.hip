@@ -9,6 +9,7 @@
 #include "tsdf_kernels.h"
 #include "tsdf_resolve.h"
 #include "tsdf_ingest.h"
+#include "tsdf_raycast.h"
 
 namespace tsdf {
 
@@ -45,24 +46,26 @@ __device__ __forceinline__ void pack_keys_wg(const EngineDev& D, ShardRec* __res
 // workgroup per 16x16 pixel tile (tiles_x per row, `tiles` in all). Every workgroup arrives at the
 // end; the last one resolves the frame's allocation (kTailResolve) or packs a shard's keys for the
 // exchange (kTailPack): block_allocate_kernel and VoxelHashTable::Allocate's launch in one.
+// wg / nwg: this workgroup among the ingest's (its own launch: the block index and the grid; the
+// fused render + ingest launch: past the raycast's workgroups)
 template <int TS>
 __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
                                            const float* __restrict__ depth,
                                            const uint8_t* __restrict__ rgb,
                                            const float* __restrict__ ht,
-                                           const float* __restrict__ lt, int tiles_x, int tiles) {
-  __shared__ IngestLds<TS> S;
+                                           const float* __restrict__ lt, int tiles_x, int tiles,
+                                           IngestLds<TS>& S, int wg, int nwg) {
   // device-clock span of the ingest (WG 0 is dispatched first; the end is the last arrival)
-  if (blockIdx.x == 0 && threadIdx.x == 0)
+  if (wg == 0 && threadIdx.x == 0)
     st_co(&D.arrive[kArrStart + 8], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-  if ((int)blockIdx.x < kVisWorkgroups) {
+  if (wg < kVisWorkgroups) {
     TSDF_STAMP(D, 2, 0);
-    vis_sweep(D, P, blockIdx.x, S);
+    vis_sweep(D, P, wg, S);
     TSDF_STAMP(D, 2, 1);
-  } else if ((int)blockIdx.x - kVisWorkgroups < tiles) {  // tiles [P.tile_lo, P.tile_lo + tiles)
-    ingest_tile<TS, kTileFull>(D, P, depth, rgb, ht, lt, tiles_x, P.tile_lo + (int)blockIdx.x - kVisWorkgroups, S);
+  } else if (wg - kVisWorkgroups < tiles) {  // tiles [P.tile_lo, P.tile_lo + tiles)
+    ingest_tile<TS, kTileFull>(D, P, depth, rgb, ht, lt, tiles_x, P.tile_lo + wg - kVisWorkgroups, S);
   }
-  if (!arrive_last(D.arrive + kArrIngest, 0ull, &S.last)) return;
+  if (!arrive_last(D.arrive + kArrIngest, 0ull, &S.last, true, (uint32_t)nwg, (uint32_t)wg)) return;
   const unsigned long long tend = __builtin_amdgcn_s_memrealtime();
   TSDF_STAMP(D, 6, 0);
   if (threadIdx.x == 0) arrive_reset(D.arrive + kArrIngest);  // (no loads: the resolver starts at once)
@@ -94,12 +97,40 @@ __global__ __launch_bounds__(256) INGEST_WAVES(TS) void k_ingest_dda(EngineDev D
                                                     const float* __restrict__ ht,
                                                     const float* __restrict__ lt, int tiles_x,
                                                     int tiles) {
-  ingest_dda<TS>(D, P, depth, rgb, ht, lt, tiles_x, tiles);
+  __shared__ IngestLds<TS> S;
+  ingest_dda<TS>(D, P, depth, rgb, ht, lt, tiles_x, tiles, S, (int)blockIdx.x, (int)gridDim.x);
 }
 template <int TS>
 __global__ __launch_bounds__(256) INGEST_WAVES(TS) void k_ingest_dda_g(EngineDev D, const FrameArgs* __restrict__ A) {
+  __shared__ IngestLds<TS> S;
   const FrameParams P = A->P;
-  ingest_dda<TS>(D, P, A->depth, A->rgb, A->ht, A->lt, A->tiles_x, A->tiles);
+  ingest_dda<TS>(D, P, A->depth, A->rgb, A->ht, A->lt, A->tiles_x, A->tiles, S, (int)blockIdx.x, (int)gridDim.x);
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_render_ingest: frame n's raycast (its view grid built before the launch) and frame n + 1's ingest
+// (k_ingest_dda: pixel records, DDA, probes, visibility sweep, the allocation in its last arriver) in
+// one launch. With a view grid the raycast reads only the grid, its bitmaps and the pool; the ingest
+// writes none of them (it writes the table, the occupancy bitmap, the new-key set, the pixel records
+// and frame n + 1's lists; the blocks it allocates are written by frame n + 1's update, a later
+// launch). So the two are independent and the ingest's workgroups fill the slots the latency-bound
+// raycast leaves (tsdf_raycast_deferred). The raycast's workgroups come first in the grid.
+// ---------------------------------------------------------------------------------------------
+union RenderIngestLds {
+  IngestLds<1024> ing;
+  uint32_t bits[kViewGraphBitmapWords];  // the raycast's staged bitmaps
+};
+__global__ __launch_bounds__(256) INGEST_WAVES(1024) void k_render_ingest(
+    EngineDev D, FrameParams R, float step_size, ViewGrid V, uchar4* __restrict__ rgba, uchar4* __restrict__ normal,
+    int rgx, int nray, FrameParams P, const float* __restrict__ depth, const uint8_t* __restrict__ rgb,
+    const float* __restrict__ ht, const float* __restrict__ lt, int tiles_x, int tiles) {
+  __shared__ RenderIngestLds U;
+  const int b = (int)blockIdx.x;
+  if (b < nray) {
+    raycast(D, R, step_size, V, U.bits, rgba, normal, b, rgx, nray);
+    return;
+  }
+  ingest_dda<1024>(D, P, depth, rgb, ht, lt, tiles_x, tiles, U.ing, b - nray, (int)gridDim.x - nray);
 }
 template __global__ void k_ingest_dda<1024>(EngineDev, FrameParams, const float*, const uint8_t*, const float*,
                                             const float*, int, int);

@@ -141,6 +141,17 @@ struct tsdf_engine {
   // without -- the two cross-stream event waits per frame and the ingest's workgroups beside the
   // raycast's cost more than the overlap hides. Off by default; TSDF_RENDER_OVERLAP=1 enables it.
   bool render_overlap = false;
+  // a deferred raycast (tsdf_raycast_deferred): its view grid is built; the k_raycast launch waits
+  // for the engine's next call -- fused with the next frame's ingest (k_render_ingest) when that call
+  // is tsdf_integrate, alone otherwise (join_render)
+  struct DeferredRender {
+    bool pending = false;
+    FrameParams P{};
+    ViewGrid V{};
+    float step = 0.f;
+    uchar4* rgba = nullptr;
+    uchar4* normal = nullptr;
+  } rd;
   EngineDev D{};
   int maxs = 3;
   int64_t order_range = 0;  // candidate order space: max_pixels * maxs
@@ -361,7 +372,17 @@ int launch_resolve_alloc(tsdf_engine* e, const FrameParams& P, uint32_t range, i
 }
 
 // the engine stream waits for a raycast still running on the render stream
-int join_render(tsdf_engine* e) {
+// (keep_deferred: a deferred raycast stays pending -- tsdf_stream_wait orders the engine stream after
+// another stream's work, which the raycast may follow as well)
+int join_render(tsdf_engine* e, bool keep_deferred = false) {
+  if (e->rd.pending && !keep_deferred) {  // a deferred raycast no ingest took up: launched alone, before anything else
+    e->rd.pending = false;
+    const tsdf_engine::DeferredRender& r = e->rd;
+    const dim3 rgrid((r.P.W + 15) / 16, (r.P.nrows + 15) / 16);
+    hipLaunchKernelGGL(k_raycast, rgrid, dim3(256), (size_t)r.V.nw * 4, e->stream, e->D, r.P, r.step, r.V, r.rgba,
+                       r.normal);
+    HIP_OK(hipGetLastError());
+  }
   if (!e->render_pending) return TSDF_OK;
   e->render_pending = false;
   HIP_OK(hipStreamWaitEvent(e->stream, e->rs_done, 0));
@@ -378,9 +399,9 @@ int flush_pending(tsdf_engine* e);
 // update (pipelined frames) and joins the render stream
 #define ENTER(e)                       \
   do {                                 \
-    int _rc = flush_pending(e);        \
+    int _rc = join_render(e);          \
     if (_rc) return _rc;               \
-    _rc = join_render(e);              \
+    _rc = flush_pending(e);            \
     if (_rc) return _rc;               \
   } while (0)
 
@@ -649,6 +670,7 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
 int tsdf_destroy(tsdf_engine* e) {
   if (!e) return TSDF_ERR_INVALID_ARG;
   (void)hipSetDevice(e->device);
+  (void)join_render(e);  // (a deferred raycast's outputs are still written)
   if (e->rstream) (void)hipStreamSynchronize(e->rstream);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   free_all(e);
@@ -796,6 +818,17 @@ int frame_ingest(tsdf_engine* e, const EngineDev& Dv, const tsdf_frame* f, const
   // ---- allocate (voxel_tsdf.cu:377-386) + visibility (:388-397) ----
   // k_ingest_dda sweeps the blocks that already exist for visibility beside the DDA; its last
   // workgroup resolves the new keys and appends the blocks it creates to the visible lists
+  if (e->rd.pending && e->maxs <= 3 && slice_count == 1 && !keys_out && e->cfg.shard_count <= 1) {
+    // the deferred raycast of the previous frame in the same launch (k_render_ingest)
+    e->rd.pending = false;
+    const tsdf_engine::DeferredRender& r = e->rd;
+    const int rgx = (r.P.W + 15) / 16, nray = rgx * ((r.P.nrows + 15) / 16);
+    hipLaunchKernelGGL(k_render_ingest, dim3(nray + kVisWorkgroups + tiles), dim3(256), 0, s, Dv, r.P, r.step, r.V,
+                       r.rgba, r.normal, rgx, nray, *P, depth, rgb, ht, lt, tiles_x, tiles);
+    LAUNCH_OK("k_render_ingest");
+    return TSDF_OK;
+  }
+  JOIN_RENDER(e);  // (a deferred raycast this ingest cannot take up)
   if (e->maxs <= 3)
     hipLaunchKernelGGL(k_ingest_dda<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, s, Dv, *P, depth,
                        rgb, ht, lt, tiles_x, tiles);
@@ -1217,7 +1250,8 @@ int tsdf_stream_wait(tsdf_engine* e, void* stream) {
   hipStream_t other = reinterpret_cast<hipStream_t>(stream);
   if (other == e->stream) return TSDF_OK;
   HIP_OK(hipSetDevice(e->device));
-  JOIN_RENDER(e);
+  int rc = join_render(e, true);
+  if (rc) return rc;
   if (!e->order_ev) HIP_OK(hipEventCreateWithFlags(&e->order_ev, hipEventDisableTiming));
   HIP_OK(hipEventRecord(e->order_ev, other));
   HIP_OK(hipStreamWaitEvent(e->stream, e->order_ev, 0));
@@ -1744,7 +1778,8 @@ int tsdf_feed_rgbd_frame(tsdf_engine* e, const uint8_t* rgb, const uint16_t* dep
 
 namespace {
 int raycast_impl(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const tsdf_pose* pose,
-                 float max_depth, int row0, int nrows, uint8_t* rgba, uint8_t* normal, int mem_kind) {
+                 float max_depth, int row0, int nrows, uint8_t* rgba, uint8_t* normal, int mem_kind,
+                 bool deferred = false) {
   if (!e || !K || !pose || W <= 0 || H <= 0 || (int64_t)W * H > e->max_pixels || row0 < 0 || nrows < 1 ||
       row0 + nrows > H || (mem_kind != TSDF_MEM_HOST && mem_kind != TSDF_MEM_DEVICE)) {
     set_error("tsdf_raycast: invalid argument");
@@ -1766,6 +1801,16 @@ int raycast_impl(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const t
     LAUNCH_OK("k_view_grid");
     hipLaunchKernelGGL(k_view_pack, dim3(kViewPackGrid), dim3(256), 0, e->stream, V);
     LAUNCH_OK("k_view_pack");
+  }
+  if (deferred && V.n && V.nw <= kViewGraphBitmapWords && mem_kind == TSDF_MEM_DEVICE) {
+    // (tsdf_raycast_deferred: the launch waits for the next call, join_render / frame_ingest)
+    e->rd.pending = true;
+    e->rd.P = P;
+    e->rd.V = V;
+    e->rd.step = step;
+    e->rd.rgba = o1;
+    e->rd.normal = o2;
+    return TSDF_OK;
   }
   const size_t lds = V.n ? (size_t)V.nw * 4 : 0;
   // With a view grid the raycast reads only the pool, the grid and its bitmaps, none of which the
@@ -1799,6 +1844,12 @@ int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const t
                  float max_depth, uint8_t* rgba, uint8_t* normal, int mem_kind) {
   TraceRange trace_("tsdf_raycast");
   return raycast_impl(e, K, W, H, pose, max_depth, 0, H, rgba, normal, mem_kind);
+}
+
+int tsdf_raycast_deferred(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const tsdf_pose* pose,
+                          float max_depth, uint8_t* rgba, uint8_t* normal) {
+  TraceRange trace_("tsdf_raycast_deferred");
+  return raycast_impl(e, K, W, H, pose, max_depth, 0, H, rgba, normal, TSDF_MEM_DEVICE, true);
 }
 
 int tsdf_raycast_rows(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const tsdf_pose* pose,

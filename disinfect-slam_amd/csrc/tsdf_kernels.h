@@ -253,6 +253,11 @@ __global__ void k_mesh(EngineDev D, const VisRec* sel, const int32_t* nsel, Mesh
 __global__ void k_scan_counts(const int32_t* counts, const int32_t* nsel, int32_t* offsets, int64_t* total);
 __global__ void k_raycast(EngineDev D, FrameParams P, float step_size, ViewGrid V, uchar4* rgba,
                           uchar4* normal);
+// frame n's raycast (R, V: its view grid, built before) + frame n + 1's ingest (k_ingest_dda<1024>) in
+// one launch: nray raycast workgroups (rgx tiles per row) first, then kVisWorkgroups + tiles (tsdf_alloc.hip)
+__global__ void k_render_ingest(EngineDev D, FrameParams R, float step_size, ViewGrid V, uchar4* rgba,
+                                uchar4* normal, int rgx, int nray, FrameParams P, const float* depth,
+                                const uint8_t* rgb, const float* ht, const float* lt, int tiles_x, int tiles);
 // view grid of a raycast: grid kOccWords / 256 workgroups of 256
 __global__ void k_view_grid(EngineDev D, FrameParams P, ViewGrid V);
 __global__ void k_view_grid_g(EngineDev D, const FrameArgs* A);

@@ -550,8 +550,20 @@ class Engine:
         _lib.check(_lib.load().tsdf_flush(self._h), "tsdf_flush")
 
     # ---- extraction ----
-    def raycast(self, K, width, height, cam_T_world: SE3, max_depth: float, rgba=None, normal=None):
+    def raycast(self, K, width, height, cam_T_world: SE3, max_depth: float, rgba=None, normal=None,
+                deferred=False):
+        """tsdf_raycast; deferred=True (device tensors only): tsdf_raycast_deferred -- the images are
+        written by the engine's next call (fused with the next frame's ingest when that is integrate;
+        flush() otherwise), so read them after that call."""
         Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        if deferred:
+            if rgba is None or not _is_torch_cuda(rgba) or (normal is not None and not _is_torch_cuda(normal)):
+                raise ValueError("a deferred raycast writes device tensors")
+            self._wait_torch(rgba, normal)
+            _lib.check(_lib.load().tsdf_raycast_deferred(self._h, C.byref(Kc), width, height,
+                                                         C.byref(cam_T_world._c()), max_depth, _ptr(rgba),
+                                                         _ptr(normal)), "tsdf_raycast_deferred")
+            return rgba, normal
         if rgba is not None and _is_torch_cuda(rgba):
             self._wait_torch(rgba, normal)
             _lib.check(_lib.load().tsdf_raycast(self._h, C.byref(Kc), width, height,

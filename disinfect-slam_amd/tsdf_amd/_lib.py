@@ -109,7 +109,7 @@ EXPORTS = [
     "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame", "tsdf_graph_destroy",
     "tsdf_snapshot_bytes", "tsdf_snapshot_save", "tsdf_snapshot_load",
     "tsdf_render_blocks", "tsdf_import_blocks", "tsdf_reset", "tsdf_pack_blocks",
-    "tsdf_raycast_rows", "tsdf_render_bands", "tsdf_pack_halo", "tsdf_extract_mesh_owned",
+    "tsdf_raycast_rows", "tsdf_raycast_deferred", "tsdf_render_bands", "tsdf_pack_halo", "tsdf_extract_mesh_owned",
     "tsdf_graph_create_shard", "tsdf_graph_shard_begin", "tsdf_graph_shard_update", "tsdf_graph_shard_end",
     "tsdf_integrate_shard_pipe",
 ]
@@ -164,6 +164,7 @@ def load(path: str | None = None):
                                      C.POINTER(i64), i]
     L.tsdf_import_blocks.argtypes = [P, P, i64, i, i]
     L.tsdf_raycast_rows.argtypes = [P, C.POINTER(Intrinsics), i, i, C.POINTER(Pose), f, i, i, P, P, i]
+    L.tsdf_raycast_deferred.argtypes = [P, C.POINTER(Intrinsics), i, i, C.POINTER(Pose), f, P, P]
     L.tsdf_render_bands.argtypes = [P, C.POINTER(Intrinsics), i, i, C.POINTER(Pose), f, i, P, P, i64,
                                     P, i]
     L.tsdf_pack_halo.argtypes = [P, P, i64, P, i]
@@ -205,7 +206,7 @@ def load(path: str | None = None):
                  "tsdf_integrate_shard_abort", "tsdf_stream_wait", "tsdf_stream_signal", "tsdf_get_stream",
                  "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame",
                  "tsdf_graph_destroy", "tsdf_snapshot_bytes", "tsdf_snapshot_save", "tsdf_snapshot_load",
-                 "tsdf_extract_mesh", "tsdf_raycast_rows", "tsdf_render_bands", "tsdf_pack_halo",
+                 "tsdf_extract_mesh", "tsdf_raycast_rows", "tsdf_raycast_deferred", "tsdf_render_bands", "tsdf_pack_halo",
                  "tsdf_extract_mesh_owned", "tsdf_render_blocks", "tsdf_import_blocks", "tsdf_reset",
                  "tsdf_pack_blocks", "tsdf_graph_create_shard", "tsdf_graph_shard_begin",
                  "tsdf_graph_shard_update", "tsdf_graph_shard_end", "tsdf_integrate_shard_pipe",

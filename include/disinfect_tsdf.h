@@ -264,6 +264,17 @@ int tsdf_graph_shard_end(tsdf_graph* g);
 int tsdf_raycast(tsdf_engine* e, const tsdf_intrinsics* K, int width, int height,
                  const tsdf_pose* cam_T_world, float max_depth, uint8_t* rgba, uint8_t* normal,
                  int mem_kind);
+/* tsdf_raycast into device buffers with its k_raycast launch deferred to the engine's next call: when
+ * that call is tsdf_integrate, the raycast runs in ONE launch with the new frame's ingest (pixel
+ * records, DDA, visibility sweep, allocation -- which write nothing the raycast reads), filling the
+ * slots the latency-bound raycast leaves; any other call (tsdf_flush, tsdf_synchronize, a query, ...)
+ * launches it alone first. The images are those of the volume at this call (bit-identical to
+ * tsdf_raycast); they are written in engine-stream order by that next call, so a consumer orders
+ * after it (or calls tsdf_flush). rgba / normal must stay valid until then. Views too deep for a view
+ * grid take tsdf_raycast's immediate path. (The C5 loop: examples/tsdf/online.cc:60 +
+ * modules/renderer_module.cc:105 integrate then render every frame.) */
+int tsdf_raycast_deferred(tsdf_engine* e, const tsdf_intrinsics* K, int width, int height,
+                          const tsdf_pose* cam_T_world, float max_depth, uint8_t* rgba, uint8_t* normal);
 
 /* TSDFGrid::GatherVoxels (bounds = {xmin, xmax, ymin, ymax, zmin, zmax}, voxel_tsdf.cu:427-454)
  * or GatherValid (bounds == NULL, :399-425). Two-call pattern: *count receives the number of

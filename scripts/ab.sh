@@ -6,6 +6,7 @@
 #   scripts/ab.sh tree "<label>:<dir>:<ENV=a ...>[:<extra args>]" ...
 #                                                  whole trees (an older round's bench.py + package + library
 #                                                  staged under abtree/<name>, git-ignored; dir "." = this tree)
+#   scripts/ab.sh args "<bench args>" ...          bench arguments on the driver's command (e.g. "--loop c5 --no-defer")
 #   scripts/ab.sh c5   <lib.so> ...                k_raycast kernel time (kernel trace) on the C5 loop
 #                                                  (pass disinfect-slam_amd/libdisinfect_tsdf.so for this tree's)
 set -uo pipefail
@@ -30,6 +31,8 @@ for rep in $(seq 1 ${AB_REPS:-2}); do
     log=$PWD/$OUT/r${i}_$rep.log
     case $MODE in
       env) env $spec timeout -k 10 120 python3 bench.py $DRIVER ${AB_ARGS:-} > $log 2>&1 || { echo "$spec failed"; tail -5 $log; exit 1; }
+           show $log "$spec" ;;
+      args) timeout -k 10 120 python3 bench.py $DRIVER $spec > $log 2>&1 || { echo "$spec failed"; tail -5 $log; exit 1; }
            show $log "$spec" ;;
       lib) TSDF_AMD_LIB=$spec timeout -k 10 120 python3 bench.py $DRIVER ${AB_ARGS:-} > $log 2>&1 || { echo "$spec failed"; tail -5 $log; exit 1; }
            show $log "$spec" ;;

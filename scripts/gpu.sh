@@ -19,6 +19,7 @@
 #   raysq             SQ / FETCH / WRITE passes of k_raycast on the C5 loop -> <tag>/r4_raycast_sq.json
 #   raydiag           raycast step statistics and wave lifetimes (diagnostic library, scripts/diag_raycast.py)
 #   framediag[:A=1,B=2]  k_frame per-part timeline (diagnostic library, scripts/diag_frame.py), optional env
+#   abargs:<a1>,<a2>  interleaved A/B of bench arguments (scripts/ab.sh args; spaces as '+', e.g. --loop+c5)
 #   ab:<lib1>,<lib2>  interleaved A/B of engine builds on the driver command (scripts/ab.sh lib; the other
 #                     A/B forms -- env, tree, c5 -- are run directly; variants: scripts/build_variant.sh)
 set -uo pipefail
@@ -85,6 +86,7 @@ for st in "$@"; do
            tail -12 $OUT/raycast_diag.txt ;;
     framediag*) e=${st#framediag}; e=${e#:}; f=$OUT/frame_diag${e:+_$e}.txt; env ${e//,/ } TSDF_AMD_LIB=disinfect-slam_amd/libdisinfect_tsdf_diag.so timeout -k 10 120 python3 scripts/diag_frame.py > $f 2>&1 || fail $st $f
            tail -9 $f ;;
+    abargs:*) IFS=, read -ra SP <<< "${st#abargs:}"; SP=("${SP[@]//+/ }"); bash scripts/ab.sh args "${SP[@]}" || exit 1 ;;
     ab:*) IFS=, read -ra LIBS <<< "${st#ab:}"; bash scripts/ab.sh lib "${LIBS[@]}" || exit 1 ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac

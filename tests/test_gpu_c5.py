@@ -135,3 +135,58 @@ def test_raycast_view_grid_generations_wrap():
         assert np.array_equal(img[0], ref[0]) and np.array_equal(img[1], ref[1])
     finally:
         eng.close()
+
+
+def test_c5_deferred_raycast_equals_immediate():
+    """tsdf_raycast_deferred (the raycast launched beside the next frame's ingest, k_render_ingest)
+    renders what tsdf_raycast renders, frame by frame over the 640x480 C5 stream; also when the next
+    call is not an integrate (stats, a second raycast, mesh extraction, flush: the pending raycast is
+    launched alone first) and with host frames (the upload ring) for the fused ingest."""
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H, n = 640, 480, 24
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    a = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=18)
+    b = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=18)
+    try:
+        ref = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(2)]
+        out = [[torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(2)] for _ in range(3)]
+        pending = None  # (frame, image pair, the immediate render's copies)
+        for i in range(n):
+            fr = synth.render(cam, i)
+            pose = tsdf_amd.SE3(fr["q"], fr["t"])
+            src = fr if i % 3 == 2 else {k: torch.from_numpy(fr[k]).to("cuda") for k in ("rgb", "depth", "ht", "lt")}
+            a.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K, pose, 4.0)
+            b.integrate(src["rgb"], src["depth"], src["ht"], src["lt"], cam.K, pose, 4.0)
+            if pending is not None:  # the previous deferred raycast is written by now
+                j, o, r0, r1 = pending
+                torch.cuda.synchronize()
+                assert torch.equal(o[0], r0) and torch.equal(o[1], r1), f"frame {j}: deferred != immediate"
+            a.raycast(K, W, H, pose, 4.0, rgba=ref[0], normal=ref[1])
+            o = out[i % 3]
+            b.raycast(K, W, H, pose, 4.0, rgba=o[0], normal=o[1], deferred=True)
+            pending = (i, o, ref[0].clone(), ref[1].clone())
+            if i == 7:
+                assert b.stats()["status"] == 0  # (joins the pending raycast)
+            elif i == 12:  # a second deferred raycast: the first is launched alone
+                o2 = out[(i + 1) % 3]
+                b.raycast(K, W, H, pose, 4.0, rgba=o2[0], normal=o2[1], deferred=True)
+                torch.cuda.synchronize()
+                assert torch.equal(o[0], ref[0]) and torch.equal(o[1], ref[1]), "first of two deferred"
+                pending = (i, o2, ref[0].clone(), ref[1].clone())
+            elif i == 17:
+                m_a, m_b = a.extract_mesh(None, 0.99, 0), b.extract_mesh(None, 0.99, 0)
+                np.testing.assert_array_equal(np.asarray(m_a).view(np.uint32), np.asarray(m_b).view(np.uint32))
+        b.flush()
+        torch.cuda.synchronize()
+        j, o, r0, r1 = pending
+        assert torch.equal(o[0], r0) and torch.equal(o[1], r1), "last frame after flush"
+        assert (r0[..., 3] == 255).float().mean().item() > 0.5
+        assert a.stats()["status"] == 0 and b.stats()["status"] == 0
+        with pytest.raises(ValueError):
+            b.raycast(K, W, H, pose, 4.0, deferred=True)  # (host images: immediate only)
+    finally:
+        a.close(), b.close()
