@@ -103,8 +103,9 @@ def parse():
                    help="diagnostic: no HIP events in the timed loop (kernel roofline then from the "
                         "device clock)")
     p.add_argument("--no-defer", action="store_true",
-                   help="C5 eager loop: immediate tsdf_raycast instead of tsdf_raycast_deferred (the "
-                        "raycast then runs in its own launch instead of beside the next frame's ingest)")
+                   help="C5 loop: immediate tsdf_raycast / tsdf_graph_create instead of tsdf_raycast_deferred / "
+                        "tsdf_graph_create_deferred (the raycast then runs in its own launch instead of "
+                        "beside the next frame's ingest)")
     return p.parse_args()
 
 
@@ -162,7 +163,7 @@ class Run:
                 self.sgraph = self.eng.shard_frame_graph(W, H, rank if split else 0, world if split else 1)
             else:
                 rw, rh = (W, H) if a.loop == "c5" else (0, 0)
-                self.graph = self.eng.frame_graph(W, H, rw, rh)
+                self.graph = self.eng.frame_graph(W, H, rw, rh, deferred=bool(rw) and not a.no_defer)
 
     def step(self, i):
         from tsdf_amd import dist as tdist

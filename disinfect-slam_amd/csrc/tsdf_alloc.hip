@@ -132,6 +132,23 @@ __global__ __launch_bounds__(256) INGEST_WAVES(1024) void k_render_ingest(
   }
   ingest_dda<1024>(D, P, depth, rgb, ht, lt, tiles_x, tiles, U.ing, b - nray, (int)gridDim.x - nray);
 }
+__global__ __launch_bounds__(256) INGEST_WAVES(1024) void k_render_ingest_g(EngineDev D,
+                                                                            const FrameArgs* __restrict__ A,
+                                                                            int rgx, int nray) {
+  __shared__ RenderIngestLds U;
+  const int b = (int)blockIdx.x;
+  if (b < nray) {
+    const FrameArgs* Q = A->prev;
+    if (!Q) return;
+    const FrameParams R = Q->R;
+    const ViewGrid V = Q->V;
+    raycast(D, R, Q->step_size, V, U.bits, Q->rgba, Q->normal, b, rgx, nray);
+    return;
+  }
+  const FrameParams P = A->P;
+  ingest_dda<1024>(D, P, A->depth, A->rgb, A->ht, A->lt, A->tiles_x, A->tiles, U.ing, b - nray,
+                   (int)gridDim.x - nray);
+}
 template __global__ void k_ingest_dda<1024>(EngineDev, FrameParams, const float*, const uint8_t*, const float*,
                                             const float*, int, int);
 template __global__ void k_ingest_dda<2048>(EngineDev, FrameParams, const float*, const uint8_t*, const float*,

@@ -152,6 +152,15 @@ struct tsdf_engine {
     uchar4* rgba = nullptr;
     uchar4* normal = nullptr;
   } rd;
+  // the deferred raycast of a render-deferring graph frame (tsdf_graph_create_deferred): its args slot
+  // (camera, view grid, outputs) on the device; taken up by the graph's next frame (k_render_ingest_g),
+  // launched alone (k_raycast_g) by any other call
+  struct DeferredGraphRender {
+    bool pending = false;
+    const tsdf_graph* g = nullptr;
+    const FrameArgs* args = nullptr;
+    int W = 0, H = 0;
+  } rdg;
   EngineDev D{};
   int maxs = 3;
   int64_t order_range = 0;  // candidate order space: max_pixels * maxs
@@ -375,6 +384,12 @@ int launch_resolve_alloc(tsdf_engine* e, const FrameParams& P, uint32_t range, i
 // (keep_deferred: a deferred raycast stays pending -- tsdf_stream_wait orders the engine stream after
 // another stream's work, which the raycast may follow as well)
 int join_render(tsdf_engine* e, bool keep_deferred = false) {
+  if (e->rdg.pending && !keep_deferred) {  // (a graph frame's deferred raycast: its args slot)
+    e->rdg.pending = false;
+    const dim3 rgrid((e->rdg.W + 15) / 16, (e->rdg.H + 15) / 16);
+    hipLaunchKernelGGL(k_raycast_g, rgrid, dim3(256), 0, e->stream, e->D, e->rdg.args);
+    HIP_OK(hipGetLastError());
+  }
   if (e->rd.pending && !keep_deferred) {  // a deferred raycast no ingest took up: launched alone, before anything else
     e->rd.pending = false;
     const tsdf_engine::DeferredRender& r = e->rd;
@@ -1283,6 +1298,18 @@ namespace {
 // (|direction| = 1 up to rounding), plus the binary search, the +-1 gradient neighbours and the
 // rounding to the nearest voxel (2.5 voxels). n = 0 (hash lookups) when the cube would exceed
 // kViewMaxN cells per axis, the brick bitmap `lds_words` of LDS, or the pool a cell's index bits.
+int view_grid_for(tsdf_engine* e, const FrameParams& P, float step_size, int lds_words, ViewGrid* V);
+// whether view_grid_for(P) would clear or reallocate the grid's cells (a deferred raycast reading the
+// previous grid must run first)
+bool view_grid_resets(const tsdf_engine* e, const FrameParams& P, float step_size) {
+  const double max_step = std::ceil((double)P.max_depth / (double)step_size);
+  const double reach = max_step * (double)step_size / (double)P.voxel * (1.0 + 1e-5) + 2.5;
+  if (!(reach < 1e6)) return false;
+  const int half = (int)std::ceil(reach / kBlockLen) + 1;
+  const int nb = (2 * half + 1 + 3) / 4;
+  return e->vg_gen == kViewGenMax || (int64_t)nb * nb * nb * 64 > e->vg_cap;
+}
+
 int view_grid_for(tsdf_engine* e, const FrameParams& P, float step_size, int lds_words, ViewGrid* V) {
   *V = ViewGrid{};
   V->flags = e->vg_flags;
@@ -1332,6 +1359,10 @@ int view_grid_for(tsdf_engine* e, const FrameParams& P, float step_size, int lds
 // pointers) from a pinned host slot, so one instantiated graph serves every frame; kSlots graphs
 // with their own slots let the host fill frame i+1 while frame i runs.
 // ---------------------------------------------------------------------------------------------
+#ifndef TSDF_GRAPH_DONE_FLAGS
+#define TSDF_GRAPH_DONE_FLAGS hipEventDisableTiming
+#endif
+constexpr unsigned kGraphDoneFlags = TSDF_GRAPH_DONE_FLAGS;
 struct tsdf_graph {
   static constexpr int kSlots = 4;
   static constexpr int kSegs = 3;  // a shard's frame: begin / update / end around the exchanges
@@ -1339,6 +1370,8 @@ struct tsdf_graph {
   int W = 0, H = 0, RW = 0, RH = 0;
   bool shard = false;     // a shard engine's graph (tsdf_graph_create_shard)
   bool pipe = false;      // pipelined frames: each launch is one k_frame_g (no render camera)
+  bool defer = false;     // render-deferring graph (tsdf_graph_create_deferred): each launch renders the
+                          // previous frame's camera beside its ingest (k_render_ingest_g)
   int slice_index = 0, slice_count = 1;
   int cur = -1;           // a shard's frame in flight: its slot
   hipStream_t cap = nullptr;  // capture stream (the engine stream may be a legacy default stream)
@@ -1369,8 +1402,9 @@ void graph_free(tsdf_graph* g) {
 
 }  // namespace
 
-int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, int render_height,
-                      tsdf_graph** out) {
+namespace {
+int graph_create(tsdf_engine* e, int width, int height, int render_width, int render_height, bool defer,
+                 tsdf_graph** out) {
   if (e && e->cfg.shard_count > 1) {
     set_error("tsdf_graph_create: a shard's graph frames are tsdf_graph_create_shard / tsdf_graph_shard_*");
     return TSDF_ERR_INVALID_ARG;
@@ -1392,6 +1426,7 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
   // frames without a render camera pipeline like tsdf_integrate; a render camera needs each frame
   // complete before its raycast, so those graphs keep the two-launch frame
   g->pipe = render_width == 0 && e->pipeline && e->maxs <= 3 && pipe_frame_size(e, width, height);
+  g->defer = defer && render_width && e->maxs <= 3;  // (k_render_ingest_g is the 1024-slot ingest)
   auto fail = [&](hipError_t err, const char* what) {
     set_error(what, err);
     graph_free(g);
@@ -1408,7 +1443,7 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
   if ((err = hipStreamSynchronize(e->stream)) != hipSuccess) return fail(err, "graph sync");
   for (int k = 0; k < tsdf_graph::kSlots; ++k) {
     const FrameArgs* A = g->d_args + k;
-    if ((err = hipEventCreateWithFlags(&g->done[k], hipEventDisableTiming)) != hipSuccess) return fail(err, "graph event");
+    if ((err = hipEventCreateWithFlags(&g->done[k], kGraphDoneFlags)) != hipSuccess) return fail(err, "graph event");
     if ((err = hipStreamBeginCapture(g->cap, hipStreamCaptureModeThreadLocal)) != hipSuccess)
       return fail(err, "hipStreamBeginCapture");
     if (e->env.graph_memcpy_node)  // A/B: a memcpy node instead of the copy kernel
@@ -1420,7 +1455,11 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
       const int nwg = kPipeHead + kPipeFreshWG + e->D.integrate_grid_pre + tiles + kVisWorkgroups;
       hipLaunchKernelGGL(k_frame_g, dim3(nwg), dim3(kIntegrateThreads), 0, g->cap, e->D, A);
     } else {
-      if (e->maxs <= 3)
+      const int rgx = (render_width + 15) / 16, nray = rgx * ((render_height + 15) / 16);
+      if (g->defer)  // the previous frame's raycast (args->prev; none: its workgroups exit) + this ingest
+        hipLaunchKernelGGL(k_render_ingest_g, dim3(nray + kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D,
+                           A, rgx, nray);
+      else if (e->maxs <= 3)
         hipLaunchKernelGGL(k_ingest_dda_g<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
       else
         hipLaunchKernelGGL(k_ingest_dda_g<2048>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
@@ -1431,7 +1470,7 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
       hipLaunchKernelGGL(k_view_grid_g, dim3(kOccWords / 256), dim3(256), 0, g->cap, e->D, A);
       hipLaunchKernelGGL(k_view_pack_g, dim3(kViewPackGrid), dim3(256), 0, g->cap, A);
       const dim3 rgrid((render_width + 15) / 16, (render_height + 15) / 16);
-      hipLaunchKernelGGL(k_raycast_g, rgrid, dim3(256), 0, g->cap, e->D, A);
+      if (!g->defer) hipLaunchKernelGGL(k_raycast_g, rgrid, dim3(256), 0, g->cap, e->D, A);
     }
     if ((err = hipStreamEndCapture(g->cap, &g->graph[k][0])) != hipSuccess) return fail(err, "hipStreamEndCapture");
     if ((err = hipGraphInstantiate(&g->exec[k][0], g->graph[k][0], nullptr, nullptr, 0)) != hipSuccess)
@@ -1439,6 +1478,17 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
   }
   *out = g;
   return TSDF_OK;
+}
+}  // namespace
+
+int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, int render_height,
+                      tsdf_graph** out) {
+  return graph_create(e, width, height, render_width, render_height, false, out);
+}
+
+int tsdf_graph_create_deferred(tsdf_engine* e, int width, int height, int render_width, int render_height,
+                               tsdf_graph** out) {
+  return graph_create(e, width, height, render_width, render_height, true, out);
 }
 
 // A shard's graph frame: three captured segments per args slot -- (0) the args upload + k_ingest_dda_g
@@ -1480,7 +1530,7 @@ int tsdf_graph_create_shard(tsdf_engine* e, int width, int height, int slice_ind
   if ((err = hipStreamSynchronize(e->stream)) != hipSuccess) return fail(err, "graph sync");
   for (int k = 0; k < tsdf_graph::kSlots; ++k) {
     const FrameArgs* A = g->d_args + k;
-    if ((err = hipEventCreateWithFlags(&g->done[k], hipEventDisableTiming)) != hipSuccess) return fail(err, "graph event");
+    if ((err = hipEventCreateWithFlags(&g->done[k], kGraphDoneFlags)) != hipSuccess) return fail(err, "graph event");
     for (int seg = 0; seg < tsdf_graph::kSegs; ++seg) {
       if ((err = hipStreamBeginCapture(g->cap, hipStreamCaptureModeThreadLocal)) != hipSuccess)
         return fail(err, "hipStreamBeginCapture");
@@ -1615,6 +1665,12 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
+  // this graph's deferred raycast of the previous frame: rendered by this launch (k_render_ingest_g)
+  const FrameArgs* prev = nullptr;
+  if (g->defer && e->rdg.pending && e->rdg.g == g) {
+    prev = e->rdg.args;
+    e->rdg.pending = false;
+  }
   if (g->pipe)
     JOIN_RENDER(e);  // (the pending frames continue in this launch)
   else
@@ -1633,9 +1689,16 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
   a.normal = reinterpret_cast<uchar4*>(normal);
   a.step_size = e->cfg.truncation / 2;
   if (g->RW) {
+    if (prev && view_grid_resets(e, a.R, a.step_size)) {  // (the pending raycast reads the old grid)
+      hipLaunchKernelGGL(k_raycast_g, dim3((g->RW + 15) / 16, (g->RH + 15) / 16), dim3(256), 0, e->stream, e->D,
+                         prev);
+      LAUNCH_OK("k_raycast_g");
+      prev = nullptr;
+    }
     int rc = view_grid_for(e, a.R, a.step_size, kViewGraphBitmapWords, &a.V);
     if (rc) return rc;
   }
+  a.prev = prev;
   a.range = (uint32_t)((size_t)f->width * f->height * e->maxs);
   a.tiles_x = (f->width + 15) / 16;
   a.tiles = a.tiles_x * ((f->height + 15) / 16);
@@ -1653,6 +1716,21 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
     if (e->profiling && a.pipe.has_update) ++e->prof_pipelined;
   }
   HIP_OK(hipGraphLaunch(g->exec[k][0], e->stream));
+  if (g->defer) {
+    // a view grid's raycast waits for the next launch; a hash-lookup raycast (no grid: it reads the
+    // table the next ingest writes) runs now, after the graph
+    if (a.V.n) {
+      e->rdg.pending = true;
+      e->rdg.g = g;
+      e->rdg.args = g->d_args + k;
+      e->rdg.W = g->RW;
+      e->rdg.H = g->RH;
+    } else {
+      hipLaunchKernelGGL(k_raycast_g, dim3((g->RW + 15) / 16, (g->RH + 15) / 16), dim3(256), 0, e->stream, e->D,
+                         g->d_args + k);
+      LAUNCH_OK("k_raycast_g");
+    }
+  }
   HIP_OK(hipEventRecord(g->done[k], e->stream));
   g->used[k] = true;
   if (g->pipe) pipe_advance(e, fid, a.P);

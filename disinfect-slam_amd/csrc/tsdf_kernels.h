@@ -182,6 +182,9 @@ struct FrameArgs {
   // camera / pixel records of the frame whose allocation and update run, pipe what the launch does
   FrameParams Pu;
   PipeArgs pipe;
+  // a render-deferring graph frame: the previous frame's args slot, whose raycast this launch runs
+  // beside its ingest (k_render_ingest_g); null: none
+  const FrameArgs* prev;
 };
 
 __global__ void k_init_table(int4* table);
@@ -258,6 +261,8 @@ __global__ void k_raycast(EngineDev D, FrameParams P, float step_size, ViewGrid 
 __global__ void k_render_ingest(EngineDev D, FrameParams R, float step_size, ViewGrid V, uchar4* rgba,
                                 uchar4* normal, int rgx, int nray, FrameParams P, const float* depth,
                                 const uint8_t* rgb, const float* ht, const float* lt, int tiles_x, int tiles);
+// (graph form: A->prev's raycast, none when null, beside A's ingest)
+__global__ void k_render_ingest_g(EngineDev D, const FrameArgs* A, int rgx, int nray);
 // view grid of a raycast: grid kOccWords / 256 workgroups of 256
 __global__ void k_view_grid(EngineDev D, FrameParams P, ViewGrid V);
 __global__ void k_view_grid_g(EngineDev D, const FrameArgs* A);

@@ -182,13 +182,13 @@ class FrameGraph:
     """One instantiated per-frame hipGraph of an Engine (tsdf_graph_create). frame() takes device
     tensors only; rgba / normal are device tensors (render_height, render_width, 4) u8 or None."""
 
-    def __init__(self, eng, width, height, render_width=0, render_height=0):
+    def __init__(self, eng, width, height, render_width=0, render_height=0, deferred=False):
         self._eng = eng
         self.width, self.height = width, height
         self.render_width, self.render_height = render_width, render_height
         h = C.c_void_p()
-        _lib.check(_lib.load().tsdf_graph_create(eng._h, width, height, render_width, render_height,
-                                                 C.byref(h)), "tsdf_graph_create")
+        fn = "tsdf_graph_create_deferred" if deferred else "tsdf_graph_create"
+        _lib.check(getattr(_lib.load(), fn)(eng._h, width, height, render_width, render_height, C.byref(h)), fn)
         self._g = h
 
     def frame(self, rgb, depth, ht, lt, K, cam_T_world, max_depth, render_K=None,
@@ -390,10 +390,12 @@ class Engine:
                    "tsdf_feed_rgbd_frame")
         self._signal_torch(depth_u16)
 
-    def frame_graph(self, width: int, height: int, render_width: int = 0, render_height: int = 0):
+    def frame_graph(self, width: int, height: int, render_width: int = 0, render_height: int = 0,
+                    deferred: bool = False):
         """Graph-captured frame loop (tsdf_graph_*, BASELINE config C5): integrate (+ raycast of
-        a render camera) as one hipGraph launch per frame."""
-        return FrameGraph(self, width, height, render_width, render_height)
+        a render camera) as one hipGraph launch per frame. deferred=True (tsdf_graph_create_deferred):
+        each frame's images are written by the next frame's launch (or the engine's next other call)."""
+        return FrameGraph(self, width, height, render_width, render_height, deferred)
 
     def shard_frame_graph(self, width: int, height: int, slice_index: int = 0, slice_count: int = 1):
         """A shard's graph-captured sharded frame (tsdf_graph_create_shard)."""

@@ -106,7 +106,7 @@ EXPORTS = [
     "tsdf_hash_block", "tsdf_block_owner", "tsdf_error_string", "tsdf_last_error",
     "tsdf_shard_slot_bytes", "tsdf_integrate_shard_begin", "tsdf_integrate_shard_update",
     "tsdf_integrate_shard_end", "tsdf_integrate_shard_abort", "tsdf_stream_wait", "tsdf_stream_signal", "tsdf_get_stream",
-    "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame", "tsdf_graph_destroy",
+    "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_create_deferred", "tsdf_graph_frame", "tsdf_graph_destroy",
     "tsdf_snapshot_bytes", "tsdf_snapshot_save", "tsdf_snapshot_load",
     "tsdf_render_blocks", "tsdf_import_blocks", "tsdf_reset", "tsdf_pack_blocks",
     "tsdf_raycast_rows", "tsdf_raycast_deferred", "tsdf_render_bands", "tsdf_pack_halo", "tsdf_extract_mesh_owned",
@@ -149,6 +149,7 @@ def load(path: str | None = None):
     L.tsdf_feed_rgbd_frame.argtypes = [P, P, P, P, i, i, f, C.POINTER(Intrinsics), C.POINTER(Pose), f, i]
     L.tsdf_rgbd_half.argtypes = [P, P, P, P, i, i, f, P, P, i]
     L.tsdf_graph_create.argtypes = [P, i, i, i, i, C.POINTER(P)]
+    L.tsdf_graph_create_deferred.argtypes = [P, i, i, i, i, C.POINTER(P)]
     L.tsdf_graph_frame.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f,
                                    C.POINTER(Intrinsics), C.POINTER(Pose), P, P]
     L.tsdf_graph_destroy.argtypes = [P]
@@ -204,7 +205,7 @@ def load(path: str | None = None):
     for name in ("tsdf_create", "tsdf_destroy", "tsdf_integrate", "tsdf_raycast", "tsdf_query",
                  "tsdf_integrate_shard_begin", "tsdf_integrate_shard_update", "tsdf_integrate_shard_end",
                  "tsdf_integrate_shard_abort", "tsdf_stream_wait", "tsdf_stream_signal", "tsdf_get_stream",
-                 "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_frame",
+                 "tsdf_feed_rgbd_frame", "tsdf_rgbd_half", "tsdf_graph_create", "tsdf_graph_create_deferred", "tsdf_graph_frame",
                  "tsdf_graph_destroy", "tsdf_snapshot_bytes", "tsdf_snapshot_save", "tsdf_snapshot_load",
                  "tsdf_extract_mesh", "tsdf_raycast_rows", "tsdf_raycast_deferred", "tsdf_render_bands", "tsdf_pack_halo",
                  "tsdf_extract_mesh_owned", "tsdf_render_blocks", "tsdf_import_blocks", "tsdf_reset",

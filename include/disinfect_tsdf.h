@@ -235,6 +235,15 @@ int tsdf_rgbd_half(tsdf_engine* e, const uint8_t* rgb, const uint16_t* depth, co
  * not recorded for graph frames. */
 int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, int render_height,
                       tsdf_graph** out);
+/* A render-deferring graph (the C5 loop's form of tsdf_raycast_deferred): each frame's raycast is
+ * rendered by the graph's NEXT launch, in one kernel with that frame's ingest (k_render_ingest_g), or
+ * by the engine's next other call (tsdf_flush, tsdf_synchronize, a query, ...), which launches it
+ * alone first. So frame i's rgba / normal are complete once tsdf_graph_frame(i + 1) -- or any other
+ * call -- has run, in engine-stream order, and must stay valid until then. Images, volume and
+ * statistics are identical to tsdf_graph_create's. Views too deep for a view grid render right after
+ * their frame's graph launch. */
+int tsdf_graph_create_deferred(tsdf_engine* e, int width, int height, int render_width, int render_height,
+                               tsdf_graph** out);
 int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* frame, const tsdf_intrinsics* K,
                      const tsdf_pose* cam_T_world, float max_depth, const tsdf_intrinsics* render_K,
                      const tsdf_pose* render_cam_T_world, uint8_t* rgba, uint8_t* normal);

@@ -190,3 +190,56 @@ def test_c5_deferred_raycast_equals_immediate():
             b.raycast(K, W, H, pose, 4.0, deferred=True)  # (host images: immediate only)
     finally:
         a.close(), b.close()
+
+
+def test_c5_deferred_graph_equals_graph():
+    """tsdf_graph_create_deferred: frame i's raycast runs in graph launch i + 1 (k_render_ingest_g) or
+    in the engine's next other call; images equal the immediate graph's frame by frame, the volume
+    equals it block for block (mesh), also across a stats() call, a far view (hash-lookup raycast, not
+    deferred) and the final flush."""
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H, n = 640, 480, 20
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    a = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=18)
+    b = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=18)
+    ga, gb = a.frame_graph(W, H, W, H), b.frame_graph(W, H, W, H, deferred=True)
+    try:
+        ref = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(2)]
+        out = [[torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(2)] for _ in range(3)]
+        pending = None
+        frames = []
+        for i in range(n):
+            fr = synth.render(cam, i)
+            pose = tsdf_amd.SE3(fr["q"], fr["t"])
+            dev = {k: torch.from_numpy(fr[k]).to("cuda") for k in ("rgb", "depth", "ht", "lt")}
+            frames.append(dev)  # (graph frames stay valid until they have run)
+            md = 9.0 if i == 11 else 4.0  # frame 11: too deep for a view grid
+            ga.frame(dev["rgb"], dev["depth"], dev["ht"], dev["lt"], K, pose, md, K, pose, ref[0], ref[1])
+            o = out[i % 3]
+            gb.frame(dev["rgb"], dev["depth"], dev["ht"], dev["lt"], K, pose, md, K, pose, o[0], o[1])
+            if pending is not None:
+                j, po, r0, r1 = pending
+                torch.cuda.synchronize()
+                assert torch.equal(po[0], r0) and torch.equal(po[1], r1), f"frame {j}: deferred graph != graph"
+            torch.cuda.synchronize()
+            pending = (i, o, ref[0].clone(), ref[1].clone())
+            if i == 6:
+                assert b.stats()["status"] == 0  # launches the pending raycast alone
+                torch.cuda.synchronize()
+                assert torch.equal(o[0], ref[0]) and torch.equal(o[1], ref[1]), "frame 6 after stats"
+        b.flush()
+        torch.cuda.synchronize()
+        j, po, r0, r1 = pending
+        assert torch.equal(po[0], r0) and torch.equal(po[1], r1), "last frame after flush"
+        assert (r0[..., 3] == 255).float().mean().item() > 0.5
+        sa, sb = a.stats(), b.stats()
+        assert sa["status"] == 0 and sb["status"] == 0 and sa["active_blocks"] == sb["active_blocks"]
+        m_a, m_b = a.extract_mesh(None, 0.99, 0), b.extract_mesh(None, 0.99, 0)
+        np.testing.assert_array_equal(np.asarray(m_a).view(np.uint32), np.asarray(m_b).view(np.uint32))
+    finally:
+        ga.close(), gb.close()
+        a.close(), b.close()
