@@ -78,18 +78,16 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
   if (threadIdx.x == 0) D.ctr->ingest_ticks += tend - ld_co(&D.arrive[kArrStart + 8]);
   TSDF_STAMP(D, 6, 2);
 }
-// at least 6 waves per SIMD (<= 80 VGPRs): the whole 640x480 grid (1456 workgroups) resident at once;
-// the resolver tail alone would raise the kernel to 81 VGPRs (5 waves: 1280 workgroups, +2 us span)
-#ifndef TSDF_INGEST_WAVES_ATTR
-#define TSDF_INGEST_WAVES_ATTR 1
+// k_ingest_dda at 8 waves per SIMD (<= 64 VGPRs): 2048 resident workgroups, so a 1280x720 frame's 3,856
+// take 1.9 rounds instead of 2.5. Measured at C4 (300 frames, same box, interleaved): ingest span
+// 24.6 -> 23.1 us, the tail's resolver 3.35 -> 4.45 us (a few spills), 16.85k -> 17.02k frames/s;
+// 7 waves 16.91k. At 640x480 every tile is resident at 6 waves (1456 workgroups) already. The fused
+// render + ingest launch keeps 6 (<= 80 VGPRs; its raycast part is register-hungry).
+#ifndef TSDF_INGEST_MIN_WAVES
+#define TSDF_INGEST_MIN_WAVES 8
 #endif
-#if TSDF_INGEST_WAVES_ATTR == 1
-#define INGEST_WAVES(TS) __attribute__((amdgpu_waves_per_eu(TS <= 1024 ? 6 : 5)))
-#elif TSDF_INGEST_WAVES_ATTR == 2
-#define INGEST_WAVES(TS) __attribute__((amdgpu_waves_per_eu(TS <= 1024 ? 6 : 5, TS <= 1024 ? 6 : 5)))
-#else
-#define INGEST_WAVES(TS)
-#endif
+#define INGEST_WAVES(TS) __attribute__((amdgpu_waves_per_eu(TS <= 1024 ? TSDF_INGEST_MIN_WAVES : 5)))
+#define RENDER_INGEST_WAVES __attribute__((amdgpu_waves_per_eu(6)))
 template <int TS>
 __global__ __launch_bounds__(256) INGEST_WAVES(TS) void k_ingest_dda(EngineDev D, FrameParams P,
                                                     const float* __restrict__ depth,
@@ -120,7 +118,7 @@ union RenderIngestLds {
   IngestLds<1024> ing;
   uint32_t bits[kViewGraphBitmapWords];  // the raycast's staged bitmaps
 };
-__global__ __launch_bounds__(256) INGEST_WAVES(1024) void k_render_ingest(
+__global__ __launch_bounds__(256) RENDER_INGEST_WAVES void k_render_ingest(
     EngineDev D, FrameParams R, float step_size, ViewGrid V, uchar4* __restrict__ rgba, uchar4* __restrict__ normal,
     int rgx, int nray, FrameParams P, const float* __restrict__ depth, const uint8_t* __restrict__ rgb,
     const float* __restrict__ ht, const float* __restrict__ lt, int tiles_x, int tiles) {
@@ -132,7 +130,7 @@ __global__ __launch_bounds__(256) INGEST_WAVES(1024) void k_render_ingest(
   }
   ingest_dda<1024>(D, P, depth, rgb, ht, lt, tiles_x, tiles, U.ing, b - nray, (int)gridDim.x - nray);
 }
-__global__ __launch_bounds__(256) INGEST_WAVES(1024) void k_render_ingest_g(EngineDev D,
+__global__ __launch_bounds__(256) RENDER_INGEST_WAVES void k_render_ingest_g(EngineDev D,
                                                                             const FrameArgs* __restrict__ A,
                                                                             int rgx, int nray) {
   __shared__ RenderIngestLds U;

@@ -33,11 +33,12 @@ def main():
     L = _lib.load()
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
-    cam = synth.camera(640, 480, synth.TUM_FR1)
+    W, H = int(os.environ.get("DIAG_W", 640)), int(os.environ.get("DIAG_H", 480))
+    cam = synth.camera(W, H, synth.TUM_FR1)
     nwarm, nmeas = 60, 20
     fr = synth.render_torch(cam, list(range(nwarm + nmeas)), device=dev)
     torch.cuda.synchronize()
-    eng = tsdf_amd.Engine(0.005, 0.03, max_width=640, max_height=480, num_block_bits=18,
+    eng = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=18,
                           device=0, stream=torch.cuda.current_stream().cuda_stream)
     en = C.c_int(0)
     L.tsdf_debug_stamps(eng._h, None, 0, C.byref(en))
@@ -91,6 +92,11 @@ def main():
                 dur = (s[:, j + 1] - s[:, j]) * 10e-3
                 d[p].append(np.median(dur))
                 d[p + "_max"].append(dur.max())
+            if k == 0 and (s[:, 6] > 0).all():  # the tile's tail: corner tests (4 -> 6), probes + inserts (6 -> 5)
+                for p, a, b in (("corners", 4, 6), ("probe_insert", 6, 5)):
+                    dur = (s[:, b] - s[:, a]) * 10e-3
+                    d.setdefault(p, []).append(np.median(dur))
+                    d.setdefault(p + "_max", []).append(dur.max())
         if S[1, 0, 7] > 0:  # TSDF_EXP & 16 diag build: the resolver's sort repeated (warm)
             acc.setdefault("resolve_alloc sort repeated", {}).setdefault("sort2", []).append(
                 (S[1, 0, 7] - S[1, 0, 2]) * 10e-3)
