@@ -98,12 +98,14 @@ hipError_t dmalloc(T** p, size_t count) {
 //   TSDF_MESH_GRID=n              (tests) fewer k_mesh workgroups, to exercise its grid stride
 //   TSDF_RENDER_OVERLAP=1         raycast on a second stream overlapping the next frame
 //   TSDF_GRAPH_MEMCPY_NODE=1      (A/B) graph frames upload their arguments with a memcpy node
+//   TSDF_UPLOAD_STREAMS=n         (A/B) host frames: upload streams a frame's copies spread over (1-4, default 2)
 // ---------------------------------------------------------------------------------------------
 struct EnvKnobs {
   bool pipeline = true;
   int64_t pipe_max_pixels = -1;
   int frame_order = -1, frame_wg_per_cu = 0, integrate_wg_per_cu = 0, cand_cap = 0, mesh_grid = 0;
   bool render_overlap = false, graph_memcpy_node = false;
+  int upload_streams = 2;
 };
 static EnvKnobs read_env_knobs() {
   EnvKnobs k;
@@ -124,6 +126,7 @@ static EnvKnobs read_env_knobs() {
   k.mesh_grid = (int)num("TSDF_MESH_GRID", 0);
   k.render_overlap = flag("TSDF_RENDER_OVERLAP", false);
   k.graph_memcpy_node = flag("TSDF_GRAPH_MEMCPY_NODE", false);
+  k.upload_streams = (int)num("TSDF_UPLOAD_STREAMS", 2);
   return k;
 }
 
@@ -172,8 +175,11 @@ struct tsdf_engine {
   float* s_depth = nullptr;
   float* s_ht = nullptr;
   float* s_lt = nullptr;
-  hipStream_t ustream = nullptr;          // upload stream
-  hipEvent_t up_done[2] = {nullptr, nullptr};  // slot k's upload complete (the engine stream waits)
+  // upload streams: a frame's copies spread over them (several DMA engines share the host link)
+  static constexpr int kUpStreams = 4;
+  hipStream_t ustream[kUpStreams] = {};
+  hipEvent_t up_done[2][kUpStreams] = {};  // slot k's copies on stream j complete (the engine stream waits)
+  int up_nstreams = 0;                     // streams the pending upload used
   hipEvent_t up_free[2] = {nullptr, nullptr};  // slot k's last reader launched before this (the upload waits)
   bool up_used[2] = {false, false};       // up_free[k] has been recorded
   int up_next = 0;                        // the slot of the next host frame
@@ -282,9 +288,12 @@ void free_all(tsdf_engine* e) {
     for (hipEvent_t x : ev) (void)hipEventDestroy(x);
   if (e->order_ev) (void)hipEventDestroy(e->order_ev);
   if (e->rstream) (void)hipStreamDestroy(e->rstream);
-  if (e->ustream) (void)hipStreamDestroy(e->ustream);
+  for (int j = 0; j < tsdf_engine::kUpStreams; ++j) {
+    if (e->ustream[j]) (void)hipStreamDestroy(e->ustream[j]);
+    for (int k = 0; k < 2; ++k)
+      if (e->up_done[k][j]) (void)hipEventDestroy(e->up_done[k][j]);
+  }
   for (int k = 0; k < 2; ++k) {
-    if (e->up_done[k]) (void)hipEventDestroy(e->up_done[k]);
     if (e->up_free[k]) (void)hipEventDestroy(e->up_free[k]);
   }
   if (e->rs_ready) (void)hipEventDestroy(e->rs_ready);
@@ -663,10 +672,15 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
       return fail(TSDF_ERR_HIP);
     e->own_stream = true;
   }
-  if (hipStreamCreateWithFlags(&e->ustream, hipStreamNonBlocking) != hipSuccess)
-    return fail(TSDF_ERR_HIP);
+  for (int j = 0; j < tsdf_engine::kUpStreams; ++j) {
+    if (hipStreamCreateWithFlags(&e->ustream[j], hipStreamNonBlocking) != hipSuccess)
+      return fail(TSDF_ERR_HIP);
+    for (int k = 0; k < 2; ++k)
+      if (hipEventCreateWithFlags(&e->up_done[k][j], hipEventDisableTiming) != hipSuccess)
+        return fail(TSDF_ERR_HIP);
+  }
   for (int k = 0; k < 2; ++k)
-    if (hipEventCreateWithFlags(&e->up_done[k], hipEventDisableTiming) != hipSuccess ||
+    if (
         hipEventCreateWithFlags(&e->up_free[k], hipEventDisableTiming) != hipSuccess)
       return fail(TSDF_ERR_HIP);
   if (hipStreamCreateWithFlags(&e->rstream, hipStreamNonBlocking) != hipSuccess ||
@@ -726,7 +740,7 @@ int upload_release(tsdf_engine* e) {
   e->up_pending = -1;
   HIP_OK(hipEventRecord(e->up_free[k], e->stream));
   e->up_used[k] = true;
-  HIP_OK(hipEventSynchronize(e->up_done[k]));
+  for (int j = 0; j < e->up_nstreams; ++j) HIP_OK(hipEventSynchronize(e->up_done[k][j]));
   return TSDF_OK;
 }
 
@@ -767,7 +781,7 @@ int frame_ingest(tsdf_engine* e, const EngineDev& Dv, const tsdf_frame* f, const
   const float* ht = f->ht;
   const float* lt = f->lt;
   if (f->mem_kind == TSDF_MEM_HOST) {  // voxel_tsdf.cu:358-365 (H2D; pageable or pinned host memory)
-    // The upload runs on the upload stream into the next of two staging slots, beside the frames the
+    // The upload runs on the upload streams into the next of two staging slots, beside the frames the
     // engine stream is still running; the engine stream waits for it (up_done) and the slot's next
     // upload waits until the launch reading this frame is enqueued and done (up_free, recorded by
     // upload_release). The call returns once the copies are complete, so the caller may reuse its
@@ -775,24 +789,29 @@ int frame_ingest(tsdf_engine* e, const EngineDev& Dv, const tsdf_frame* f, const
     if (int rc = upload_release(e)) return rc;
     const int k = e->up_next;
     e->up_next ^= 1;
-    hipStream_t u = e->ustream;
-    if (e->up_used[k]) HIP_OK(hipStreamWaitEvent(u, e->up_free[k], 0));
-    uint8_t* d_rgb = e->s_rgb + (size_t)k * e->max_pixels * 3;
-    float* d_depth = e->s_depth + (size_t)k * e->max_pixels;
-    HIP_OK(hipMemcpyAsync(d_rgb, rgb, np * 3, hipMemcpyHostToDevice, u));
-    HIP_OK(hipMemcpyAsync(d_depth, depth, np * 4, hipMemcpyHostToDevice, u));
-    rgb = d_rgb;
-    depth = d_depth;
-    if (ht) {
-      float* d_ht = e->s_ht + (size_t)k * e->max_pixels;
-      float* d_lt = e->s_lt + (size_t)k * e->max_pixels;
-      HIP_OK(hipMemcpyAsync(d_ht, ht, np * 4, hipMemcpyHostToDevice, u));
-      HIP_OK(hipMemcpyAsync(d_lt, lt, np * 4, hipMemcpyHostToDevice, u));
-      ht = d_ht;
-      lt = d_lt;
+    // the copies round-robin over the upload streams (TSDF_UPLOAD_STREAMS, default 2): the copies run on several DMA
+    // engines at once; the engine stream waits for each
+    const int nu = std::max(1, std::min(e->env.upload_streams, (int)tsdf_engine::kUpStreams));
+    const void* src[4] = {rgb, depth, ht, lt};
+    const size_t bytes[4] = {np * 3, np * 4, np * 4, np * 4};
+    void* dst[4] = {e->s_rgb + (size_t)k * e->max_pixels * 3, e->s_depth + (size_t)k * e->max_pixels,
+                    e->s_ht + (size_t)k * e->max_pixels, e->s_lt + (size_t)k * e->max_pixels};
+    const int ncopy = ht ? 4 : 2;
+    e->up_nstreams = std::min(nu, ncopy);
+    for (int j = 0; j < e->up_nstreams; ++j)
+      if (e->up_used[k]) HIP_OK(hipStreamWaitEvent(e->ustream[j], e->up_free[k], 0));
+    for (int c = 0; c < ncopy; ++c)
+      HIP_OK(hipMemcpyAsync(dst[c], src[c], bytes[c], hipMemcpyHostToDevice, e->ustream[c % e->up_nstreams]));
+    for (int j = 0; j < e->up_nstreams; ++j) {
+      HIP_OK(hipEventRecord(e->up_done[k][j], e->ustream[j]));
+      HIP_OK(hipStreamWaitEvent(s, e->up_done[k][j], 0));
     }
-    HIP_OK(hipEventRecord(e->up_done[k], u));
-    HIP_OK(hipStreamWaitEvent(s, e->up_done[k], 0));
+    rgb = static_cast<const uint8_t*>(dst[0]);
+    depth = static_cast<const float*>(dst[1]);
+    if (ht) {
+      ht = static_cast<const float*>(dst[2]);
+      lt = static_cast<const float*>(dst[3]);
+    }
     // (the host waits for the copies in upload_release, after the launch that reads them is enqueued:
     // the enqueue overlaps the transfer)
     e->up_pending = k;
@@ -1102,7 +1121,8 @@ int tsdf_integrate_shard_begin(tsdf_engine* e, const tsdf_frame* f, const tsdf_i
   // exchange): it resolves the allocation right away, like one volume
   int rc = frame_ingest(e, e->D, f, K, pose, max_depth, slice_index, slice_count, &P, &ev, keys_out, key_cap);
   // (a host frame: its upload is complete on return -- the slot itself is released after _update)
-  if (e->up_pending >= 0) HIP_OK(hipEventSynchronize(e->up_done[e->up_pending]));
+  if (e->up_pending >= 0)
+    for (int j = 0; j < e->up_nstreams; ++j) HIP_OK(hipEventSynchronize(e->up_done[e->up_pending][j]));
   if (rc) return rc;
   P.tail = kTailResolve;
   P.slot = nullptr;
