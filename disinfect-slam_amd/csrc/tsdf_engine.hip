@@ -93,6 +93,7 @@ hipError_t dmalloc(T** p, size_t count) {
 //   TSDF_PIPE_MAX_PIXELS=n        largest frame (pixels) that is pipelined (default 2^19; C4 above it)
 //   TSDF_FRAME_ORDER=0..4         k_frame grid order of its parts (PipeArgs.order; default 2)
 //   TSDF_FRAME_WG_PER_CU=n        k_frame update workgroups per CU (default kFrameWgPerCu = 3)
+//   TSDF_FRAME_TILES_PER_WG=n     (A/B) k_frame pixel tiles per tile workgroup (default 1)
 //   TSDF_INTEGRATE_WG_PER_CU=n    cap on k_integrate's resident workgroups per CU
 //   TSDF_CAND_CAP=n               (tests) smaller carve-candidate list, to exercise its overflow
 //   TSDF_MESH_GRID=n              (tests) fewer k_mesh workgroups, to exercise its grid stride
@@ -104,6 +105,7 @@ struct EnvKnobs {
   bool pipeline = true;
   int64_t pipe_max_pixels = -1;
   int frame_order = -1, frame_wg_per_cu = 0, integrate_wg_per_cu = 0, cand_cap = 0, mesh_grid = 0;
+  int frame_tiles_per_wg = 1;
   bool render_overlap = false, graph_memcpy_node = false;
   int upload_streams = 2;
 };
@@ -121,6 +123,7 @@ static EnvKnobs read_env_knobs() {
   k.pipe_max_pixels = num("TSDF_PIPE_MAX_PIXELS", -1);
   k.frame_order = (int)std::max(-1ll, num("TSDF_FRAME_ORDER", -1));
   k.frame_wg_per_cu = (int)num("TSDF_FRAME_WG_PER_CU", 0);
+  k.frame_tiles_per_wg = (int)std::max(1ll, num("TSDF_FRAME_TILES_PER_WG", 1));
   k.integrate_wg_per_cu = (int)num("TSDF_INTEGRATE_WG_PER_CU", 0);
   k.cand_cap = (int)num("TSDF_CAND_CAP", 0);
   k.mesh_grid = (int)num("TSDF_MESH_GRID", 0);
@@ -912,6 +915,8 @@ void finish_args(tsdf_engine* e, PipeArgs& A, const FrameParams& Pu) {
   A.order = e->frame_order;
   A.range = A.has_alloc ? (uint32_t)((size_t)Pu.W * Pu.H * e->maxs) : 0u;
   if (!A.has_frame) A.tiles = A.tiles_x = 0;
+  A.tiles_per_wg = std::max(1, e->env.frame_tiles_per_wg);
+  A.tile_wgs = (A.tiles + A.tiles_per_wg - 1) / A.tiles_per_wg;
 }
 
 // One k_frame launch (tsdf_fuse.hip): frame A.fid_carve's carving, frame A.fid_alloc's allocation and
@@ -922,7 +927,7 @@ int launch_frame(tsdf_engine* e, PipeArgs A, const FrameParams& Pu, const FrameP
   JOIN_RENDER(e);
   finish_args(e, A, Pu);
   const int nwg = kPipeHead + (A.has_update ? A.nint : 0) + pipe_fresh_wgs(A) +
-                  (A.has_frame ? A.tiles + kVisWorkgroups : 0);
+                  (A.has_frame ? A.tile_wgs + kVisWorkgroups : 0);
   if (e->profiling && A.has_frame) ++e->prof_pipelined;  // (frame launches; not the flush's)
   if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
     hipExtLaunchKernelGGL(k_frame, dim3(nwg), dim3(kIntegrateThreads), 0, s, (*ev)[2], (*ev)[3], 0, e->D, Pu, Pn, A);
@@ -1472,7 +1477,8 @@ int graph_create(tsdf_engine* e, int width, int height, int render_width, int re
       hipLaunchKernelGGL(k_copy_words, dim3(1), dim3(64), 0, g->cap, reinterpret_cast<uint32_t*>(g->d_args + k),
                          reinterpret_cast<const uint32_t*>(g->h_args + k), (int)(sizeof(FrameArgs) / 4));
     if (g->pipe) {  // one k_frame per frame, its grid sized for the largest launch (steady state)
-      const int nwg = kPipeHead + kPipeFreshWG + e->D.integrate_grid_pre + tiles + kVisWorkgroups;
+      const int tpw = std::max(1, e->env.frame_tiles_per_wg);
+      const int nwg = kPipeHead + kPipeFreshWG + e->D.integrate_grid_pre + (tiles + tpw - 1) / tpw + kVisWorkgroups;
       hipLaunchKernelGGL(k_frame_g, dim3(nwg), dim3(kIntegrateThreads), 0, g->cap, e->D, A);
     } else {
       const int rgx = (render_width + 15) / 16, nray = rgx * ((render_height + 15) / 16);

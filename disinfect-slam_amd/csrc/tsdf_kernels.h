@@ -130,6 +130,8 @@ struct PipeArgs {
   uint32_t tag;         // this launch's flag value
   uint32_t range;       // candidate order space of frame b (W H maxs)
   int tiles_x, tiles;   // frame c's pixel tiles
+  int tile_wgs;         // the workgroups that run them (tiles_per_wg consecutive tiles each)
+  int tiles_per_wg;
   int nint;             // update workgroups (a multiple of 8)
   int order;            // grid order of the parts after the head (TSDF_FRAME_ORDER): 0 fresh, update,
                         //   tiles, sweep; 1 fresh, tiles, sweep, update; 2 fresh, sweep, update, tiles;
