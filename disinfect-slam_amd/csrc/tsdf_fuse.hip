@@ -763,10 +763,24 @@ __device__ __forceinline__ bool head_fast(const EngineDev& D, const PipeArgs& A,
   return true;
 }
 
+// an update workgroup's LDS (pipe_update)
+struct PipeUpdLds {
+  int upd[4], vis[4];
+  int ncand;
+  VisRec cand[kIntegrateCandBuf];
+  VisRec def[kPipeDefer];
+  VisRec list[kPipeList];
+  int n, ndef;
+  float pmin[2 * kPipeList];
+  int pdone[kPipeList];
+  uint32_t fb;
+};
+// one allocation for the launch's parts (a workgroup runs one part)
 union FrameLds {
   DeleteLds del;
   IngestLds<1024> ing;
   HeadLds head;
+  PipeUpdLds upd;
 };
 
 __device__ __forceinline__ void merge_cands_inbox(const EngineDev& D, VisRec* cand, int32_t* ncand, const ShardRec* __restrict__ cands_in,
@@ -863,12 +877,14 @@ __device__ __forceinline__ bool lane_kept(uint32_t* rtag, int32_t idx, uint32_t 
 }
 // (D: the base view; frame b's lists are addressed through scalar pointers here -- an EngineDev view
 // copied by value, or captured by reference in a lambda, can be materialised in scratch)
-__device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParams& P, const PipeArgs& A, int kind, int wi) {
-  __shared__ int s_upd[4], s_vis[4];
-  __shared__ int s_ncand;
-  __shared__ VisRec s_cand[kIntegrateCandBuf];  // this workgroup's carve candidates
-  __shared__ VisRec s_def[kPipeDefer];          // deferred (candidate of frame b - 1) blocks
-  __shared__ VisRec s_list[kPipeList];          // the records of one collection
+__device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParams& P, const PipeArgs& A, int kind, int wi,
+                                            PipeUpdLds& L) {
+  int* s_upd = L.upd;
+  int* s_vis = L.vis;
+  int& s_ncand = L.ncand;
+  VisRec* s_cand = L.cand;  // this workgroup's carve candidates
+  VisRec* s_def = L.def;    // deferred (candidate of frame b - 1) blocks
+  VisRec* s_list = L.list;  // the records of one collection
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pair = wave >> 1, hf = wave & 1;
@@ -920,11 +936,12 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
   // the collection is wave 0's: one record per lane (its list record and candidate tag gathered
   // together, two dependent round trips per collection instead of two per record), compacted into
   // s_list by ballot; the deferred candidates' release tags likewise one per lane
-  __shared__ int s_n, s_ndef;
-  __shared__ float s_pmin[2 * kPipeList];  // the two halves' carve minima of each collected record
-  __shared__ int s_pdone[kPipeList];       // halves of the record done
-  __shared__ uint32_t s_fb;                // fb for the candidate path (read from LDS: in a register the
-                                           // frame id was spilled to scratch, reloaded behind a vmcnt(0))
+  int& s_n = L.n;
+  int& s_ndef = L.ndef;
+  float* s_pmin = L.pmin;  // the two halves' carve minima of each collected record
+  int* s_pdone = L.pdone;  // halves of the record done
+  uint32_t& s_fb = L.fb;   // fb for the candidate path (read from LDS: in a register the
+                           // frame id was spilled to scratch, reloaded behind a vmcnt(0))
   if (t0) s_fb = fb;
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
   if (t0) s_ndef = 0;  // (ordered before its first read by the loop's barrier)
@@ -1109,7 +1126,7 @@ __device__ __forceinline__ int frame_part(const EngineDev& D, const FrameParams&
   const int nfr = pipe_fresh_wgs(A);
   if (w < nfr) {  // the blocks this launch's allocation creates (they wait for it: dispatched early)
     if (TSDF_PRIO_UPD) __builtin_amdgcn_s_setprio(TSDF_PRIO_UPD);
-    pipe_update(D, Pu, A, 1, w);
+    pipe_update(D, Pu, A, 1, w, U.upd);
     return 2;
   }
   w -= nfr;
@@ -1133,7 +1150,7 @@ __device__ __forceinline__ int frame_part(const EngineDev& D, const FrameParams&
     // (its XCD split takes o % 8 as the XCD: exact when the parts before it are multiples of 8 long,
     // as at 640x480; correct either way)
     if (TSDF_PRIO_UPD) __builtin_amdgcn_s_setprio(TSDF_PRIO_UPD);
-    pipe_update(D, Pu, A, 0, o);
+    pipe_update(D, Pu, A, 0, o, U.upd);
     return 3;
   }
   if (TSDF_PRIO_TILE) __builtin_amdgcn_s_setprio(TSDF_PRIO_TILE);

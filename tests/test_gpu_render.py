@@ -248,7 +248,7 @@ def test_import_errors():
         _close(full, small)
 
 
-def _render_worker(rank, world, port, q):
+def _render_worker(rank, world, port, q, pipe=False):
     import os
     import sys
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -277,8 +277,14 @@ def _render_worker(rank, world, port, q):
             _integrate([full], cam, 6)
         for f in range(6):  # the sharded frames: key and candidate slots all-gathered over gloo
             fr = synth.render(cam, 2 * f)
-            tdist.integrate_sharded(shard, bufs, fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K,
-                                    tsdf_amd.SE3(fr["q"], fr["t"]), 4.0)
+            if pipe:  # one k_frame and one candidate all-gather per frame (tsdf_integrate_shard_pipe)
+                tdist.integrate_sharded_pipe(shard, bufs, fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K,
+                                             tsdf_amd.SE3(fr["q"], fr["t"]), 4.0)
+            else:
+                tdist.integrate_sharded(shard, bufs, fr["rgb"], fr["depth"], fr["ht"], fr["lt"], cam.K,
+                                        tsdf_amd.SE3(fr["q"], fr["t"]), 4.0)
+        if pipe:
+            tdist.flush_sharded_pipe(shard, bufs)
         for K, pose in _views(cam):
             got = tdist.render_sharded(shard, replica, K, W, H, pose, 4.0, device=False)
             if rank == 0:
@@ -298,9 +304,12 @@ def _render_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_render_sharded_two_ranks():
+@pytest.mark.parametrize("pipe", [False, True])
+def test_render_sharded_two_ranks(pipe):
     """tsdf_amd.dist.render_sharded across 2 processes (gloo all-gather of host records, both ranks
-    on this GPU): rank 0's image equals its unsharded engine's raycast bit for bit."""
+    on this GPU): rank 0's image equals its unsharded engine's raycast bit for bit, and the mesh its
+    mesh. pipe: the frames through integrate_sharded_pipe (one candidate exchange per frame, across
+    the processes) and flush_sharded_pipe."""
     import socket
 
     import torch.multiprocessing as mp
@@ -310,7 +319,7 @@ def test_render_sharded_two_ranks():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.start_processes(_render_worker, args=(2, port, q), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_render_worker, args=(2, port, q, pipe), nprocs=2, join=True, start_method="spawn")
     res = dict(q.get(timeout=5) for _ in range(2))
     assert res == {0: "ok", 1: "ok"}, res
 
