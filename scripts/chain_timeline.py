@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Per-frame kernel chain of a rocprofv3 kernel trace of a frame loop (diagnostic).
 
-A frame starts at each dispatch of its first kernel (regex, default k_ingest_dda / k_frame /
-k_copy_words); frames holding only engine kernels (k_* and the runtime's copies) are kept. Prints
+A frame starts at each dispatch of its first kernel (regex, default k_ingest_dda /
+k_render_ingest / k_frame / k_copy_words); frames holding only engine kernels (k_* and the runtime's copies) are kept. Prints
 the frame period (median over the plain frames, and each marching-cubes frame's period with its
 kernels) and, per kernel, the median duration in the plain frames.
 Usage: chain_timeline.py <rocprofv3 output dir> [first-kernel regex]"""
@@ -20,7 +20,7 @@ def short(n):
 
 def main():
     d = sys.argv[1]
-    first = re.compile(sys.argv[2] if len(sys.argv) > 2 else r"k_ingest_dda|k_frame|k_copy_words")
+    first = re.compile(sys.argv[2] if len(sys.argv) > 2 else r"k_ingest_dda|k_render_ingest|k_frame|k_copy_words")
     f = sorted(glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True))[0]
     rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]))
                   for r in csv.DictReader(open(f)))
@@ -32,6 +32,8 @@ def main():
     print(f"{f}: {len(idx)} frames, {len(plain)} plain frames of {plain_len} dispatches")
     per = [(s[-1][1] - s[0][0]) / 1e3 for s in plain]
     print(f"plain frame, first start -> last end: median {st.median(per):.1f} us")
+    gaps = [sum(max(0, s[k + 1][0] - s[k][1]) for k in range(len(s) - 1)) / 1e3 for s in plain]
+    print(f"plain frame, idle gaps between its kernels: median {st.median(gaps):.1f} us")
     dur = defaultdict(list)
     for s in plain:
         for a, b, n in s:
