@@ -619,15 +619,17 @@ def host_frames(a, fr, reps=20):
         e1.record(st)
         st.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
-    # the same copies alternating over two streams (the engine's default upload split)
+    # the same copies split over two streams (the engine's default upload split): even keys on one,
+    # odd keys on the other, each stream's reps back to back
     st2 = torch.cuda.Stream()
     e2, e3, e4 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
     e2.record(st)
     st2.wait_event(e2)
-    for _ in range(reps):
-        for j, k in enumerate(keys):
-            with torch.cuda.stream(st if j % 2 == 0 else st2):
-                dst[k].copy_(src[k], non_blocking=True)
+    for j, stream in enumerate((st, st2)):
+        with torch.cuda.stream(stream):
+            for _ in range(reps):
+                for k in keys[j::2]:
+                    dst[k].copy_(src[k], non_blocking=True)
     e4.record(st2)
     st.wait_event(e4)
     e3.record(st)
