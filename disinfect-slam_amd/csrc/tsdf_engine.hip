@@ -99,6 +99,7 @@ hipError_t dmalloc(T** p, size_t count) {
 //   TSDF_MESH_GRID=n              (tests) fewer k_mesh workgroups, to exercise its grid stride
 //   TSDF_RENDER_OVERLAP=1         raycast on a second stream overlapping the next frame
 //   TSDF_GRAPH_MEMCPY_NODE=1      (A/B) graph frames upload their arguments with a memcpy node
+//   TSDF_FUSE_VIEW_GRID=0         (A/B) the C5 loop's view grid in its own launch, not in the update's
 //   TSDF_UPLOAD_STREAMS=n         (A/B) host frames: upload streams a frame's copies spread over (1-4, default 2)
 // ---------------------------------------------------------------------------------------------
 struct EnvKnobs {
@@ -108,6 +109,7 @@ struct EnvKnobs {
   int frame_tiles_per_wg = 1;
   bool render_overlap = false, graph_memcpy_node = false;
   int upload_streams = 2;
+  bool fuse_view_grid = true;
 };
 static EnvKnobs read_env_knobs() {
   EnvKnobs k;
@@ -130,6 +132,7 @@ static EnvKnobs read_env_knobs() {
   k.render_overlap = flag("TSDF_RENDER_OVERLAP", false);
   k.graph_memcpy_node = flag("TSDF_GRAPH_MEMCPY_NODE", false);
   k.upload_streams = (int)num("TSDF_UPLOAD_STREAMS", 2);
+  k.fuse_view_grid = flag("TSDF_FUSE_VIEW_GRID", true);
   return k;
 }
 
@@ -1034,6 +1037,41 @@ int flush_pending(tsdf_engine* e) {
   return launch_frame(e, C, none, none, nullptr);
 }
 
+// The pending unpipelined update (ps == kPipeU) with the view grid of render camera R built in the same
+// launch (k_integrate_vg; raycast_impl's deferred C5 path). Events as flush_pending + frame_update.
+int update_with_grid(tsdf_engine* e, const FrameParams& R, const ViewGrid& V) {
+  hipStream_t s = e->stream;
+  std::array<hipEvent_t, 5>* ev = nullptr;
+  if (e->p_sampled && e->profiling) {
+    int rc = take_events(e, &ev);
+    if (rc) return rc;
+    if (e->prof_mode == TSDF_PROFILE_PHASES) HIP_OK(hipEventRecord((*ev)[0], s));
+  }
+  e->p_sampled = false;
+  e->ps = tsdf_engine::kPipeNone;
+  const EngineDev Dv = frame_view(e->D, e->p_fid);
+  FrameParams P = e->p_P;
+  P.tail = kTailResolve;
+  P.slot = nullptr;
+  P.slot_cap = 0;
+  const uint32_t vtag = 0x80000000u | (uint32_t)(e->vg_calls & 0x7FFFFFFFu);  // (never a frame id)
+  const int nint = e->D.integrate_grid;
+  const dim3 grid(nint + kOccWords / 256);
+  const bool all_ev = ev && e->prof_mode == TSDF_PROFILE_PHASES;
+  if (all_ev) HIP_OK(hipEventRecord((*ev)[1], s));
+  if (ev && e->prof_mode == TSDF_PROFILE_KERNEL) {
+    hipExtLaunchKernelGGL(k_integrate_vg, grid, dim3(kIntegrateThreads), 0, s, (*ev)[2], (*ev)[3], 0, Dv, P, R, V,
+                          vtag, nint);
+  } else {
+    if (ev) HIP_OK(hipEventRecord((*ev)[2], s));
+    hipLaunchKernelGGL(k_integrate_vg, grid, dim3(kIntegrateThreads), 0, s, Dv, P, R, V, vtag, nint);
+    if (ev) HIP_OK(hipEventRecord((*ev)[3], s));
+  }
+  LAUNCH_OK("k_integrate_vg");
+  if (all_ev) HIP_OK(hipEventRecord((*ev)[4], s));
+  return TSDF_OK;
+}
+
 }  // namespace
 
 // One frame (TSDFGrid::Integrate). Pipelined (one volume, <= 3 DDA samples per pixel):
@@ -1890,7 +1928,6 @@ int raycast_impl(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const t
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  ENTER(e);
   FrameParams P = make_params(e, K, W, H, pose, max_depth);
   P.row0 = row0;
   P.nrows = nrows;
@@ -1898,11 +1935,31 @@ int raycast_impl(tsdf_engine* e, const tsdf_intrinsics* K, int W, int H, const t
   uchar4* o2 = mem_kind == TSDF_MEM_DEVICE ? reinterpret_cast<uchar4*>(normal) : (normal ? e->rc_norm : nullptr);
   const float step = e->cfg.truncation / 2;
   ViewGrid V;
-  int rc = view_grid_for(e, P, step, kViewBitmapWords, &V);
-  if (rc) return rc;
+  int rc;
+  // The C5 loop (a deferred raycast while the frame's unpipelined update is still pending): that
+  // update's launch builds the view grid too (k_integrate_vg), one launch and boundary fewer
+  bool fused = false;
+  if (deferred && mem_kind == TSDF_MEM_DEVICE && e->ps == tsdf_engine::kPipeU && !sharded(e) &&
+      e->p_P.pack_pixels && e->env.fuse_view_grid) {
+    JOIN_RENDER(e);  // (a deferred raycast still pending reads the previous grid)
+    rc = view_grid_for(e, P, step, kViewGraphBitmapWords, &V);
+    if (rc) return rc;
+    if (V.n) {
+      rc = update_with_grid(e, P, V);
+      if (rc) return rc;
+      fused = true;
+    }
+  }
+  if (!fused) {
+    ENTER(e);
+    rc = view_grid_for(e, P, step, kViewBitmapWords, &V);
+    if (rc) return rc;
+    if (V.n) {
+      hipLaunchKernelGGL(k_view_grid, dim3(kOccWords / 256), dim3(256), 0, e->stream, e->D, P, V);
+      LAUNCH_OK("k_view_grid");
+    }
+  }
   if (V.n) {
-    hipLaunchKernelGGL(k_view_grid, dim3(kOccWords / 256), dim3(256), 0, e->stream, e->D, P, V);
-    LAUNCH_OK("k_view_grid");
     hipLaunchKernelGGL(k_view_pack, dim3(kViewPackGrid), dim3(256), 0, e->stream, V);
     LAUNCH_OK("k_view_pack");
   }

@@ -112,14 +112,48 @@ __global__ __launch_bounds__(256) void k_shard_abort(EngineDev D) {
 // space carving of the candidates (voxel_tsdf.cu:483-488, kTailResolve) or, in a shard's frame,
 // the packing of its candidates for the exchange (kTailPack; k_resolve_delete follows it).
 // The statistics (their loads) come after the carving, off its path.
-__device__ __forceinline__ void integrate_tail(const EngineDev& D, const FrameParams& P, DeleteLds& L) {
+// The C5 loop's raycast view grid built inside the update launch (k_integrate_vg): the render camera,
+// its grid and the launch's release tag (the carving tags the pool blocks it releases with it)
+struct ViewFuse {
+  FrameParams R;
+  ViewGrid V;
+  uint32_t vtag;
+};
+// the grid's cells of the blocks this launch's carving released read as missing again: the grid
+// workgroups listed them before the carving (their cells are written through and drained before they
+// arrive, so these stores, after every arrival, are the cells' last writes)
+__device__ __forceinline__ void view_patch_carved(const EngineDev& D, const ViewFuse& F) {
+  __builtin_amdgcn_s_waitcnt(0);  // (the carving's rtag stores of every wave)
+  __syncthreads();
+  const ViewGrid& V = F.V;
+  const int n = min(ld_co(D.ncand), D.cand_cap);
+  const int ox = view_origin(F.R.wt.x, F.R.voxel, V.half), oy = view_origin(F.R.wt.y, F.R.voxel, V.half),
+            oz = view_origin(F.R.wt.z, F.R.voxel, V.half);
+  const unsigned long long* rq = reinterpret_cast<const unsigned long long*>(D.cand);
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const unsigned long long a = ld_co(&rq[2 * k]), b = ld_co(&rq[2 * k + 1]);
+    const int lx = (int16_t)(a & 0xFFFF) - ox, ly = (int16_t)((a >> 16) & 0xFFFF) - oy,
+              lz = (int16_t)((a >> 32) & 0xFFFF) - oz;
+    const int32_t idx = (int32_t)(uint32_t)b;
+    if ((unsigned)lx >= (unsigned)V.n || (unsigned)ly >= (unsigned)V.n || (unsigned)lz >= (unsigned)V.n || idx < 0)
+      continue;
+    if (__hip_atomic_load(&D.rtag[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != F.vtag) continue;
+    const int kb = ((lz >> 2) * V.nb + (ly >> 2)) * V.nb + (lx >> 2);
+    __hip_atomic_store(&V.cell[view_cell(kb, lx, ly, lz)], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+__device__ __forceinline__ void integrate_tail(const EngineDev& D, const FrameParams& P, DeleteLds& L,
+                                               const ViewFuse* F = nullptr) {
   const int t = threadIdx.x;
   const unsigned long long tend = __builtin_amdgcn_s_memrealtime();  // the update's span ends here
   TSDF_STAMP(D, 7, 0);
   if (P.tail == kTailPack)
     pack_cands_wg(D, D.cand, D.ncand, P.slot, P.slot_cap);
   else
-    resolve_delete_wg(D, D.cand, D.ncand, 0, L);
+    resolve_delete_wg(D, D.cand, D.ncand, 0, L, F ? F->vtag : 0u);
+#ifndef TSDF_NO_VIEW_PATCH  // (a test build leaves the released blocks' cells: the C5 tests must fail)
+  if (F) view_patch_carved(D, *F);
+#endif
   TSDF_STAMP(D, 7, 1);
   lds_barrier();  // (L.scan is reused below)
   const int bc = t < kBands ? D.band[t * kBandStride] : 0;
@@ -362,7 +396,8 @@ __device__ __forceinline__ size_t band_find(const EngineDev& D, int bst, int lan
 // returns true in the workgroup that arrived last (and ran the carving tail)
 template <bool Graph, bool Raw>
 __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FrameParams& Pv,
-                                               const FrameArgs* __restrict__ A, int nint, DeleteLds& L) {
+                                               const FrameArgs* __restrict__ A, int nint, DeleteLds& L,
+                                               int narrive = 0, const ViewFuse* F = nullptr) {
   FrameParams P = Graph ? A->P : Pv;
   if (Graph && A->cands_out) {  // a shard's graph frame: the tail packs the carve candidates
     P.tail = kTailPack;
@@ -470,8 +505,9 @@ __device__ __forceinline__ bool integrate_body(const EngineDev& D, const FramePa
   // waves that published drain their stores before the workgroup arrives (wave 0: the buffer;
   // the even waves' lane 0: overflow records)
   const bool drain = (wave == 0 && nc > 0) || (s_ovf && (wave & 1) == 0);
-  if (!arrive_last(D.arrive + kArrIntegrate, wg_upd, &s_last, drain, (uint32_t)nint)) return false;
-  integrate_tail(D, P, L);
+  if (!arrive_last(D.arrive + kArrIntegrate, wg_upd, &s_last, drain, (uint32_t)(narrive ? narrive : nint)))
+    return false;
+  integrate_tail(D, P, L, F);
   return true;
 }
 
@@ -481,6 +517,46 @@ __attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES)))
     EngineDev D, FrameParams Pv, const FrameArgs* __restrict__ A) {
   __shared__ DeleteLds L;  // the last-arriving workgroup's carving resolve
   integrate_body<Graph, Raw>(D, Pv, A, (int)gridDim.x, L);
+}
+
+// k_integrate with the C5 loop's view grid (tsdf_raycast_deferred after an unpipelined update):
+// workgroups [0, nint) update, the rest build the render camera's view grid from the table as the
+// update leaves it (nothing in the launch but the carving changes the table) -- its cells written
+// through (sc1) -- and the carving's last arriver clears the cells of the blocks it released. The
+// k_view_grid launch and its kernel boundary drop out of the frame.
+__global__ __launch_bounds__(kIntegrateThreads)
+__attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES))) void k_integrate_vg(
+    EngineDev D, FrameParams Pv, FrameParams R, ViewGrid V, uint32_t vtag, int nint) {
+  __shared__ DeleteLds L;
+  const ViewFuse F{R, V, vtag};
+  const int narr = (int)gridDim.x;
+  if ((int)blockIdx.x < nint) {
+    integrate_body<false, false>(D, Pv, nullptr, nint, L, narr, &F);
+    return;
+  }
+  const int w = ((int)blockIdx.x - nint) * 256 + (int)threadIdx.x;  // (one occupancy word per thread)
+  if (V.n && threadIdx.x < 256) {
+    const int ox = view_origin(R.wt.x, R.voxel, V.half), oy = view_origin(R.wt.y, R.voxel, V.half),
+              oz = view_origin(R.wt.z, R.voxel, V.half);
+    unsigned long long occ = D.occ[w];
+    while (occ) {
+      const int b = __ffsll((long long)occ) - 1;
+      occ &= occ - 1;
+      const Ent en = load_ent(D.table, (uint32_t)(w * 64 + b));
+      const int lx = en.x - ox, ly = en.y - oy, lz = en.z - oz;
+      if ((unsigned)lx >= (unsigned)V.n || (unsigned)ly >= (unsigned)V.n || (unsigned)lz >= (unsigned)V.n ||
+          !local_idx(en.idx))
+        continue;
+      const int k = ((lz >> 2) * V.nb + (ly >> 2)) * V.nb + (lx >> 2);
+      __hip_atomic_store(&V.cell[view_cell(k, lx, ly, lz)], (V.gen << kViewIdxBits) | (uint32_t)en.idx,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      V.flags[k] = 1;
+      V.flags[V.nbw * 32 + ((lz >> 4) * V.ns + (ly >> 4)) * V.ns + (lx >> 4)] = 1;
+    }
+  }
+  __shared__ int s_last;
+  if (!arrive_last(D.arrive + kArrIntegrate, 0ull, &s_last, true, (uint32_t)narr)) return;
+  integrate_tail(D, Pv, L, &F);
 }
 
 // =============================================================================================

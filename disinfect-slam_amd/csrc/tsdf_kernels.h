@@ -265,6 +265,8 @@ __global__ void k_render_ingest(EngineDev D, FrameParams R, float step_size, Vie
                                 const uint8_t* rgb, const float* ht, const float* lt, int tiles_x, int tiles);
 // (graph form: A->prev's raycast, none when null, beside A's ingest)
 __global__ void k_render_ingest_g(EngineDev D, const FrameArgs* A, int rgx, int nray);
+// k_integrate plus the render camera's view grid (the C5 loop's deferred raycast; tsdf_fuse.hip)
+__global__ void k_integrate_vg(EngineDev D, FrameParams Pv, FrameParams R, ViewGrid V, uint32_t vtag, int nint);
 // view grid of a raycast: grid kOccWords / 256 workgroups of 256
 __global__ void k_view_grid(EngineDev D, FrameParams P, ViewGrid V);
 __global__ void k_view_grid_g(EngineDev D, const FrameArgs* A);

@@ -243,3 +243,49 @@ def test_c5_deferred_graph_equals_graph():
     finally:
         ga.close(), gb.close()
         a.close(), b.close()
+
+
+def test_deferred_raycast_heavy_carving():
+    """The C5 loop's view grid built inside the update launch (k_integrate_vg) before that launch's
+    carving, which then clears the cells of the blocks it released: 2 cm voxels at 96x72 carve many
+    blocks per frame; the deferred images equal the immediate raycast's frame by frame (also with
+    TSDF_FUSE_VIEW_GRID's separate launch as the reference, the immediate path)."""
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H, n = 96, 72, 16
+    cam = synth.camera(W, H)
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    a = tsdf_amd.Engine(0.02, 0.08, max_width=W, max_height=H, num_block_bits=13)
+    b = tsdf_amd.Engine(0.02, 0.08, max_width=W, max_height=H, num_block_bits=13)
+    try:
+        ref = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(2)]
+        out = [[torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(2)] for _ in range(2)]
+        pending = None
+        deleted = 0
+        for i in range(n):
+            fr = synth.render(cam, i)
+            pose = tsdf_amd.SE3(fr["q"], fr["t"])
+            dev = {k: torch.from_numpy(fr[k]).to("cuda") for k in ("rgb", "depth", "ht", "lt")}
+            a.integrate(dev["rgb"], dev["depth"], dev["ht"], dev["lt"], cam.K, pose, 4.0)
+            b.integrate(dev["rgb"], dev["depth"], dev["ht"], dev["lt"], cam.K, pose, 4.0)
+            if pending is not None:
+                j, o, r0, r1 = pending
+                torch.cuda.synchronize()
+                assert torch.equal(o[0], r0) and torch.equal(o[1], r1), f"frame {j}"
+            a.raycast(K, W, H, pose, 4.0, rgba=ref[0], normal=ref[1])
+            deleted += a.stats()["last_num_deleted"]
+            o = out[i % 2]
+            b.raycast(K, W, H, pose, 4.0, rgba=o[0], normal=o[1], deferred=True)
+            pending = (i, o, ref[0].clone(), ref[1].clone())
+        b.flush()
+        torch.cuda.synchronize()
+        j, o, r0, r1 = pending
+        assert torch.equal(o[0], r0) and torch.equal(o[1], r1), "last frame"
+        assert deleted > 20, deleted  # (the carving ran inside the fused launches)
+        assert (r0[..., 3] == 255).float().mean().item() > 0.3
+        sa, sb = a.stats(), b.stats()
+        assert sa["status"] == 0 and sb["status"] == 0 and sa["total_deleted"] == sb["total_deleted"]
+    finally:
+        a.close(), b.close()
