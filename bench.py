@@ -504,7 +504,9 @@ def main():
             parallelism += ", one hipGraph launch per frame"
         pf = pipe_fraction(prof)
         roof = {
-            "kernel": "k_integrate" if pf == 0 else
+            "kernel": ("k_integrate_vg (k_integrate + the deferred raycast's view grid)"
+                       if a.loop == "c5" and not a.graph and not a.no_defer and world == 1 else "k_integrate")
+                      if pf == 0 else
                       "k_frame (one launch per frame: frame b-1's carving then frame b's allocation in "
                       "workgroup 0, frame b's update beside them, frame b+1's pixel records, DDA, key "
                       "dedupe, probe / insert and visibility sweep)",

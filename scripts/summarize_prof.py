@@ -109,7 +109,7 @@ def main(out):
     if b0:
         res["bench"] = b0
     # the frame launch of the line: k_frame for pipelined frames, else k_integrate
-    kn = next((k for k in ("k_frame", "k_frame_g", "k_integrate", "k_integrate_graph") if k in res["pmc"]), None)
+    kn = next((k for k in ("k_frame", "k_frame_g", "k_integrate_vg", "k_integrate", "k_integrate_graph") if k in res["pmc"]), None)
     ki = res["pmc"].get(kn, {}) if kn else {}
     if "FETCH_SIZE" in ki and "WRITE_SIZE" in ki:
         bf, bw = pmc_lines["FETCH_SIZE"], pmc_lines["WRITE_SIZE"]
