@@ -206,17 +206,24 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
   const unsigned long long d_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
   // The lanes of a wave step together (a tight per-lane loop through empty regions measured slower:
-  // the lanes' dependent loads then no longer overlap in time).
-  int i = 1;
+  // the lanes' dependent loads then no longer overlap in time), over a scalar step counter: a lane
+  // that has hit (or never marches) is frozen in an endless empty region -- no lookups, no reads, no
+  // state that matters -- so the loop needs no per-lane exit masks (their exec bookkeeping was ~2/3
+  // of the march's scalar instructions) and ends when no lane of the wave is live.
   auto in_region = [&](const f3& q) -> bool {
     return fmaxf(fmaxf(fmaf(q.x, sgn.x, ne.x), fmaf(q.y, sgn.y, ne.y)), fmaf(q.z, sgn.z, ne.z)) < 0.0f;
   };
-  while (active) {
+  // (the lane's state as an integer in a VGPR: a bool would live as an exec-style mask whose merges
+  // after every branch cost scalar instructions)
+  int live = active ? 1 : 0;
+  if (!active) ne = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+  for (int i = 1; i < max_step; ++i) {
+    if (__builtin_amdgcn_ballot_w64(live != 0) == 0ull) break;
     const bool inside = in_region(pos);
 #ifdef TSDF_DIAG_STAMPS
-    d_it += 1;
-    d_blk += !inside;
-    d_ld += ridx >= 0;
+    d_it += live != 0;
+    d_blk += live != 0 && !inside;
+    d_ld += live != 0 && ridx >= 0;
 #endif
     // a lane inside an empty region reads +1 and needs nothing else this step (no rounding either:
     // when every lane of the wave is there, the wave skips the block below)
@@ -243,15 +250,16 @@ __device__ __forceinline__ void raycast(const EngineDev& D, const FrameParams& P
         cur = reinterpret_cast<const float*>(D.pool + (size_t)ridx * kBlockBytes)[voxel_off(px, py, pz)];
         if (prev > 0 && cur <= 0 && (double)(prev - cur) <= 1.5) {
           hit_pos = pos;  // shaded after the march (below)
-          hit = true;
+          live = 0;  // frozen: an endless empty region from here on
+          ne = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+          ridx = -1;
         }
       }
     }
     prev = cur;
     pos = {pos.x + sg.x, pos.y + sg.y, pos.z + sg.z};
-    ++i;
-    active = !hit && i < max_step;
   }
+  hit = active && live == 0;
   // The hits are shaded together after the march: inside it, the lanes of a wave hit at different
   // steps, and each step with a hit ran the whole shading (binary search + 7 lookups) for a few lanes.
   // The shading reads only the static volume (the block cache is a memo), so where it runs changes
