@@ -16,7 +16,7 @@
 #   shard8            bench.py --width 1280 --height 720 --shard 8 (single-GPU 8-shard rehearsal)
 #   sq:<kernel>       SQ counter passes of one kernel on the default command (profile_kernel_sq.sh)
 #   c5trace|c5gtrace  kernel trace (eager / graph) of the C5 loop -> per-frame kernel chain and gaps (scripts/chain_timeline.py)
-#   raysq             SQ / FETCH / WRITE passes of k_raycast on the C5 loop -> <tag>/r4_raycast_sq.json
+#   raysq             SQ / FETCH / WRITE passes of k_raycast on the C5 loop -> <tag>/r5_raycast_sq.json
 #   raydiag           raycast step statistics and wave lifetimes (diagnostic library, scripts/diag_raycast.py)
 #   framediag[:A=1,B=2]  k_frame per-part timeline (diagnostic library, scripts/diag_frame.py), optional env
 #   abargs:<a1>,<a2>  interleaved A/B of bench arguments (scripts/ab.sh args; spaces as '+', e.g. --loop+c5)
@@ -78,8 +78,8 @@ for st in "$@"; do
            timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$st -o run -- python3 bench.py --no-cpu --loop c5 --steps 120 $g > $OUT/$st.log 2>&1 || fail $st $OUT/$st.log
            python3 scripts/chain_timeline.py $OUT/$st > $OUT/${st}_chain.txt && tail -30 $OUT/${st}_chain.txt ;;
     raysq) bash scripts/profile_kernel_sq.sh $OUT/sq_ray k_raycast --loop c5 --steps 30 > $OUT/sq_ray.txt 2>&1 || fail $st $OUT/sq_ray.txt
-           python3 scripts/sq_json.py $OUT/sq_ray k_raycast "python3 bench.py --no-cpu --loop c5 --steps 30" 640 480 > $OUT/r4_raycast_sq.json
-           grep -E "VALU_per_wave|SALU_per_wave" $OUT/r4_raycast_sq.json ;;
+           python3 scripts/sq_json.py $OUT/sq_ray k_raycast "python3 bench.py --no-cpu --loop c5 --steps 30" 640 480 > $OUT/r5_raycast_sq.json
+           grep -E "VALU_per_wave|SALU_per_wave" $OUT/r5_raycast_sq.json ;;
     sq:*) k=${st#sq:}; bash scripts/profile_kernel_sq.sh $OUT/sq_$k $k > $OUT/sq_$k.txt 2>&1 || fail $st $OUT/sq_$k.txt
            tail -8 $OUT/sq_$k.txt ;;
     raydiag) TSDF_AMD_LIB=disinfect-slam_amd/libdisinfect_tsdf_diag.so timeout -k 10 180 python3 scripts/diag_raycast.py > $OUT/raycast_diag.txt 2>&1 || fail $st $OUT/raycast_diag.txt
