@@ -59,7 +59,8 @@ def _functions(asm):
 
 def test_arrivals_follow_a_drained_barrier():
     funcs = _functions(_disassemble())
-    frame = {n: body for n, body in funcs.items() if "k_ingest_dda" in n or "k_integrate_t" in n}
+    frame = {n: body for n, body in funcs.items()
+             if "k_ingest_dda" in n or "k_integrate_t" in n or "k_integrate_vg" in n}
     assert len(frame) >= 8, sorted(funcs)[:20]
     checked = 0
     for name, body in frame.items():
@@ -86,6 +87,10 @@ def test_publication_is_agent_scope():
     assert any(i.startswith("global_store_dwordx2") and "sc1" in i for i in ing)   # nk_list entries
     assert any(i.startswith("global_load_dwordx2") and "sc1" in i for i in ing)    # resolver prologue
     assert any(i.startswith("global_store_dwordx2") and "sc1" in i for i in integ)  # candidate records
+    # k_integrate_vg: the view-grid cells its grid workgroups write are written through (the carving's
+    # last arriver clears some of them after every arrival: its stores must be the cells' last writes)
+    vg = next(b for n, b in funcs.items() if n.startswith("_ZN4tsdf14k_integrate_vg"))
+    assert any(i.startswith("global_store_dword ") and "sc1" in i for i in vg)
 
 
 def _kframe():
@@ -187,8 +192,8 @@ def test_update_loops_keep_their_state_in_registers():
     funcs = _functions(_disassemble())
     seen = set()
     for name, body in funcs.items():
-        kern = next((k for k in ("_ZN4tsdf7k_frame", "_ZN4tsdf9k_frame_g", "_ZN4tsdf13k_integrate_t")
-                     if name.startswith(k)), None)
+        kern = next((k for k in ("_ZN4tsdf7k_frame", "_ZN4tsdf9k_frame_g", "_ZN4tsdf13k_integrate_t",
+                                 "_ZN4tsdf14k_integrate_vg") if name.startswith(k)), None)
         if kern:
             for j, i in _loops(body):
                 ops = [x.split()[0] for x in body[j:i + 1]]
@@ -197,7 +202,8 @@ def test_update_loops_keep_their_state_in_registers():
                     assert not any(o.startswith("scratch_") for o in ops), (name, j, i)
         if name.startswith("_ZN4tsdf9k_raycast"):
             assert not any(x.startswith("scratch_") for x in body), name
-    assert seen == {"_ZN4tsdf7k_frame", "_ZN4tsdf9k_frame_g", "_ZN4tsdf13k_integrate_t"}, seen
+    assert seen == {"_ZN4tsdf7k_frame", "_ZN4tsdf9k_frame_g", "_ZN4tsdf13k_integrate_t",
+                    "_ZN4tsdf14k_integrate_vg"}, seen
 
 
 def test_frame_kernels_make_no_calls():
@@ -207,7 +213,8 @@ def test_frame_kernels_make_no_calls():
     and the k_frame update ran from scratch)."""
     funcs = _functions(_disassemble())
     kernels = [n for n in funcs if n.startswith(("_ZN4tsdf7k_frame", "_ZN4tsdf9k_frame_g", "_ZN4tsdf13k_integrate_t",
-                                                 "_ZN4tsdf12k_ingest_dda", "_ZN4tsdf9k_raycast"))]
+                                                 "_ZN4tsdf14k_integrate_vg", "_ZN4tsdf12k_ingest_dda",
+                                                 "_ZN4tsdf9k_raycast"))]
     assert kernels
     for name in kernels:
         assert not any(x.startswith("s_swappc") for x in funcs[name]), name
