@@ -621,26 +621,10 @@ def host_frames(a, fr, reps=20):
         e1.record(st)
         st.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
-    # the same copies split over two streams (the engine's default upload split): even keys on one,
-    # odd keys on the other, each stream's reps back to back
-    st2 = torch.cuda.Stream()
-    e2, e3, e4 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-    e2.record(st)
-    st2.wait_event(e2)
-    for j, stream in enumerate((st, st2)):
-        with torch.cuda.stream(stream):
-            for _ in range(reps):
-                for k in keys[j::2]:
-                    dst[k].copy_(src[k], non_blocking=True)
-    e4.record(st2)
-    st.wait_event(e4)
-    e3.record(st)
-    st.synchronize()
-    us2 = e2.elapsed_time(e3) * 1e3 / reps
     return out, {"kind": a.host_frames, "bytes_per_frame": int(nbytes), "h2d_us_per_frame": round(us, 2),
-                 "h2d_gbs": round(nbytes / (us * 1e-6) / 1e9, 2), "h2d_us_per_frame_2streams": round(us2, 2),
-                 "note": "upload alone: 4 host-to-device copies of one frame on a side stream (and alternating "
-                         f"over two streams), events, {reps} reps; the line's value includes the engine's own "
+                 "h2d_gbs": round(nbytes / (us * 1e-6) / 1e9, 2),
+                 "note": "upload alone: 4 host-to-device copies of one frame on a side stream, events, "
+                         f"{reps} reps; the line's value includes the engine's own "
                          "uploads (copies over two upload streams, overlapped with the previous frames' kernels; "
                          "each call returns once its frame's copies are complete)"}
 
