@@ -92,7 +92,8 @@ hipError_t dmalloc(T** p, size_t count) {
 //   TSDF_PIPELINE=0               unpipelined frames: two launches per frame (k_ingest_dda, k_integrate)
 //   TSDF_PIPE_MAX_PIXELS=n        largest frame (pixels) that is pipelined (default 2^19; C4 above it)
 //   TSDF_FRAME_ORDER=0..4         k_frame grid order of its parts (PipeArgs.order; default 2)
-//   TSDF_FRAME_WG_PER_CU=n        k_frame update workgroups per CU (default kFrameWgPerCu = 3)
+//   TSDF_FRAME_WG_PER_CU=n        k_frame update workgroups per CU (default kFrameUpdWgsPer2Cu / 2 = 2.5)
+//   TSDF_FRAME_UPD_WGS=n          (A/B) k_frame update workgroups in total (overrides the per-CU count)
 //   TSDF_FRAME_TILES_PER_WG=n     (A/B) k_frame pixel tiles per tile workgroup (default 1)
 //   TSDF_INTEGRATE_WG_PER_CU=n    cap on k_integrate's resident workgroups per CU
 //   TSDF_CAND_CAP=n               (tests) smaller carve-candidate list, to exercise its overflow
@@ -106,7 +107,7 @@ struct EnvKnobs {
   bool pipeline = true;
   int64_t pipe_max_pixels = -1;
   int frame_order = -1, frame_wg_per_cu = 0, integrate_wg_per_cu = 0, cand_cap = 0, mesh_grid = 0;
-  int frame_tiles_per_wg = 1;
+  int frame_tiles_per_wg = 1, frame_upd_wgs = 0;
   bool render_overlap = false, graph_memcpy_node = false;
   int upload_streams = 2;
   bool fuse_view_grid = true;
@@ -126,6 +127,7 @@ static EnvKnobs read_env_knobs() {
   k.frame_order = (int)std::max(-1ll, num("TSDF_FRAME_ORDER", -1));
   k.frame_wg_per_cu = (int)num("TSDF_FRAME_WG_PER_CU", 0);
   k.frame_tiles_per_wg = (int)std::max(1ll, num("TSDF_FRAME_TILES_PER_WG", 1));
+  k.frame_upd_wgs = (int)num("TSDF_FRAME_UPD_WGS", 0);
   k.integrate_wg_per_cu = (int)num("TSDF_INTEGRATE_WG_PER_CU", 0);
   k.cand_cap = (int)num("TSDF_CAND_CAP", 0);
   k.mesh_grid = (int)num("TSDF_MESH_GRID", 0);
@@ -631,13 +633,15 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_pre, reinterpret_cast<const void*>(k_frame),
                                                      kIntegrateThreads, 0) != hipSuccess)
       return fail(TSDF_ERR_HIP);
-    // 3 update workgroups per CU by default (of 7 that fit): the other slots take the sweep's and the
-    // tiles' workgroups from the start (driver command, same box: 22.3-22.5k frames/s at 3, 22.0-22.1k
-    // at 4, 21.0-21.3k at 5, 18.5-18.7k at 7, 17.9-18.1k at 2; 300 frames: 24.0k at 3 and at 5)
-    int want = kFrameWgPerCu;
-    if (e->env.frame_wg_per_cu > 0) want = e->env.frame_wg_per_cu;
-    per_cu_pre = std::min(per_cu_pre, want);
-    D.integrate_grid_pre = std::max(8, std::min(kIntegrateGrid, (per_cu_pre * ncu) & ~7));
+    // 2.5 update workgroups per CU by default (of 7 that fit): the other slots take the sweep's and
+    // the tiles' workgroups from the start. Same box, interleaved (profiles/ab/r5_upd_wgs_*.txt): 640
+    // update workgroups 23.9k frames/s on the driver command and 25.2-25.3k over 300 frames, 768 (3 per
+    // CU, the round-3/4 default) 23.3-23.5k / 24.8-25.1k, 512 (2 per CU) 23.4-23.7k / 24.3-24.6k;
+    // earlier rounds: 4 per CU 22.0-22.5k, 5 21.0-21.3k, 7 18.5-18.7k, 1 15.4-15.7k
+    int upd = kFrameUpdWgsPer2Cu * ncu / 2;
+    if (e->env.frame_wg_per_cu > 0) upd = e->env.frame_wg_per_cu * ncu;
+    if (e->env.frame_upd_wgs > 0) upd = e->env.frame_upd_wgs;
+    D.integrate_grid_pre = std::max(8, std::min({kIntegrateGrid, upd, per_cu_pre * ncu}) & ~7);
   }
   ALLOC(D.pixA, 2 * e->max_pixels);  // two buffers: a pipelined frame's and the next one's
   e->pipeline = e->env.pipeline;
