@@ -271,7 +271,7 @@ class Run:
         self.eng.close()
 
 
-PIX_RECORD_BYTES = 16  # pixA {depth, range, log-odds, rgb}, written once per pixel
+PIX_RECORD_BYTES = 20  # pixA {depth, range, logf ht, logf lt} + pixC rgb, written once per pixel
 
 
 def pipe_fraction(prof):

@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256) void k_fresh_init(EngineDev D) {
     const int b = q >> 7, v = (q & 127) * 4;
     uint8_t* blk = D.pool + (size_t)D.fresh[b] * kBlockBytes;
     *reinterpret_cast<float4*>(blk + v * 4) = make_float4(-1.f, -1.f, -1.f, -1.f);
-    *reinterpret_cast<float4*>(blk + kProbOffset + v * 4) = make_float4(0.f, 0.f, 0.f, 0.f);  // p = 0.5
+    *reinterpret_cast<float4*>(blk + kProbOffset + v * 4) = make_float4(0.5f, 0.5f, 0.5f, 0.5f);  // p = 0.5
     // weight 0; the colour of a weight-0 voxel is defined as 0 (see k_integrate / the oracle)
     *reinterpret_cast<uint4*>(blk + kRgbwOffset + v * 4) = make_uint4(0u, 0u, 0u, 0u);
   }

@@ -6,18 +6,17 @@
 //              voxel_mem.cuh:73-93; NUM_BUCKET 2^21 x 2, voxel_hash.cuh:12-25).
 //   lock_tag : 2^21 u32 bucket locks, "locked" == current lock epoch (no per-launch reset pass;
 //              reference resets 8 MiB twice per frame, voxel_tsdf.cu:385,487).
-//   pool     : 2^bits voxel blocks x 6 KiB, block-major {f32 tsdf[512] | f32 logodds[512] |
+//   pool     : 2^bits voxel blocks x 6 KiB, block-major {f32 tsdf[512] | f32 prob[512] |
 //              u8x4 rgbw[512]} so one block's state is one contiguous 6 KiB run (reference: three
-//              SoA arrays of 2^27 voxels, voxel_mem.cu:13-27). The semantic state is kept as the
-//              base-2 log-odds L = log2(p / (1 - p)) of the reference's probability p
-//              (VoxelSEGM, voxel_types.cuh): its update is linear in L (see k_integrate), and
-//              every reader converts with prob_of_logodds (p = 0.5 <-> L = 0, p = 0 <-> L = -inf).
+//              SoA arrays of 2^27 voxels, voxel_mem.cu:13-27). prob is VoxelSEGM::probability
+//              (voxel_types.cuh:36-43) itself, updated with the reference's own float chain.
 //   occ      : 2^22-bit occupancy bitmap of the table (replaces the full 48 MiB table scans of
 //              check_visibility_kernel / check_valid_kernel with a 512 KiB bitmap sweep).
 //
 // Float math restates utils/cuda/{camera,lie_group}.cuh with Eigen 3.3's evaluation order; the
 // library is compiled with -ffp-contract=off and IEEE division / sqrt so results are bit-identical
-// to the CPU oracle (oracle/tsdf_oracle.c) for everything except expf/logf (probability only).
+// to the CPU oracle (oracle/tsdf_oracle.c), the semantic update's logf / expf included (sem_logf /
+// sem_expf below restate the oracle's fixed float algorithms, oracle/ora_math.c).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -36,7 +35,7 @@ constexpr uint32_t kNumEntry = kNumBucket * 2;
 constexpr uint32_t kEntryMask = kNumEntry - 1;
 constexpr uint32_t kOccWords = kNumEntry / 64;
 constexpr int kBlockBytes = kBlockVolume * 12;  // 6 KiB per voxel block
-constexpr int kProbOffset = kBlockVolume * 4;   // byte offsets inside a block record (log-odds)
+constexpr int kProbOffset = kBlockVolume * 4;   // byte offsets inside a block record (probability)
 constexpr int kRgbwOffset = kBlockVolume * 8;
 constexpr uint32_t kNewKeyCap = 1u << 17;       // unique new blocks per frame
 constexpr int kMaxDdaSamples = 6;               // DDA samples per pixel the ingest kernel supports
@@ -147,12 +146,6 @@ struct DevCounters {
 // ------------------------------------------------------------------------------------------
 // float math (bit-exact restatement; see header comment)
 // ------------------------------------------------------------------------------------------
-// VoxelSEGM::probability from the stored base-2 log-odds: 1 / (1 + 2^-L) on the raw v_exp /
-// v_rcp (~1 ulp each; exact at L = 0, 0 at L = -inf, 1 at large L)
-__device__ __forceinline__ float prob_of_logodds(float L) {
-  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-L));
-}
-
 __device__ __forceinline__ f3 cross3(f3 a, f3 b) {  // Eigen MatrixBase::cross
   f3 r;
   r.x = a.y * b.z - a.z * b.y;
@@ -302,6 +295,154 @@ __device__ __forceinline__ v2f div_pair(v2f a, v2f b, v2f y, bool act0, bool act
   if (__builtin_expect(act1 && !(fa1 >= 0x1p-40f && fa1 <= 0x1p40f && fb1 >= 0x1p-40f && fb1 <= 0x1p40f), 0))
     o.y = a.y / b.y;
   return o;
+}
+
+// div_pair that also takes a == 0 on its fast path (the Newton expansion gives the signed zero
+// exactly); the semantic update's numerators are 0 wherever w_old == 0 and ln ht == 0.
+__device__ __forceinline__ v2f div_pair0(v2f a, v2f b, v2f y, bool act0, bool act1) {
+  const v2f e = vfma(-b, y, v2(1.0f, 1.0f));
+  const v2f y1 = vfma(e, y, y);
+  const v2f q = a * y1;
+  const v2f r = vfma(-b, q, a);
+  const v2f q1 = vfma(r, y1, q);
+  const v2f r1 = vfma(-b, q1, a);
+  v2f o = vfma(r1, y1, q1);
+  const float fa0 = fabsf(a.x), fb0 = fabsf(b.x), fa1 = fabsf(a.y), fb1 = fabsf(b.y);
+  const bool ok0 = (fa0 == 0.0f || (fa0 >= 0x1p-40f && fa0 <= 0x1p40f)) && fb0 >= 0x1p-40f && fb0 <= 0x1p40f;
+  const bool ok1 = (fa1 == 0.0f || (fa1 >= 0x1p-40f && fa1 <= 0x1p40f)) && fb1 >= 0x1p-40f && fb1 <= 0x1p40f;
+  if (__builtin_expect(act0 && !ok0, 0)) o.x = a.x / b.x;
+  if (__builtin_expect(act1 && !ok1, 0)) o.y = a.y / b.y;
+  return o;
+}
+
+// ---- logf / expf of the semantic update (voxel_tsdf.cu:196-202). CUDA's own (libdevice, <= 1 /
+// 2 ulp) cannot be reproduced here, and the reference's float chain is ill-conditioned near p = 1
+// (one ulp of p there moves a later p by up to ~1e-2), so the oracle fixes both functions as
+// explicit single-precision algorithms (oracle/ora_math.c, < 0.87 / 0.99 ulp from the correctly
+// rounded values over every input) and these are the same operations -- frexp, rint, ldexp, fma and
+// + - * with one IEEE rounding each -- so they return the oracle's bits for all 2^32 inputs
+// (libtsdf_selfcheck digests, tests/test_gpu_numerics.py). Pairs run on packed v_pk_fma_f32.
+constexpr float kSemQ[9] = {0x1.555554p-2f,  -0x1.fffffcp-3f, 0x1.999d5ap-3f,  -0x1.555b4ap-3f, 0x1.23d21ap-3f,
+                            -0x1.fcf4c6p-4f, 0x1.dea282p-4f,  -0x1.d635bcp-4f, 0x1.1d8ea4p-4f};
+constexpr float kSemE[6] = {0x1p-1f, 0x1.555556p-3f, 0x1.5554eap-5f, 0x1.1110e0p-7f, 0x1.6d4316p-10f,
+                            0x1.a124e4p-13f};
+constexpr float kSemLn2Hi = 0x1.62e4p-1f;     // 16 significant bits: e * kSemLn2Hi is exact
+constexpr float kSemLn2Lo = 0x1.7f7d1cp-20f;
+constexpr float kSemInvLn2 = 0x1.715476p+0f;
+constexpr float kSemSqrtHalf = 0x1.6a09e6p-1f;
+
+// x = z 2^k with z in [sqrt(1/2), sqrt(2)) for positive finite x: the oracle's frexp + doubling, done
+// on the bits (a subnormal x is scaled by 2^24 first, k compensated) -- the same z and k, so the same
+// f = z - 1 (exact) and dk = k. Other inputs give garbage, replaced by the callers' special cases.
+__device__ __forceinline__ float sem_log_reduce(float x, float& dk) {
+  const bool sub = x < 0x1p-126f;
+  const uint32_t ix = __float_as_uint(sub ? x * 0x1p24f : x);
+  const int32_t k = (int32_t)(ix - 0x3f3504f3u) >> 23;  // 0x3f3504f3 = kSemSqrtHalf
+  dk = (float)(sub ? k - 24 : k);
+  return __uint_as_float(ix - ((uint32_t)k << 23)) - 1.0f;
+}
+// log1p(f) - f = f^3 Q(f) - f^2 / 2 and the result, on pairs (the oracle's operations)
+__device__ __forceinline__ v2f sem_log_core2(v2f f, v2f dk) {
+  v2f q = v2(kSemQ[8], kSemQ[8]);
+#pragma unroll
+  for (int i = 7; i >= 0; --i) q = vfma(q, f, v2(kSemQ[i], kSemQ[i]));
+  const v2f f2 = f * f;
+  const v2f hf2 = v2(0.5f, 0.5f) * f2;
+  const v2f t = vfma(f2 * f, q, -hf2);
+  return vfma(dk, v2(kSemLn2Hi, kSemLn2Hi), vfma(dk, v2(kSemLn2Lo, kSemLn2Lo), t) + f);
+}
+// logf of x in [0, 1] or NaN (the update's p and 1 - p): 0 -> -inf, NaN -> NaN
+__device__ __forceinline__ v2f sem_log_unit2(v2f x) {
+  float dk0, dk1;
+  const v2f f = v2(sem_log_reduce(x.x, dk0), sem_log_reduce(x.y, dk1));
+  const v2f y = sem_log_core2(f, v2(dk0, dk1));
+  const float ninf = -__builtin_inff();
+  return v2(x.x > 0.0f ? y.x : (x.x == 0.0f ? ninf : x.x), x.y > 0.0f ? y.y : (x.y == 0.0f ? ninf : x.y));
+}
+// logf of any float: -0 / 0 -> -inf, negative -> NaN, +inf -> +inf, NaN -> NaN
+__device__ __forceinline__ float sem_log_special(float x, float y) {
+  y = x == __builtin_inff() ? x : y;
+  return x > 0.0f ? y : (x == 0.0f ? -__builtin_inff() : __builtin_nanf(""));
+}
+__device__ __forceinline__ v2f sem_logf2(v2f x) {
+  float dk0, dk1;
+  const v2f f = v2(sem_log_reduce(x.x, dk0), sem_log_reduce(x.y, dk1));
+  const v2f y = sem_log_core2(f, v2(dk0, dk1));
+  return v2(sem_log_special(x.x, y.x), sem_log_special(x.y, y.y));
+}
+__device__ __forceinline__ float sem_logf(float x) { return sem_logf2(v2(x, x)).x; }
+// expf: the oracle's thresholds (x > 89 -> inf, x < -104 -> 0) are met by clamping x to
+// [-104.5, 89.5] and evaluating (e^89.5 overflows to inf, e^-104 and below round to 0 in ldexp), NaN
+// -> NaN
+__device__ __forceinline__ v2f sem_expf2(v2f x) {
+  const v2f xc = v2(__builtin_amdgcn_fmed3f(x.x, -104.5f, 89.5f), __builtin_amdgcn_fmed3f(x.y, -104.5f, 89.5f));
+  const v2f xk = xc * v2(kSemInvLn2, kSemInvLn2);
+  const v2f n = v2(__builtin_rintf(xk.x), __builtin_rintf(xk.y));
+  v2f r = vfma(-n, v2(kSemLn2Hi, kSemLn2Hi), xc);
+  r = vfma(-n, v2(kSemLn2Lo, kSemLn2Lo), r);
+  v2f p = v2(kSemE[5], kSemE[5]);
+#pragma unroll
+  for (int i = 4; i >= 0; --i) p = vfma(p, r, v2(kSemE[i], kSemE[i]));
+  const v2f s = vfma(r * r, p, r) + v2(1.0f, 1.0f);
+  const float y0 = __builtin_amdgcn_ldexpf(s.x, (int)n.x), y1 = __builtin_amdgcn_ldexpf(s.y, (int)n.y);
+  return v2(x.x != x.x ? x.x : y0, x.y != x.y ? x.y : y1);
+}
+__device__ __forceinline__ float sem_expf(float x) { return sem_expf2(v2(x, x)).x; }
+
+// ---- the semantic update's fast path (k_frame / k_integrate): the same operations without the
+// special-value handling, exact where every operand stays in range: p and 1 - p normal, the
+// numerators in {0} U [2^-40, 2^40] and wc in [2^-40, 2^40] (div_pair's exact range, zero added: the
+// expansion returns the signed zero), P in [2^-40, 2^40] and P + N <= 2^40. A voxel qualifies when its
+// pixel does (sem_pixel_fast: ht, lt in [2^-39, 1], so their logs lie in [-27.03, 0], and d <=
+// 0.9999 max_depth, so w_new >= 4e-4) and p lies in [2^-39, 1) (sem_voxel_fast). Then both numerators
+// are sums of two non-positive terms, each 0 or of magnitude >= 4e-4 * 5.96e-8 (the smallest |ln x| of
+// a float x < 1) > 2^-40, and at most 44 * 27.03; wc lies in [4e-4, 44]; the quotients in [-27.03, 0],
+// so P and N lie in [e^-27.03, 1] (> 2^-40) and P + N <= 2. Every other voxel is recomputed with
+// sem_update_exact.
+__device__ __forceinline__ bool sem_pixel_fast(float h, float l, float d, float max_depth) {
+  return h >= 0x1p-39f && h <= 1.0f && l >= 0x1p-39f && l <= 1.0f && d <= max_depth * 0.9999f;
+}
+__device__ __forceinline__ bool sem_voxel_fast(bool pixel_fast, float p) {
+  return pixel_fast && p >= 0x1p-39f && p < 1.0f;
+}
+__device__ __forceinline__ float sem_log_reduce_n(float x, float& dk) {  // x normal, positive
+  const uint32_t ix = __float_as_uint(x);
+  const int32_t k = (int32_t)(ix - 0x3f3504f3u) >> 23;
+  dk = (float)k;
+  return __uint_as_float(ix - ((uint32_t)k << 23)) - 1.0f;
+}
+__device__ __forceinline__ v2f sem_log_fast2(v2f x) {
+  float dk0, dk1;
+  const v2f f = v2(sem_log_reduce_n(x.x, dk0), sem_log_reduce_n(x.y, dk1));
+  return sem_log_core2(f, v2(dk0, dk1));
+}
+__device__ __forceinline__ v2f sem_exp_fast2(v2f x) {  // x in [-104, 89]
+  const v2f xk = x * v2(kSemInvLn2, kSemInvLn2);
+  const v2f n = v2(__builtin_rintf(xk.x), __builtin_rintf(xk.y));
+  v2f r = vfma(-n, v2(kSemLn2Hi, kSemLn2Hi), x);
+  r = vfma(-n, v2(kSemLn2Lo, kSemLn2Lo), r);
+  v2f p = v2(kSemE[5], kSemE[5]);
+#pragma unroll
+  for (int i = 4; i >= 0; --i) p = vfma(p, r, v2(kSemE[i], kSemE[i]));
+  const v2f s = vfma(r * r, p, r) + v2(1.0f, 1.0f);
+  return v2(__builtin_amdgcn_ldexpf(s.x, (int)n.x), __builtin_amdgcn_ldexpf(s.y, (int)n.y));
+}
+// div_pair's expansion in two parts: the refined reciprocal y1 of b (shared by every numerator over
+// the same b), then RN(a / b) for |a| in {0} U [2^-40, 2^40], |b| in [2^-40, 2^40]
+__device__ __forceinline__ v2f div_refine(v2f b, v2f y) { return vfma(vfma(-b, y, v2(1.0f, 1.0f)), y, y); }
+__device__ __forceinline__ v2f div_expand(v2f a, v2f b, v2f y1) {
+  const v2f q = a * y1;
+  const v2f r = vfma(-b, q, a);
+  const v2f q1 = vfma(r, y1, q);
+  const v2f r1 = vfma(-b, q1, a);
+  return vfma(r1, y1, q1);
+}
+// the whole update with every special case (IEEE divides, sem_logf / sem_expf)
+__device__ __forceinline__ float sem_update_exact(float p, float w_old, float w_new, float wc, float lnh,
+                                                  float lnl) {
+  const float sp = sem_expf((w_old * sem_logf(p) + w_new * lnh) / wc);
+  const float sn = sem_expf((w_old * sem_logf(1.0f - p) + w_new * lnl) / wc);
+  return sp / (sp + sn);
 }
 
 // min(roundf(w), 40) as an integer for 0 <= w < 2^23 (the weight update, voxel_tsdf.cu:188):
@@ -512,8 +653,6 @@ __device__ __forceinline__ f3 pixel_ray(const FrameParams& P, int x, int y) {
 __device__ __forceinline__ float pixel_w_new(const FrameParams& P, float d) {
   return (1.0f - quot_const(d, P.max_depth, P.inv_max_depth)) * 4.0f;
 }
-//   base-2 log-odds of the pixel's ht / lt; the hardware log2 (1 ulp) is far inside the 1e-4 prob
-//   tolerance and still gives exactly 0 when ht == lt
-__device__ __forceinline__ float pixel_logodds(float h, float l) { return __log2f(h) - __log2f(l); }
+//   logf(ht), logf(lt) (sem_logf)
 
 }  // namespace tsdf

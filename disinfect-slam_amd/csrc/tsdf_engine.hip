@@ -92,7 +92,7 @@ hipError_t dmalloc(T** p, size_t count) {
 //   TSDF_PIPELINE=0               unpipelined frames: two launches per frame (k_ingest_dda, k_integrate)
 //   TSDF_PIPE_MAX_PIXELS=n        largest frame (pixels) that is pipelined (default 2^19; C4 above it)
 //   TSDF_FRAME_ORDER=0..4         k_frame grid order of its parts (PipeArgs.order; default 2)
-//   TSDF_FRAME_WG_PER_CU=n        k_frame update workgroups per CU (default kFrameUpdWgsPer2Cu / 2 = 2.5)
+//   TSDF_FRAME_WG_PER_CU=n        k_frame update workgroups per CU (default kFrameUpdWgsPer2Cu / 2 = 3)
 //   TSDF_FRAME_UPD_WGS=n          (A/B) k_frame update workgroups in total (overrides the per-CU count)
 //   TSDF_FRAME_TILES_PER_WG=n     (A/B) k_frame pixel tiles per tile workgroup (default 1)
 //   TSDF_INTEGRATE_WG_PER_CU=n    cap on k_integrate's resident workgroups per CU
@@ -284,7 +284,7 @@ void free_all(tsdf_engine* e) {
                   D.table,   D.lock_tag, D.heap,     D.pool,    D.occ,
                   D.ctr,     D.nk_key,   D.nk_order, D.nk_list, D.pairs, D.fresh,
                   e->fe_rgb, e->fe_depth, e->fe_mask, e->fe_out_rgb, e->fe_out_depth,
-                  D.vis,     D.band,    D.cand,     D.arrive, D.swdirty, D.fresh_vis, D.pend, D.pixA,     D.visbits,    D.wgcnt, D.dbg,
+                  D.vis,     D.band,    D.cand,     D.arrive, D.swdirty, D.fresh_vis, D.pend, D.pixA, D.pixC,     D.visbits,    D.wgcnt, D.dbg,
                   e->s_rgb,  e->s_depth, e->s_ht,    e->s_lt,   e->rc_rgba,   e->rc_norm,
                   e->vg_cell, e->vg_flags, e->vg_bits, e->g_visbits, e->g_wgcnt, e->g_sel, e->g_count,
                   e->q_sel,  e->q_count, e->q_out, e->m_counts, e->m_offsets, e->m_total, e->m_nbr, e->m_out,   e->t_keys, e->t_recs,    e->t_count,
@@ -504,7 +504,7 @@ int32_t tsdf_num_entries(void) { return (int32_t)kNumEntry; }
 int32_t tsdf_num_blocks(const tsdf_engine* e) { return e ? e->D.nblocks : 0; }
 
 namespace {
-// empty volume: table, occupancy, free stack, log-odds pool, counters and key sets (tsdf_create,
+// empty volume: table, occupancy, free stack, voxel pool, counters and key sets (tsdf_create,
 // tsdf_reset); with_pool false leaves the voxel pool as it is (tsdf_import_blocks replace: every
 // block that becomes live is written by the import, free blocks are never read)
 bool init_state(tsdf_engine* e, bool with_pool = true) {
@@ -531,7 +531,7 @@ bool init_state(tsdf_engine* e, bool with_pool = true) {
   hipLaunchKernelGGL(k_init_table, dim3(kNumEntry / 256), dim3(256), 0, s, D.table);
   hipLaunchKernelGGL(k_init_heap, dim3((nb + 255) / 256), dim3(256), 0, s, D.heap, nb);
   if (with_pool)
-    hipLaunchKernelGGL(k_init_logodds, dim3((unsigned)(((size_t)nb * (kBlockVolume / 4) + 255) / 256)),
+    hipLaunchKernelGGL(k_init_prob, dim3((unsigned)(((size_t)nb * (kBlockVolume / 4) + 255) / 256)),
                        dim3(256), 0, s, D.pool, nb);
   ok &= hipGetLastError() == hipSuccess;
   ok &= hipStreamSynchronize(s) == hipSuccess;
@@ -633,17 +633,18 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_pre, reinterpret_cast<const void*>(k_frame),
                                                      kIntegrateThreads, 0) != hipSuccess)
       return fail(TSDF_ERR_HIP);
-    // 2.5 update workgroups per CU by default (of 7 that fit): the other slots take the sweep's and
-    // the tiles' workgroups from the start. Same box, interleaved (profiles/ab/r5_upd_wgs_*.txt): 640
-    // update workgroups 23.9k frames/s on the driver command and 25.2-25.3k over 300 frames, 768 (3 per
-    // CU, the round-3/4 default) 23.3-23.5k / 24.8-25.1k, 512 (2 per CU) 23.4-23.7k / 24.3-24.6k;
-    // earlier rounds: 4 per CU 22.0-22.5k, 5 21.0-21.3k, 7 18.5-18.7k, 1 15.4-15.7k
+    // 3 update workgroups per CU by default (of 6 that fit): the other slots take the sweep's and
+    // the tiles' workgroups from the start. Round 6 (the semantic update's exact chain, 6 waves per
+    // SIMD): 768 update workgroups 19.6k frames/s on the driver command, 640 18.7-19.4k, 896 19.2k,
+    // 1024 18.6k, 512 17.6k (profiles/ab/r6_*). Round 5 (log-odds state, 7 waves): 640 23.9k, 768
+    // 23.3-23.5k, 512 23.4-23.7k; earlier rounds: 4 per CU 22.0-22.5k, 5 21.0-21.3k, 7 18.5-18.7k
     int upd = kFrameUpdWgsPer2Cu * ncu / 2;
     if (e->env.frame_wg_per_cu > 0) upd = e->env.frame_wg_per_cu * ncu;
     if (e->env.frame_upd_wgs > 0) upd = e->env.frame_upd_wgs;
     D.integrate_grid_pre = std::max(8, std::min({kIntegrateGrid, upd, per_cu_pre * ncu}) & ~7);
   }
   ALLOC(D.pixA, 2 * e->max_pixels);  // two buffers: a pipelined frame's and the next one's
+  ALLOC(D.pixC, 2 * e->max_pixels);
   e->pipeline = e->env.pipeline;
   if (e->env.pipe_max_pixels >= 0) e->pipe_max_pixels = e->env.pipe_max_pixels;
   if (e->env.frame_order >= 0) e->frame_order = std::min(4, e->env.frame_order);

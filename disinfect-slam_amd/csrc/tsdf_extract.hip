@@ -21,13 +21,12 @@ __global__ void k_init_heap(int32_t* heap, int n) {  // voxel_mem.cu:6-11
 __global__ void k_copy_words(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, int n) {
   for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = __builtin_nontemporal_load(src + i);
 }
-// never-acquired blocks read like the reference's zeroed probability array: log-odds -inf (p 0)
-__global__ void k_init_logodds(uint8_t* pool, int nb) {
+// never-acquired blocks read like the reference's zeroed probability array (p 0)
+__global__ void k_init_prob(uint8_t* pool, int nb) {
   const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // one float4 per thread
   if (q >= (size_t)nb * (kBlockVolume / 4)) return;
-  const float ninf = -__builtin_inff();
   *reinterpret_cast<float4*>(pool + (q >> 7) * kBlockBytes + kProbOffset + (q & 127) * 16) =
-      make_float4(ninf, ninf, ninf, ninf);
+      make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -343,7 +342,7 @@ __global__ void k_hash_retrieve(EngineDev D, const int16_t* __restrict__ pts, in
   const uint8_t* blk = D.pool + (size_t)en.idx * kBlockBytes;
   rgbw[i] = reinterpret_cast<const uint32_t*>(blk + kRgbwOffset)[o];
   tsdf[i] = reinterpret_cast<const float*>(blk)[o];
-  prob[i] = prob_of_logodds(reinterpret_cast<const float*>(blk + kProbOffset)[o]);
+  prob[i] = reinterpret_cast<const float*>(blk + kProbOffset)[o];
   bpo[i] = make_short4(en.x, en.y, en.z, en.off);
   bidx[i] = en.idx;
 }
@@ -375,7 +374,7 @@ __global__ void k_pool_acquire(EngineDev D, int n, int32_t* out) {
     uint8_t* blk = D.pool + (size_t)idx * kBlockBytes;
     for (int v = 0; v < kBlockVolume; ++v) {
       reinterpret_cast<float*>(blk)[v] = -1.0f;
-      reinterpret_cast<float*>(blk + kProbOffset)[v] = 0.0f;  // p = 0.5
+      reinterpret_cast<float*>(blk + kProbOffset)[v] = 0.5f;  // p = 0.5
       reinterpret_cast<uint32_t*>(blk + kRgbwOffset)[v] = 0u;  // weight 0 (rgb defined as 0)
     }
     out[k] = idx;
@@ -411,7 +410,7 @@ __global__ void k_dump_pool(EngineDev D, float* tsdf, float* prob, uint32_t* rgb
   const size_t b = v >> kBlockVolumeBits, o = v & (kBlockVolume - 1);
   const uint8_t* blk = D.pool + b * kBlockBytes;
   tsdf[v] = reinterpret_cast<const float*>(blk)[o];
-  prob[v] = prob_of_logodds(reinterpret_cast<const float*>(blk + kProbOffset)[o]);
+  prob[v] = reinterpret_cast<const float*>(blk + kProbOffset)[o];
   rgbw[v] = reinterpret_cast<const uint32_t*>(blk + kRgbwOffset)[o];
 }
 

@@ -190,7 +190,7 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
   const bool fresh = r.pad != 0;
   if (fresh) {  // wave-uniform: a block created this frame loads nothing
     ts = make_float4(-1.f, -1.f, -1.f, -1.f);
-    pr = make_float4(0.f, 0.f, 0.f, 0.f);  // log-odds of AquireBlock's p = 0.5
+    pr = make_float4(0.5f, 0.5f, 0.5f, 0.5f);  // AquireBlock's p = 0.5
     // weight 0; AquireBlock leaves rgb as it was (voxel_mem.cu:43-51): uninitialised memory
     // or a previous block's colour, i.e. unspecified, visible only on weight-0 voxels. It is
     // defined as 0 here and in the oracle (a sharded volume's pool indices differ).
@@ -220,7 +220,7 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
   const float w_uvx = qw * uvx, qz_uvx = qz * uvx, qy_uvx = qy * uvx;
   v2f hzs[2];
   float4 px[4];
-  float lg[4];
+  uint32_t pc[4];   // rgb
   bool inb[4];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -248,41 +248,57 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
       const int j = 2 * k + e;
       inb[j] = uu[e] >= 0 && uu[e] < P.W && vv[e] >= 0 && vv[e] < P.H;
 #if defined(TSDF_EXP) && (TSDF_EXP & 1)  // experiment build: no pixel gathers
-      if (inb[j]) px[j] = make_float4(pcz[e] + 0.01f, 1.0f, 1.0f, __uint_as_float(0x00808080u));
+      if (inb[j]) px[j] = make_float4(pcz[e] + 0.01f, 1.0f, 0.0f, 0.0f), pc[j] = 0x00808080u;
 #else
       // unconditional gathers at a clamped index (pixel 0 when out of the image): no exec-
       // masked region around the loads, so all 8 stay in flight until pass 2
       const int img = inb[j] ? vv[e] * P.W + uu[e] : 0;
-      if (Raw) {  // x: depth, y: pixel x, z: pixel y, w: rgb (range / w_new computed in pass 2)
-        const uint32_t c = (uint32_t)P.rgb[3 * img] | ((uint32_t)P.rgb[3 * img + 1] << 8) |
-                           ((uint32_t)P.rgb[3 * img + 2] << 16);
-        px[j] = make_float4(P.depth[img], __int_as_float(uu[e]), __int_as_float(vv[e]), __uint_as_float(c));
-        lg[j] = P.ht ? pixel_logodds(P.ht[img], P.lt[img]) : 0.0f;
-      } else {  // x: depth, y: range, z: log-odds, w: rgb (w_new computed in pass 2)
+      if (Raw) {  // x: depth, y / z: ht / lt (their logs, range and w_new computed in pass 2)
+        pc[j] = (uint32_t)P.rgb[3 * img] | ((uint32_t)P.rgb[3 * img + 1] << 8) |
+                ((uint32_t)P.rgb[3 * img + 2] << 16);
+        px[j] = make_float4(P.depth[img], P.ht ? P.ht[img] : 1.0f, P.lt ? P.lt[img] : 1.0f,
+                            __int_as_float((uu[e] & 0xFFFF) | (vv[e] << 16)));  // w: the pixel (u, v)
+      } else {  // x: depth, y: range, z: logf(ht), w: logf(lt) (w_new computed in pass 2)
         px[j] = D.pixA[P.pix_off + img];
+        pc[j] = D.pixC[P.pix_off + img];
       }
 #endif
     }
   }
-  // ---- pass 2: tsdf_integrate_kernel's update (voxel_tsdf.cu:174-203), branch-free on
-  // packed pairs; each voxel's result is kept only where it is updated (the reference's
-  // conditions: in image, 0 < d <= max_depth, sdf > -trunc).
+  // ---- pass 2: tsdf_integrate_kernel's update (voxel_tsdf.cu:174-203) of tsdf, colour and weight,
+  // branch-free on packed pairs; each voxel's result is kept only where it is updated (the
+  // reference's conditions: in image, 0 < d <= max_depth, sdf > -trunc). The semantic update
+  // follows in pass 3, once the pixel records and the other state are dead (its chain of logs and
+  // exponentials beside them spilled the loop out of 72 VGPRs).
+  const uint32_t wold4 = (compu(cw, 0) >> 24) | ((compu(cw, 1) >> 24) << 8) | ((compu(cw, 2) >> 24) << 16) |
+                         ((compu(cw, 3) >> 24) << 24);  // the old weights, one byte per voxel
+  float wn[4] = {0.f, 0.f, 0.f, 0.f};
+  int pfast = 0;  // sem_pixel_fast per voxel
+  v2f lnh2[2], lnl2[2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int j0 = 2 * k, j1 = 2 * k + 1;
     const v2f d = v2(px[j0].x, px[j1].x);
-    v2f rng, w_new = v2(0.f, 0.f);
+    v2f rng, w_new = v2(0.f, 0.f), lnh, lnl;
+    bool pf0, pf1;  // sem_pixel_fast
     if (Raw) {  // the ingest's per-pixel terms (identical operations)
-      const f3 r0 = pixel_ray(P, __float_as_int(px[j0].y), __float_as_int(px[j0].z));
-      const f3 r1 = pixel_ray(P, __float_as_int(px[j1].y), __float_as_int(px[j1].z));
+      const int w0 = __float_as_int(px[j0].w), w1 = __float_as_int(px[j1].w);
+      const f3 r0 = pixel_ray(P, w0 & 0xFFFF, w0 >> 16);
+      const f3 r1 = pixel_ray(P, w1 & 0xFFFF, w1 >> 16);
       rng = v2(sqrtf(dot3(r0, r0)), sqrtf(dot3(r1, r1)));
       w_new = v2(pixel_w_new(P, d.x), pixel_w_new(P, d.y));
+      lnh = sem_logf2(v2(px[j0].y, px[j1].y));
+      lnl = sem_logf2(v2(px[j0].z, px[j1].z));
+      pf0 = sem_pixel_fast(px[j0].y, px[j0].z, d.x, P.max_depth);
+      pf1 = sem_pixel_fast(px[j1].y, px[j1].z, d.y, P.max_depth);
     } else {
-      rng = v2(px[j0].y, px[j1].y);
-      lg[j0] = px[j0].z;
-      lg[j1] = px[j1].z;
+      rng = v2(fabsf(px[j0].y), fabsf(px[j1].y));
+      pf0 = px[j0].y > 0.0f;
+      pf1 = px[j1].y > 0.0f;
+      lnh = v2(px[j0].z, px[j1].z);
+      lnl = v2(px[j0].w, px[j1].w);
     }
-    const uint32_t n0 = __float_as_uint(px[j0].w), n1 = __float_as_uint(px[j1].w);
+    const uint32_t n0 = pc[j0], n1 = pc[j1];
     const v2f sdf = rng * (d - hzs[k]);
     const bool a0 = inb[j0] && !(d.x == 0 || d.x > P.max_depth) && sdf.x > neg_trunc;
     const bool a1 = inb[j1] && !(d.y == 0 || d.y > P.max_depth) && sdf.y > neg_trunc;
@@ -311,26 +327,58 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
       const v2f wr = wc + v2(0x1.fffffep-2f, 0x1.fffffep-2f);
       c0 |= weight_round_cap(wr.x, 40u) << 24;
       c1 |= weight_round_cap(wr.y, 40u) << 24;
-      // semantic fusion (voxel_tsdf.cu:196-202): p' = P / (P + N) with
-      //   P = exp((w_old ln p + w_new ln ht) / wc), N = exp((w_old ln(1 - p) + w_new ln lt) / wc)
-      // is exactly the logistic of  L' = (w_old L + w_new log2(ht / lt)) / wc  in the base-2
-      // log-odds L = log2(p / (1 - p)) the pool stores (the pixel record holds log2 ht - log2 lt), so the
-      // update is two products and a sum; readers convert with prob_of_logodds (within 1e-4
-      // of the reference's float chain, and L stays exactly 0 -- p 0.5 -- when ht == lt)
-      const v2f pn = (w_old * v2(comp(pr, j0), comp(pr, j1)) + w_new * v2(lg[j0], lg[j1])) * iwc;
+      wn[j0] = w_new.x;
+      wn[j1] = w_new.y;
       if (a0) {
         setc(ts, j0, tq.x);
-        setc(pr, j0, pn.x);
         setu(cw, j0, c0);
       }
       if (a1) {
         setc(ts, j1, tq.y);
-        setc(pr, j1, pn.y);
         setu(cw, j1, c1);
       }
       upd_mask |= (a0 ? 1 << j0 : 0) | (a1 ? 1 << j1 : 0);
     }
+    lnh2[k] = lnh;
+    lnl2[k] = lnl;
+    pfast |= (pf0 ? 1 << j0 : 0) | (pf1 ? 1 << j1 : 0);
     mn = fminf(mn, fminf(fabsf(comp(ts, j0)), fabsf(comp(ts, j1))));
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // ---- pass 3: semantic fusion (voxel_tsdf.cu:196-202), the reference's float chain operation for
+  // operation:
+  //   P = expf((w_old logf(p) + w_new logf(ht)) / wc), N = expf((w_old logf(1 - p) + w_new logf(lt)) / wc),
+  //   p' = P / (P + N)
+  // (logf / expf: the oracle's fixed algorithms, sem_logf / sem_expf; the quotients IEEE-exact). The
+  // fast path runs on both voxels of a pair; a voxel whose operands leave its range -- p 0 or 1, ht or
+  // lt 0, extreme quotients -- is recomputed with every special case (sem_update_exact).
+#if defined(TSDF_EXP) && (TSDF_EXP & 8)  // experiment build: no semantic update (timing only)
+  if (upd_mask < 0)
+#endif
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int j0 = 2 * k, j1 = 2 * k + 1;
+    const bool a0 = (upd_mask >> j0) & 1, a1 = (upd_mask >> j1) & 1;
+    if (a0 || a1) {
+      const v2f w_old = v2((float)((wold4 >> (8 * j0)) & 0xFF), (float)((wold4 >> (8 * j1)) & 0xFF));
+      const v2f w_new = v2(wn[j0], wn[j1]);
+      const v2f wc = w_old + w_new;
+      const v2f lnh = lnh2[k], lnl = lnl2[k];
+      const v2f pv = v2(comp(pr, j0), comp(pr, j1));
+      const v2f an = w_old * sem_log_fast2(pv) + w_new * lnh;
+      const v2f bn = w_old * sem_log_fast2(v2(1.0f, 1.0f) - pv) + w_new * lnl;
+      const v2f y1 = div_refine(wc, v2(__builtin_amdgcn_rcpf(wc.x), __builtin_amdgcn_rcpf(wc.y)));
+      const v2f sp = sem_exp_fast2(div_expand(an, wc, y1));
+      const v2f sn = sem_exp_fast2(div_expand(bn, wc, y1));
+      const v2f ss = sp + sn;
+      v2f pn = div_expand(sp, ss, div_refine(ss, v2(__builtin_amdgcn_rcpf(ss.x), __builtin_amdgcn_rcpf(ss.y))));
+      if (__builtin_expect(a0 && !sem_voxel_fast((pfast >> j0) & 1, pv.x), 0))
+        pn.x = sem_update_exact(pv.x, w_old.x, w_new.x, wc.x, lnh.x, lnl.x);
+      if (__builtin_expect(a1 && !sem_voxel_fast((pfast >> j1) & 1, pv.y), 0))
+        pn.y = sem_update_exact(pv.y, w_old.y, w_new.y, wc.y, lnh.y, lnl.y);
+      if (a0) setc(pr, j0, pn.x);
+      if (a1) setc(pr, j1, pn.y);
+    }
   }
 #if defined(TSDF_EXP) && (TSDF_EXP & 4)  // experiment build: no pool state stores
   if (upd_mask < 0) {
@@ -387,10 +435,10 @@ __device__ __forceinline__ size_t band_find(const EngineDev& D, int bst, int lan
 // The visible blocks are the sweep's band lists (blocks that existed before the frame) followed by
 // the blocks k_resolve_alloc created (D.fresh_vis, flagged fresh).
 // Raw: a shard's frame -- the pixel terms come from the raw frame (depth, rgb, ht, lt gathers) and
-// are computed per voxel with the ingest's operations (pixel_w_new, pixel_logodds, the range of
+// are computed per voxel with the ingest's operations (pixel_w_new, sem_logf of ht / lt, the range of
 // pixel_ray), instead of from pixel records packed for the whole frame.
-#ifndef TSDF_INTEGRATE_WAVES
-#define TSDF_INTEGRATE_WAVES 7
+#ifndef TSDF_INTEGRATE_WAVES  // 6: the semantic update's chain (pass 3) spills the update loop at 7
+#define TSDF_INTEGRATE_WAVES 6
 #endif
 // nint: the update's workgroups (the whole grid). L: the LDS of the last arriver's carving resolve.
 // returns true in the workgroup that arrived last (and ran the carving tail)

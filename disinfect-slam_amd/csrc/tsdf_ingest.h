@@ -14,7 +14,8 @@ namespace tsdf {
 // ---------------------------------------------------------------------------------------------
 // k_ingest_dda: 16x16 pixel tile per workgroup.
 //  1. pack the frame into per-pixel records the integrate kernel gathers (one 16-B gather per voxel):
-//       pixA = {depth, range = |K^-1 [x y 1]|, log2 ht - log2 lt, rgb}
+//       pixA = {depth, +-range (range = |K^-1 [x y 1]|; negative: the pixel takes the semantic update's
+//       exact path, sem_pixel_fast), logf(ht), logf(lt)} (sem_logf), pixC = rgb
 //     (exactly the values tsdf_integrate_kernel recomputes per voxel, voxel_tsdf.cu:174-201; the
 //     update computes w_new = (1 - d / max_depth) * 4 from the depth with the same operations)
 //  2. DDA of [p - trunc dir, p + trunc dir] (voxel_tsdf.cu:116-146); block keys deduplicated in
@@ -478,7 +479,10 @@ __device__ __forceinline__ void ingest_tile(const EngineDev& D, const FrameParam
                          ((uint32_t)rgb[3 * i + 2] << 16);
       const float h = ht ? ht[i] : 1.0f;
       const float l = lt ? lt[i] : 1.0f;
-      D.pixA[P.pix_off + i] = make_float4(d, range, pixel_logodds(h, l), __uint_as_float(c));
+      // the range's sign carries sem_pixel_fast (range >= 1): negative = the update's exact path
+      D.pixA[P.pix_off + i] = make_float4(d, sem_pixel_fast(h, l, d, P.max_depth) ? range : -range,
+                                          sem_logf(h), sem_logf(l));
+      D.pixC[P.pix_off + i] = c;
     }
     TSDF_STAMP(D, 0, 2);
     if (!(d == 0 || d > P.max_depth)) {

@@ -53,7 +53,8 @@ struct EngineDev {
   VisRec* pend;                 // kNewKeyCap: a shard's owned entries its exhausted pool left without
                                 // voxels this frame (ctr->n_pend); carved in the same frame
   // packed frame: two buffers of max_pixels records each (FrameParams.pix_off selects one)
-  float4* pixA;                 // {depth, range, log2 ht - log2 lt (the pixel's base-2 log-odds), rgb}
+  float4* pixA;                 // {depth, range, logf(ht), logf(lt)} (sem_logf)
+  uint32_t* pixC;               // rgb (r | g << 8 | b << 16)
   // pipelined frames (k_frame): flags, per-frame statistics and the per-pool-block tags
   unsigned long long* pipe;     // kPipeWords (layout below)
   uint32_t* ctag;               // 2 x nblocks: ctag[(f & 1) * nblocks + b] == f: block b was a carve
@@ -113,7 +114,7 @@ constexpr int kPipeAPub = kPipeIngEnd + 32;     // + 16 p: allocation published 
 constexpr int kPipeStats = 512;                 // + 1024 p + 16 i: payload (blocks << 40 | voxels) and,
 constexpr int kPipeStatLines = 64;              //   at +1, the latest end stamp of update counter i
 constexpr int kPipeWords = kPipeStats + 2 * kPipeStatLines * 16;
-constexpr int kFrameUpdWgsPer2Cu = 5;           // default k_frame update workgroups per two CUs (TSDF_FRAME_WG_PER_CU)
+constexpr int kFrameUpdWgsPer2Cu = 6;           // default k_frame update workgroups per two CUs (TSDF_FRAME_WG_PER_CU)
 constexpr int kPipeHead = 8;                    // workgroups before the update's (0: carving + allocation)
 constexpr int kPipeFreshWG = 64;                // workgroups that update the blocks allocated in the launch
 constexpr int kPipeDefer = 32;                  // deferred (carve-pending) blocks one update workgroup holds
@@ -192,7 +193,7 @@ struct FrameArgs {
 __global__ void k_init_table(int4* table);
 __global__ void k_copy_words(uint32_t* dst, const uint32_t* src, int n);
 __global__ void k_init_heap(int32_t* heap, int n);
-__global__ void k_init_logodds(uint8_t* pool, int nb);
+__global__ void k_init_prob(uint8_t* pool, int nb);
 // last-arriver counters (tsdf_resolve.h arrive_last), one 128-B line each: lines [0, 9) k_ingest_dda,
 // [16, 25) k_integrate, line 32 k_integrate's start stamp
 // first-level arrival counters per kernel (workgroup b arrives at counter b % kArrGroups: a multiple

@@ -109,7 +109,7 @@ __device__ __forceinline__ void ray_shade(const EngineDev& D, const RayView& R, 
     const uint8_t* blk = D.pool + (size_t)c.idx * kBlockBytes;
     const int o = voxel_off(fx, fy, fz);
     col = reinterpret_cast<const uint32_t*>(blk + kRgbwOffset)[o];
-    prob = prob_of_logodds(reinterpret_cast<const float*>(blk + kProbOffset)[o]);
+    prob = reinterpret_cast<const float*>(blk + kProbOffset)[o];
   }
   const float gxp = ray_tsdf(D, R, c, (int16_t)(fx + 1), fy, fz);
   const float gxn = ray_tsdf(D, R, c, (int16_t)(fx - 1), fy, fz);

@@ -2,7 +2,8 @@
 // quotient helpers (tsdf_device.h: round_quot_i/_u8/_pos2, div_pair, quot_const, quot_for_cmp,
 // f2i / f2u8 / round_s16) bit-for-bit against the
 // correctly rounded IEEE divide and the saturating conversions, on the GPU, over exhaustive and
-// adversarial input sets. Not part of the product library; tests/test_gpu_numerics.py drives it.
+// adversarial input sets; and digests the semantic update's sem_logf / sem_expf over every input for
+// comparison with the oracle's (ora_math_digest). Not part of the product library; tests/test_gpu_numerics.py drives it.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -152,6 +153,28 @@ __global__ void k_convert(uint32_t lo, uint32_t hi, unsigned long long* bad, uin
   }
 }
 
+// order-independent digest of the semantic-update functions over the input bit patterns [lo, hi)
+// (NaN results as one pattern): the sum ora_math_digest forms. kind 0: sem_logf2 (any float),
+// 1: sem_expf2, 2: sem_log_unit2 (the update's p and 1 - p: meant for [0, 1] and NaN). Pairs are
+// two consecutive inputs, so both lanes of the packed forms are exercised.
+__device__ __forceinline__ unsigned long long sem_mix(uint64_t i, float y) {
+  const uint32_t b = y != y ? 0x7fc00000u : __float_as_uint(y);
+  return ((unsigned long long)b ^ (i * 0x9E3779B97F4A7C15ull)) * 0xBF58476D1CE4E5B9ull;
+}
+__global__ void k_sem_digest(int kind, uint64_t lo, uint64_t hi, unsigned long long* out) {
+  unsigned long long h = 0;
+  for (uint64_t i = lo + 2 * (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x); i < hi;
+       i += 2 * (uint64_t)gridDim.x * blockDim.x) {
+    const bool two = i + 1 < hi;
+    const v2f x = v2(__uint_as_float((uint32_t)i), __uint_as_float((uint32_t)(two ? i + 1 : i)));
+    const v2f y = kind == 0 ? sem_logf2(x) : kind == 1 ? sem_expf2(x) : sem_log_unit2(x);
+    h += sem_mix(i, y.x);
+    if (two) h += sem_mix(i + 1, y.y);
+  }
+  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, h);
+}
+
 struct Out {
   unsigned long long bad;
   uint32_t first;
@@ -231,6 +254,21 @@ int tsdf_selfcheck_convert(uint32_t lo, uint32_t hi, unsigned long long* bad, ui
   if (!d) return -1;
   hipLaunchKernelGGL(k_convert, dim3(8192), dim3(256), 0, 0, lo, hi, &d->bad, &d->first);
   return finish(d, bad, first);
+}
+
+// digest of the semantic-update function `kind` over the input bit patterns [lo, hi) (k_sem_digest)
+int tsdf_selfcheck_sem_digest(int kind, uint64_t lo, uint64_t hi, unsigned long long* digest) {
+  unsigned long long* d = nullptr;
+  if (hipMalloc(&d, sizeof(*d)) != hipSuccess || hipMemset(d, 0, sizeof(*d)) != hipSuccess) return -1;
+  hipLaunchKernelGGL(k_sem_digest, dim3(4096), dim3(256), 0, 0, kind, lo, hi, d);
+  hipError_t err = hipGetLastError();
+  if (err == hipSuccess) err = hipMemcpy(digest, d, sizeof(*d), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (err != hipSuccess) {
+    std::fprintf(stderr, "tsdf_selfcheck: %s\n", hipGetErrorString(err));
+    return -2;
+  }
+  return 0;
 }
 
 }  // extern "C"

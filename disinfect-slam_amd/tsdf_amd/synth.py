@@ -8,7 +8,15 @@ run in this repo integrates a deterministic analytic scene:
 * depth: analytic ray cast, + N(0, 1 mm) noise (seeded), quantised to uint16 / 5000 (TUM factor,
   configs/TUM_RGBD_rgbd_1.yaml:44) and back to float32 metres, 2 % holes, readings beyond 3.9 m
   dropped so that depth != max_depth (the reference's 0/0 case, voxel_tsdf.cu:182-191);
-* ht: a smooth per-surface field in [0.02, 0.98]; lt = 1 - ht (no log(0), voxel_tsdf.cu:196-202);
+* ht / lt (`touch`): "complement" (default) -- a smooth per-surface field ht in [0.02, 0.98] and
+  lt = 1 - ht (no log(0), voxel_tsdf.cu:196-202); "independent" -- two independent fields over
+  (0, 1] as a segmentation network's two output channels give them (examples/tsdf/online.cc:59-60,
+  segmentation/inference.cc:57-65), with regions and sprinkled pixels at the extremes 1e-6,
+  1 - 1e-6, the largest float below 1 and 1; "u16" -- those fields stored as uint16 PNG maps and
+  read back with convertTo(CV_32FC1, 1 / 65535) (examples/tsdf/offline.cc:76-82), with exact zeros
+  in the lt channel (the shelf, a strip of the walls and sprinkled pixels: p becomes exactly 1);
+  "u16z" -- as "u16" with exact zeros in the ht channel too (another strip; pixels or voxels that see ht = lt = 0 fuse to NaN in
+  the reference's own arithmetic, 0 / 0 -- the reference leaves that input undefined);
 * rgb: a deterministic per-surface checker pattern (uint8, RGB order as TSDFGrid expects).
 
 Frames are produced on the host with numpy (float64 geometry, one float32 rounding at the end), so
@@ -158,7 +166,88 @@ _PALETTE = np.array(
 _TOUCH_BASE = np.array([0.05, 0.06, 0.04, 0.08, 0.15, 0.02, 0.0, 0.85, 0.6, 0.35, 0.9, 0.7])
 
 
-def render(cam: Camera, frame: int, noise: bool = True, holes: float = 0.02):
+TOUCH_MODES = ("complement", "independent", "u16", "u16z")
+_LT_BASE = np.array([0.9, 0.3, 0.7, 0.35, 0.5, 0.95, 0.2, 0.1, 1.0, 0.6, 1e-6, 1e-6])
+_U16_SCALE = np.float32(1.0 / 65535)  # cv::Mat::convertTo scale, a float in OpenCV's 16u -> 32f loop
+_ONE_MINUS = np.float32(1.0 - 1e-6)
+_BELOW_ONE = np.nextafter(np.float32(1.0), np.float32(0.0))
+
+
+def _touch_fields(xp, pts, sid, wave, u1, u2, mode):
+    """ht, lt (float32) of one frame for a non-default touch mode (module docstring). xp: numpy or torch; pts
+    (N, 3) float64, sid (N,) int, wave the complement mode's field, u1 / u2 (N,) uniforms in [0, 1)."""
+    def f32(a):
+        return a.astype(np.float32) if xp is np else a.to(xp.float32)
+
+    def const(v, like):
+        return xp.full_like(like, float(v))
+
+    def where(c, a, b):
+        return xp.where(c, a, b)
+
+    if mode not in TOUCH_MODES:
+        raise ValueError(f"touch mode {mode!r} not in {TOUCH_MODES}")
+    w2 = xp.sin(1.3 * pts[:, 0] - 2.9 * pts[:, 1] + 0.7 * pts[:, 2]) * xp.cos(3.7 * pts[:, 1] + 1.1 * pts[:, 2])
+    hb = xp.asarray(_TOUCH_BASE)[sid] if xp is np else _TOUCH_BASE_T(xp, sid)
+    lb = xp.asarray(_LT_BASE)[sid] if xp is np else xp.tensor(_LT_BASE, dtype=xp.float64, device=sid.device)[sid]
+    ht = hb + 0.3 * wave
+    lt = lb + 0.3 * w2
+    ht = ht.clip(1e-6, 1.0) if xp is np else ht.clamp(1e-6, 1.0)
+    lt = lt.clip(1e-6, 1.0) if xp is np else lt.clamp(1e-6, 1.0)
+    ht, lt = f32(ht), f32(lt)
+    # regions at the extremes (the orbit sees the cabinet, the x+ / y+ walls and, later, the shelf):
+    # the cabinet ht = 1 - 1e-6, lt = 1e-6 (p -> 1 - 1e-6); the lowest 0.35 m of the walls ht = 1e-6,
+    # lt = 1 (p -> 1e-6); a band of the walls 1.3-1.45 m high and sphere 11 ht = lt = 1e-6 (p stays
+    # 0.5 from two tiny channels)
+    z = pts[:, 2]
+    wall = (sid == 1) | (sid == 3)
+    low = wall & (z < 0.35)
+    band = (wall & (z > 1.3) & (z < 1.45)) | (sid == 11)
+    ht = where(sid == 8, const(_ONE_MINUS, ht), ht)
+    lt = where(sid == 8, const(1e-6, lt), lt)
+    ht = where(low | band, const(1e-6, ht), ht)
+    lt = where(low, const(1.0, lt), lt)
+    lt = where(band, const(1e-6, lt), lt)
+    # sprinkled pixels at 1e-6, the largest float below 1 and exactly 1, per channel
+    for ch, u in ((0, u1), (1, u2)):
+        x = ht if ch == 0 else lt
+        x = where(u < 0.004, const(1e-6, x), x)
+        x = where((u >= 0.004) & (u < 0.008), const(_BELOW_ONE, x), x)
+        x = where((u >= 0.008) & (u < 0.012), const(1.0, x), x)
+        if ch == 0:
+            ht = x
+        else:
+            lt = x
+    if mode == "independent":
+        return ht, lt
+
+    # uint16 maps (rounded, as a PNG stores a network's probabilities), read back as f32(k) * f32(1/65535)
+    def q16(x):
+        k = (x.astype(np.float64) * 65535).round() if xp is np else (x.double() * 65535).round()
+        return k.clip(0, 65535) if xp is np else k.clamp(0, 65535)
+
+    kh, kl = q16(ht), q16(lt)
+    kh = where(kh < 1, const(1, kh), kh)  # ht stays > 0 (zeros only where the mode asks)
+    kl = where(kl < 1, const(1, kl), kl)
+    # exact zeros in lt (the shelf, 12 cm strips every metre of the walls, 1 % of the pixels): p -> 1 exactly
+    along = pts[:, 0] + pts[:, 1]  # along either wall (x or y is constant on it)
+    strip = wall & ((along - (along // 1.0) * 1.0) < 0.12)
+    kl = where((sid == 9) | strip | (u2 >= 0.990), const(0, kl), kl)
+    if mode == "u16z":  # and in ht (8 cm strips between, 0.5 % of the pixels): p -> 0; where a
+        # voxel sees both, ht = lt = 0 or p = 0 then lt = 0, the reference fuses 0 / 0 = NaN
+        strip_h = wall & ((along + 0.5 - ((along + 0.5) // 1.0) * 1.0) < 0.08)
+        kh = where(strip_h | (u1 >= 0.995), const(0, kh), kh)
+    scale = float(_U16_SCALE)
+    if xp is np:
+        return (kh.astype(np.float32) * _U16_SCALE).astype(np.float32), (kl.astype(np.float32) * _U16_SCALE).astype(np.float32)
+    return kh.to(xp.float32) * scale, kl.to(xp.float32) * scale
+
+
+def _TOUCH_BASE_T(torch, sid):
+    return torch.tensor(_TOUCH_BASE, dtype=torch.float64, device=sid.device)[sid]
+
+
+def render(cam: Camera, frame: int, noise: bool = True, holes: float = 0.02, touch: str = "complement"):
     """Render frame `frame`: returns dict(rgb HxWx3 u8, depth HxW f32, ht, lt HxW f32, q, t)."""
     (R_wc, p), (q, t) = pose(frame)
     H, W = cam.height, cam.width
@@ -178,8 +267,13 @@ def render(cam: Camera, frame: int, noise: bool = True, holes: float = 0.02):
         depth[rng.random(depth.shape) < holes] = 0.0
     # per-surface smooth touch field and checker colour
     wave = np.sin(3.1 * pts[:, 0] + 1.7 * pts[:, 1]) * np.cos(2.3 * pts[:, 2] + 0.4 * pts[:, 0])
-    ht = np.clip(_TOUCH_BASE[sid] + 0.08 * wave, 0.02, 0.98).astype(np.float32)
-    lt = (np.float32(1.0) - ht).astype(np.float32)
+    if touch == "complement":
+        ht = np.clip(_TOUCH_BASE[sid] + 0.08 * wave, 0.02, 0.98).astype(np.float32)
+        lt = (np.float32(1.0) - ht).astype(np.float32)
+    else:  # its own generator: the depth noise and holes stay those of the complement stream
+        trng = np.random.Generator(np.random.PCG64(SEED + 7919 * (frame + 1)))
+        u1, u2 = trng.random(sid.shape), trng.random(sid.shape)
+        ht, lt = _touch_fields(np, pts, sid, wave, u1, u2, touch)
     chk = ((np.floor(pts[:, 0] / 0.2) + np.floor(pts[:, 1] / 0.2) + np.floor(pts[:, 2] / 0.2)) % 2)
     shade = 0.75 + 0.25 * chk
     rgb = np.clip(_PALETTE[sid] * shade[:, None] + 10 * wave[:, None], 0, 255).astype(np.uint8)
@@ -200,7 +294,7 @@ def frames(cam: Camera, start: int, count: int, **kw):
 
 
 def render_torch(cam: Camera, frame_ids, device="cuda", noise: bool = True, holes: float = 0.02,
-                 seed: int = SEED):
+                 seed: int = SEED, touch: str = "complement"):
     """Same scene rendered with torch on `device` (float64 geometry) for benchmark streams.
 
     Returns dict of stacked tensors: rgb (F,H,W,3) u8, depth/ht/lt (F,H,W) f32, and host numpy
@@ -225,7 +319,7 @@ def render_torch(cam: Camera, frame_ids, device="cuda", noise: bool = True, hole
     room_min = torch.tensor(ROOM_MIN, **dd)
     room_max = torch.tensor(ROOM_MAX, **dd)
     pal = torch.tensor(_PALETTE, **dd)
-    touch = torch.tensor(_TOUCH_BASE, **dd)
+    touch_base = torch.tensor(_TOUCH_BASE, **dd)
     gen = torch.Generator(device=device)
     for k, f in enumerate(frame_ids):
         (R_wc, p), (q, t) = pose(f)
@@ -268,13 +362,19 @@ def render_torch(cam: Camera, frame_ids, device="cuda", noise: bool = True, hole
         if holes > 0:
             depth[torch.rand(depth.shape, generator=gen, **dd) < holes] = 0.0
         wave = torch.sin(3.1 * pts[:, 0] + 1.7 * pts[:, 1]) * torch.cos(2.3 * pts[:, 2] + 0.4 * pts[:, 0])
-        ht = (touch[sid] + 0.08 * wave).clamp(0.02, 0.98).to(torch.float32)
+        if touch == "complement":
+            ht = (touch_base[sid] + 0.08 * wave).clamp(0.02, 0.98).to(torch.float32)
+            lt = (1.0 - ht)
+        else:
+            u1 = torch.rand(sid.shape, generator=gen, **dd)
+            u2 = torch.rand(sid.shape, generator=gen, **dd)
+            ht, lt = _touch_fields(torch, pts, sid, wave, u1, u2, touch)
         chk = torch.remainder(torch.floor(pts[:, 0] / 0.2) + torch.floor(pts[:, 1] / 0.2)
                               + torch.floor(pts[:, 2] / 0.2), 2)
         shade = 0.75 + 0.25 * chk
         rgb = (pal[sid] * shade[:, None] + 10 * wave[:, None]).clamp(0, 255).to(torch.uint8)
         out["depth"][k] = depth.reshape(H, W)
         out["ht"][k] = ht.reshape(H, W)
-        out["lt"][k] = (1.0 - ht).reshape(H, W)
+        out["lt"][k] = lt.reshape(H, W)
         out["rgb"][k] = rgb.reshape(H, W, 3)
     return out

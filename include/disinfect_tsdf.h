@@ -295,7 +295,7 @@ int tsdf_query(tsdf_engine* e, const float* bounds, tsdf_voxel* out, int64_t cap
 /* Render replicas of a spatially sharded volume (the raycast composite SURVEY.md 8e
  * names). The blocks a raycast of (K, W, H, pose, max_depth) can read -- a conservative superset --
  * are packed as TSDF_BLOCK_RECORD_BYTES records {int16 x, y, z, 0; 8 zero bytes; the 6 KiB block:
- * tsdf f32[512], log-odds f32[512], rgbw u8x4[512]} in entry order. Two-call: out == NULL returns
+ * tsdf f32[512], prob f32[512], rgbw u8x4[512]} in entry order. Two-call: out == NULL returns
  * *count only; then out must hold capacity >= *count records (host or device memory per mem_kind).
  * tsdf_import_blocks allocates every record's block in the engine (resolver launches until none is
  * missing) and writes its payload; replace != 0 first empties the volume (table, occupancy, free

@@ -581,8 +581,9 @@ static int update_and_carve_test(ora_grid* g, const frame_params* Pp, const uint
           const float p = g->prob[a];
           const float h = ht ? ht[img] : 1.0f;
           const float l = lt ? lt[img] : 1.0f;
-          const float pos = expf((w_old * logf(p) + w_new * logf(h)) / wc);
-          const float neg = expf((w_old * logf(1 - p) + w_new * logf(l)) / wc);
+          /* CUDA logf / expf restated as the oracle's fixed algorithms (ora_math.c: why) */
+          const float pos = ora_expf((w_old * ora_logf(p) + w_new * ora_logf(h)) / wc);
+          const float neg = ora_expf((w_old * ora_logf(1 - p) + w_new * ora_logf(l)) / wc);
           g->prob[a] = pos / (pos + neg);
           ++nupd;
         }

@@ -127,6 +127,15 @@ uint32_t ora_hash(int16_t x, int16_t y, int16_t z);
 void ora_rgbd_half(const uint8_t* rgb, const uint16_t* depth, const uint8_t* mask, int W, int H,
                    float depth_factor, uint8_t* rgb_out, float* depth_out);
 
+/* The logf / expf of the semantic update (voxel_tsdf.cu:196-202), fixed as explicit float
+ * algorithms (ora_math.c: why, and how accurate). Test support: ora_math_digest sums a mix of every
+ * result over the input bit patterns [lo, hi) (kind 0 logf, 1 expf) for the GPU comparison;
+ * ora_math_accuracy compares with the correctly rounded values (out: inputs, differing, max ulp). */
+float ora_logf(float x);
+float ora_expf(float x);
+uint64_t ora_math_digest(int kind, uint64_t lo, uint64_t hi);
+void ora_math_accuracy(int kind, uint64_t lo, uint64_t hi, uint64_t step, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -84,6 +84,13 @@ def lib():
         L.ora_hash.restype = C.c_uint32
         L.ora_hash.argtypes = [C.c_int16, C.c_int16, C.c_int16]
         L.ora_rgbd_half.argtypes = [P, P, P, C.c_int, C.c_int, C.c_float, P, P]
+        L.ora_logf.restype = C.c_float
+        L.ora_logf.argtypes = [C.c_float]
+        L.ora_expf.restype = C.c_float
+        L.ora_expf.argtypes = [C.c_float]
+        L.ora_math_digest.restype = C.c_uint64
+        L.ora_math_digest.argtypes = [C.c_int, C.c_uint64, C.c_uint64]
+        L.ora_math_accuracy.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(C.c_double)]
         _lib = L
     return _lib
 

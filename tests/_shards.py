@@ -53,10 +53,16 @@ def live_blocks(dump):
     return {tuple(map(int, p)): (t, c, q) for p, t, c, q in zip(pos, tsdf, rgbw, prob)}
 
 
-def assert_shard_matches(shard_dump, full_dump, full=None, prob_atol=1e-4, tag=""):
+def _prob_same(a, b):
+    na, nb = np.isnan(a), np.isnan(b)
+    return np.array_equal(na, nb) and np.array_equal(a[~na].view(np.uint32), b[~nb].view(np.uint32))
+
+
+def assert_shard_matches(shard_dump, full_dump, full=None, prob_atol=0.0, tag=""):
     """One shard against the unsharded volume: its hash index (occupied entries, positions, list
     offsets) equals the unsharded table, and each block it holds equals the unsharded block (tsdf /
-    rgb / weight bit-identical, probability within prob_atol). Returns its block positions."""
+    rgb / weight bit-identical; probability bit-identical, NaN == NaN, or within prob_atol > 0).
+    Returns its block positions."""
     full = live_blocks(full_dump) if full is None else full
     focc = full_dump["entry_idx"] >= 0
     occ = shard_dump["entry_idx"] >= 0
@@ -69,11 +75,14 @@ def assert_shard_matches(shard_dump, full_dump, full=None, prob_atol=1e-4, tag="
         ft, fc, fq = full[k]
         np.testing.assert_array_equal(v[0], ft, err_msg=f"{tag}: tsdf of block {k}")
         np.testing.assert_array_equal(v[1], fc, err_msg=f"{tag}: rgbw of block {k}")
-        np.testing.assert_allclose(v[2], fq, atol=prob_atol, rtol=0, err_msg=f"{tag}: prob of block {k}")
+        if prob_atol > 0:
+            np.testing.assert_allclose(v[2], fq, atol=prob_atol, rtol=0, err_msg=f"{tag}: prob of block {k}")
+        else:
+            assert _prob_same(v[2], fq), f"{tag}: prob of block {k}"
     return set(mine)
 
 
-def assert_union_equals(shard_dumps, full_dump, prob_atol=1e-4, tag=""):
+def assert_union_equals(shard_dumps, full_dump, prob_atol=0.0, tag=""):
     """Every shard matches the unsharded volume (assert_shard_matches), the shards' blocks are
     disjoint, and their union has exactly the unsharded volume's block positions."""
     full = live_blocks(full_dump)

@@ -56,18 +56,19 @@ KAT = {
 }
 
 
-def make_integrate():
+def make_integrate(touch="complement", nframes=6, bits=11):
     from _oracle import OracleGrid
     from tsdf_amd import synth
 
-    W, H, voxel, trunc, bits, nframes = 48, 36, 0.02, 0.08, 11, 6
+    W, H, voxel, trunc = 48, 36, 0.02, 0.08
     cam = synth.camera(W, H, synth.TUM_FR1)
     ora = OracleGrid(voxel, trunc, bits)
     rgb, depth, ht, lt, q, t, stats = [], [], [], [], [], [], []
     for f in range(nframes):
-        fr = synth.render(cam, 3 * f)
+        fr = synth.render(cam, 3 * f, touch=touch)
         ora.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], 4.0, cam.K, fr["q"], fr["t"])
         s = ora.stats()
+        assert not s["pool_exhausted"], (touch, f)
         stats.append([s["last_num_visible"], s["last_num_updated"], s["last_num_deleted"],
                       s["active_blocks"]])
         rgb.append(fr["rgb"]); depth.append(fr["depth"]); ht.append(fr["ht"]); lt.append(fr["lt"])
@@ -80,7 +81,7 @@ def make_integrate():
     rgba, normal = ora.raycast(cam.K, W, H, rq, rt, 4.0)
     query = ora.query(None)
     out = dict(
-        W=W, H=H, voxel=voxel, trunc=trunc, num_block_bits=bits, max_depth=4.0,
+        W=W, H=H, voxel=voxel, trunc=trunc, num_block_bits=bits, max_depth=4.0, touch=touch,
         K=np.asarray(cam.K, np.float32),
         rgb=np.stack(rgb), depth=np.stack(depth), ht=np.stack(ht), lt=np.stack(lt),
         q=np.stack(q).astype(np.float32), t=np.stack(t).astype(np.float32),
@@ -96,12 +97,60 @@ def make_integrate():
     return out
 
 
+# 3. the semantic streams: ht / lt as two independent channels over (0, 1] with the
+#    extremes 1e-6, 1 - 1e-6, the largest float below 1 and 1; and uint16 / 65535 PNG maps with exact
+#    zeros (lt only, and both channels: the reference's 0 / 0 NaN), 40 frames so that much of the
+#    surface reaches the weight cap (40)
+SEMANTIC = {"independent": "integrate_48x36_independent.npz", "u16": "integrate_48x36_u16.npz",
+            "u16z": "integrate_48x36_u16z.npz"}
+
+# 4. sem_math_digests.json -- the oracle's logf / expf (oracle/ora_math.c) digested over every input
+#    bit pattern in chunks of 2^24 (ora_math_digest), the target of the GPU restatement's exhaustive
+#    check (tests/test_gpu_numerics.py); kind 2 (the update's p and 1 - p) over [0, 1] and the NaNs.
+CHUNK = 1 << 24
+
+
+def sem_chunks(kind):
+    if kind in (0, 1):
+        return [(i * CHUNK, (i + 1) * CHUNK) for i in range(256)]
+    one = 0x3F800001
+    out = [(lo, min(lo + CHUNK, one)) for lo in range(0, one, CHUNK)]
+    return out + [(0x7F800001, 0x80000000), (0xFF800001, 0x100000000)]
+
+
+def _digest(args):
+    from _oracle import lib
+    L = lib()
+    kind, lo, hi = args
+    return str(L.ora_math_digest(kind, lo, hi))
+
+
+def make_sem_digests():
+    from multiprocessing import Pool
+    out = {}
+    with Pool(min(8, os.cpu_count() or 1)) as pool:
+        for kind in (0, 1, 2):
+            ch = sem_chunks(kind)
+            dig = pool.map(_digest, [(kind, lo, hi) for lo, hi in ch])
+            out[str(kind)] = [[lo, hi, d] for (lo, hi), d in zip(ch, dig)]
+    return out
+
+
 def main():
     json.dump(KAT, open(os.path.join(HERE, "kat_reference.json"), "w"), indent=1)
     g = make_integrate()
     np.savez_compressed(os.path.join(HERE, "integrate_48x36.npz"), **g)
     print("live blocks", g["live_entry"].size, "query voxels", int(g["query_count"]),
           "stats", g["stats"].tolist())
+    for touch, name in SEMANTIC.items():
+        g = make_integrate(touch, nframes=40, bits=12)
+        np.savez_compressed(os.path.join(HERE, name), **g)
+        w = g["rgbw"][..., 3]
+        print(touch, "live blocks", g["live_entry"].size, "weight-40 voxels", int((w == 40).sum()),
+              "NaN prob", int(np.isnan(g["prob"]).sum()), "prob 0 / 1", int((g["prob"] == 0).sum()),
+              int((g["prob"] == 1).sum()))
+    if "--digests" in sys.argv:
+        json.dump(make_sem_digests(), open(os.path.join(HERE, "sem_math_digests.json"), "w"))
 
 
 if __name__ == "__main__":

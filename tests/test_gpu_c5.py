@@ -20,9 +20,9 @@ pytestmark = pytest.mark.gpu
 def _check_render(rgba, nrm, rgba_o, nrm_o, tag):
     hit = rgba[..., 3] == 255
     assert np.array_equal(rgba[..., 3], rgba_o[..., 3]), f"{tag}: hit mask differs"
-    # colour / shading within 1 LSB (log-odds probability state)
-    assert np.abs(rgba.astype(int) - rgba_o).max() <= 1, tag
-    assert np.abs(nrm.astype(int) - nrm_o).max() <= 1, tag
+    # colour / shading blend with the probability: bit-exact (the reference's own chain)
+    np.testing.assert_array_equal(rgba, rgba_o, err_msg=tag)
+    np.testing.assert_array_equal(nrm, nrm_o, err_msg=tag)
     return hit.mean()
 
 

@@ -7,7 +7,7 @@
  - the reference's largest frame, MAX_IMG = 1920x1080 (voxel_tsdf.cu:10-12), and frames larger
    than the engine was sized for (rejected, volume untouched);
  - device-resident (torch) frames give the same volume as host frames.
-Entries, pool indices, free stack, tsdf, colour and weight bit-exact; prob within 1e-4.
+Entries, pool indices, free stack, tsdf, colour, weight and probability bit-exact.
 """
 import numpy as np
 import pytest

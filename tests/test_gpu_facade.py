@@ -45,7 +45,7 @@ def test_tsdf_system_matches_oracle(tmp_path, semantic):
     (_, _), (q, t) = synth.pose(n - 1)
     _, nrm = ora.raycast(cam.K, W, H, q, t, 4.0)
     got_n = np.fromfile(tmp_path / "out_render.bin", np.uint8).reshape(H, W, 4)
-    assert np.abs(got_n.astype(int) - nrm).max() <= 1
+    np.testing.assert_array_equal(got_n, nrm)
     ora.close()
 
 

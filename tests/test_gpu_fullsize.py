@@ -158,14 +158,13 @@ def test_bench_stream_oracle_parity_120_frames_pipelined():
     does -- pipelined k_frame launches, nothing read between frames -- against the CPU oracle: the
     running totals of visible / updated / deleted blocks and voxels, the hash table, free stack and
     every voxel at frames 40, 80 and 120 (each compare completes the pending frames). By frame 120
-    much of the surface sits at the weight cap (40), so the log-odds state's probability bound (1e-4,
-    DESIGN.md 2) is checked at capped weight over a long orbit."""
+    much of the surface sits at the weight cap (40): the probability stays bit-exact at capped weight
+    over a long orbit."""
     import torch
 
     import tsdf_amd
     from tsdf_amd import synth
     from _oracle import OracleGrid
-    from test_gpu_parity import PROB_TOL
 
     def host(x):
         return x.cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
@@ -198,7 +197,6 @@ def test_bench_stream_oracle_parity_120_frames_pipelined():
         live = d["entry_idx"][d["entry_idx"] >= 0]
         w = d["rgbw"].reshape(-1, 512, 4)[live, :, 3]
         assert (w == 40).sum() > 100000, "the long orbit should drive many voxels to the weight cap"
-        assert PROB_TOL <= 1e-4
         assert eng.stats()["active_blocks"] > 8000
     finally:
         eng.close()

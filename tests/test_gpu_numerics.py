@@ -14,6 +14,9 @@ The integrate and ingest kernels replace the 11-op IEEE divide where an exact sh
  - f2i / f2s / f2u8 via v_cvt_{i,u}32_f32, and round_s16 (= f2s(roundf(f)), the raycast's voxel
    rounding) -- checked on every float bit pattern.
 Each must agree bit for bit with the correctly rounded divide / cvt.rzi semantics.
+And the semantic update's sem_logf / sem_expf (and the update's unit-interval logf form) must return
+the oracle's bits (oracle/ora_math.c) for EVERY float input: digests of all 2^32 results per function,
+in chunks of 2^24, against the committed oracle digests (tests/golden/sem_math_digests.json).
 """
 import ctypes as C
 import os
@@ -41,6 +44,7 @@ def lib():
     L.tsdf_selfcheck_convert.argtypes = [u32, u32, P64, P32]
     L.tsdf_selfcheck_quot_cmp.argtypes = [u32, u64, f, f, f, P64, P32]
     L.tsdf_selfcheck_div_pair.argtypes = [f, u32, u32, u32, u64, f, f, P64, P32]
+    L.tsdf_selfcheck_sem_digest.argtypes = [C.c_int, u64, u64, P64]
     return L
 
 
@@ -107,3 +111,18 @@ def test_div_pair_sweep(lib, b):
 def test_div_pair_random(lib, bmin, bmax):
     bad, first = _run(lib.tsdf_selfcheck_div_pair, 0.0, 0, 0, 4242, 1 << 28, bmin, bmax)
     assert bad == 0, f"{bad} mismatches, first sample {first}"
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_semantic_math_matches_oracle_on_every_input(lib, kind):
+    """kind 0: sem_logf (pixels' ht / lt), 1: sem_expf, 2: the update's logf of p and 1 - p (inputs
+    [0, 1] and NaN): every chunk's digest equals the oracle's."""
+    import json
+    dig = json.load(open(os.path.join(ROOT, "tests", "golden", "sem_math_digests.json")))[str(kind)]
+    bad = []
+    for lo, hi, d in dig:
+        got = C.c_ulonglong()
+        assert lib.tsdf_selfcheck_sem_digest(kind, lo, hi, C.byref(got)) == 0
+        if got.value != int(d):
+            bad.append((hex(lo), hex(hi)))
+    assert not bad, f"{len(bad)} chunks differ from the oracle, first {bad[:4]}"

@@ -4,7 +4,7 @@ their key and carve-candidate slots by device copies where a multi-GPU job all-g
 
 The bar (SURVEY 8e "compared to single-GPU as sets keyed by block position"):
 the union of the shards equals the UNSHARDED volume -- the same live block positions, every voxel's
-tsdf / rgb / weight bit-identical, probability within 1e-4 -- and every shard's hash index equals
+tsdf / rgb / weight / probability bit-identical -- and every shard's hash index equals
 the unsharded table. Each shard is also bit-exact against the oracle's sharded restatement
 (tests/_shards.py: pool indices and free stacks included). The configurations are ones where
 keys of different owners contend for bucket locks (the oracle counts those cross-shard lock
