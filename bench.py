@@ -81,6 +81,9 @@ def parse():
                    help="sharded modes: carve-candidate records per rank per frame (0 = 16384 / G)")
     p.add_argument("--cpu-frames", type=int, default=-1, help="oracle sample size (-1 = auto)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-cpp-loop", action="store_true",
+                   help="skip the C++ timed loop over the C ABI (disinfect-slam_amd/bench_main) that the "
+                        "single-GPU C3 line runs after its own loop (the host enqueue floor without Python)")
     p.add_argument("--broadcast-frames", dest="broadcast_frames", action="store_true", default=None,
                    help="sharded modes: rank 0 broadcasts every frame to the other ranks inside the timed "
                         "loop (one camera feeding the node) -- the default with the nccl backend")
@@ -486,6 +489,9 @@ def main():
     bcast = None
     if world > 1 and mode in ("routed", "sharded"):
         bcast = frame_broadcast_ms(a, dist, None, dev)
+    cpp = None
+    if rank == 0 and world == 1 and a.loop == "c3" and not a.graph and not a.host_frames and not a.no_cpp_loop:
+        cpp = cpp_loop(a, cam, nframes)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         fr_host = synth.render_torch(cam, list(range(0, min(nframes, 80))), device=dev)
@@ -578,6 +584,8 @@ def main():
         }
         if ray is not None:
             out["raycast"] = ray
+        if cpp is not None:
+            out["cpp_loop"] = cpp
         if upload is not None:
             out["host_frames"] = upload
         if world > 1:
@@ -591,6 +599,43 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def cpp_loop(a, cam, nframes):
+    """The same stream and timed window through disinfect-slam_amd/bench_main (C++, the C ABI with
+    device frames on the engine's own stream, no Python in the loop): frames/s and the host enqueue per
+    frame -- the facade's own overhead, beside the Python line's host_enqueue_ms_per_step. The frames
+    are this bench's (synth.render_torch), written to a scratch directory for the child process."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    from tsdf_amd import synth
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "disinfect-slam_amd", "bench_main")
+    if not os.path.exists(exe):
+        return {"skipped": "bench_main not built"}
+    n = a.warmup + a.steps
+    fr = synth.render_torch(cam, list(range(0, n)), device="cuda")
+    d = tempfile.mkdtemp(prefix="tsdf_cpp_loop_")
+    try:
+        lines = [f"{a.width} {a.height} {n} " + " ".join(repr(float(v)) for v in cam.K) +
+                 f" {a.voxel} {a.trunc} {a.max_depth} {int(not a.depth_only)} {a.block_bits}"]
+        for i in range(n):
+            for k in ("rgb", "depth", "ht", "lt"):
+                fr[k][i].cpu().numpy().tofile(os.path.join(d, f"f{i}_{k}.bin"))
+            lines.append(" ".join(repr(float(v)) for v in list(fr["q"][i]) + list(fr["t"][i])))
+        with open(os.path.join(d, "meta.txt"), "w") as f:
+            f.write("\n".join(lines) + "\n")
+        del fr
+        r = subprocess.run([exe, d, str(a.warmup), str(a.steps)], capture_output=True, text=True, timeout=120)
+        if r.returncode != 0:
+            return {"failed": (r.stdout + r.stderr)[-400:]}
+        out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+        out["what"] = ("bench_main: this line's stream and window through the C ABI from C++ (tsdf_integrate "
+                       "with device frames, tsdf_flush, tsdf_synchronize; no Python) -- the host enqueue floor")
+        return out
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def host_frames(a, fr, reps=20):

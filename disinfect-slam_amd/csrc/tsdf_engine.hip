@@ -399,9 +399,11 @@ int launch_resolve_alloc(tsdf_engine* e, const FrameParams& P, uint32_t range, i
 
 // the engine stream waits for a raycast still running on the render stream
 // (keep_deferred: a deferred raycast stays pending -- tsdf_stream_wait orders the engine stream after
-// another stream's work, which the raycast may follow as well)
-int join_render(tsdf_engine* e, bool keep_deferred = false) {
-  if (e->rdg.pending && !keep_deferred) {  // (a graph frame's deferred raycast: its args slot)
+// another stream's work, which the raycast may follow as well; wait_overlap false: launch the deferred
+// raycasts only, without joining a TSDF_RENDER_OVERLAP raycast on the render stream -- the next
+// frame's ingest writes nothing it reads; keep_graph: the graph frame that renders rdg itself calls)
+int join_render(tsdf_engine* e, bool keep_deferred = false, bool wait_overlap = true, bool keep_graph = false) {
+  if (e->rdg.pending && !keep_deferred && !keep_graph) {  // (a graph frame's deferred raycast: its args slot)
     e->rdg.pending = false;
     const dim3 rgrid((e->rdg.W + 15) / 16, (e->rdg.H + 15) / 16);
     hipLaunchKernelGGL(k_raycast_g, rgrid, dim3(256), 0, e->stream, e->D, e->rdg.args);
@@ -415,7 +417,7 @@ int join_render(tsdf_engine* e, bool keep_deferred = false) {
                        r.normal);
     HIP_OK(hipGetLastError());
   }
-  if (!e->render_pending) return TSDF_OK;
+  if (!e->render_pending || !wait_overlap) return TSDF_OK;
   e->render_pending = false;
   HIP_OK(hipStreamWaitEvent(e->stream, e->rs_done, 0));
   return TSDF_OK;
@@ -495,6 +497,7 @@ const char* tsdf_error_string(int code) {
   }
 }
 const char* tsdf_last_error(void) { return g_last_error.c_str(); }
+void tsdf_set_last_error(const char* what) { g_last_error = what ? what : ""; }
 
 uint32_t tsdf_hash_block(int16_t x, int16_t y, int16_t z) { return hash_block(x, y, z); }
 int32_t tsdf_block_owner(int16_t x, int16_t y, int16_t z, int32_t n) {
@@ -873,7 +876,11 @@ int frame_ingest(tsdf_engine* e, const EngineDev& Dv, const tsdf_frame* f, const
     LAUNCH_OK("k_render_ingest");
     return TSDF_OK;
   }
-  JOIN_RENDER(e);  // (a deferred raycast this ingest cannot take up)
+  {  // a deferred raycast this ingest cannot take up runs first; a TSDF_RENDER_OVERLAP raycast on the
+     // render stream keeps overlapping this ingest (it writes nothing the raycast reads; the update joins it)
+    int rc = join_render(e, false, false);
+    if (rc) return rc;
+  }
   if (e->maxs <= 3)
     hipLaunchKernelGGL(k_ingest_dda<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, s, Dv, *P, depth,
                        rgb, ht, lt, tiles_x, tiles);
@@ -1232,16 +1239,12 @@ int tsdf_integrate_shard_end(tsdf_engine* e, const void* cands_in, int32_t cand_
 // (cands_in: the all-gathered slots of call n - 1), frame n - 1's allocation and update (its
 // candidates into cands_out, for the exchange after this call), frame n's ingest.
 // ---------------------------------------------------------------------------------------------
-int tsdf_integrate_shard_pipe(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
-                              const tsdf_pose* pose, float max_depth, const void* cands_in, void* cands_out,
-                              int32_t cand_cap, int32_t* pending) {
-  TraceRange trace_("tsdf_integrate_shard_pipe");
-  if (!e || !sharded(e) || e->shard_phase != 0 || !cands_in || !cands_out || cand_cap < 1 || !pending ||
-      (f && (!K || !pose)) || e->maxs > 3) {
-    set_error("tsdf_integrate_shard_pipe: invalid argument (a shard engine between frames, both slots, "
-              "<= 3 DDA samples per pixel)");
-    return TSDF_ERR_INVALID_ARG;
-  }
+// tsdf_integrate_shard_pipe, and a group's form (dsts: the update's last workgroup writes the
+// candidate slot into the ndst device slots listed at dsts -- a device array; dsts_host: the same
+// pointers, for the zeroed headers of the first call -- instead of cands_out)
+static int shard_pipe_impl(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K, const tsdf_pose* pose,
+                           float max_depth, const void* cands_in, void* cands_out, ShardRec* const* dsts,
+                           ShardRec* const* dsts_host, int ndst, int32_t cand_cap, int32_t* pending) {
   HIP_OK(hipSetDevice(e->device));
   JOIN_RENDER(e);
   *pending = 0;
@@ -1250,6 +1253,8 @@ int tsdf_integrate_shard_pipe(tsdf_engine* e, const tsdf_frame* f, const tsdf_in
   auto shard_args = [&](PipeArgs& A) {
     A.cands_in = A.has_carve ? in : nullptr;
     A.cands_out = A.has_update ? out : nullptr;
+    A.cands_dst = A.has_update ? dsts : nullptr;
+    A.ndst = ndst;
     A.cand_cap = cand_cap;
     A.nshard = e->cfg.shard_count;
   };
@@ -1293,7 +1298,11 @@ int tsdf_integrate_shard_pipe(tsdf_engine* e, const tsdf_frame* f, const tsdf_in
     hipLaunchKernelGGL(k_ingest_dda<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, e->stream, Dv, P, P.depth,
                        P.rgb, P.ht, P.lt, tiles_x, tiles);
     LAUNCH_OK("k_ingest_dda");
-    HIP_OK(hipMemsetAsync(out, 0, sizeof(ShardRec), e->stream));  // (no candidates from this call)
+    if (dsts_host) {  // (no candidates from this call)
+      for (int d = 0; d < ndst; ++d) HIP_OK(hipMemsetAsync(dsts_host[d], 0, sizeof(ShardRec), e->stream));
+    } else {
+      HIP_OK(hipMemsetAsync(out, 0, sizeof(ShardRec), e->stream));
+    }
     if (ev) --e->ev_used;
     e->ps = tsdf_engine::kPipeU;
     e->p_fid = fid;
@@ -1306,6 +1315,37 @@ int tsdf_integrate_shard_pipe(tsdf_engine* e, const tsdf_frame* f, const tsdf_in
   if (rc) return rc;
   pipe_advance(e, fid, P);
   return upload_release(e);
+}
+
+// the group's entry (csrc/tsdf_group.hip, declared in csrc/tsdf_internal.h): tsdf_integrate_shard_pipe
+// with the candidate slot written into the ndst slots at dsts_dev (device array) instead of an
+// outgoing slot
+int tsdf_integrate_shard_pipe_fanout(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
+                                     const tsdf_pose* pose, float max_depth, const void* cands_in,
+                                     void* const* dsts_dev, void* const* dsts_host, int ndst, int32_t cand_cap,
+                                     int32_t* pending) {
+  TraceRange trace_("tsdf_integrate_shard_pipe_fanout");
+  if (!e || !sharded(e) || e->shard_phase != 0 || !cands_in || !dsts_dev || !dsts_host || ndst < 1 ||
+      cand_cap < 1 || !pending || (f && (!K || !pose)) || e->maxs > 3) {
+    set_error("tsdf_integrate_shard_pipe_fanout: invalid argument");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  ShardRec* self = reinterpret_cast<ShardRec*>(dsts_host[e->cfg.shard_index % ndst]);
+  return shard_pipe_impl(e, f, K, pose, max_depth, cands_in, self, reinterpret_cast<ShardRec* const*>(dsts_dev),
+                         reinterpret_cast<ShardRec* const*>(dsts_host), ndst, cand_cap, pending);
+}
+
+int tsdf_integrate_shard_pipe(tsdf_engine* e, const tsdf_frame* f, const tsdf_intrinsics* K,
+                              const tsdf_pose* pose, float max_depth, const void* cands_in, void* cands_out,
+                              int32_t cand_cap, int32_t* pending) {
+  TraceRange trace_("tsdf_integrate_shard_pipe");
+  if (!e || !sharded(e) || e->shard_phase != 0 || !cands_in || !cands_out || cand_cap < 1 || !pending ||
+      (f && (!K || !pose)) || e->maxs > 3) {
+    set_error("tsdf_integrate_shard_pipe: invalid argument (a shard engine between frames, both slots, "
+              "<= 3 DDA samples per pixel)");
+    return TSDF_ERR_INVALID_ARG;
+  }
+  return shard_pipe_impl(e, f, K, pose, max_depth, cands_in, cands_out, nullptr, nullptr, 0, cand_cap, pending);
 }
 
 int tsdf_integrate_shard_abort(tsdf_engine* e) {
@@ -1366,32 +1406,44 @@ namespace {
 // (|direction| = 1 up to rounding), plus the binary search, the +-1 gradient neighbours and the
 // rounding to the nearest voxel (2.5 voxels). n = 0 (hash lookups) when the cube would exceed
 // kViewMaxN cells per axis, the brick bitmap `lds_words` of LDS, or the pool a cell's index bits.
-int view_grid_for(tsdf_engine* e, const FrameParams& P, float step_size, int lds_words, ViewGrid* V);
-// whether view_grid_for(P) would clear or reallocate the grid's cells (a deferred raycast reading the
-// previous grid must run first)
-bool view_grid_resets(const tsdf_engine* e, const FrameParams& P, float step_size) {
+// The cube's shape for a camera: ok = false when a view grid does not apply (hash lookups)
+struct ViewShape {
+  bool ok = false;
+  int n = 0, nb = 0, ns = 0, nbw = 0, nw = 0, half = 0;
+  int64_t cells = 0;  // brick-major (view_cell)
+};
+void view_shape(const tsdf_engine* e, const FrameParams& P, float step_size, int lds_words, ViewShape* out) {
+  ViewShape& S = *out;
+  S = ViewShape{};
   const double max_step = std::ceil((double)P.max_depth / (double)step_size);
   const double reach = max_step * (double)step_size / (double)P.voxel * (1.0 + 1e-5) + 2.5;
-  if (!(reach < 1e6)) return false;
-  const int half = (int)std::ceil(reach / kBlockLen) + 1;
-  const int nb = (2 * half + 1 + 3) / 4;
-  return e->vg_gen == kViewGenMax || (int64_t)nb * nb * nb * 64 > e->vg_cap;
+  if (!(reach < 1e6)) return;
+  S.half = (int)std::ceil(reach / kBlockLen) + 1;
+  S.n = 2 * S.half + 1;
+  S.nb = (S.n + 3) / 4;
+  S.ns = (S.nb + 3) / 4;
+  S.nbw = (S.nb * S.nb * S.nb + 31) / 32;
+  S.nw = S.nbw + (S.ns * S.ns * S.ns + 31) / 32;
+  S.cells = (int64_t)S.nb * S.nb * S.nb * 64;
+  S.ok = S.n <= kViewMaxN && S.nw <= lds_words && e->D.nblocks <= (1 << kViewIdxBits);
+}
+// whether view_grid_for(P) would clear or reallocate the grid's cells (a deferred raycast reading the
+// previous grid must run first): the same shape and the same two conditions view_grid_for acts on
+bool view_grid_resets(const tsdf_engine* e, const FrameParams& P, float step_size, int lds_words) {
+  ViewShape S;
+  view_shape(e, P, step_size, lds_words, &S);
+  return S.ok && (S.cells > e->vg_cap || e->vg_gen == kViewGenMax);
 }
 
 int view_grid_for(tsdf_engine* e, const FrameParams& P, float step_size, int lds_words, ViewGrid* V) {
   *V = ViewGrid{};
   V->flags = e->vg_flags;
   V->bits = e->vg_bits;
-  const double max_step = std::ceil((double)P.max_depth / (double)step_size);
-  const double reach = max_step * (double)step_size / (double)P.voxel * (1.0 + 1e-5) + 2.5;
-  const int half = (int)std::ceil(reach / kBlockLen) + 1;
-  const int n = 2 * half + 1;
-  const int nb = (n + 3) / 4, ns = (nb + 3) / 4;
-  const int nbw = (nb * nb * nb + 31) / 32, nw = nbw + (ns * ns * ns + 31) / 32;
-  if (!(reach < 1e6) || n > kViewMaxN || nw > lds_words ||
-      e->D.nblocks > (1 << kViewIdxBits))
-    return TSDF_OK;
-  const int64_t cells = (int64_t)nb * nb * nb * 64;  // brick-major (view_cell)
+  ViewShape S;
+  view_shape(e, P, step_size, lds_words, &S);
+  if (!S.ok) return TSDF_OK;
+  const int n = S.n, nb = S.nb, ns = S.ns, nbw = S.nbw, nw = S.nw, half = S.half;
+  const int64_t cells = S.cells;
   if (cells > e->vg_cap) {
     if (e->vg_cell) HIP_OK(hipFree(e->vg_cell));
     e->vg_cell = nullptr;
@@ -1734,16 +1786,15 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
-  // this graph's deferred raycast of the previous frame: rendered by this launch (k_render_ingest_g)
-  const FrameArgs* prev = nullptr;
-  if (g->defer && e->rdg.pending && e->rdg.g == g) {
-    prev = e->rdg.args;
-    e->rdg.pending = false;
+  // this graph's deferred raycast of the previous frame: rendered by this launch (k_render_ingest_g).
+  // It stays pending (a later call launches it) until the graph launch below, so an error return on
+  // the way leaves it to the engine's next call instead of dropping its images.
+  const FrameArgs* prev = (g->defer && e->rdg.pending && e->rdg.g == g) ? e->rdg.args : nullptr;
+  {
+    int rc = join_render(e, false, true, prev != nullptr);  // (not the raycast this launch takes)
+    if (!rc && !g->pipe) rc = flush_pending(e);  // (pipelined: the pending frames continue in this launch)
+    if (rc) return rc;
   }
-  if (g->pipe)
-    JOIN_RENDER(e);  // (the pending frames continue in this launch)
-  else
-    ENTER(e);
   const int k = g->next;
   g->next = (k + 1) % tsdf_graph::kSlots;
   if (g->used[k]) HIP_OK(hipEventSynchronize(g->done[k]));  // slot k's upload has run
@@ -1758,7 +1809,8 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
   a.normal = reinterpret_cast<uchar4*>(normal);
   a.step_size = e->cfg.truncation / 2;
   if (g->RW) {
-    if (prev && view_grid_resets(e, a.R, a.step_size)) {  // (the pending raycast reads the old grid)
+    if (prev && view_grid_resets(e, a.R, a.step_size, kViewGraphBitmapWords)) {  // (it reads the old grid)
+      e->rdg.pending = false;
       hipLaunchKernelGGL(k_raycast_g, dim3((g->RW + 15) / 16, (g->RH + 15) / 16), dim3(256), 0, e->stream, e->D,
                          prev);
       LAUNCH_OK("k_raycast_g");
@@ -1784,6 +1836,7 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
     finish_args(e, a.pipe, a.Pu);
     if (e->profiling && a.pipe.has_update) ++e->prof_pipelined;
   }
+  if (prev) e->rdg.pending = false;  // rendered by this launch
   HIP_OK(hipGraphLaunch(g->exec[k][0], e->stream));
   if (g->defer) {
     // a view grid's raycast waits for the next launch; a hash-lookup raycast (no grid: it reads the

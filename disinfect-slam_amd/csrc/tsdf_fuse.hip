@@ -45,9 +45,11 @@ __device__ __forceinline__ void frame_end(const EngineDev& D) {
 // a shard's frame: its carve candidates into the exchange slot, then the owned entries its
 // exhausted pool left without voxels this frame (D.pend, written by the allocation resolver before
 // this launch)
-// (cand / ncand: the frame's candidate list, D.cand / D.ncand of its view)
+// (cand / ncand: the frame's candidate list, D.cand / D.ncand of its view). dsts (a group's frame,
+// tsdf_group_*): the slot is written into each of the ndst destinations instead -- this shard's slot in
+// every shard's inbox, across GPUs by peer stores -- so no exchange runs between the launches.
 __device__ __forceinline__ void pack_cands_wg(const EngineDev& D, const VisRec* cand, const int32_t* ncand, ShardRec* __restrict__ out,
-                              int cap) {
+                              int cap, ShardRec* const* dsts = nullptr, int ndst = 0) {
   const int nc = ld_co(ncand);
   const int np = min(ld_co(&D.ctr->n_pend), (int)kNewKeyCap);
   const int n = nc + np;
@@ -69,12 +71,20 @@ __device__ __forceinline__ void pack_cands_wg(const EngineDev& D, const VisRec* 
     r.pad = 0;
     r.val = (uint32_t)(b >> 32);  // hash entry
     r.zero = 0u;
-    out[1 + i] = r;
+    if (dsts) {
+      for (int d = 0; d < ndst; ++d) dsts[d][1 + i] = r;
+    } else {
+      out[1 + i] = r;
+    }
   }
   if (threadIdx.x == 0) {
     ShardRec h{};
     h.val = (uint32_t)min(n, cap);
-    out[0] = h;
+    if (dsts) {
+      for (int d = 0; d < ndst; ++d) dsts[d][0] = h;
+    } else {
+      out[0] = h;
+    }
     if (n > cap) atomicOr(&D.ctr->status, 16u);  // TSDF_STATUS_SHARD_OVERFLOW
   }
 }
@@ -1207,7 +1217,7 @@ __device__ __forceinline__ void pipe_update(const EngineDev& D, const FrameParam
     const uint32_t idx = (uint32_t)(kind ? nold + wi : wi);  // (this workgroup among the update's)
     if (arrive_last(D.arrive + kArrIntegrate, 0ull, &s_last, true, (uint32_t)(nold + nfr), idx)) {
       if (t0) arrive_reset(D.arrive + kArrIntegrate);
-      pack_cands_wg(D, cand, ncand, A.cands_out, A.cand_cap);
+      pack_cands_wg(D, cand, ncand, A.cands_out, A.cand_cap, A.cands_dst, A.ndst);
     }
   }
 }

@@ -145,6 +145,10 @@ struct PipeArgs {
   const struct ShardRec* cands_in;
   struct ShardRec* cands_out;
   int cand_cap, nshard;
+  // a group's frame (tsdf_group_*): the update's last workgroup writes the slot into each of these
+  // ndst slots (device array: this shard's slot of every shard's inbox) instead of cands_out
+  struct ShardRec* const* cands_dst;
+  int ndst;
 };
 // frame f's view of the engine: its visible lists, their counts, its carve candidates and count
 __device__ __host__ __forceinline__ EngineDev frame_view(const EngineDev& D, uint32_t f) {

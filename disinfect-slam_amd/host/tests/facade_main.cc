@@ -4,8 +4,11 @@
 //                    then per frame: qx qy qz qw tx ty tz
 //   <dir>/f<i>_{rgb,depth,ht,lt}.bin
 // Outputs: <dir>/out_query.bin (GatherValid voxels), out_render.bin (RayCast normal of the last
-// pose), out_stats.txt.
+// pose), out_stats.txt. facade_main <dir> <G>: the same through a volume sharded over G shards of
+// device 0 (TSDFSystem's group constructor, tsdf_group_*).
 #include <cstdio>
+#include <cstdlib>
+#include <memory>
 #include <fstream>
 #include <iostream>
 #include <string>
@@ -23,10 +26,11 @@ static std::vector<uint8_t> read_file(const std::string& p) {
 
 int main(int argc, char** argv) {
   if (argc < 2) {
-    std::cerr << "usage: facade_main <dir>\n";
+    std::cerr << "usage: facade_main <dir> [shards]\n";
     return 2;
   }
   const std::string dir = argv[1];
+  const int shards = argc > 2 ? std::atoi(argv[2]) : 1;
   std::ifstream meta(dir + "/meta.txt");
   int W, H, n, semantic, nb_bits;
   float fx, fy, cx, cy, voxel, trunc, max_depth;
@@ -50,7 +54,10 @@ int main(int argc, char** argv) {
   tsdf_stats st;
   {
     // extrinsics = identity; the poses are the cam_T_world of the stream
-    TSDFSystem sys(cfg, 0, max_depth, K);
+    std::unique_ptr<TSDFSystem> sysp =
+        shards > 1 ? std::make_unique<TSDFSystem>(cfg, std::vector<int>(shards, 0), max_depth, K)
+                   : std::make_unique<TSDFSystem>(cfg, 0, max_depth, K);
+    TSDFSystem& sys = *sysp;
     std::vector<std::vector<uint8_t>> keep;
     for (int i = 0; i < n; ++i) {
       const std::string p = dir + "/f" + std::to_string(i) + "_";

@@ -21,6 +21,14 @@ TSDFSystem::TSDFSystem(const tsdf_config& cfg, int device, float max_depth,
       cam_T_posecam_(extrinsics),
       t_(&TSDFSystem::Run, this) {}
 
+TSDFSystem::TSDFSystem(const tsdf_config& cfg, const std::vector<int>& devices, float max_depth,
+                       const CameraIntrinsics<float>& intrinsics, const SE3<float>& extrinsics)
+    : tsdf_(cfg, devices),
+      max_depth_(max_depth),
+      intrinsics_(intrinsics),
+      cam_T_posecam_(extrinsics),
+      t_(&TSDFSystem::Run, this) {}
+
 TSDFSystem::~TSDFSystem() {
   {
     std::lock_guard<std::mutex> lock(mtx_queue_);
@@ -76,7 +84,7 @@ void TSDFSystem::Flush() {
   std::unique_lock<std::mutex> lock(mtx_queue_);
   cv_idle_.wait(lock, [&] { return inputs_.empty() && !busy_; });
   std::lock_guard<std::mutex> lr(mtx_read_);
-  check_tsdf(tsdf_synchronize(tsdf_.engine()), "tsdf_synchronize");
+  tsdf_.Synchronize();
 }
 
 tsdf_stats TSDFSystem::Stats() {

@@ -41,6 +41,11 @@ class TSDFSystem {
   TSDFSystem(const tsdf_config& cfg, int device, float max_depth,
              const CameraIntrinsics<float>& intrinsics,
              const SE3<float>& extrinsics = SE3<float>::Identity());
+  // one volume spatially sharded over `devices` (TSDFGrid's group constructor): a C++ caller gets a
+  // multi-GPU (or multi-shard) volume without Python or a collective library
+  TSDFSystem(const tsdf_config& cfg, const std::vector<int>& devices, float max_depth,
+             const CameraIntrinsics<float>& intrinsics,
+             const SE3<float>& extrinsics = SE3<float>::Identity());
   ~TSDFSystem();
 
   void Integrate(const SE3<float>& posecam_T_world, const Mat& img_rgb, const Mat& img_depth,

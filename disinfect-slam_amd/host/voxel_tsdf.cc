@@ -25,8 +25,21 @@ TSDFGrid::TSDFGrid(const tsdf_config& cfg, int device)
   check_tsdf(tsdf_create(&cfg, device, &engine_), "tsdf_create");
 }
 
+TSDFGrid::TSDFGrid(const tsdf_config& cfg, const std::vector<int>& devices)
+    : voxel_size_(cfg.voxel_size), truncation_(cfg.truncation) {
+  check_tsdf(tsdf_group_create(&cfg, devices.data(), (int)devices.size(), &group_), "tsdf_group_create");
+}
+
 TSDFGrid::~TSDFGrid() {
   if (engine_) tsdf_destroy(engine_);
+  if (group_) tsdf_group_destroy(group_);
+}
+
+void TSDFGrid::Synchronize() {
+  if (group_)
+    check_tsdf(tsdf_group_synchronize(group_), "tsdf_group_synchronize");
+  else
+    check_tsdf(tsdf_synchronize(engine_), "tsdf_synchronize");
 }
 
 static tsdf_pose to_pose(const SE3<float>& T) {
@@ -56,7 +69,10 @@ void TSDFGrid::Integrate(const Mat& img_rgb, const Mat& img_depth, const Mat& im
   f.mem_kind = TSDF_MEM_HOST;
   const tsdf_intrinsics K{intrinsics.fx, intrinsics.fy, intrinsics.cx, intrinsics.cy};
   const tsdf_pose P = to_pose(cam_T_world);
-  check_tsdf(tsdf_integrate(engine_, &f, &K, &P, max_depth), "tsdf_integrate");
+  if (group_)
+    check_tsdf(tsdf_group_integrate(group_, &f, &K, &P, max_depth), "tsdf_group_integrate");
+  else
+    check_tsdf(tsdf_integrate(engine_, &f, &K, &P, max_depth), "tsdf_integrate");
 }
 
 void TSDFGrid::FeedRGBD(const Mat& img_rgb, const Mat& img_depth_raw, const Mat& mask, float depth_factor,
@@ -66,6 +82,7 @@ void TSDFGrid::FeedRGBD(const Mat& img_rgb, const Mat& img_depth_raw, const Mat&
       img_rgb.rows != img_depth_raw.rows ||
       (!mask.empty() && (mask.type() != CV_8UC1 || mask.total() != img_depth_raw.total())))
     throw std::invalid_argument("TSDFGrid::FeedRGBD: expects CV_8UC3 rgb, CV_16UC1 depth, CV_8UC1 mask");
+  if (group_) throw std::invalid_argument("TSDFGrid::FeedRGBD: not available on a sharded volume");
   const tsdf_intrinsics K{intrinsics.fx, intrinsics.fy, intrinsics.cx, intrinsics.cy};
   const tsdf_pose P = to_pose(cam_T_world);
   check_tsdf(tsdf_feed_rgbd_frame(engine_, img_rgb.ptr<uint8_t>(), img_depth_raw.ptr<uint16_t>(),
@@ -82,18 +99,24 @@ void TSDFGrid::RayCast(float max_depth, const CameraParams& cam, const SE3<float
     *normal = Mat(cam.img_h, cam.img_w, CV_8UC4);
   const tsdf_intrinsics K{cam.intrinsics.fx, cam.intrinsics.fy, cam.intrinsics.cx, cam.intrinsics.cy};
   const tsdf_pose P = to_pose(cam_T_world);
-  check_tsdf(tsdf_raycast(engine_, &K, cam.img_w, cam.img_h, &P, max_depth,
-                          rgba ? rgba->data : nullptr, normal ? normal->data : nullptr, TSDF_MEM_HOST),
-             "tsdf_raycast");
+  if (group_)
+    check_tsdf(tsdf_group_raycast(group_, &K, cam.img_w, cam.img_h, &P, max_depth, rgba ? rgba->data : nullptr,
+                                  normal ? normal->data : nullptr, TSDF_MEM_HOST),
+               "tsdf_group_raycast");
+  else
+    check_tsdf(tsdf_raycast(engine_, &K, cam.img_w, cam.img_h, &P, max_depth,
+                            rgba ? rgba->data : nullptr, normal ? normal->data : nullptr, TSDF_MEM_HOST),
+               "tsdf_raycast");
 }
 
 std::vector<VoxelSpatialTSDF> TSDFGrid::Query(const float* bounds) {
   int64_t n = 0;
-  check_tsdf(tsdf_query(engine_, bounds, nullptr, 0, &n), "tsdf_query");
+  auto query = [&](tsdf_voxel* o, int64_t cap) {
+    return group_ ? tsdf_group_query(group_, bounds, o, cap, &n) : tsdf_query(engine_, bounds, o, cap, &n);
+  };
+  check_tsdf(query(nullptr, 0), "tsdf_query");
   std::vector<VoxelSpatialTSDF> out((size_t)n);
-  if (n)
-    check_tsdf(tsdf_query(engine_, bounds, reinterpret_cast<tsdf_voxel*>(out.data()), n, &n),
-               "tsdf_query");
+  if (n) check_tsdf(query(reinterpret_cast<tsdf_voxel*>(out.data()), n), "tsdf_query");
   return out;
 }
 
@@ -106,7 +129,10 @@ std::vector<VoxelSpatialTSDF> TSDFGrid::GatherVoxels(const BoundingCube<float>& 
 
 tsdf_stats TSDFGrid::Stats(bool clear_status) {
   tsdf_stats s;
-  check_tsdf(tsdf_get_stats(engine_, &s, clear_status ? 1 : 0), "tsdf_get_stats");
+  if (group_)
+    check_tsdf(tsdf_group_get_stats(group_, &s, clear_status ? 1 : 0), "tsdf_group_get_stats");
+  else
+    check_tsdf(tsdf_get_stats(engine_, &s, clear_status ? 1 : 0), "tsdf_get_stats");
   return s;
 }
 

@@ -15,6 +15,10 @@ class TSDFGrid {
   // (2^18 blocks, images up to 1920x1080), overridable through cfg.
   TSDFGrid(float voxel_size, float truncation);
   TSDFGrid(const tsdf_config& cfg, int device = 0);
+  // one volume spatially sharded over `devices` (one shard per entry; a device may repeat), the
+  // exchange inside the library (tsdf_group_*): same results as one volume. FeedRGBD is not
+  // available on a sharded volume (integrate the preprocessed frame).
+  TSDFGrid(const tsdf_config& cfg, const std::vector<int>& devices);
   ~TSDFGrid();
   TSDFGrid(const TSDFGrid&) = delete;
   TSDFGrid& operator=(const TSDFGrid&) = delete;
@@ -40,11 +44,15 @@ class TSDFGrid {
   std::vector<VoxelSpatialTSDF> GatherVoxels(const BoundingCube<float>& volumn);  // :427-454
 
   tsdf_stats Stats(bool clear_status = false);
-  tsdf_engine* engine() { return engine_; }
+  tsdf_engine* engine() { return engine_; }  // (NULL for a sharded volume)
+  tsdf_group* group() { return group_; }      // (NULL for one engine)
+  // block until every integrated frame is in the volume
+  void Synchronize();
 
  private:
   std::vector<VoxelSpatialTSDF> Query(const float* bounds);
   tsdf_engine* engine_ = nullptr;
+  tsdf_group* group_ = nullptr;
   float voxel_size_, truncation_;
 };
 

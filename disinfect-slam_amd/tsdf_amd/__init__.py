@@ -190,6 +190,7 @@ class FrameGraph:
         fn = "tsdf_graph_create_deferred" if deferred else "tsdf_graph_create"
         _lib.check(getattr(_lib.load(), fn)(eng._h, width, height, render_width, render_height, C.byref(h)), fn)
         self._g = h
+        self.deferred = deferred
 
     def frame(self, rgb, depth, ht, lt, K, cam_T_world, max_depth, render_K=None,
               render_cam_T_world=None, rgba=None, normal=None):
@@ -204,12 +205,16 @@ class FrameGraph:
             Rk = render_K._c() if isinstance(render_K, CameraIntrinsics) else \
                 _lib.Intrinsics(*[float(v) for v in render_K])
         self._eng._wait_torch(depth)
+        prev = self._eng._pending
         _lib.check(_lib.load().tsdf_graph_frame(
             self._g, C.byref(fr), C.byref(Kc), C.byref(cam_T_world._c()), max_depth,
             C.byref(Rk) if Rk is not None else None,
             C.byref(render_cam_T_world._c()) if render_cam_T_world is not None else None,
             _ptr(rgba), _ptr(normal)), "tsdf_graph_frame")
         self._eng._signal_torch(depth)
+        self._eng._after_call(prev)
+        if self.deferred and (rgba is not None or normal is not None):
+            self._eng._pending = (rgba, normal)  # written by the next launch (or engine call)
 
     def close(self):
         if getattr(self, "_g", None):
@@ -306,8 +311,23 @@ class Engine:
         self.device = device
         self.shard_index = shard_index
         self.shard_count = shard_count
+        # device images of a deferred raycast (raycast(deferred=True), deferred graph frames) that the
+        # engine's NEXT call writes: referenced until then (torch's allocator must not reuse them), and
+        # torch's current stream is ordered after that call -- see _after_call
+        self._pending = None
+
+    def _after_call(self, prev):
+        """Engine call wrapper epilogue: the call launched the deferred raycast `prev` was waiting for
+        (every engine entry point does, tsdf_raycast_deferred included), so torch's current stream now
+        waits for the engine's queued work -- the images may be read there -- and the reference goes."""
+        if prev is None:
+            return
+        if self._pending is prev:
+            self._pending = None
+        self._signal_torch(*(t for t in prev if t is not None))
 
     def close(self):
+        self._pending = None
         if getattr(self, "_h", None):
             _lib.load().tsdf_destroy(self._h)
             self._h = None
@@ -520,11 +540,26 @@ class Engine:
 
     def integrate(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float):
         dev = _is_torch_cuda(depth)
-        if dev:
+        if dev:  # (the hot path: torch's stream is looked up once, no extra ordering calls when the
+            # engine runs on it)
             H, W = int(depth.shape[0]), int(depth.shape[1])
             for a in (rgb, depth, ht, lt):
                 if a is not None and not a.is_contiguous():
                     raise ValueError("device frames must be contiguous")
+            if tuple(rgb.shape[:2]) != (H, W):
+                raise ValueError("rgb / depth size mismatch (voxel_tsdf.cu:352-353)")
+            fr = _lib.Frame(W, H, rgb.data_ptr(), depth.data_ptr(), ht.data_ptr() if ht is not None else None,
+                            lt.data_ptr() if lt is not None else None, TSDF_MEM_DEVICE)
+            Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+            cur = self._torch_stream((depth,))
+            L = _lib.load()
+            if cur is not None:
+                _lib.check(L.tsdf_stream_wait(self._h, C.c_void_p(cur)), "tsdf_stream_wait")
+            _lib.check(L.tsdf_integrate(self._h, C.byref(fr), C.byref(Kc), C.byref(cam_T_world._c()), max_depth),
+                       "tsdf_integrate")
+            if cur is not None:
+                _lib.check(L.tsdf_stream_signal(self._h, C.c_void_p(cur)), "tsdf_stream_signal")
+            return
         else:
             rgb = _np(rgb, np.uint8)
             depth = _np(depth, np.float32)
@@ -556,7 +591,8 @@ class Engine:
                 deferred=False):
         """tsdf_raycast; deferred=True (device tensors only): tsdf_raycast_deferred -- the images are
         written by the engine's next call (fused with the next frame's ingest when that is integrate;
-        flush() otherwise), so read them after that call."""
+        flush() otherwise); after that call they may be read on torch's current stream (the engine keeps
+        them referenced until then and orders torch's stream after the call)."""
         Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
         if deferred:
             if rgba is None or not _is_torch_cuda(rgba) or (normal is not None and not _is_torch_cuda(normal)):
@@ -565,6 +601,7 @@ class Engine:
             _lib.check(_lib.load().tsdf_raycast_deferred(self._h, C.byref(Kc), width, height,
                                                          C.byref(cam_T_world._c()), max_depth, _ptr(rgba),
                                                          _ptr(normal)), "tsdf_raycast_deferred")
+            self._pending = (rgba, normal)
             return rgba, normal
         if rgba is not None and _is_torch_cuda(rgba):
             self._wait_torch(rgba, normal)
@@ -832,6 +869,122 @@ class Engine:
         out = np.zeros(BLOCK_VOLUME, np.uint8)
         _lib.check(_lib.load().tsdf_pool_get_weights(self._h, int(block), _ptr(out)), "tsdf_pool_get_weights")
         return out
+
+
+def _engine_call(fn):
+    """Every public Engine method that enters the library settles a pending deferred raycast after
+    its call (Engine._after_call)."""
+    def wrapper(self, *a, **k):
+        prev = self._pending
+        r = fn(self, *a, **k)
+        self._after_call(prev)
+        return r
+    wrapper.__name__, wrapper.__doc__, wrapper.__wrapped__ = fn.__name__, fn.__doc__, fn
+    return wrapper
+
+
+for _name, _fn in list(vars(Engine).items()):
+    if callable(_fn) and not _name.startswith("_") and _name not in ("close", "frame_graph", "shard_frame_graph") \
+            and not isinstance(_fn, (staticmethod, classmethod)):
+        setattr(Engine, _name, _engine_call(_fn))
+del _name, _fn
+
+
+class Group:
+    """One volume spatially sharded over `devices` (one shard per entry; a device may repeat) with the
+    exchange inside the library (tsdf_group_*, csrc/tsdf_group.hip): each shard's update kernel
+    writes its carve candidates into every shard's inbox, so a frame is one launch per shard and no
+    collective. Same results as one volume (the union of the shards)."""
+
+    def __init__(self, devices, voxel_size=0.005, truncation=0.03, max_width=1920, max_height=1080,
+                 num_block_bits=18):
+        L = _lib.load()
+        cfg = _lib.Config()
+        L.tsdf_config_default(C.byref(cfg))
+        cfg.voxel_size, cfg.truncation = voxel_size, truncation
+        cfg.max_width, cfg.max_height, cfg.num_block_bits = max_width, max_height, num_block_bits
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        _lib.check(L.tsdf_group_create(C.byref(cfg), devs, len(devices), C.byref(h)), "tsdf_group_create")
+        self._g = h
+        self.n = len(devices)
+        self.devices = list(devices)
+        self.num_blocks = 1 << num_block_bits
+        self.voxel_size, self.truncation = voxel_size, truncation
+
+    def integrate(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float):
+        """Host arrays, or device tensors on devices[0] (contiguous; torch's stream is synchronised
+        first: the group runs on its own streams)."""
+        dev = _is_torch_cuda(depth)
+        if dev:
+            import torch
+            torch.cuda.current_stream().synchronize()
+            for a in (rgb, depth, ht, lt):
+                if a is not None and not a.is_contiguous():
+                    raise ValueError("device frames must be contiguous")
+            H, W = int(depth.shape[0]), int(depth.shape[1])
+        else:
+            rgb, depth = _np(rgb, np.uint8), _np(depth, np.float32)
+            ht, lt = _np(ht, np.float32), _np(lt, np.float32)
+            H, W = depth.shape
+        fr = _lib.Frame(W, H, _ptr(rgb), _ptr(depth), _ptr(ht), _ptr(lt), TSDF_MEM_DEVICE if dev else TSDF_MEM_HOST)
+        Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        _lib.check(_lib.load().tsdf_group_integrate(self._g, C.byref(fr), C.byref(Kc), C.byref(cam_T_world._c()),
+                                                    max_depth), "tsdf_group_integrate")
+
+    def flush(self):
+        _lib.check(_lib.load().tsdf_group_flush(self._g), "tsdf_group_flush")
+
+    def synchronize(self):
+        _lib.check(_lib.load().tsdf_group_synchronize(self._g), "tsdf_group_synchronize")
+
+    def stats(self, clear_status=False) -> dict:
+        s = _lib.Stats()
+        _lib.check(_lib.load().tsdf_group_get_stats(self._g, C.byref(s), int(clear_status)), "tsdf_group_get_stats")
+        return {k: getattr(s, k) for k, _ in _lib.Stats._fields_}
+
+    def query(self, bounds=None) -> np.ndarray:
+        b = None if bounds is None else np.ascontiguousarray(
+            bounds.as_array() if isinstance(bounds, BoundingCube) else bounds, dtype=np.float32)
+        n = C.c_int64()
+        L = _lib.load()
+        _lib.check(L.tsdf_group_query(self._g, _ptr(b), None, 0, C.byref(n)), "tsdf_group_query")
+        out = np.zeros(n.value, VOXEL_DTYPE)
+        if n.value:
+            _lib.check(L.tsdf_group_query(self._g, _ptr(b), out.ctypes.data_as(C.c_void_p), n.value, C.byref(n)),
+                       "tsdf_group_query")
+        return out
+
+    def raycast(self, K, width, height, cam_T_world: SE3, max_depth: float):
+        Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
+        rgba = np.zeros((height, width, 4), np.uint8)
+        normal = np.zeros((height, width, 4), np.uint8)
+        _lib.check(_lib.load().tsdf_group_raycast(self._g, C.byref(Kc), width, height, C.byref(cam_T_world._c()),
+                                                  max_depth, _ptr(rgba), _ptr(normal), TSDF_MEM_HOST),
+                   "tsdf_group_raycast")
+        return rgba, normal
+
+    def shard_dump(self, i: int, pool: bool = True) -> dict:
+        """tsdf_debug_dump of shard i's engine (tsdf_group_shard)."""
+        h = C.c_void_p()
+        _lib.check(_lib.load().tsdf_group_shard(self._g, i, C.byref(h)), "tsdf_group_shard")
+        eng = Engine.__new__(Engine)  # a borrowed handle: the group owns the engine
+        eng._h, eng.num_blocks, eng._pending, eng._stream = h, self.num_blocks, None, -1
+        try:
+            return Engine.dump.__wrapped__(eng, pool)
+        finally:
+            eng._h = None
+
+    def close(self):
+        if getattr(self, "_g", None):
+            _lib.load().tsdf_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class ShardGroup:

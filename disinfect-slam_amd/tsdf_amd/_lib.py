@@ -112,6 +112,8 @@ EXPORTS = [
     "tsdf_raycast_rows", "tsdf_raycast_deferred", "tsdf_render_bands", "tsdf_pack_halo", "tsdf_extract_mesh_owned",
     "tsdf_graph_create_shard", "tsdf_graph_shard_begin", "tsdf_graph_shard_update", "tsdf_graph_shard_end",
     "tsdf_integrate_shard_pipe",
+    "tsdf_group_create", "tsdf_group_destroy", "tsdf_group_size", "tsdf_group_integrate", "tsdf_group_flush",
+    "tsdf_group_synchronize", "tsdf_group_shard", "tsdf_group_get_stats", "tsdf_group_query", "tsdf_group_raycast",
 ]
 
 _lib = None
@@ -143,6 +145,16 @@ def load(path: str | None = None):
     L.tsdf_integrate_shard_abort.argtypes = [P]
     L.tsdf_integrate_shard_pipe.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f, P, P,
                                             C.c_int32, C.POINTER(C.c_int32)]
+    L.tsdf_group_create.argtypes = [C.POINTER(Config), C.POINTER(i), i, C.POINTER(P)]
+    L.tsdf_group_destroy.argtypes = [P]
+    L.tsdf_group_size.argtypes = [P]
+    L.tsdf_group_integrate.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f]
+    L.tsdf_group_flush.argtypes = [P]
+    L.tsdf_group_synchronize.argtypes = [P]
+    L.tsdf_group_shard.argtypes = [P, i, C.POINTER(P)]
+    L.tsdf_group_get_stats.argtypes = [P, C.POINTER(Stats), i]
+    L.tsdf_group_query.argtypes = [P, P, P, i64, C.POINTER(i64)]
+    L.tsdf_group_raycast.argtypes = [P, C.POINTER(Intrinsics), i, i, C.POINTER(Pose), f, P, P, i]
     L.tsdf_stream_wait.argtypes = [P, P]
     L.tsdf_stream_signal.argtypes = [P, P]
     L.tsdf_get_stream.argtypes = [P, C.POINTER(P)]
@@ -215,7 +227,10 @@ def load(path: str | None = None):
                  "tsdf_debug_dump", "tsdf_debug_stamps", "tsdf_hash_allocate", "tsdf_hash_delete",
                  "tsdf_hash_retrieve",
                  "tsdf_hash_assign", "tsdf_num_active_blocks", "tsdf_pool_acquire",
-                 "tsdf_pool_release", "tsdf_pool_set_weight", "tsdf_pool_get_weights"):
+                 "tsdf_pool_release", "tsdf_pool_set_weight", "tsdf_pool_get_weights",
+                 "tsdf_group_create", "tsdf_group_destroy", "tsdf_group_size", "tsdf_group_integrate",
+                 "tsdf_group_flush", "tsdf_group_synchronize", "tsdf_group_shard", "tsdf_group_get_stats",
+                 "tsdf_group_query", "tsdf_group_raycast"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

@@ -201,6 +201,38 @@ int tsdf_integrate_shard_end(tsdf_engine* e, const void* cands_in, int32_t cand_
  * from a snapshot (or reset, which also drops pending pipelined shard frames). No pending frame: OK. */
 int tsdf_integrate_shard_abort(tsdf_engine* e);
 
+/* ---- A sharded volume owned by the library (SURVEY.md 8b tsdf_create_sharded; no reference
+ * counterpart: TSDFGrid, voxel_tsdf.cu:309-375, is single-GPU). ONE volume spatially sharded over n
+ * engines of this process -- shard i on devices[i]; a device may repeat (several shards of one GPU) --
+ * running the pipelined sharded frames of tsdf_integrate_shard_pipe with the exchange inside the
+ * library: each shard's update kernel writes its carve candidates straight into every shard's inbox
+ * (device stores, peer stores over xGMI between GPUs; no copy, no host round trip, no collective
+ * library), inboxes double-buffered by call parity. Shards of one device share one stream; across
+ * devices each call waits for the previous call of every other device (events). The union of the
+ * shards equals the unsharded volume block for block and voxel for voxel; truncation / voxel <= 6.
+ * cfg: as tsdf_create (shard_index / shard_count / stream are the group's). Frames: host memory, or
+ * device memory on devices[0] (copied to the other devices). tsdf_group_integrate is pipelined like
+ * tsdf_integrate; every other group call (flush, stats, query, raycast, shard, synchronize) first
+ * completes the pending frames. tsdf_group_query returns the unsharded volume's voxels shard by shard
+ * (each shard in entry order); tsdf_group_raycast renders exactly what the unsharded volume renders
+ * (render replicas into an engine on devices[0]); tsdf_group_shard gives shard i's engine (e.g. for
+ * tsdf_debug_dump); tsdf_group_get_stats sums the shards' voxel counts (visible, updated, free) and
+ * reports the index counts (active, allocated, deleted) once. */
+typedef struct tsdf_group tsdf_group;
+int tsdf_group_create(const tsdf_config* cfg, const int* devices, int n, tsdf_group** out);
+int tsdf_group_destroy(tsdf_group* g);
+int tsdf_group_size(const tsdf_group* g);
+int tsdf_group_integrate(tsdf_group* g, const tsdf_frame* frame, const tsdf_intrinsics* K,
+                         const tsdf_pose* cam_T_world, float max_depth);
+int tsdf_group_flush(tsdf_group* g);
+int tsdf_group_synchronize(tsdf_group* g);
+int tsdf_group_shard(tsdf_group* g, int index, tsdf_engine** out);
+int tsdf_group_get_stats(tsdf_group* g, tsdf_stats* out, int clear_status);
+int tsdf_group_query(tsdf_group* g, const float* bounds, tsdf_voxel* out, int64_t capacity, int64_t* count);
+int tsdf_group_raycast(tsdf_group* g, const tsdf_intrinsics* K, int width, int height,
+                       const tsdf_pose* cam_T_world, float max_depth, uint8_t* rgba, uint8_t* normal,
+                       int mem_kind);
+
 /* Stream ordering with a caller's HIP stream (e.g. torch's current stream) for device buffers
  * passed to an engine that runs on its own stream: tsdf_stream_wait makes the engine stream wait
  * for the work queued on `stream` so far (before the engine reads a buffer the caller wrote);

@@ -8,7 +8,7 @@ OUT=build/var_$NAME
 mkdir -p $OUT
 HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function -I../include -Icsrc $FLAGS"
 pids=()
-for f in csrc/tsdf_alloc.hip csrc/tsdf_fuse.hip csrc/tsdf_extract.hip csrc/tsdf_mesh.hip csrc/tsdf_frontend.hip csrc/tsdf_engine.hip; do
+for f in csrc/tsdf_alloc.hip csrc/tsdf_fuse.hip csrc/tsdf_extract.hip csrc/tsdf_mesh.hip csrc/tsdf_frontend.hip csrc/tsdf_engine.hip csrc/tsdf_group.hip; do
   /opt/rocm/bin/hipcc $HIPFLAGS -c $f -o $OUT/$(basename $f .hip).o & pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done

@@ -1,0 +1,6 @@
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_c5.py tests/test_gpu_graph.py tests/test_gpu_render.py > gpurun_out/r6_t5.log 2>&1
+rc=$?
+grep -E "PASS|FAIL|ERROR" gpurun_out/r6_t5.log | tail -40
+exit $rc

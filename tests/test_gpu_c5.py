@@ -289,3 +289,124 @@ def test_deferred_raycast_heavy_carving():
         assert sa["status"] == 0 and sb["status"] == 0 and sa["total_deleted"] == sb["total_deleted"]
     finally:
         a.close(), b.close()
+
+
+def test_deferred_raycast_images_without_device_sync():
+    """a deferred raycast into temporaries the caller drops at once, on an engine-owned
+    stream, read on torch's current stream after a HOST-frame integrate (the call that renders them)
+    -- no torch.cuda.synchronize in between: the engine keeps the tensors referenced until that call
+    and orders torch's stream after it, so the images equal the immediate raycast. Then the same
+    through flush() and through stats()."""
+    import gc
+
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H = 160, 120
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    a = tsdf_amd.Engine(0.01, 0.04, max_width=W, max_height=H, num_block_bits=15)
+    b = tsdf_amd.Engine(0.01, 0.04, max_width=W, max_height=H, num_block_bits=15)
+    try:
+        frames = [synth.render(cam, f) for f in range(0, 30, 3)]
+        for i, fr in enumerate(frames[:-1]):
+            pose = tsdf_amd.SE3(fr["q"], fr["t"])
+            for e in (a, b):
+                e.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], K, pose, 4.0)
+            out = b.raycast(K, W, H, pose, 4.0, rgba=torch.empty((H, W, 4), dtype=torch.uint8, device="cuda"),
+                            normal=torch.empty((H, W, 4), dtype=torch.uint8, device="cuda"), deferred=True)
+            keep = [t.data_ptr() for t in out]
+            del out
+            gc.collect()
+            # torch reuses freed blocks at once: garbage written into any block the images sat in
+            junk = [torch.full((H, W, 4), 7, dtype=torch.uint8, device="cuda") for _ in range(4)]
+            assert not any(j.data_ptr() in keep for j in junk), "the deferred images were freed early"
+            nxt = frames[i + 1]
+            how = i % 3
+            if how == 0:  # a host-frame integrate renders the images
+                b.integrate(nxt["rgb"], nxt["depth"], nxt["ht"], nxt["lt"], K, tsdf_amd.SE3(nxt["q"], nxt["t"]), 4.0)
+                a.integrate(nxt["rgb"], nxt["depth"], nxt["ht"], nxt["lt"], K, tsdf_amd.SE3(nxt["q"], nxt["t"]), 4.0)
+            elif how == 1:
+                b.flush()
+            else:
+                b.stats()
+            del junk
+            assert b._pending is None  # rendered by that call, reference dropped
+    finally:
+        a.close(), b.close()
+
+
+def test_deferred_raycast_read_on_torch_stream():
+    """The deferred images read on torch's stream right after the engine's next call equal the
+    immediate raycast (no device synchronisation)."""
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H = 160, 120
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    eng = tsdf_amd.Engine(0.01, 0.04, max_width=W, max_height=H, num_block_bits=15)
+    try:
+        frames = [synth.render(cam, f) for f in range(0, 24, 3)]
+        for i, fr in enumerate(frames):
+            pose = tsdf_amd.SE3(fr["q"], fr["t"])
+            eng.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], K, pose, 4.0)
+            rgba = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+            nrm = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+            eng.raycast(K, W, H, pose, 4.0, rgba=rgba, normal=nrm, deferred=True)
+            eng.flush() if i % 2 else eng.stats()
+            got = (rgba.clone(), nrm.clone())  # on torch's stream, after the call that rendered them
+            ref = eng.raycast(K, W, H, pose, 4.0)
+            np.testing.assert_array_equal(got[0].cpu().numpy(), ref[0])
+            np.testing.assert_array_equal(got[1].cpu().numpy(), ref[1])
+    finally:
+        eng.close()
+
+
+def test_deferred_graph_across_grid_growth_and_generation_wrap():
+    """a deferred graph frame pending while the next frame's view grid is reallocated (a
+    deeper render camera: the cube grows) or its generations wrap (more than kViewGenMax = 1023 grid
+    builds): the pending raycast must run before the grid it reads is reset (view_grid_resets, one
+    shape computation with view_grid_for). Images equal the immediate graph's frame by frame."""
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H = 32, 24
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    a = tsdf_amd.Engine(0.01, 0.04, max_width=W, max_height=H, num_block_bits=14)
+    b = tsdf_amd.Engine(0.01, 0.04, max_width=W, max_height=H, num_block_bits=14)
+    ga, gb = a.frame_graph(W, H, W, H), b.frame_graph(W, H, W, H, deferred=True)
+    try:
+        fr0 = [synth.render(cam, f) for f in range(0, 30, 3)]
+        dev = [{k: torch.from_numpy(fr[k]).to("cuda") for k in ("rgb", "depth", "ht", "lt")} for fr in fr0]
+        ref = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(2)]
+        out = [[torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(2)] for _ in range(2)]
+        pending = None
+        n = 1040  # > kViewGenMax grid builds in b
+        checked = 0
+        for i in range(n):
+            d = dev[i % len(dev)]
+            pose = tsdf_amd.SE3(fr0[i % len(fr0)]["q"], fr0[i % len(fr0)]["t"])
+            md = 2.0 if i < 5 else (4.0 if i < 600 else 3.0)  # frame 5: the cube grows
+            ga.frame(d["rgb"], d["depth"], d["ht"], d["lt"], K, pose, md, K, pose, ref[0], ref[1])
+            o = out[i % 2]
+            gb.frame(d["rgb"], d["depth"], d["ht"], d["lt"], K, pose, md, K, pose, o[0], o[1])
+            if pending is not None and (i < 12 or i % 97 == 0 or 1015 <= i <= 1035):
+                j, po, r0, r1 = pending
+                torch.cuda.synchronize()
+                assert torch.equal(po[0], r0) and torch.equal(po[1], r1), f"frame {j}: deferred graph != graph"
+                checked += 1
+            ra, rn = ref[0].clone(), ref[1].clone()
+            pending = (i, o, ra, rn)
+        b.flush()
+        torch.cuda.synchronize()
+        j, po, r0, r1 = pending
+        assert torch.equal(po[0], r0) and torch.equal(po[1], r1), "last frame after flush"
+        assert checked > 40 and (r0[..., 3] == 255).float().mean().item() > 0.3
+    finally:
+        ga.close(), gb.close()
+        a.close(), b.close()

@@ -14,8 +14,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "disinfect-slam_amd", "facade_main")
 
 
-@pytest.mark.parametrize("semantic", [True, False])
-def test_tsdf_system_matches_oracle(tmp_path, semantic):
+@pytest.mark.parametrize("semantic,shards", [(True, 1), (False, 1), (True, 2), (True, 5)])
+def test_tsdf_system_matches_oracle(tmp_path, semantic, shards):
+    """shards > 1: TSDFSystem over a volume sharded across that many shards of one GPU (the C++
+    group constructor, tsdf_group_*): the same voxels (shard by shard, compared as a set), statistics
+    and images as the unsharded oracle."""
     from tsdf_amd import synth
     from _oracle import OracleGrid
     W, H, n, voxel, trunc, nb = 96, 72, 5, 0.005, 0.03, 13
@@ -31,13 +34,18 @@ def test_tsdf_system_matches_oracle(tmp_path, semantic):
         ora.integrate(fr["rgb"], fr["depth"], fr["ht"] if semantic else None,
                       fr["lt"] if semantic else None, 4.0, cam.K, fr["q"], fr["t"])
     (tmp_path / "meta.txt").write_text("\n".join(lines) + "\n")
-    r = subprocess.run([BIN, str(tmp_path)], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([BIN, str(tmp_path), str(shards)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     got = np.fromfile(tmp_path / "out_query.bin", np.float32).reshape(-1, 4)
     exp = ora.query(None)
     assert got.shape == exp.shape and got.shape[0] > 0
-    np.testing.assert_array_equal(got[:, :3], exp[:, :3])
-    np.testing.assert_array_equal(got[:, 3].view(np.uint32), exp[:, 3].view(np.uint32))
+    if shards > 1:  # shard by shard: the same set of voxels
+        got = np.sort(np.ascontiguousarray(got).view(np.uint32).view("V16").ravel())
+        exp = np.sort(np.ascontiguousarray(exp).view(np.uint32).view("V16").ravel())
+        assert np.array_equal(got, exp)
+    else:
+        np.testing.assert_array_equal(got[:, :3], exp[:, :3])
+        np.testing.assert_array_equal(got[:, 3].view(np.uint32), exp[:, 3].view(np.uint32))
     frames, active, nvis, nupd, status = map(int, (tmp_path / "out_stats.txt").read_text().split())
     so = ora.stats()
     assert (frames, active, nvis, nupd, status) == (n, so["active_blocks"], so["last_num_visible"],
