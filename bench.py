@@ -72,6 +72,9 @@ def parse():
                         "marching cubes of the whole volume every 30 frames (eager chain)")
     p.add_argument("--graph", action="store_true",
                    help="frames through the graph-captured frame (one hipGraph launch per frame)")
+    p.add_argument("--graph-batch", type=int, default=1,
+                   help="with --graph: frames per graph launch (tsdf_graph_create_batch; the launch's fixed "
+                        "cost paid once per batch)")
     p.add_argument("--shard", default=None, metavar="G",
                    help="single-GPU rehearsal of the routed sharded volume: G shard engines on this GPU "
                         "exchanging their slots with device copies; reports the per-shard frame time")
@@ -166,7 +169,8 @@ class Run:
                 self.sgraph = self.eng.shard_frame_graph(W, H, rank if split else 0, world if split else 1)
             else:
                 rw, rh = (W, H) if a.loop == "c5" else (0, 0)
-                self.graph = self.eng.frame_graph(W, H, rw, rh, deferred=bool(rw) and not a.no_defer)
+                self.graph = self.eng.frame_graph(W, H, rw, rh, deferred=bool(rw) and not a.no_defer,
+                                                  batch=a.graph_batch)
 
     def step(self, i):
         from tsdf_amd import dist as tdist
@@ -568,6 +572,7 @@ def main():
                 "width": W, "height": H, "voxel_m": a.voxel, "truncation_m": a.trunc,
                 "pool_blocks": 1 << a.block_bits,
                 "parallelism": parallelism,
+                "graph_frames_per_launch": a.graph_batch if a.graph else None,
             },
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -172,6 +172,9 @@ struct tsdf_engine {
     const FrameArgs* args = nullptr;
     int W = 0, H = 0;
   } rdg;
+  // a batched graph (tsdf_graph_create_batch) whose current batch holds frames not launched yet:
+  // every other call launches them first (join_render -> graph_flush_batch)
+  struct tsdf_graph* gbatch = nullptr;
   EngineDev D{};
   int maxs = 3;
   int64_t order_range = 0;  // candidate order space: max_pixels * maxs
@@ -402,7 +405,12 @@ int launch_resolve_alloc(tsdf_engine* e, const FrameParams& P, uint32_t range, i
 // another stream's work, which the raycast may follow as well; wait_overlap false: launch the deferred
 // raycasts only, without joining a TSDF_RENDER_OVERLAP raycast on the render stream -- the next
 // frame's ingest writes nothing it reads; keep_graph: the graph frame that renders rdg itself calls)
+int graph_flush_batch(tsdf_graph* g);
 int join_render(tsdf_engine* e, bool keep_deferred = false, bool wait_overlap = true, bool keep_graph = false) {
+  if (e->gbatch) {  // the frames of a batched graph not launched yet, before anything else
+    int rc = graph_flush_batch(e->gbatch);
+    if (rc) return rc;
+  }
   if (e->rdg.pending && !keep_deferred && !keep_graph) {  // (a graph frame's deferred raycast: its args slot)
     e->rdg.pending = false;
     const dim3 rgrid((e->rdg.W + 15) / 16, (e->rdg.H + 15) / 16);
@@ -1502,15 +1510,27 @@ struct tsdf_graph {
   hipEvent_t done[kSlots] = {};
   bool used[kSlots] = {};
   int next = 0;
+  // batched graphs (tsdf_graph_create_batch): slot k's graph runs `batch` frames, args entries
+  // [k batch, (k + 1) batch); one[k][j] runs entry j alone (a batch launched before it is full)
+  static constexpr int kMaxBatch = 32;
+  int batch = 1;
+  int fill = 0;           // frames of the current slot's batch written, not launched
+  hipGraph_t one_g[kSlots][kMaxBatch] = {};
+  hipGraphExec_t one[kSlots][kMaxBatch] = {};
 };
 
 namespace {
 
 void graph_free(tsdf_graph* g) {
+  if (g->e && g->e->gbatch == g) g->e->gbatch = nullptr;
   for (int i = 0; i < tsdf_graph::kSlots; ++i) {
     for (int j = 0; j < tsdf_graph::kSegs; ++j) {
       if (g->exec[i][j]) (void)hipGraphExecDestroy(g->exec[i][j]);
       if (g->graph[i][j]) (void)hipGraphDestroy(g->graph[i][j]);
+    }
+    for (int j = 0; j < tsdf_graph::kMaxBatch; ++j) {
+      if (g->one[i][j]) (void)hipGraphExecDestroy(g->one[i][j]);
+      if (g->one_g[i][j]) (void)hipGraphDestroy(g->one_g[i][j]);
     }
     if (g->done[i]) (void)hipEventDestroy(g->done[i]);
   }
@@ -1524,20 +1544,21 @@ void graph_free(tsdf_graph* g) {
 
 namespace {
 int graph_create(tsdf_engine* e, int width, int height, int render_width, int render_height, bool defer,
-                 tsdf_graph** out) {
+                 tsdf_graph** out, int batch = 1) {
   if (e && e->cfg.shard_count > 1) {
     set_error("tsdf_graph_create: a shard's graph frames are tsdf_graph_create_shard / tsdf_graph_shard_*");
     return TSDF_ERR_INVALID_ARG;
   }
   if (!e || !out || width <= 0 || height <= 0 || width > e->cfg.max_width || height > e->cfg.max_height ||
       render_width < 0 || render_height < 0 || (int64_t)render_width * render_height > e->max_pixels ||
-      (render_width == 0) != (render_height == 0)) {
+      (render_width == 0) != (render_height == 0) || batch < 1 || batch > tsdf_graph::kMaxBatch) {
     set_error("tsdf_graph_create: invalid argument");
     return TSDF_ERR_INVALID_ARG;
   }
   HIP_OK(hipSetDevice(e->device));
   ENTER(e);
   auto* g = new tsdf_graph();
+  g->batch = batch;
   g->e = e;
   g->W = width;
   g->H = height;
@@ -1554,23 +1575,16 @@ int graph_create(tsdf_engine* e, int width, int height, int render_width, int re
   };
   hipError_t err;
   if ((err = hipStreamCreateWithFlags(&g->cap, hipStreamNonBlocking)) != hipSuccess) return fail(err, "graph stream");
-  if ((err = hipMalloc(&g->d_args, sizeof(FrameArgs) * tsdf_graph::kSlots)) != hipSuccess) return fail(err, "graph args");
-  if ((err = hipHostMalloc(&g->h_args, sizeof(FrameArgs) * tsdf_graph::kSlots)) != hipSuccess)
+  const int nargs = tsdf_graph::kSlots * batch;
+  if ((err = hipMalloc(&g->d_args, sizeof(FrameArgs) * nargs)) != hipSuccess) return fail(err, "graph args");
+  if ((err = hipHostMalloc(&g->h_args, sizeof(FrameArgs) * nargs)) != hipSuccess)
     return fail(err, "graph host args");
-  std::memset(g->h_args, 0, sizeof(FrameArgs) * tsdf_graph::kSlots);
+  std::memset(g->h_args, 0, sizeof(FrameArgs) * nargs);
   const int tiles = ((width + 15) / 16) * ((height + 15) / 16);
   // the engine's queued work must be done before the capture stream records anything
   if ((err = hipStreamSynchronize(e->stream)) != hipSuccess) return fail(err, "graph sync");
-  for (int k = 0; k < tsdf_graph::kSlots; ++k) {
-    const FrameArgs* A = g->d_args + k;
-    if ((err = hipEventCreateWithFlags(&g->done[k], kGraphDoneFlags)) != hipSuccess) return fail(err, "graph event");
-    if ((err = hipStreamBeginCapture(g->cap, hipStreamCaptureModeThreadLocal)) != hipSuccess)
-      return fail(err, "hipStreamBeginCapture");
-    if (e->env.graph_memcpy_node)  // A/B: a memcpy node instead of the copy kernel
-      (void)hipMemcpyAsync(g->d_args + k, g->h_args + k, sizeof(FrameArgs), hipMemcpyHostToDevice, g->cap);
-    else  // one wave reads the pinned slot over the fabric: a kernel node, no DMA engine in the graph
-      hipLaunchKernelGGL(k_copy_words, dim3(1), dim3(64), 0, g->cap, reinterpret_cast<uint32_t*>(g->d_args + k),
-                         reinterpret_cast<const uint32_t*>(g->h_args + k), (int)(sizeof(FrameArgs) / 4));
+  // the nodes of one frame (args entry A)
+  auto frame_nodes = [&](const FrameArgs* A) {
     if (g->pipe) {  // one k_frame per frame, its grid sized for the largest launch (steady state)
       const int tpw = std::max(1, e->env.frame_tiles_per_wg);
       const int nwg = kPipeHead + kPipeFreshWG + e->D.integrate_grid_pre + (tiles + tpw - 1) / tpw + kVisWorkgroups;
@@ -1593,11 +1607,48 @@ int graph_create(tsdf_engine* e, int width, int height, int render_width, int re
       const dim3 rgrid((render_width + 15) / 16, (render_height + 15) / 16);
       if (!g->defer) hipLaunchKernelGGL(k_raycast_g, rgrid, dim3(256), 0, g->cap, e->D, A);
     }
-    if ((err = hipStreamEndCapture(g->cap, &g->graph[k][0])) != hipSuccess) return fail(err, "hipStreamEndCapture");
-    if ((err = hipGraphInstantiate(&g->exec[k][0], g->graph[k][0], nullptr, nullptr, 0)) != hipSuccess)
-      return fail(err, "hipGraphInstantiate");
+  };
+  // the args upload of entries [a0, a0 + n): one wave reads the pinned slots over the fabric (a kernel
+  // node, no DMA engine in the graph), or a memcpy node (A/B)
+  auto upload_node = [&](int a0, int n) {
+    if (e->env.graph_memcpy_node)
+      (void)hipMemcpyAsync(g->d_args + a0, g->h_args + a0, sizeof(FrameArgs) * n, hipMemcpyHostToDevice, g->cap);
+    else
+      hipLaunchKernelGGL(k_copy_words, dim3(1), dim3(n > 1 ? 256 : 64), 0, g->cap,
+                         reinterpret_cast<uint32_t*>(g->d_args + a0), reinterpret_cast<const uint32_t*>(g->h_args + a0),
+                         (int)(sizeof(FrameArgs) * n / 4));
+  };
+  auto capture = [&](hipGraph_t* gr, hipGraphExec_t* ex, int a0, int n) -> hipError_t {
+    hipError_t er = hipStreamBeginCapture(g->cap, hipStreamCaptureModeThreadLocal);
+    if (er != hipSuccess) return er;
+    upload_node(a0, n);
+    for (int j = 0; j < n; ++j) frame_nodes(g->d_args + a0 + j);
+    if ((er = hipStreamEndCapture(g->cap, gr)) != hipSuccess) return er;
+    return hipGraphInstantiate(ex, *gr, nullptr, nullptr, 0);
+  };
+  for (int k = 0; k < tsdf_graph::kSlots; ++k) {
+    if ((err = hipEventCreateWithFlags(&g->done[k], kGraphDoneFlags)) != hipSuccess) return fail(err, "graph event");
+    if ((err = capture(&g->graph[k][0], &g->exec[k][0], k * batch, batch)) != hipSuccess)
+      return fail(err, "graph capture");
+    for (int j = 0; batch > 1 && j < batch; ++j)  // (a batch launched before it is full)
+      if ((err = capture(&g->one_g[k][j], &g->one[k][j], k * batch + j, 1)) != hipSuccess)
+        return fail(err, "graph capture (single frame)");
   }
   *out = g;
+  return TSDF_OK;
+}
+
+// launch the frames of g's current batch that were written but not launched (each alone)
+int graph_flush_batch(tsdf_graph* g) {
+  tsdf_engine* e = g->e;
+  if (e->gbatch == g) e->gbatch = nullptr;
+  if (g->fill == 0) return TSDF_OK;
+  const int k = g->next, n = g->fill;
+  g->fill = 0;
+  g->next = (k + 1) % tsdf_graph::kSlots;
+  for (int j = 0; j < n; ++j) HIP_OK(hipGraphLaunch(g->one[k][j], e->stream));
+  HIP_OK(hipEventRecord(g->done[k], e->stream));
+  g->used[k] = true;
   return TSDF_OK;
 }
 }  // namespace
@@ -1610,6 +1661,11 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
 int tsdf_graph_create_deferred(tsdf_engine* e, int width, int height, int render_width, int render_height,
                                tsdf_graph** out) {
   return graph_create(e, width, height, render_width, render_height, true, out);
+}
+
+int tsdf_graph_create_batch(tsdf_engine* e, int width, int height, int render_width, int render_height,
+                            int deferred, int frames_per_launch, tsdf_graph** out) {
+  return graph_create(e, width, height, render_width, render_height, deferred != 0, out, frames_per_launch);
 }
 
 // A shard's graph frame: three captured segments per args slot -- (0) the args upload + k_ingest_dda_g
@@ -1788,17 +1844,22 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
   HIP_OK(hipSetDevice(e->device));
   // this graph's deferred raycast of the previous frame: rendered by this launch (k_render_ingest_g).
   // It stays pending (a later call launches it) until the graph launch below, so an error return on
-  // the way leaves it to the engine's next call instead of dropping its images.
+  // the way leaves it to the engine's next call instead of dropping its images. (Batched
+  // graphs: the previous frame may sit in this batch, not launched yet; nothing else ran since.)
   const FrameArgs* prev = (g->defer && e->rdg.pending && e->rdg.g == g) ? e->rdg.args : nullptr;
-  {
+  if (g->fill == 0) {
+    if (e->gbatch && e->gbatch != g) {
+      int rc = graph_flush_batch(e->gbatch);
+      if (rc) return rc;
+    }
     int rc = join_render(e, false, true, prev != nullptr);  // (not the raycast this launch takes)
     if (!rc && !g->pipe) rc = flush_pending(e);  // (pipelined: the pending frames continue in this launch)
     if (rc) return rc;
   }
-  const int k = g->next;
-  g->next = (k + 1) % tsdf_graph::kSlots;
-  if (g->used[k]) HIP_OK(hipEventSynchronize(g->done[k]));  // slot k's upload has run
-  FrameArgs& a = g->h_args[k];
+  const int k = g->next, j = g->fill;
+  if (j == 0 && g->used[k]) HIP_OK(hipEventSynchronize(g->done[k]));  // slot k's last batch has run
+  const int ai = k * g->batch + j;  // this frame's args entry
+  FrameArgs& a = g->h_args[ai];
   a.P = make_params(e, K, f->width, f->height, pose, max_depth);
   if (g->RW) a.R = make_params(e, render_K, g->RW, g->RH, render_pose, max_depth);
   a.depth = f->depth;
@@ -1809,6 +1870,13 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
   a.normal = reinterpret_cast<uchar4*>(normal);
   a.step_size = e->cfg.truncation / 2;
   if (g->RW) {
+    if (g->fill > 0 && view_grid_resets(e, a.R, a.step_size, kViewGraphBitmapWords)) {
+      // the batch's frames read the grid this call resets or reallocates: they run first, and this
+      // frame opens the next batch (recomputed from the start)
+      int rc = graph_flush_batch(g);
+      if (rc) return rc;
+      return tsdf_graph_frame(g, f, K, pose, max_depth, render_K, render_pose, rgba, normal);
+    }
     if (prev && view_grid_resets(e, a.R, a.step_size, kViewGraphBitmapWords)) {  // (it reads the old grid)
       e->rdg.pending = false;
       hipLaunchKernelGGL(k_raycast_g, dim3((g->RW + 15) / 16, (g->RH + 15) / 16), dim3(256), 0, e->stream, e->D,
@@ -1837,24 +1905,35 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
     if (e->profiling && a.pipe.has_update) ++e->prof_pipelined;
   }
   if (prev) e->rdg.pending = false;  // rendered by this launch
-  HIP_OK(hipGraphLaunch(g->exec[k][0], e->stream));
+  g->fill = j + 1;
+  e->gbatch = g;
+  const bool hash_raycast = g->defer && !a.V.n;  // (no grid: it reads the table the next ingest writes)
+  if (g->fill == g->batch) {  // the batch is full: one launch runs its frames
+    e->gbatch = nullptr;
+    g->fill = 0;
+    g->next = (k + 1) % tsdf_graph::kSlots;
+    HIP_OK(hipGraphLaunch(g->exec[k][0], e->stream));
+    HIP_OK(hipEventRecord(g->done[k], e->stream));
+    g->used[k] = true;
+  } else if (hash_raycast) {  // it must run after this frame, before the next one's ingest
+    int rc = graph_flush_batch(g);
+    if (rc) return rc;
+  }
   if (g->defer) {
-    // a view grid's raycast waits for the next launch; a hash-lookup raycast (no grid: it reads the
-    // table the next ingest writes) runs now, after the graph
+    // a view grid's raycast waits for the next frame's launch; a hash-lookup raycast runs now, after
+    // this frame's graph
     if (a.V.n) {
       e->rdg.pending = true;
       e->rdg.g = g;
-      e->rdg.args = g->d_args + k;
+      e->rdg.args = g->d_args + ai;
       e->rdg.W = g->RW;
       e->rdg.H = g->RH;
     } else {
       hipLaunchKernelGGL(k_raycast_g, dim3((g->RW + 15) / 16, (g->RH + 15) / 16), dim3(256), 0, e->stream, e->D,
-                         g->d_args + k);
+                         g->d_args + ai);
       LAUNCH_OK("k_raycast_g");
     }
   }
-  HIP_OK(hipEventRecord(g->done[k], e->stream));
-  g->used[k] = true;
   if (g->pipe) pipe_advance(e, fid, a.P);
   return TSDF_OK;
 }
@@ -1862,6 +1941,7 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
 int tsdf_graph_destroy(tsdf_graph* g) {
   if (!g) return TSDF_ERR_INVALID_ARG;
   (void)hipSetDevice(g->e->device);
+  (void)graph_flush_batch(g);
   (void)join_render(g->e);
   (void)hipStreamSynchronize(g->e->stream);
   graph_free(g);

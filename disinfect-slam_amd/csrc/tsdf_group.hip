@@ -322,16 +322,18 @@ int tsdf_group_get_stats(tsdf_group* g, tsdf_stats* out, int clear_status) {
   for (int s = 0; s < g->n; ++s) {
     tsdf_stats a{};
     GRC(tsdf_get_stats(g->shard[s], &a, clear_status));
-    if (s == 0) {  // the hash index (and its allocations / deletions) is every shard's
+    if (s == 0) {  // every shard runs the same frames and finds the same new keys (the index is each one's)
       t.frames = a.frames;
-      t.active_blocks = a.active_blocks;
-      t.last_num_alloc = a.last_num_alloc;
-      t.last_num_deleted = a.last_num_deleted;
       t.last_num_new_keys = a.last_num_new_keys;
-      t.total_alloc = a.total_alloc;
-      t.total_deleted = a.total_deleted;
     }
-    t.free_blocks += a.free_blocks;  // the voxels are divided
+    // the voxels and pool blocks are divided: each shard counts the blocks it holds, acquires and
+    // releases, and the visible / updated ones among them
+    t.active_blocks += a.active_blocks;
+    t.free_blocks += a.free_blocks;
+    t.last_num_alloc += a.last_num_alloc;
+    t.last_num_deleted += a.last_num_deleted;
+    t.total_alloc += a.total_alloc;
+    t.total_deleted += a.total_deleted;
     t.last_num_visible += a.last_num_visible;
     t.last_num_updated += a.last_num_updated;
     t.total_visible += a.total_visible;

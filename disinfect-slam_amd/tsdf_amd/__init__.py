@@ -182,13 +182,18 @@ class FrameGraph:
     """One instantiated per-frame hipGraph of an Engine (tsdf_graph_create). frame() takes device
     tensors only; rgba / normal are device tensors (render_height, render_width, 4) u8 or None."""
 
-    def __init__(self, eng, width, height, render_width=0, render_height=0, deferred=False):
+    def __init__(self, eng, width, height, render_width=0, render_height=0, deferred=False, batch=1):
         self._eng = eng
         self.width, self.height = width, height
         self.render_width, self.render_height = render_width, render_height
         h = C.c_void_p()
-        fn = "tsdf_graph_create_deferred" if deferred else "tsdf_graph_create"
-        _lib.check(getattr(_lib.load(), fn)(eng._h, width, height, render_width, render_height, C.byref(h)), fn)
+        if batch > 1:  # tsdf_graph_create_batch: `batch` frames per graph launch
+            _lib.check(_lib.load().tsdf_graph_create_batch(eng._h, width, height, render_width, render_height,
+                                                           int(deferred), batch, C.byref(h)), "tsdf_graph_create_batch")
+        else:
+            fn = "tsdf_graph_create_deferred" if deferred else "tsdf_graph_create"
+            _lib.check(getattr(_lib.load(), fn)(eng._h, width, height, render_width, render_height, C.byref(h)), fn)
+        self.batch = batch
         self._g = h
         self.deferred = deferred
 
@@ -212,6 +217,12 @@ class FrameGraph:
             C.byref(render_cam_T_world._c()) if render_cam_T_world is not None else None,
             _ptr(rgba), _ptr(normal)), "tsdf_graph_frame")
         self._eng._signal_torch(depth)
+        if self.batch > 1:
+            # a batched graph writes a frame's images when its batch launches (full, or at the engine's
+            # next other call): every image of the unlaunched frames stays referenced until such a call
+            if rgba is not None or normal is not None:
+                self._eng._pending = (prev or ()) + (rgba, normal)
+            return
         self._eng._after_call(prev)
         if self.deferred and (rgba is not None or normal is not None):
             self._eng._pending = (rgba, normal)  # written by the next launch (or engine call)
@@ -411,11 +422,11 @@ class Engine:
         self._signal_torch(depth_u16)
 
     def frame_graph(self, width: int, height: int, render_width: int = 0, render_height: int = 0,
-                    deferred: bool = False):
+                    deferred: bool = False, batch: int = 1):
         """Graph-captured frame loop (tsdf_graph_*, BASELINE config C5): integrate (+ raycast of
         a render camera) as one hipGraph launch per frame. deferred=True (tsdf_graph_create_deferred):
         each frame's images are written by the next frame's launch (or the engine's next other call)."""
-        return FrameGraph(self, width, height, render_width, render_height, deferred)
+        return FrameGraph(self, width, height, render_width, render_height, deferred, batch)
 
     def shard_frame_graph(self, width: int, height: int, slice_index: int = 0, slice_count: int = 1):
         """A shard's graph-captured sharded frame (tsdf_graph_create_shard)."""

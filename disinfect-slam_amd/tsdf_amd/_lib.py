@@ -112,6 +112,7 @@ EXPORTS = [
     "tsdf_raycast_rows", "tsdf_raycast_deferred", "tsdf_render_bands", "tsdf_pack_halo", "tsdf_extract_mesh_owned",
     "tsdf_graph_create_shard", "tsdf_graph_shard_begin", "tsdf_graph_shard_update", "tsdf_graph_shard_end",
     "tsdf_integrate_shard_pipe",
+    "tsdf_graph_create_batch",
     "tsdf_group_create", "tsdf_group_destroy", "tsdf_group_size", "tsdf_group_integrate", "tsdf_group_flush",
     "tsdf_group_synchronize", "tsdf_group_shard", "tsdf_group_get_stats", "tsdf_group_query", "tsdf_group_raycast",
 ]
@@ -162,6 +163,7 @@ def load(path: str | None = None):
     L.tsdf_rgbd_half.argtypes = [P, P, P, P, i, i, f, P, P, i]
     L.tsdf_graph_create.argtypes = [P, i, i, i, i, C.POINTER(P)]
     L.tsdf_graph_create_deferred.argtypes = [P, i, i, i, i, C.POINTER(P)]
+    L.tsdf_graph_create_batch.argtypes = [P, i, i, i, i, i, i, C.POINTER(P)]
     L.tsdf_graph_frame.argtypes = [P, C.POINTER(Frame), C.POINTER(Intrinsics), C.POINTER(Pose), f,
                                    C.POINTER(Intrinsics), C.POINTER(Pose), P, P]
     L.tsdf_graph_destroy.argtypes = [P]
@@ -228,6 +230,7 @@ def load(path: str | None = None):
                  "tsdf_hash_retrieve",
                  "tsdf_hash_assign", "tsdf_num_active_blocks", "tsdf_pool_acquire",
                  "tsdf_pool_release", "tsdf_pool_set_weight", "tsdf_pool_get_weights",
+                 "tsdf_graph_create_batch",
                  "tsdf_group_create", "tsdf_group_destroy", "tsdf_group_size", "tsdf_group_integrate",
                  "tsdf_group_flush", "tsdf_group_synchronize", "tsdf_group_shard", "tsdf_group_get_stats",
                  "tsdf_group_query", "tsdf_group_raycast"):

@@ -216,8 +216,8 @@ int tsdf_integrate_shard_abort(tsdf_engine* e);
  * completes the pending frames. tsdf_group_query returns the unsharded volume's voxels shard by shard
  * (each shard in entry order); tsdf_group_raycast renders exactly what the unsharded volume renders
  * (render replicas into an engine on devices[0]); tsdf_group_shard gives shard i's engine (e.g. for
- * tsdf_debug_dump); tsdf_group_get_stats sums the shards' voxel counts (visible, updated, free) and
- * reports the index counts (active, allocated, deleted) once. */
+ * tsdf_debug_dump); tsdf_group_get_stats sums the shards' counts (each holds, acquires, releases,
+ * sees and updates its own blocks: the sums are the unsharded volume's), frames and new keys once. */
 typedef struct tsdf_group tsdf_group;
 int tsdf_group_create(const tsdf_config* cfg, const int* devices, int n, tsdf_group** out);
 int tsdf_group_destroy(tsdf_group* g);
@@ -276,6 +276,16 @@ int tsdf_graph_create(tsdf_engine* e, int width, int height, int render_width, i
  * their frame's graph launch. */
 int tsdf_graph_create_deferred(tsdf_engine* e, int width, int height, int render_width, int render_height,
                                tsdf_graph** out);
+/* A batched graph: each hipGraphLaunch runs frames_per_launch (<= 32) consecutive frames -- their
+ * arguments uploaded by one node, their nodes back to back -- so the launch's fixed cost (on this ROCm
+ * ~13.5 us of idle GPU between launches) is paid once per batch. tsdf_graph_frame writes a
+ * frame into the current batch and launches the batch when it is full; the engine's next other call
+ * (tsdf_flush, tsdf_synchronize, a query, another graph's frame, ...) launches a partly filled batch
+ * first (its frames one by one). So a frame's outputs (its volume update, rgba / normal) are written
+ * once its batch has launched, in engine-stream order; everything else as tsdf_graph_create (deferred
+ * != 0: tsdf_graph_create_deferred), results identical. */
+int tsdf_graph_create_batch(tsdf_engine* e, int width, int height, int render_width, int render_height,
+                            int deferred, int frames_per_launch, tsdf_graph** out);
 int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* frame, const tsdf_intrinsics* K,
                      const tsdf_pose* cam_T_world, float max_depth, const tsdf_intrinsics* render_K,
                      const tsdf_pose* render_cam_T_world, uint8_t* rgba, uint8_t* normal);

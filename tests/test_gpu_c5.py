@@ -410,3 +410,42 @@ def test_deferred_graph_across_grid_growth_and_generation_wrap():
     finally:
         ga.close(), gb.close()
         a.close(), b.close()
+
+
+@pytest.mark.parametrize("batch", [4])
+def test_c5_batched_deferred_graph_equals_eager(batch):
+    """The C5 loop as a batched, render-deferring graph (tsdf_graph_create_batch(deferred=1)): frames'
+    images equal the eager loop's (integrate + immediate raycast) once their batch has run; a far view
+    (hash-lookup raycast) and the render camera's cube growing mid-batch break a batch early; marching
+    cubes at the end equal."""
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H, n = 160, 120, 22
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    fr = synth.render_torch(cam, list(range(n)), device="cuda")
+    a = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=15)
+    b = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=15)
+    g = b.frame_graph(W, H, W, H, deferred=True, batch=batch)
+    outs = [(torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda"),
+             torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")) for _ in range(n)]
+    refs = []
+    try:
+        for i in range(n):
+            pose = tsdf_amd.SE3(fr["q"][i], fr["t"][i])
+            md = 9.0 if i == 9 else (2.0 if i < 3 else 4.0)  # 9: no view grid; 3: the cube grows
+            a.integrate(fr["rgb"][i], fr["depth"][i], fr["ht"][i], fr["lt"][i], K, pose, md)
+            refs.append(a.raycast(K, W, H, pose, md))
+            g.frame(fr["rgb"][i], fr["depth"][i], fr["ht"][i], fr["lt"][i], K, pose, md, K, pose, outs[i][0], outs[i][1])
+        b.flush()
+        torch.cuda.synchronize()
+        for i in range(n):
+            np.testing.assert_array_equal(outs[i][0].cpu().numpy(), refs[i][0], err_msg=f"rgba {i}")
+            np.testing.assert_array_equal(outs[i][1].cpu().numpy(), refs[i][1], err_msg=f"normal {i}")
+        m_a, m_b = a.extract_mesh(None, 0.99, 0), b.extract_mesh(None, 0.99, 0)
+        np.testing.assert_array_equal(np.asarray(m_a).view(np.uint32), np.asarray(m_b).view(np.uint32))
+    finally:
+        g.close()
+        a.close(), b.close()

@@ -99,3 +99,41 @@ def test_pipelined_graph_frames_equal_unpipelined():
     finally:
         g.close()
         a.close(), b.close()
+
+
+@pytest.mark.parametrize("batch", [3, 8])
+def test_batched_graph_frames_equal_eager(batch):
+    """tsdf_graph_create_batch: `batch` pipelined C3 frames per graph launch == eager tsdf_integrate, bit
+    for bit, also when other calls (stats, query) launch a partly filled batch in between."""
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    W, H, n = 160, 120, 29
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    K = tsdf_amd.CameraIntrinsics(*[float(v) for v in cam.K])
+    fr = synth.render_torch(cam, list(range(n)), device="cuda")
+    a = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=15)
+    b = tsdf_amd.Engine(0.005, 0.03, max_width=W, max_height=H, num_block_bits=15)
+    g = b.frame_graph(W, H, batch=batch)
+    try:
+        for i in range(n):
+            pose = tsdf_amd.SE3(fr["q"][i], fr["t"][i])
+            a.integrate(fr["rgb"][i], fr["depth"][i], fr["ht"][i], fr["lt"][i], K, pose, 4.0)
+            g.frame(fr["rgb"][i], fr["depth"][i], fr["ht"][i], fr["lt"][i], K, pose, 4.0)
+            if i in (4, 13):  # a partly filled batch, launched by the read
+                sa, sb = a.stats(), b.stats()
+                assert sa["active_blocks"] == sb["active_blocks"] and sb["status"] == 0, (i, sa, sb)
+                qa, qb = a.query(None), b.query(None)
+                assert qa.shape == qb.shape and np.array_equal(qa["tsdf"].view(np.uint32), qb["tsdf"].view(np.uint32))
+        b.synchronize()
+        torch.cuda.synchronize()
+        da, db = a.dump(), b.dump()
+        for k in ("entry_pos", "entry_idx", "heap", "rgbw"):
+            assert np.array_equal(da[k], db[k]), k
+        for k in ("tsdf", "prob"):
+            assert np.array_equal(da[k].view(np.uint32), db[k].view(np.uint32)), k
+        assert da["free"] == db["free"]
+    finally:
+        g.close()
+        a.close(), b.close()
