@@ -84,6 +84,8 @@ def parse():
                    help="sharded modes: carve-candidate records per rank per frame (0 = 16384 / G)")
     p.add_argument("--cpu-frames", type=int, default=-1, help="oracle sample size (-1 = auto)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--native-group", action="store_true",
+                   help="with --shard G: the library-owned group (tsdf_group_*) instead of tsdf_amd.ShardGroup")
     p.add_argument("--no-cpp-loop", action="store_true",
                    help="skip the C++ timed loop over the C ABI (disinfect-slam_amd/bench_main) that the "
                         "single-GPU C3 line runs after its own loop (the host enqueue floor without Python)")
@@ -138,6 +140,12 @@ class Run:
         from tsdf_amd import dist as tdist
         self.a, self.mode, self.world, self.dist, self.dev = a, mode, world, dist, dev
         self.frames, self.K, self.poses = frames, K, poses
+        # the frames are inputs already resident in HBM: split them into per-frame views (and the poses
+        # into their C structs) once, so the timed loop's host time is the engine's enqueue, not
+        # torch's tensor indexing
+        self.frame_views = {k: (list(v.unbind(0)) if hasattr(v, "unbind") else v) for k, v in frames.items()}
+        for p_ in poses:
+            p_._c()
         self.sharded = mode in ("routed", "sharded") and world > 1
         si, sc = (rank, world) if self.sharded else (0, 1)
         self.shard_index, self.shard_count = si, sc
@@ -174,7 +182,7 @@ class Run:
 
     def step(self, i):
         from tsdf_amd import dist as tdist
-        a, fr, K, pose = self.a, self.frames, self.K, self.poses[i]
+        a, fr, K, pose = self.a, self.frame_views, self.K, self.poses[i]
         ht = None if a.depth_only else fr["ht"][i]
         lt = None if a.depth_only else fr["lt"][i]
         c5 = a.loop == "c5"
@@ -719,11 +727,16 @@ def rehearsal(a, cam, K, dev):
     fr = synth.render_torch(cam, list(range(nframes)), device=dev)
     poses = [tsdf_amd.SE3(fr["q"][i], fr["t"][i]) for i in range(nframes)]
     pipe = a.mode == "sharded" and not a.graph  # pipelined sharded frames: one exchange per frame
-    grp = tsdf_amd.ShardGroup(G, a.voxel, a.trunc, max_width=a.width, max_height=a.height,
-                              num_block_bits=a.block_bits, device=torch.cuda.current_device(),
-                              key_cap=a.key_cap or max(1024, 32768 // G),
-                              cand_cap=a.cand_cap or max(1024, 16384 // G), split=a.mode != "sharded",
-                              graph=(a.width, a.height) if a.graph else None, pipe=pipe)
+    if a.native_group:  # the library-owned group (tsdf_group_*): the update kernels write every inbox
+        grp = tsdf_amd.Group([torch.cuda.current_device()] * G, a.voxel, a.trunc, max_width=a.width,
+                             max_height=a.height, num_block_bits=a.block_bits)
+        grp.engines = None
+    else:
+        grp = tsdf_amd.ShardGroup(G, a.voxel, a.trunc, max_width=a.width, max_height=a.height,
+                                  num_block_bits=a.block_bits, device=torch.cuda.current_device(),
+                                  key_cap=a.key_cap or max(1024, 32768 // G),
+                                  cand_cap=a.cand_cap or max(1024, 16384 // G), split=a.mode != "sharded",
+                                  graph=(a.width, a.height) if a.graph else None, pipe=pipe)
 
     def step(i):
         ht = None if a.depth_only else fr["ht"][i]
@@ -734,6 +747,8 @@ def rehearsal(a, cam, K, dev):
         step(i)
     grp.flush()
     torch.cuda.synchronize()
+    if a.native_group:
+        grp.engines = [grp.shard(i) for i in range(G)]
     for e in grp.engines:
         e.profile_begin(integrate_only=True, every=1 << 30)
     t0 = time.perf_counter()
@@ -765,7 +780,10 @@ def rehearsal(a, cam, K, dev):
         "dtype": "f32",
         "data": "synthetic (analytic room scene rendered on GPU, resident in HBM)",
         "config": {"workload": workload_name(a), "width": a.width, "height": a.height,
-                   "parallelism": f"{G} {'routed' if a.mode != 'sharded' else 'sharded (pipelined, one exchange per frame)'} shards on one GPU"},
+                   "parallelism": (f"{G} shards on one GPU, library-owned group (tsdf_group_*: pipelined shard "
+                                   "frames, candidates written into every inbox by the update kernels)")
+                   if a.native_group else
+                   f"{G} {'routed' if a.mode != 'sharded' else 'sharded (pipelined, one exchange per frame)'} shards on one GPU"},
         "shards": G,
         "group_ms_per_frame": round(el / n * 1e3, 4),
         "per_shard_device_us": spans,

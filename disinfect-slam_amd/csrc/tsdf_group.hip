@@ -105,6 +105,11 @@ void free_group(tsdf_group* g) {
 // one call of every shard (frames[u]: the frame staged on distinct device u, or NULL: a flush step)
 int group_call(tsdf_group* g, const std::vector<tsdf_frame>* frames, const tsdf_intrinsics* K,
                const tsdf_pose* pose, float max_depth, int32_t* pending) {
+  if (g->n == 1) {  // one shard is one volume: the plain pipelined frames, nothing to exchange
+    g->calls += 1;
+    if (pending) *pending = 0;
+    return frames ? tsdf_integrate(g->shard[0], &(*frames)[0], K, pose, max_depth) : tsdf_flush(g->shard[0]);
+  }
   const int par = (int)(g->calls & 1), prv = par ^ 1;
   const int nu = (int)g->udev.size();
   if (nu > 1 && g->ev_valid) {
@@ -185,7 +190,7 @@ int tsdf_group_create(const tsdf_config* cfg_in, const int* devices, int n, tsdf
   g->shard.assign(n, nullptr);
   for (int i = 0; i < n; ++i) {
     tsdf_config c = g->cfg;
-    c.shard_index = i;
+    c.shard_index = n > 1 ? i : 0;
     c.shard_count = n;
     c.stream = g->stream[g->slot[i]];
     c.use_stream = 1;
@@ -370,6 +375,7 @@ int tsdf_group_raycast(tsdf_group* g, const tsdf_intrinsics* K, int width, int h
   if (!g || !K || !pose || width < 1 || height < 1 || width > g->cfg.max_width || height > g->cfg.max_height)
     return invalid("tsdf_group_raycast: invalid argument");
   GRC(group_flush(g));
+  if (g->n == 1) return tsdf_raycast(g->shard[0], K, width, height, pose, max_depth, rgba, normal, mem_kind);
   // every shard's blocks the view can read (render replicas, tsdf_render_blocks) into one replica
   // engine on the first device, which raycasts exactly what the unsharded volume renders
   int64_t total = 0;

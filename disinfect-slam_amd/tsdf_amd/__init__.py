@@ -165,6 +165,20 @@ def _is_torch_cuda(x) -> bool:
     return hasattr(x, "data_ptr") and hasattr(x, "is_cuda") and bool(x.is_cuda)
 
 
+_raw_stream = None
+
+
+def _current_raw_stream(device: int) -> int:
+    """torch's current stream on `device` as a raw hipStream_t (the cheap accessor when this torch has
+    it: torch.cuda.current_stream() builds a Stream object per call)."""
+    global _raw_stream
+    if _raw_stream is None:
+        import torch
+        f = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        _raw_stream = f if f is not None else (lambda d: torch.cuda.current_stream(d).cuda_stream)
+    return int(_raw_stream(device) or 0)
+
+
 def _ptr(x):
     if x is None:
         return None
@@ -439,7 +453,7 @@ class Engine:
         if not any(_is_torch_cuda(t) for t in tensors if t is not None):
             return None
         import torch
-        cur = int(torch.cuda.current_stream().cuda_stream or 0)
+        cur = _current_raw_stream(torch.cuda.current_device())
         return None if cur == self._stream else cur
 
     def _wait_torch(self, *tensors):
@@ -550,25 +564,26 @@ class Engine:
             self._release_shard_frame()
 
     def integrate(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float):
-        dev = _is_torch_cuda(depth)
+        dev = getattr(depth, "is_cuda", False) is True and hasattr(depth, "data_ptr")
         if dev:  # (the hot path: torch's stream is looked up once, no extra ordering calls when the
-            # engine runs on it)
-            H, W = int(depth.shape[0]), int(depth.shape[1])
-            for a in (rgb, depth, ht, lt):
-                if a is not None and not a.is_contiguous():
-                    raise ValueError("device frames must be contiguous")
-            if tuple(rgb.shape[:2]) != (H, W):
+            # engine runs on it; ctypes passes the structs by reference itself)
+            H, W = depth.shape[0], depth.shape[1]
+            if not (rgb.is_contiguous() and depth.is_contiguous() and (ht is None or ht.is_contiguous())
+                    and (lt is None or lt.is_contiguous())):
+                raise ValueError("device frames must be contiguous")
+            if rgb.shape[0] != H or rgb.shape[1] != W:
                 raise ValueError("rgb / depth size mismatch (voxel_tsdf.cu:352-353)")
             fr = _lib.Frame(W, H, rgb.data_ptr(), depth.data_ptr(), ht.data_ptr() if ht is not None else None,
                             lt.data_ptr() if lt is not None else None, TSDF_MEM_DEVICE)
             Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
-            cur = self._torch_stream((depth,))
+            cur = _current_raw_stream(depth.get_device())
             L = _lib.load()
-            if cur is not None:
+            if cur != self._stream:
                 _lib.check(L.tsdf_stream_wait(self._h, C.c_void_p(cur)), "tsdf_stream_wait")
-            _lib.check(L.tsdf_integrate(self._h, C.byref(fr), C.byref(Kc), C.byref(cam_T_world._c()), max_depth),
-                       "tsdf_integrate")
-            if cur is not None:
+            rc = L.tsdf_integrate(self._h, fr, Kc, cam_T_world._c(), max_depth)
+            if rc:
+                _lib.check(rc, "tsdf_integrate")
+            if cur != self._stream:
                 _lib.check(L.tsdf_stream_signal(self._h, C.c_void_p(cur)), "tsdf_stream_signal")
             return
         else:
@@ -975,16 +990,21 @@ class Group:
                    "tsdf_group_raycast")
         return rgba, normal
 
-    def shard_dump(self, i: int, pool: bool = True) -> dict:
-        """tsdf_debug_dump of shard i's engine (tsdf_group_shard)."""
+    def shard(self, i: int) -> "Engine":
+        """Shard i's engine (tsdf_group_shard: completes the pending frames first), a borrowed handle
+        the group owns -- for dumps, statistics and profiling of one shard; do not close it."""
         h = C.c_void_p()
         _lib.check(_lib.load().tsdf_group_shard(self._g, i, C.byref(h)), "tsdf_group_shard")
-        eng = Engine.__new__(Engine)  # a borrowed handle: the group owns the engine
+        eng = Engine.__new__(Engine)
         eng._h, eng.num_blocks, eng._pending, eng._stream = h, self.num_blocks, None, -1
-        try:
-            return Engine.dump.__wrapped__(eng, pool)
-        finally:
-            eng._h = None
+        eng.device, eng.shard_index, eng.shard_count = self.devices[i], i, self.n
+        eng.voxel_size, eng.truncation = self.voxel_size, self.truncation
+        eng.close = lambda: None  # (borrowed)
+        return eng
+
+    def shard_dump(self, i: int, pool: bool = True) -> dict:
+        """tsdf_debug_dump of shard i's engine (tsdf_group_shard)."""
+        return self.shard(i).dump(pool)
 
     def close(self):
         if getattr(self, "_g", None):

@@ -217,7 +217,8 @@ int tsdf_integrate_shard_abort(tsdf_engine* e);
  * (each shard in entry order); tsdf_group_raycast renders exactly what the unsharded volume renders
  * (render replicas into an engine on devices[0]); tsdf_group_shard gives shard i's engine (e.g. for
  * tsdf_debug_dump); tsdf_group_get_stats sums the shards' counts (each holds, acquires, releases,
- * sees and updates its own blocks: the sums are the unsharded volume's), frames and new keys once. */
+ * sees and updates its own blocks: the sums are the unsharded volume's), frames and new keys once.
+ * n = 1 is one unsharded engine behind the same calls (tsdf_integrate's pipelined frames). */
 typedef struct tsdf_group tsdf_group;
 int tsdf_group_create(const tsdf_config* cfg, const int* devices, int n, tsdf_group** out);
 int tsdf_group_destroy(tsdf_group* g);

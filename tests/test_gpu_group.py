@@ -50,8 +50,9 @@ def _run(G, W, H, voxel, trunc, frames, nb_bits, shard_bits, stride=1, device_fr
         raise
 
 
-@pytest.mark.parametrize("G", [2, 8])
+@pytest.mark.parametrize("G", [1, 2, 8])
 def test_group_c3_union_equals_unsharded(G):
+    """(G = 1: one unsharded engine behind the group calls.)"""
     g, ora, cam = _run(G, 640, 480, 0.005, 0.03, 8, 18, 16, stride=2, checks=(3,))
     g.close(), ora.close()
 
