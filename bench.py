@@ -45,7 +45,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BLOCK_READ_BYTES = 512 * 12 + 12  # voxel state + metadata of one visible block
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_integrate_r5.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_integrate_r6.json")
 # SQ counters of k_raycast (rocprofv3 --pmc passes of `bench.py --loop c5`, scripts/profile_kernel_sq.sh)
 RAYCAST_SQ_FILE = os.path.join(ROOT, "profiles", "r5_raycast_sq.json")
 VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each

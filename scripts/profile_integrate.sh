@@ -17,3 +17,10 @@ for C in FETCH_SIZE WRITE_SIZE; do
     -- python3 bench.py --no-cpu "$@" > "$OUT/pmc_${C}_bench.log" 2>&1
 done
 python3 scripts/summarize_prof.py "$OUT" > "$OUT/summary.txt"
+# keep the per-kernel stats, drop the raw per-dispatch CSVs (the whole output must stay small enough to
+# come back from the GPU box); KEEP_RAW=1 keeps them
+if [ "${KEEP_RAW:-0}" != 1 ]; then
+  st=$(find "$OUT/trace" -name '*kernel_stats.csv' -print -quit)
+  [ -n "$st" ] && cp "$st" "$OUT/kernel_stats.csv"
+  rm -rf "$OUT/trace" "$OUT"/pmc_FETCH_SIZE "$OUT"/pmc_WRITE_SIZE
+fi
