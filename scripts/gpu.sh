@@ -8,11 +8,12 @@
 #   driver            the driver's bench command: bench.py --gpus 1 --steps 20 --warmup 5
 #   profile-driver    kernel trace + FETCH_SIZE / WRITE_SIZE PMC passes of the driver command
 #                     (scripts/profile_integrate.sh; summary + pmc_entry.json under <tag>/prof_driver)
-#   profile-c4|c5|c5graph|c2  the same for those bench lines (default steps) -> <tag>/prof_<name>
+#   profile-c3|c4|c5|c5graph|c2  the same for those bench lines (default steps) -> <tag>/prof_<name>
 #   default           bench.py (300 timed frames, CPU baseline)
 #   c5 | c5graph | c4 | c2 | graph   bench.py --loop c5 [--graph] / 1280x720 / --depth-only / --graph
 #   c5tests           the raycast / render / C5 GPU tests
 #   host-pinned|host-pageable  bench.py --host-frames (C3 frames from host memory through TSDF_MEM_HOST)
+#   group8            bench.py --shard 8 --mode sharded --native-group (C3, 8 shards of one tsdf_group on one GPU)
 #   shard8            bench.py --width 1280 --height 720 --shard 8 (single-GPU 8-shard rehearsal)
 #   sq:<kernel>       SQ counter passes of one kernel on the default command (profile_kernel_sq.sh)
 #   c5trace|c5gtrace  kernel trace (eager / graph) of the C5 loop -> per-frame kernel chain and gaps (scripts/chain_timeline.py)
@@ -50,8 +51,8 @@ for st in "$@"; do
            line $OUT/bench_driver.json ;;
     profile-driver) bash scripts/profile_integrate.sh $OUT/prof_driver $DRIVER || fail $st $OUT/prof_driver/trace_bench.log
            tail -14 $OUT/prof_driver/summary.txt ;;
-    profile-c4|profile-c5|profile-c5graph|profile-c2)
-           case $st in profile-c4) A="--width 1280 --height 720";; profile-c5) A="--loop c5";;
+    profile-c3|profile-c4|profile-c5|profile-c5graph|profile-c2)
+           case $st in profile-c3) A="";; profile-c4) A="--width 1280 --height 720";; profile-c5) A="--loop c5";;
                        profile-c5graph) A="--loop c5 --graph";; profile-c2) A="--depth-only";; esac
            bash scripts/profile_integrate.sh $OUT/prof_${st#profile-} $A || fail $st $OUT/prof_${st#profile-}/trace_bench.log
            tail -14 $OUT/prof_${st#profile-}/summary.txt ;;
@@ -72,6 +73,8 @@ for st in "$@"; do
            line $OUT/bench_host_$k.json; grep -o '"host_frames": {[^}]*}' $OUT/bench_host_$k.json ;;
     c5tests) timeout -k 10 600 $PYT tests/test_gpu_c5.py tests/test_gpu_render.py tests/test_gpu_parity.py tests/test_gpu_golden.py tests/test_gpu_graph.py -m gpu > $OUT/pytest_c5.log 2>&1 || fail $st $OUT/pytest_c5.log
            tail -1 $OUT/pytest_c5.log ;;
+    group8) timeout -k 10 300 python3 bench.py --no-cpu --steps 100 --shard 8 --mode sharded --native-group > $OUT/group8_c3.json 2> $OUT/group8_c3.err || fail $st $OUT/group8_c3.err
+           line $OUT/group8_c3.json ;;
     shard8) timeout -k 10 300 python3 bench.py --no-cpu --steps 100 --width 1280 --height 720 --shard 8 > $OUT/shard8_c4.json 2> $OUT/shard8_c4.err || fail $st $OUT/shard8_c4.err
            line $OUT/shard8_c4.json ;;
     c5trace|c5gtrace) g=; [ $st = c5gtrace ] && g=--graph
