@@ -182,21 +182,34 @@ __device__ __forceinline__ void integrate_tail(const EngineDev& D, const FramePa
 // One visible block's update (tsdf_integrate_kernel, voxel_tsdf.cu:149-205) by one wave of the two
 // that share it (hf: which half of its 512 voxels; 4 voxels per lane). mn: the minimum |tsdf| of the
 // lane's voxels after the update (the carving test), my_upd: + the lane's updated voxels.
-template <bool Raw>
-__device__ __forceinline__ void update_block(const EngineDev& D, const FrameParams& P, const VisRec& r, int lane,
-                                             int hf, float& mn, int& my_upd) {
-  const int rx0 = (lane & 1) * 4, ry = (lane >> 1) & 7, rz = (lane >> 4) + 4 * hf;
-  const int off = (hf * 256 + lane * 4) * 4;
-  const float neg_trunc = -P.trunc;
-  const int32_t pidx = r.idx;
-  uint8_t* blk = D.pool + (size_t)pidx * kBlockBytes;
-#if defined(TSDF_EXP) && (TSDF_EXP & 2)  // experiment build: no pool state loads
-  bool fresh;
-  float4 ts = make_float4(0.5f, 0.5f, 0.5f, 0.5f), pr = ts;
-  uint4 cw = make_uint4(0x05808080u, 0x05808080u, 0x05808080u, 0x05808080u);
-#else
+// The block's loads (pool state: update_issue_pool; projection + pixel gathers: update_issue_pix) and
+// the update itself (update_finish); update_block = all three. (Issuing the next record's loads before
+// finishing this one -- all of them, or the pool state only -- measured 5-17 % slower at 4-6 waves per
+// SIMD: the carried state spills at 5-6 waves, and 4 waves starve the launch's tiles;
+// profiles/ab/r6_update_prefetch_ab.txt.)
+struct UpdState {
   float4 ts, pr;
   uint4 cw;
+  float4 px[4];
+  uint32_t pc[4];
+  v2f hzs[2];
+  bool inb[4];
+  bool fresh;
+};
+
+__device__ __forceinline__ void update_issue_pool(const EngineDev& D, const VisRec& r, int lane, int hf,
+                                                  UpdState& S) {
+  const int off = (hf * 256 + lane * 4) * 4;
+  const int32_t pidx = r.idx;
+  uint8_t* blk = D.pool + (size_t)pidx * kBlockBytes;
+  float4& ts = S.ts;
+  float4& pr = S.pr;
+  uint4& cw = S.cw;
+#if defined(TSDF_EXP) && (TSDF_EXP & 2)  // experiment build: no pool state loads
+  bool fresh;
+  ts = make_float4(0.5f, 0.5f, 0.5f, 0.5f), pr = ts;
+  cw = make_uint4(0x05808080u, 0x05808080u, 0x05808080u, 0x05808080u);
+#else
   const bool fresh = r.pad != 0;
   if (fresh) {  // wave-uniform: a block created this frame loads nothing
     ts = make_float4(-1.f, -1.f, -1.f, -1.f);
@@ -214,10 +227,19 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
 #if defined(TSDF_EXP) && (TSDF_EXP & 2)
   fresh = r.pad != 0;
 #endif
+  S.fresh = fresh;
+}
+template <bool Raw>
+__device__ __forceinline__ void update_issue_pix(const EngineDev& D, const FrameParams& P, const VisRec& r, int lane,
+                                                 int hf, UpdState& S) {
+  const int rx0 = (lane & 1) * 4, ry = (lane >> 1) & 7, rz = (lane >> 4) + 4 * hf;
+  float4* px = S.px;
+  uint32_t* pc = S.pc;
+  v2f* hzs = S.hzs;
+  bool* inb = S.inb;
   const int16_t ax0 = (int16_t)(r.x << kBlockLenBits), ay = (int16_t)((r.y << kBlockLenBits) + ry),
                 az = (int16_t)((r.z << kBlockLenBits) + rz);
   const float fy = (float)ay * P.voxel, fz = (float)az * P.voxel;
-  int upd_mask = 0;
   // ---- pass 1: project the lane's 4 voxels (two packed pairs) and issue every pixel gather
   // before any is consumed (predicated, so all 8 stay in flight together).
   // cam_T_world * (x voxel, fy, fz) in QuaternionBase::_transformVector's exact order, with the
@@ -228,10 +250,6 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
   float uvx = qy * fz - qz * fy;
   uvx += uvx;
   const float w_uvx = qw * uvx, qz_uvx = qz * uvx, qy_uvx = qy * uvx;
-  v2f hzs[2];
-  float4 px[4];
-  uint32_t pc[4];   // rgb
-  bool inb[4];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const v2f wx = v2((float)(int16_t)(ax0 + rx0 + 2 * k), (float)(int16_t)(ax0 + rx0 + 2 * k + 1)) * P.voxel;
@@ -275,6 +293,29 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
 #endif
     }
   }
+}
+
+template <bool Raw>
+__device__ __forceinline__ void update_issue(const EngineDev& D, const FrameParams& P, const VisRec& r, int lane,
+                                             int hf, UpdState& S) {
+  update_issue_pool(D, r, lane, hf, S);
+  update_issue_pix<Raw>(D, P, r, lane, hf, S);
+}
+
+template <bool Raw>
+__device__ __forceinline__ void update_finish(const EngineDev& D, const FrameParams& P, const VisRec& r, int lane,
+                                              int hf, UpdState& S, float& mn, int& my_upd) {
+  const int off = (hf * 256 + lane * 4) * 4;
+  const float neg_trunc = -P.trunc;
+  uint8_t* blk = D.pool + (size_t)r.idx * kBlockBytes;
+  float4 ts = S.ts, pr = S.pr;
+  uint4 cw = S.cw;
+  const float4* px = S.px;
+  const uint32_t* pc = S.pc;
+  const v2f* hzs = S.hzs;
+  const bool* inb = S.inb;
+  const bool fresh = S.fresh;
+  int upd_mask = 0;
   // ---- pass 2: tsdf_integrate_kernel's update (voxel_tsdf.cu:174-203) of tsdf, colour and weight,
   // branch-free on packed pairs; each voxel's result is kept only where it is updated (the
   // reference's conditions: in image, 0 < d <= max_depth, sdf > -trunc). The semantic update
@@ -416,6 +457,14 @@ __device__ __forceinline__ void update_block(const EngineDev& D, const FramePara
       }
   }
   my_upd += __popc(upd_mask);
+}
+
+template <bool Raw>
+__device__ __forceinline__ void update_block(const EngineDev& D, const FrameParams& P, const VisRec& r, int lane,
+                                             int hf, float& mn, int& my_upd) {
+  UpdState S;
+  update_issue<Raw>(D, P, r, lane, hf, S);
+  update_finish<Raw>(D, P, r, lane, hf, S, mn, my_upd);
 }
 
 // The concatenated band lists: band i holds visible-block indices [start_i, start_i + count_i).
