@@ -118,7 +118,7 @@ union RenderIngestLds {
   IngestLds<1024> ing;
   uint32_t bits[kViewGraphBitmapWords];  // the raycast's staged bitmaps
 };
-__global__ __launch_bounds__(256) RENDER_INGEST_WAVES void k_render_ingest(
+__global__ __launch_bounds__(256) RENDER_INGEST_WAVES TSDF_RAY_PK void k_render_ingest(
     EngineDev D, FrameParams R, float step_size, ViewGrid V, uchar4* __restrict__ rgba, uchar4* __restrict__ normal,
     int rgx, int nray, FrameParams P, const float* __restrict__ depth, const uint8_t* __restrict__ rgb,
     const float* __restrict__ ht, const float* __restrict__ lt, int tiles_x, int tiles) {
@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256) RENDER_INGEST_WAVES void k_render_ingest(
   }
   ingest_dda<1024>(D, P, depth, rgb, ht, lt, tiles_x, tiles, U.ing, b - nray, (int)gridDim.x - nray);
 }
-__global__ __launch_bounds__(256) RENDER_INGEST_WAVES void k_render_ingest_g(EngineDev D,
+__global__ __launch_bounds__(256) RENDER_INGEST_WAVES TSDF_RAY_PK void k_render_ingest_g(EngineDev D,
                                                                             const FrameArgs* __restrict__ A,
                                                                             int rgx, int nray) {
   __shared__ RenderIngestLds U;

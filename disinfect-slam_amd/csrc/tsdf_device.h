@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+
 namespace tsdf {
 
 constexpr int kBlockLenBits = 3;
@@ -225,9 +226,10 @@ __device__ __forceinline__ uint32_t round_quot_u8(float a, float b, float rb) {
   return (uint32_t)min(255, max(0, round_quot_i(a, b, rb)));
 }
 
-// ---- the same helpers on voxel pairs: ext_vector float2 arithmetic lowers to gfx950's packed
-// v_pk_{mul,add,fma}_f32 (IEEE per element, so results are identical to the scalar forms); lanes
-// with act == false never take the IEEE fallback (their results are discarded by the caller) ----
+// ---- the same helpers on voxel pairs (ext_vector float2 arithmetic: IEEE per element, so results are
+// identical to the scalar forms; plain fp32 instructions: the library is built without packed fp32,
+// Makefile NOPK); lanes with act == false never take the IEEE fallback (their results are discarded by
+// the caller) ----
 typedef float v2f __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ v2f v2(float a, float b) {
   v2f r;

@@ -160,13 +160,13 @@ __device__ __forceinline__ void view_pack(const ViewGrid& V) {
 __global__ __launch_bounds__(256) void k_view_pack(ViewGrid V) { view_pack(V); }
 __global__ __launch_bounds__(256) void k_view_pack_g(const FrameArgs* __restrict__ A) { view_pack(A->V); }
 
-__global__ __launch_bounds__(256) void k_raycast(EngineDev D, FrameParams P, float step_size, ViewGrid V,
+__global__ __launch_bounds__(256) TSDF_RAY_PK void k_raycast(EngineDev D, FrameParams P, float step_size, ViewGrid V,
                                                  uchar4* __restrict__ rgba, uchar4* __restrict__ normal) {
   extern __shared__ uint32_t sbits[];
   raycast(D, P, step_size, V, sbits, rgba, normal, blockIdx.y * gridDim.x + blockIdx.x, gridDim.x,
           gridDim.x * gridDim.y);
 }
-__global__ __launch_bounds__(256) void k_raycast_g(EngineDev D, const FrameArgs* __restrict__ A) {
+__global__ __launch_bounds__(256) TSDF_RAY_PK void k_raycast_g(EngineDev D, const FrameArgs* __restrict__ A) {
   __shared__ uint32_t sbits[kViewGraphBitmapWords];
   const FrameParams R = A->R;
   const ViewGrid V = A->V;

@@ -5,6 +5,13 @@
 #include "tsdf_block.h"
 #include "tsdf_kernels.h"
 
+// The library is built without packed fp32 (Makefile NOPK); the raycast kernels (k_raycast*,
+// k_render_ingest*) turn it back on: their march keeps independent x / y / z work to pair, and on the
+// C5 loop they measured faster with it (8.07-8.09k frames/s vs 7.85-7.89k without; k_raycast 59.3 vs
+// 60.9 us; profiles/ab/r6_no_packed_fp32_ab.txt). The host pass of a kernel ignores the attribute.
+#define TSDF_RAY_PK __attribute__((target("packed-fp32-ops")))
+#pragma clang diagnostic ignored "-Wignored-attributes"
+
 namespace tsdf {
 
 // One ray's block cache (the reference's per-thread VoxelBlock cache, voxel_hash.cuh:124-161): the

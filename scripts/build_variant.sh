@@ -6,7 +6,7 @@ NAME=$1; FLAGS=$2
 cd "$(dirname "$0")/../disinfect-slam_amd"
 OUT=build/var_$NAME
 mkdir -p $OUT
-HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function -I../include -Icsrc $FLAGS"
+HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function ${NOPK--Xclang -target-feature -Xclang -packed-fp32-ops} -I../include -Icsrc $FLAGS"
 pids=()
 for f in csrc/tsdf_alloc.hip csrc/tsdf_fuse.hip csrc/tsdf_extract.hip csrc/tsdf_mesh.hip csrc/tsdf_frontend.hip csrc/tsdf_engine.hip csrc/tsdf_group.hip; do
   /opt/rocm/bin/hipcc $HIPFLAGS -c $f -o $OUT/$(basename $f .hip).o & pids+=($!)
