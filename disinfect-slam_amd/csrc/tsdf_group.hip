@@ -62,6 +62,7 @@ struct tsdf_group {
   std::vector<int> slot;                 // shard -> index in udev
   std::vector<hipStream_t> stream;       // per distinct device: the stream of its shards
   std::vector<hipEvent_t> ev;            // per distinct device: recorded after its shards' call
+  std::vector<hipEvent_t> sig;           // per distinct device: tsdf_group_stream_signal's marker
   bool ev_valid = false;
   int32_t cap = kGroupCandCap;
   std::vector<ShardRec*> inbox[2];       // per shard, on its device: n slots of cap + 1 records
@@ -96,6 +97,8 @@ void free_group(tsdf_group* g) {
     if (b) (void)hipFree(b);
   if (g->rec_all) (void)hipFree(g->rec_all);
   for (hipEvent_t e : g->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : g->sig)
     if (e) (void)hipEventDestroy(e);
   for (hipStream_t s : g->stream)
     if (s) (void)hipStreamDestroy(s);
@@ -173,10 +176,12 @@ int tsdf_group_create(const tsdf_config* cfg_in, const int* devices, int n, tsdf
   const int nu = (int)g->udev.size();
   g->stream.assign(nu, nullptr);
   g->ev.assign(nu, nullptr);
+  g->sig.assign(nu, nullptr);
   for (int u = 0; u < nu; ++u) {
     hipError_t e = hipSetDevice(g->udev[u]);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->stream[u], hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&g->ev[u], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&g->sig[u], hipEventDisableTiming);
     for (int v = 0; v < nu && e == hipSuccess; ++v) {  // peer stores into the other devices' inboxes
       if (v == u) continue;
       e = hipDeviceEnablePeerAccess(g->udev[v], 0);
@@ -367,6 +372,18 @@ int tsdf_group_query(tsdf_group* g, const float* bounds, tsdf_voxel* out, int64_
     GRC(tsdf_query(g->shard[s], bounds, out + off, capacity - off, &c));
     off += c;
   }
+  return TSDF_OK;
+}
+
+int tsdf_group_stream_signal(tsdf_group* g, void* stream) {
+  if (!g) return TSDF_ERR_INVALID_ARG;
+  const int nu = (int)g->udev.size();
+  for (int u = 0; u < nu; ++u) {
+    GHIP(hipSetDevice(g->udev[u]));
+    GHIP(hipEventRecord(g->sig[u], g->stream[u]));
+  }
+  GHIP(hipSetDevice(g->udev[0]));
+  for (int u = 0; u < nu; ++u) GHIP(hipStreamWaitEvent(static_cast<hipStream_t>(stream), g->sig[u], 0));
   return TSDF_OK;
 }
 

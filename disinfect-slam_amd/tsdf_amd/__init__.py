@@ -940,7 +940,9 @@ class Group:
 
     def integrate(self, rgb, depth, ht, lt, K, cam_T_world: SE3, max_depth: float):
         """Host arrays, or device tensors on devices[0] (contiguous; torch's stream is synchronised
-        first: the group runs on its own streams)."""
+        first: the group runs on its own streams, and torch's current stream is ordered after the
+        group's work afterwards -- tsdf_group_stream_signal -- so the frame's tensors may be reused or
+        freed on it)."""
         dev = _is_torch_cuda(depth)
         if dev:
             import torch
@@ -955,8 +957,12 @@ class Group:
             H, W = depth.shape
         fr = _lib.Frame(W, H, _ptr(rgb), _ptr(depth), _ptr(ht), _ptr(lt), TSDF_MEM_DEVICE if dev else TSDF_MEM_HOST)
         Kc = K._c() if isinstance(K, CameraIntrinsics) else _lib.Intrinsics(*[float(v) for v in K])
-        _lib.check(_lib.load().tsdf_group_integrate(self._g, C.byref(fr), C.byref(Kc), C.byref(cam_T_world._c()),
-                                                    max_depth), "tsdf_group_integrate")
+        L = _lib.load()
+        _lib.check(L.tsdf_group_integrate(self._g, C.byref(fr), C.byref(Kc), C.byref(cam_T_world._c()), max_depth),
+                   "tsdf_group_integrate")
+        if dev:
+            _lib.check(L.tsdf_group_stream_signal(self._g, C.c_void_p(_current_raw_stream(self.devices[0]))),
+                       "tsdf_group_stream_signal")
 
     def flush(self):
         _lib.check(_lib.load().tsdf_group_flush(self._g), "tsdf_group_flush")

@@ -115,6 +115,7 @@ EXPORTS = [
     "tsdf_graph_create_batch",
     "tsdf_group_create", "tsdf_group_destroy", "tsdf_group_size", "tsdf_group_integrate", "tsdf_group_flush",
     "tsdf_group_synchronize", "tsdf_group_shard", "tsdf_group_get_stats", "tsdf_group_query", "tsdf_group_raycast",
+    "tsdf_group_stream_signal",
 ]
 
 _lib = None
@@ -156,6 +157,7 @@ def load(path: str | None = None):
     L.tsdf_group_get_stats.argtypes = [P, C.POINTER(Stats), i]
     L.tsdf_group_query.argtypes = [P, P, P, i64, C.POINTER(i64)]
     L.tsdf_group_raycast.argtypes = [P, C.POINTER(Intrinsics), i, i, C.POINTER(Pose), f, P, P, i]
+    L.tsdf_group_stream_signal.argtypes = [P, P]
     L.tsdf_stream_wait.argtypes = [P, P]
     L.tsdf_stream_signal.argtypes = [P, P]
     L.tsdf_get_stream.argtypes = [P, C.POINTER(P)]
@@ -233,7 +235,7 @@ def load(path: str | None = None):
                  "tsdf_graph_create_batch",
                  "tsdf_group_create", "tsdf_group_destroy", "tsdf_group_size", "tsdf_group_integrate",
                  "tsdf_group_flush", "tsdf_group_synchronize", "tsdf_group_shard", "tsdf_group_get_stats",
-                 "tsdf_group_query", "tsdf_group_raycast"):
+                 "tsdf_group_query", "tsdf_group_raycast", "tsdf_group_stream_signal"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

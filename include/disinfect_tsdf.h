@@ -233,6 +233,12 @@ int tsdf_group_query(tsdf_group* g, const float* bounds, tsdf_voxel* out, int64_
 int tsdf_group_raycast(tsdf_group* g, const tsdf_intrinsics* K, int width, int height,
                        const tsdf_pose* cam_T_world, float max_depth, uint8_t* rgba, uint8_t* normal,
                        int mem_kind);
+/* Orders `stream` (a hipStream_t of devices[0]) after every shard's queued work: a device frame passed to
+ * tsdf_group_integrate is read by the group's own streams after the call returns (its launch, and the
+ * peer copies to the other devices), so a caller that reuses or frees the frame's memory on its stream
+ * calls this first (the Python Group does, after every device-frame integrate) -- the group's analogue of
+ * tsdf_stream_signal. Does not complete pending frames and does not wait on the host. */
+int tsdf_group_stream_signal(tsdf_group* g, void* stream);
 
 /* Stream ordering with a caller's HIP stream (e.g. torch's current stream) for device buffers
  * passed to an engine that runs on its own stream: tsdf_stream_wait makes the engine stream wait

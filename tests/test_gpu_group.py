@@ -114,3 +114,34 @@ def test_group_argument_errors():
         assert g.stats()["status"] == 0
     finally:
         g.close()
+
+
+def test_group_device_frame_buffers_reused_on_torch_stream():
+    """Device frames in ONE set of tensors, overwritten on torch's stream right after every
+    tsdf_group_integrate (the group reads them on its own streams after the call returns; Group orders
+    torch's stream after that work with tsdf_group_stream_signal): the union still equals the oracle."""
+    import torch
+
+    import tsdf_amd
+    from tsdf_amd import synth
+    from _oracle import OracleGrid
+    W, H = 160, 120
+    cam = synth.camera(W, H, synth.TUM_FR1)
+    g = tsdf_amd.Group([0, 0], 0.01, 0.04, max_width=W, max_height=H, num_block_bits=15)
+    ora = OracleGrid(0.01, 0.04, 16)
+    try:
+        frames = [synth.render(cam, 2 * f, touch="independent") for f in range(10)]
+        dv = {k: torch.from_numpy(np.ascontiguousarray(frames[0][k])).cuda() for k in ("rgb", "depth", "ht", "lt")}
+        junk = {k: torch.full_like(v, 7) for k, v in dv.items()}
+        for f, fr in enumerate(frames):
+            for k in dv:
+                dv[k].copy_(torch.from_numpy(np.ascontiguousarray(fr[k])).cuda())
+            g.integrate(dv["rgb"], dv["depth"], dv["ht"], dv["lt"], cam.K, tsdf_amd.SE3(fr["q"], fr["t"]), MAXD)
+            for k in dv:  # overwrite at once, on torch's stream (ordered after the group's reads)
+                dv[k].copy_(junk[k])
+            ora.integrate(fr["rgb"], fr["depth"], fr["ht"], fr["lt"], MAXD, cam.K, fr["q"], fr["t"])
+        s, so = g.stats(), ora.stats()
+        assert s["status"] == 0 and s["active_blocks"] == so["active_blocks"], (s, so)
+        assert_union_equals([g.shard_dump(i) for i in range(2)], ora.dump(), tag="reused buffers")
+    finally:
+        g.close(), ora.close()
