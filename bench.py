@@ -72,9 +72,10 @@ def parse():
                         "marching cubes of the whole volume every 30 frames (eager chain)")
     p.add_argument("--graph", action="store_true",
                    help="frames through the graph-captured frame (one hipGraph launch per frame)")
-    p.add_argument("--graph-batch", type=int, default=1,
+    p.add_argument("--graph-batch", type=int, default=None,
                    help="with --graph: frames per graph launch (tsdf_graph_create_batch; the launch's fixed "
-                        "cost paid once per batch)")
+                        "cost paid once per batch). Default 16 for the C3 loop (19.6k vs 16.6k frames/s at "
+                        "1), 1 for C5 (its batches measured slower: DESIGN.md 4 round 6)")
     p.add_argument("--shard", default=None, metavar="G",
                    help="single-GPU rehearsal of the routed sharded volume: G shard engines on this GPU "
                         "exchanging their slots with device copies; reports the per-shard frame time")
@@ -114,7 +115,10 @@ def parse():
                    help="C5 loop: immediate tsdf_raycast / tsdf_graph_create instead of tsdf_raycast_deferred / "
                         "tsdf_graph_create_deferred (the raycast then runs in its own launch instead of "
                         "beside the next frame's ingest)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.graph_batch is None:
+        a.graph_batch = 16 if a.loop != "c5" else 1
+    return a
 
 
 def workload_name(a):
