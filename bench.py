@@ -75,7 +75,7 @@ def parse():
     p.add_argument("--graph-batch", type=int, default=None,
                    help="with --graph: frames per graph launch (tsdf_graph_create_batch; the launch's fixed "
                         "cost paid once per batch). Default 16 for the C3 loop (19.6k vs 16.6k frames/s at "
-                        "1), 1 for C5 (its batches measured slower: DESIGN.md 4 round 6)")
+                        "1), 8 for C5 (7.2k vs 6.76k at 1 and 6.95k at 16; DESIGN.md 4 round 6)")
     p.add_argument("--shard", default=None, metavar="G",
                    help="single-GPU rehearsal of the routed sharded volume: G shard engines on this GPU "
                         "exchanging their slots with device copies; reports the per-shard frame time")
@@ -117,7 +117,7 @@ def parse():
                         "beside the next frame's ingest)")
     a = p.parse_args()
     if a.graph_batch is None:
-        a.graph_batch = 16 if a.loop != "c5" else 1
+        a.graph_batch = 16 if a.loop != "c5" else 8
     return a
 
 
