@@ -92,7 +92,7 @@ hipError_t dmalloc(T** p, size_t count) {
 //   TSDF_PIPELINE=0               unpipelined frames: two launches per frame (k_ingest_dda, k_integrate)
 //   TSDF_PIPE_MAX_PIXELS=n        largest frame (pixels) that is pipelined (default 2^19; C4 above it)
 //   TSDF_FRAME_ORDER=0..4         k_frame grid order of its parts (PipeArgs.order; default 2)
-//   TSDF_FRAME_WG_PER_CU=n        k_frame update workgroups per CU (default kFrameUpdWgsPer2Cu / 2 = 3)
+//   TSDF_FRAME_WG_PER_CU=n        k_frame update workgroups per CU (default kFrameUpdWgsPer2Cu / 2 = 2.5: 640)
 //   TSDF_FRAME_UPD_WGS=n          (A/B) k_frame update workgroups in total (overrides the per-CU count)
 //   TSDF_FRAME_TILES_PER_WG=n     (A/B) k_frame pixel tiles per tile workgroup (default 1)
 //   TSDF_INTEGRATE_WG_PER_CU=n    cap on k_integrate's resident workgroups per CU

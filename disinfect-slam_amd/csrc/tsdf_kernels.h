@@ -114,7 +114,7 @@ constexpr int kPipeAPub = kPipeIngEnd + 32;     // + 16 p: allocation published 
 constexpr int kPipeStats = 512;                 // + 1024 p + 16 i: payload (blocks << 40 | voxels) and,
 constexpr int kPipeStatLines = 64;              //   at +1, the latest end stamp of update counter i
 constexpr int kPipeWords = kPipeStats + 2 * kPipeStatLines * 16;
-constexpr int kFrameUpdWgsPer2Cu = 6;           // default k_frame update workgroups per two CUs (TSDF_FRAME_WG_PER_CU)
+constexpr int kFrameUpdWgsPer2Cu = 5;           // default k_frame update workgroups per two CUs (TSDF_FRAME_WG_PER_CU)
 constexpr int kPipeHead = 8;                    // workgroups before the update's (0: carving + allocation)
 constexpr int kPipeFreshWG = 64;                // workgroups that update the blocks allocated in the launch
 constexpr int kPipeDefer = 32;                  // deferred (carve-pending) blocks one update workgroup holds
