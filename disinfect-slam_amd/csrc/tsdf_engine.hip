@@ -644,10 +644,11 @@ int tsdf_create(const tsdf_config* cfg_in, int device, tsdf_engine** out) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_pre, reinterpret_cast<const void*>(k_frame),
                                                      kIntegrateThreads, 0) != hipSuccess)
       return fail(TSDF_ERR_HIP);
-    // 3 update workgroups per CU by default (of 6 that fit): the other slots take the sweep's and
-    // the tiles' workgroups from the start. Round 6 (the semantic update's exact chain, 6 waves per
-    // SIMD): 768 update workgroups 19.6k frames/s on the driver command, 640 18.7-19.4k, 896 19.2k,
-    // 1024 18.6k, 512 17.6k (profiles/ab/r6_*). Round 5 (log-odds state, 7 waves): 640 23.9k, 768
+    // 2.5 update workgroups per CU by default (of 6 that fit): the other slots take the sweep's and
+    // the tiles' workgroups from the start. Round 6, final build (exact semantic chain, 6 waves per
+    // SIMD, no packed fp32): 640 update workgroups 20.94-20.99k frames/s on the driver command, 704
+    // 20.8-21.0k, 768 20.6k, 896 20.2k (profiles/ab/r6_upd_wgs_nopk_ab.txt); with packed fp32 768 was
+    // ahead (19.6k vs 18.7-19.4k at 640). Round 5 (log-odds state, 7 waves): 640 23.9k, 768
     // 23.3-23.5k, 512 23.4-23.7k; earlier rounds: 4 per CU 22.0-22.5k, 5 21.0-21.3k, 7 18.5-18.7k
     int upd = kFrameUpdWgsPer2Cu * ncu / 2;
     if (e->env.frame_wg_per_cu > 0) upd = e->env.frame_wg_per_cu * ncu;
