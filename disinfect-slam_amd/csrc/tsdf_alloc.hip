@@ -87,7 +87,10 @@ __device__ __forceinline__ void ingest_dda(EngineDev D, FrameParams P,
 #define TSDF_INGEST_MIN_WAVES 8
 #endif
 #define INGEST_WAVES(TS) __attribute__((amdgpu_waves_per_eu(TS <= 1024 ? TSDF_INGEST_MIN_WAVES : 5)))
-#define RENDER_INGEST_WAVES __attribute__((amdgpu_waves_per_eu(6)))
+#ifndef TSDF_RENDER_INGEST_WAVES
+#define TSDF_RENDER_INGEST_WAVES 6
+#endif
+#define RENDER_INGEST_WAVES __attribute__((amdgpu_waves_per_eu(TSDF_RENDER_INGEST_WAVES)))
 template <int TS>
 __global__ __launch_bounds__(256) INGEST_WAVES(TS) void k_ingest_dda(EngineDev D, FrameParams P,
                                                     const float* __restrict__ depth,
