@@ -323,7 +323,7 @@ __device__ __forceinline__ v2f div_pair0(v2f a, v2f b, v2f y, bool act0, bool ac
 // explicit single-precision algorithms (oracle/ora_math.c, < 0.87 / 0.99 ulp from the correctly
 // rounded values over every input) and these are the same operations -- frexp, rint, ldexp, fma and
 // + - * with one IEEE rounding each -- so they return the oracle's bits for all 2^32 inputs
-// (libtsdf_selfcheck digests, tests/test_gpu_numerics.py). Pairs run on packed v_pk_fma_f32.
+// (libtsdf_selfcheck digests, tests/test_gpu_numerics.py). Pairs run as v2f pairs (plain fp32 instructions: the library is built without packed fp32).
 constexpr float kSemQ[9] = {0x1.555554p-2f,  -0x1.fffffcp-3f, 0x1.999d5ap-3f,  -0x1.555b4ap-3f, 0x1.23d21ap-3f,
                             -0x1.fcf4c6p-4f, 0x1.dea282p-4f,  -0x1.d635bcp-4f, 0x1.1d8ea4p-4f};
 constexpr float kSemE[6] = {0x1p-1f, 0x1.555556p-3f, 0x1.5554eap-5f, 0x1.1110e0p-7f, 0x1.6d4316p-10f,
