@@ -1599,11 +1599,16 @@ int graph_create(tsdf_engine* e, int width, int height, int render_width, int re
         hipLaunchKernelGGL(k_ingest_dda_g<1024>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
       else
         hipLaunchKernelGGL(k_ingest_dda_g<2048>, dim3(kVisWorkgroups + tiles), dim3(256), 0, g->cap, e->D, A);
-      hipLaunchKernelGGL((k_integrate_t<true, false>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0,
-                         g->cap, e->D, FrameParams{}, A);
+      if (render_width && e->env.fuse_view_grid)  // the render camera's view grid built in the update launch
+        hipLaunchKernelGGL(k_integrate_vg_g, dim3(e->D.integrate_grid + kOccWords / 256), dim3(kIntegrateThreads), 0,
+                           g->cap, e->D, A, e->D.integrate_grid);
+      else
+        hipLaunchKernelGGL((k_integrate_t<true, false>), dim3(e->D.integrate_grid), dim3(kIntegrateThreads), 0,
+                           g->cap, e->D, FrameParams{}, A);
     }
     if (render_width) {
-      hipLaunchKernelGGL(k_view_grid_g, dim3(kOccWords / 256), dim3(256), 0, g->cap, e->D, A);
+      if (g->pipe || !e->env.fuse_view_grid)
+        hipLaunchKernelGGL(k_view_grid_g, dim3(kOccWords / 256), dim3(256), 0, g->cap, e->D, A);
       hipLaunchKernelGGL(k_view_pack_g, dim3(kViewPackGrid), dim3(256), 0, g->cap, A);
       const dim3 rgrid((render_width + 15) / 16, (render_height + 15) / 16);
       if (!g->defer) hipLaunchKernelGGL(k_raycast_g, rgrid, dim3(256), 0, g->cap, e->D, A);
@@ -1887,6 +1892,7 @@ int tsdf_graph_frame(tsdf_graph* g, const tsdf_frame* f, const tsdf_intrinsics* 
     }
     int rc = view_grid_for(e, a.R, a.step_size, kViewGraphBitmapWords, &a.V);
     if (rc) return rc;
+    a.vtag = 0x80000000u | (uint32_t)(e->vg_calls & 0x7FFFFFFFu);  // (never a frame id)
   }
   a.prev = prev;
   a.range = (uint32_t)((size_t)f->width * f->height * e->maxs);

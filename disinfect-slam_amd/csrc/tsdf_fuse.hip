@@ -638,14 +638,14 @@ __attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES)))
 // update leaves it (nothing in the launch but the carving changes the table) -- its cells written
 // through (sc1) -- and the carving's last arriver clears the cells of the blocks it released. The
 // k_view_grid launch and its kernel boundary drop out of the frame.
-__global__ __launch_bounds__(kIntegrateThreads)
-__attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES))) void k_integrate_vg(
-    EngineDev D, FrameParams Pv, FrameParams R, ViewGrid V, uint32_t vtag, int nint) {
-  __shared__ DeleteLds L;
+template <bool Graph>
+__device__ __forceinline__ void integrate_vg(const EngineDev& D, const FrameParams& Pv, const FrameArgs* A,
+                                             const FrameParams& R, const ViewGrid& V, uint32_t vtag, int nint,
+                                             DeleteLds& L) {
   const ViewFuse F{R, V, vtag};
   const int narr = (int)gridDim.x;
   if ((int)blockIdx.x < nint) {
-    integrate_body<false, false>(D, Pv, nullptr, nint, L, narr, &F);
+    integrate_body<Graph, false>(D, Pv, A, nint, L, narr, &F);
     return;
   }
   const int w = ((int)blockIdx.x - nint) * 256 + (int)threadIdx.x;  // (one occupancy word per thread)
@@ -670,7 +670,27 @@ __attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES)))
   }
   __shared__ int s_last;
   if (!arrive_last(D.arrive + kArrIntegrate, 0ull, &s_last, true, (uint32_t)narr)) return;
-  integrate_tail(D, Pv, L, &F);
+  if (Graph) {  // (integrate_body's graph parameters: the frame's camera, the carving tail)
+    FrameParams P = A->P;
+    P.tail = kTailResolve;
+    integrate_tail(D, P, L, &F);
+  } else {
+    integrate_tail(D, Pv, L, &F);
+  }
+}
+__global__ __launch_bounds__(kIntegrateThreads)
+__attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES))) void k_integrate_vg(
+    EngineDev D, FrameParams Pv, FrameParams R, ViewGrid V, uint32_t vtag, int nint) {
+  __shared__ DeleteLds L;
+  integrate_vg<false>(D, Pv, nullptr, R, V, vtag, nint, L);
+}
+// the graph-captured form (a render graph's update node): camera, render camera, grid and release tag
+// from the frame's argument block
+__global__ __launch_bounds__(kIntegrateThreads)
+__attribute__((amdgpu_waves_per_eu(TSDF_INTEGRATE_WAVES, TSDF_INTEGRATE_WAVES))) void k_integrate_vg_g(
+    EngineDev D, const FrameArgs* __restrict__ A, int nint) {
+  __shared__ DeleteLds L;
+  integrate_vg<true>(D, FrameParams{}, A, A->R, A->V, A->vtag, nint, L);
 }
 
 // =============================================================================================

@@ -176,6 +176,7 @@ struct FrameArgs {
   uchar4* normal;
   float step_size;  // raycast step (truncation / 2)
   ViewGrid V;       // the raycast node's view grid (n == 0: hash lookups)
+  uint32_t vtag;    // the render graph's update node (k_integrate_vg_g): the carving's release tag
   uint32_t range;   // candidate order space W * H * maxs
   int tiles_x, tiles;
   // a shard's graph frame (tsdf_graph_shard_*): the exchange slots of its three segments
@@ -272,6 +273,7 @@ __global__ void k_render_ingest(EngineDev D, FrameParams R, float step_size, Vie
 __global__ void k_render_ingest_g(EngineDev D, const FrameArgs* A, int rgx, int nray);
 // k_integrate plus the render camera's view grid (the C5 loop's deferred raycast; tsdf_fuse.hip)
 __global__ void k_integrate_vg(EngineDev D, FrameParams Pv, FrameParams R, ViewGrid V, uint32_t vtag, int nint);
+__global__ void k_integrate_vg_g(EngineDev D, const FrameArgs* A, int nint);
 // view grid of a raycast: grid kOccWords / 256 workgroups of 256
 __global__ void k_view_grid(EngineDev D, FrameParams P, ViewGrid V);
 __global__ void k_view_grid_g(EngineDev D, const FrameArgs* A);
