@@ -100,7 +100,7 @@ hipError_t dmalloc(T** p, size_t count) {
 //   TSDF_MESH_GRID=n              (tests) fewer k_mesh workgroups, to exercise its grid stride
 //   TSDF_RENDER_OVERLAP=1         raycast on a second stream overlapping the next frame
 //   TSDF_GRAPH_MEMCPY_NODE=1      (A/B) graph frames upload their arguments with a memcpy node
-//   TSDF_FUSE_VIEW_GRID=0         (A/B) the C5 loop's view grid in its own launch, not in the update's
+//   TSDF_FUSE_VIEW_GRID=0         (A/B) the C5 loop's view grid in its own launch (render graphs: own node), not in the update's
 //   TSDF_UPLOAD_STREAMS=n         (A/B) host frames: upload streams a frame's copies spread over (1-4, default 2)
 // ---------------------------------------------------------------------------------------------
 struct EnvKnobs {
